@@ -1,0 +1,260 @@
+/*
+ * thunder_amd.h -- C-ABI of the MI355X (gfx950) expectation / insert engine.
+ *
+ * This is the drop-in boundary for THUNDER's GPU plugin surface
+ * (gpu/interface/Interface.h:16-530, C++ free functions wrapping cuthunder::*).
+ * Every entry point is extern "C", takes plain pointers and sizes, returns an
+ * int status (THX_OK == 0) and never exits the process: the reference's
+ * cudaCheckErrors -> exit(1) convention (gpu/config/Device.cuh.in:27-58)
+ * becomes THX_ERR_* + thx_last_error().
+ *
+ * Two layers:
+ *   1. Device-pointer kernels (thx_*): all array arguments are device pointers
+ *      on the current HIP device, work is enqueued on `stream` (a hipStream_t,
+ *      NULL = default stream) and nothing synchronises, allocates or frees, so
+ *      callers may capture them into a HIP graph.  Scratch comes from a
+ *      caller-provided workspace sized by the matching *_workspace() query.
+ *   2. Reference-shaped host adapters (thx_Expect*, thx_InsertFT): the same
+ *      argument lists and host-pointer ownership as Interface.h, stateless
+ *      (allocate, copy, run, copy back, free), so gpu/interface/Interface.cpp can
+ *      be replaced by one-line forwards.
+ *
+ * Data conventions (reference single-precision build, include/Precision.h):
+ *   Complex = float[2] (re, im) interleaved; RFLOAT = float; rotations are
+ *   double column-major 3x3 (Eigen, gpu/src/util/Mat33.cu:88-103);
+ *   quaternions double[4] (w, x, y, z); translations double[2] in pixels.
+ *   Half-complex volumes: [k][j][i], i in [0, vdim/2] fastest, negative j/k
+ *   wrapped by +vdim (include/Image/Volume.h:567-575); dimSize =
+ *   (vdim/2+1)*vdim*vdim.  Per-image arrays are image-major [l*nPxl + i]
+ *   (allocPreCal(pixelMajor=false), src/Optimiser.cpp:8043-8083).
+ */
+#ifndef THUNDER_AMD_H
+#define THUNDER_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define THX_ABI_VERSION 1
+
+enum {
+    THX_OK = 0,
+    THX_ERR_ARG = 1,   /* invalid shape / argument / too-small workspace */
+    THX_ERR_HIP = 2,   /* a HIP runtime call failed */
+    THX_ERR_NOMEM = 3, /* host or device allocation failed (host adapters) */
+};
+
+typedef void* thx_stream_t; /* hipStream_t */
+
+int thx_abi_version(void);
+const char* thx_last_error(void);
+
+/* ------------------------------------------------------------------ a1 ---
+ * Pixel index set of Optimiser::allocPreCalIdx (src/Optimiser.cpp:
+ * 7991-8041): half-plane pixels (i >= 0, skipping i == 0 && j < 0) with
+ * rL^2 <= i^2+j^2 < rU^2 and rL <= round(|(i,j)|) < rU, in the loop order of
+ * IMAGE_FOR_PIXEL_R_FT (include/Image/Image.h:68-70).  Host function.
+ * Outputs (any may be NULL) need `cap` entries; *nPxl receives the count. */
+int thx_pixel_set(int idim, int pf, float rU, float rL, int cap, int* iCol,
+                  int* iRow, int* iSig, int* iPxl, int* nPxl);
+
+/* ------------------------------------------------------------------ a2 ---
+ * Per-image CTF over the pixel set: CTF(RFLOAT* dst, ...) (src/CTF.cpp:
+ * 113-151), computed on device instead of on the host in allocPreCal
+ * (src/Optimiser.cpp:8088-8121).  attr: nImg x 8 floats {pixelSize, voltage,
+ * defocusU, defocusV, defocusTheta, Cs, amplitudeContrast, phaseShift}
+ * (CTFAttr, include/Database.h:302).  ctfP: nImg x nPxl. */
+int thx_ctf(const float* attr, int nImg, const int* iCol, const int* iRow,
+            int nPxl, int idim, float* ctfP, thx_stream_t stream);
+
+/* ------------------------------------------------------------------ a4 ---
+ * Translation phase table traP[t][i] = exp(-2 pi i (iCol tx + iRow ty)/idim)
+ * (translate(), src/Image/ImageFunctions.cpp:233-252; kernel_Translate,
+ * gpu/src/Kernel.cu:443-473).  trans: nT x 2; traP: nT x nPxl Complex. */
+int thx_trans_table(const double* trans, int nT, const int* iCol,
+                    const int* iRow, int nPxl, int idim, float* traP,
+                    thx_stream_t stream);
+
+/* ------------------------------------------------------------------ a5 ---
+ * Quaternion -> rotation matrix, rotate3D (src/Geometry/Euler.cpp:181-189;
+ * kernel_getRotMat, gpu/src/Kernel.cu:572-617).  quat: n x 4; mat: n x 9. */
+int thx_rotmat(const double* quat, int n, double* mat, thx_stream_t stream);
+
+/* ------------------------------------------------------------------ a6 ---
+ * Fourier-slice extraction, Projector::project(Complex*, const dmat33&, ...)
+ * (src/Projector.cpp:356-374; kernel_Project3D, gpu/src/Kernel.cu:661-697):
+ * rotP[r][i] = trilinear(vol, R_r (iCol*pf, iRow*pf, 0)).
+ * vol: dimSize Complex; mat: nR x 9; rotP: nR x nPxl Complex. */
+int thx_project3d(const float* vol, int vdim, int pf, const double* mat,
+                  int nR, const int* iCol, const int* iRow, int nPxl,
+                  float* rotP, thx_stream_t stream);
+
+/* ------------------------------------------------------------------ a7 ---
+ * Materialised log-likelihoods of the global scan, the arithmetic of
+ * kernel_logDataVS (gpu/src/Kernel.cu:947-1004) and logDataVSPrior_m_huabin
+ * (src/Optimiser.cpp:9187-9213):
+ *   dvp[l][r][t] = sum_i sigRcp_li |dat_li - ctf_li (traP_ti * rotP_ri)|^2.
+ * dat: nImg x nPxl Complex, ctf/sigRcp: nImg x nPxl, dvp: nImg x nR x nT. */
+int thx_dvp(const float* rotP, int nR, const float* traP, int nT,
+            const float* dat, const float* ctf, const float* sigRcp, int nImg,
+            int nPxl, float* dvp, thx_stream_t stream);
+
+/* ------------------------------------------------------------- a7 + a8 ---
+ * Global scan of ExpectGlobal3D (gpu/interface/Interface.h:239-256;
+ * cuthunder::expectGlobal3D, gpu/src/cuthunder.cu:1842-2198): likelihood of
+ * every image against every (rotation, translation) sample of class kIdx and
+ * the normalised marginals of the CPU online-baseline loop
+ * (src/Optimiser.cpp:834-894):
+ *   base_l   = max over visited classes, r, t of dvp
+ *   wC[l][k] = sum_rt exp(dvp - base_l) pR[r] pT[t]
+ *   wR[l][k][r] = sum_t exp(dvp - base_l) pT[t]
+ *   wT[l][k][t] = sum_r exp(dvp - base_l) pR[r]
+ * kIdx == 0 initialises wC/wR/wT/baseL; kIdx > 0 merges, rescaling earlier
+ * classes when the baseline rises (kernel_setBaseLine, Kernel.cu:1096-1128).
+ * algo: 0 = direct per-pixel formulation, materialised dvp;
+ *       1 = fused MFMA formulation (default).
+ * workspace: >= thx_global_scan_workspace(...) bytes of device memory. */
+size_t thx_global_scan_workspace(int nImg, int nR, int nT, int nPxl, int algo);
+int thx_global_scan(const float* rotP, int nR, const float* traP, int nT,
+                    const float* dat, const float* ctf, const float* sigRcp,
+                    int nImg, int nPxl, const double* pR, const double* pT,
+                    int kIdx, int nK, float* wC, float* wR, float* wT,
+                    float* baseL, int algo, void* workspace, size_t wsBytes,
+                    thx_stream_t stream);
+
+/* --------------------------------------------------------- a6 + a7 + a9 ---
+ * One particle-filter phase for a batch of images, each with its own
+ * rotation / translation samples: fused projection + likelihood + per-image
+ * normalisation (src/Optimiser.cpp:1205-1402; ExpectLocalPreI3D +
+ * ExpectLocalM, gpu/src/cuthunder.cu:2834-3140, kernel_Project3DL,
+ * kernel_logDataVSL, kernel_getMaxBaseL, kernel_UpdateWL).
+ *   quat: nImg x nR x 4, trans: nImg x nT x 2, pC: nImg, pR: nImg x nR,
+ *   pT: nImg x nT (double priors, as Particle::wC/wR/wT).
+ * Outputs wC[nImg], wR[nImg x nR], wT[nImg x nT], baseL[nImg] (float, like
+ * the reference's RFLOAT vec) and, if dvp != NULL, dvp[nImg x nR x nT]. */
+size_t thx_local_phase_workspace(int nImg, int nR, int nT);
+int thx_local_phase(const float* vol, int vdim, int pf, const double* quat,
+                    int nR, const double* trans, int nT, const double* pC,
+                    const double* pR, const double* pT, const float* dat,
+                    const float* ctf, const float* sigRcp, const int* iCol,
+                    const int* iRow, int nPxl, int idim, int nImg, float* wC,
+                    float* wR, float* wT, float* baseL, float* dvp,
+                    void* workspace, size_t wsBytes, thx_stream_t stream);
+
+/* ----------------------------------------------------------------- a10 ---
+ * Systematic resampling of Particle::resample (src/Particle.cpp:1291-1478)
+ * for nImg particles at once, on an already shuffled support: w <- w*u,
+ * normalise, CDF, u_j = u0 + j/nOut; ancestor[j]; new prior 1/u[ancestor]
+ * (PARTICLE_PRIOR_ONE, include/Config.h:63) normalised (normW,
+ * src/Particle.cpp:815-821); iMax = first argmax of u.
+ *   w: nImg x nIn double, u: nImg x nIn float, u0: nImg double,
+ *   ancestor: nImg x nOut int, wOut: nImg x nOut double, iMax: nImg int. */
+int thx_resample(int nImg, int nIn, const double* w, const float* u,
+                 int nOut, const double* u0, int* ancestor, double* wOut,
+                 int* iMax, thx_stream_t stream);
+
+/* ----------------------------------------------------------------- a12 ---
+ * Weighted trilinear Fourier-space back-projection of the CPU insert loop
+ * (src/Optimiser.cpp:7036-7241 -> Reconstructor::insertP, src/Reconstructor.
+ * cpp:782-863 -> Volume::addFT, src/Image/Volume.cpp:340-375) and of
+ * cuthunder::InsertFT (gpu/src/cuthunder.cu:5249-5826; kernel_Translate
+ * :2088, kernel_InsertT :2959, kernel_InsertF :3000, kernel_InsertO3D :3048):
+ * for image l, sample m: src = dat_l * exp(+2 pi i (i (tx-offx) + j (ty-offy))/idim),
+ * F += src ctf w_l and T += ctf^2 w_l scattered trilinearly at
+ * R_m (iCol*pf, iRow*pf, 0) (Hermitian fold conjugates the F value),
+ * O += -R_m (t - off, 0) and counter += 1 (insertDir, src/Reconstructor.cpp:
+ * 407-422).  F: dimSize Complex, T: dimSize float, O: 3 double, counter: 1
+ * int (all accumulated, not cleared).  quat: nImg x mReco x 4,
+ * trans: nImg x mReco x 2, offS: nImg x 2, w: nImg. */
+int thx_insert3d(float* F, float* T, double* O, int* counter, int vdim,
+                 int pf, const float* dat, const float* ctf,
+                 const double* quat, const double* trans, const double* offS,
+                 const float* w, int nImg, int mReco, const int* iCol,
+                 const int* iRow, int nPxl, int idim, thx_stream_t stream);
+
+/* ----------------------------------------------------------------- a14 ---
+ * Fourier shell correlation FSC(vec&, const Volume& A, const Volume& B)
+ * (src/Functions/Spectrum.cpp:302-337) of two half-complex volumes of real
+ * box vdim; shell u = rint(|(i,j,k)|), fsc[u] = sum Re(A conj B) /
+ * sqrt(sum|A|^2 sum|B|^2) for u < nShell.  fsc: nShell double (device).
+ * workspace: >= thx_fsc_workspace(nShell) bytes. */
+size_t thx_fsc_workspace(int nShell);
+int thx_fsc(const float* A, const float* B, int vdim, int nShell, double* fsc,
+            void* workspace, size_t wsBytes, thx_stream_t stream);
+
+/* ------------------------------------------------- a3..a11 expectation ---
+ * Device-resident Optimiser::expectationG (src/Optimiser.cpp:1684-3403) for
+ * one image batch, K = 1, 3D, no CTF search: global scan over the shared
+ * sample set (gQuat[nR*4], gTrans[nT*2], priors gPR[nR], gPT[nT]; a3), reseed
+ * of every particle from the scan marginals (src/Optimiser.cpp:1930-2131),
+ * then nPhase particle-filter phases (perturb -> fused projection +
+ * likelihood + marginals -> calVari -> resample; src/Optimiser.cpp:
+ * 1183-1616).  Outputs the particle sets quat[nImg*mLR*4], trans[nImg*mLT*2]
+ * with priors pR[nImg*mLR], pT[nImg*mLT] and score[nImg] (last baseline).
+ * Host code only enqueues work on `stream`; nothing synchronises. */
+typedef struct thx_expect_cfg {
+    int idim, pf, vdim;       /* image box, padding factor, vdim = pf*idim */
+    int nR, nT;               /* global sample set sizes */
+    int mLR, mLT;             /* particle-filter set sizes (125, 9) */
+    int nPhase;               /* local phases after the scan (10) */
+    int algo;                 /* global-scan algorithm (thx_global_scan) */
+    double perturbFactor;     /* perturbFactorSGlobal (0.5) */
+    double kMin, sMin;        /* scan floors: (mS^-1/3)^2, 1/chi2Qinv(.5,2)/sqrt(tsf pi) */
+    double transS, transM;    /* translation prior width, reCentre radius */
+    unsigned long long seed;  /* counter-RNG seed */
+} thx_expect_cfg;
+
+size_t thx_expectation_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl);
+int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
+                    const double* gQuat, const double* gTrans,
+                    const double* gPR, const double* gPT, const float* dat,
+                    const float* ctf, const float* sigRcp, const int* iCol,
+                    const int* iRow, int nPxl, int nImg, double* quat,
+                    double* trans, double* pR, double* pT, float* score,
+                    void* workspace, size_t wsBytes, thx_stream_t stream);
+
+/* ====================================================================== *
+ * Reference-shaped host adapters (host pointers, stateless, synchronous).  *
+ * ====================================================================== */
+
+/* gpu/interface/Interface.h:222-231 ExpectRotran: traP[nT][npxl] and
+ * rotMat[nR][9] from trans[nT*2] and rot[nR*4]. */
+int thx_ExpectRotran(float* traP, const double* trans, const double* rot,
+                     double* rotMat, const int* iCol, const int* iRow, int nR,
+                     int nT, int idim, int npxl);
+
+/* gpu/interface/Interface.h:233-242 ExpectProject: rotP[nR][npxl] from the
+ * half-complex projectee `vol` (vdim box).  interp must be LINEAR_INTERP (1),
+ * the only mode the search uses (include/Model.h:90-93). */
+int thx_ExpectProject(const float* vol, float* rotP, const double* rotMat,
+                      const int* iCol, const int* iRow, int nR, int pf,
+                      int interp, int vdim, int npxl);
+
+/* gpu/interface/Interface.h:244-260 ExpectGlobal3D.  pR[nR], pT[nT]; wC
+ * [imgNum*nK], wR[imgNum*nK*nR], wT[imgNum*nK*nT], baseL[imgNum] in/out
+ * (kIdx > 0 merges into them). */
+int thx_ExpectGlobal3D(const float* rotP, const float* traP, const float* datP,
+                       const float* ctfP, const float* sigRcpP, float* wC,
+                       float* wR, float* wT, const double* pR,
+                       const double* pT, float* baseL, int kIdx, int nK,
+                       int nR, int nT, int npxl, int imgNum);
+
+/* gpu/interface/Interface.h:291-318 InsertFT (K = 1, cSearch off): F3D
+ * [dimSize*2], T3D[dimSize] (real), O3D[3], counter[1] are read-modify-write
+ * host buffers; nR[imgNum*mReco*4], nT[imgNum*mReco*2], offS[imgNum*2],
+ * w[imgNum]; iCol/iRow the unpadded pixel set; opf the padding factor.
+ * The MPI/NCCL hemisphere reduction of the reference call is the caller's
+ * (thunder_amd.halfmap_allreduce over RCCL). */
+int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
+                 const float* datP, const float* ctfP, const double* offS,
+                 const float* w, const double* nR, const double* nT,
+                 const int* iCol, const int* iRow, int opf, int npxl,
+                 int mReco, int idim, int vdim, int imgNum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* THUNDER_AMD_H */

@@ -1,0 +1,259 @@
+"""GPU parity: every HIP kernel of the C-ABI against the CPU restatement.
+
+Tolerances (written here, per north_star "within 1e-4 relative"):
+  * integer / index work (pixel set, resample ancestors, counter): bit-exact;
+  * per-particle log-likelihoods dvp: 1e-5 relative (bar: 1e-4);
+  * projections / phase tables / CTF: FP32 rounding of the reference formula;
+  * marginal weights exp(dvp - base): 1e-3 relative on entries >= 1e-4 of the
+    image maximum (one FP32 ulp of a dvp of magnitude |dvp| moves a weight by
+    ~|dvp| * 6e-8 relative), normalisations and baselines 1e-5;
+  * half-map F / T after atomic scatter: 1e-5 of max|F| (summation order is
+    not reproducible on either side), FSC 1e-6 absolute.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from stacks import np_dvp, small_stack
+from thunder_amd import ops, synth
+from thunder_amd._lib import lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def T(a, dtype=None):
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).to(DEV)
+
+
+@pytest.fixture(scope="module")
+def stack(orc):
+    return small_stack(orc, N=32, nImg=8, nR=12, nT=11, seed=3)
+
+
+def dev_pixels(s):
+    px = ops.PixelSet(s["N"], s["pf"], s["rU"], s["rL"], device=DEV)
+    assert np.array_equal(px.iCol, s["px"].iCol) and np.array_equal(px.iRow, s["px"].iRow)
+    return px
+
+
+def test_ctf_trans_rotmat(orc, stack):
+    s = stack
+    px = dev_pixels(s)
+    attrs = synth.ctf_attrs(5, seed=8)
+    got = ops.ctf(T(attrs), px).cpu().numpy()
+    for l, a in enumerate(attrs):
+        assert np.max(np.abs(got[l] - orc.ctf(s["px"], a, s["N"]))) < 5e-5
+    tr = np.array([[0.0, 0.0], [3.3, -2.1], [-9.75, 12.5]])
+    gt = ops.trans_table(T(tr), px).cpu().numpy()
+    for t in range(3):
+        assert np.max(np.abs(gt[t] - orc.translate(s["px"], tr[t, 0], tr[t, 1], s["N"]))) < 2e-5
+    q = synth.uniform_quaternions(7, np.random.default_rng(2))
+    m = ops.rotmat(T(q)).cpu().numpy()
+    for r in range(7):
+        assert np.allclose(m[r], orc.rotate3d(q[r]), atol=1e-15, rtol=0)
+
+
+def test_project3d(orc, stack):
+    s = stack
+    px = dev_pixels(s)
+    vol = T(s["vol"])
+    mat = np.stack([orc.rotate3d(q) for q in s["quat"]])
+    got = ops.project3d(vol, T(mat), px).cpu().numpy()
+    for r in range(len(mat)):
+        ref = orc.project3d(s["vol"], s["vdim"], s["pf"], mat[r], s["px"])
+        assert np.max(np.abs(got[r] - ref)) <= 1e-5 * np.max(np.abs(ref))
+
+
+def gpu_tables(orc, s, px):
+    mat = ops.rotmat(T(s["quat"]))
+    rotP = ops.project3d(T(s["vol"]), mat, px)
+    traP = ops.trans_table(T(s["trans"]), px)
+    return rotP, traP
+
+
+def test_dvp_direct(orc, stack):
+    s = stack
+    px = dev_pixels(s)
+    rotP, traP = gpu_tables(orc, s, px)
+    d = ops.dvp(rotP, traP, T(s["dat"]), T(s["ctf"]), T(s["sig"])).cpu().numpy()
+    ref = orc.dvp_global(s["vol"], s["vdim"], s["pf"], s["quat"], s["trans"], s["dat"], s["ctf"],
+                         s["sig"], s["px"], s["N"])
+    assert np.max(np.abs(d - ref) / np.abs(ref)) < 1e-5
+
+
+def check_weights(got, ref, nR, nT):
+    wC, wR, wT, base = [x.cpu().numpy() for x in got]
+    rC, rR, rT, rb = ref
+    assert np.allclose(base, rb, rtol=1e-5, atol=0)
+    rR = rR.reshape(wR.shape)
+    rT = rT.reshape(wT.shape)
+    rC = rC.reshape(wC.shape)
+    for a, b in ((wR, rR), (wT, rT), (wC, rC)):
+        m = b >= 1e-4 * b.max(axis=-1, keepdims=True)
+        assert np.all(np.abs(a - b)[m] <= 1e-3 * b[m]), np.max(np.abs(a - b)[m] / b[m])
+        assert np.allclose(a.sum(-1), b.sum(-1), rtol=1e-4)
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_global_scan(orc, stack, algo):
+    s = stack
+    px = dev_pixels(s)
+    rotP, traP = gpu_tables(orc, s, px)
+    nR, nT = len(s["quat"]), len(s["trans"])
+    pR = np.full(nR, 1.0 / nR)
+    pT = np.random.default_rng(1).uniform(0.2, 1.0, nT)
+    pT /= pT.sum()
+    got = ops.global_scan(rotP, traP, T(s["dat"]), T(s["ctf"]), T(s["sig"]), T(pR), T(pT),
+                          algo=algo)
+    dref = orc.dvp_global(s["vol"], s["vdim"], s["pf"], s["quat"], s["trans"], s["dat"],
+                          s["ctf"], s["sig"], s["px"], s["N"])
+    check_weights(got, orc.weights_global(dref, pR, pT), nR, nT)
+
+
+@pytest.mark.parametrize("algo", [0, 1])
+def test_global_scan_two_classes(orc, stack, algo):
+    """kIdx > 0 merges into the running baseline (kernel_setBaseLine)."""
+    s = stack
+    px = dev_pixels(s)
+    nR, nT = len(s["quat"]), len(s["trans"])
+    pR = np.full(nR, 1.0 / nR)
+    pT = np.full(nT, 1.0 / nT)
+    vol2 = (s["vol"] * 1.3).astype(np.complex64)
+    state = None
+    ostate = None
+    for k, v in enumerate((s["vol"], vol2)):
+        rotP = ops.project3d(T(v), ops.rotmat(T(s["quat"])), px)
+        traP = ops.trans_table(T(s["trans"]), px)
+        state = ops.global_scan(rotP, traP, T(s["dat"]), T(s["ctf"]), T(s["sig"]), T(pR), T(pT),
+                                kIdx=k, nK=2, state=state, algo=algo)
+        d = orc.dvp_global(v, s["vdim"], s["pf"], s["quat"], s["trans"], s["dat"], s["ctf"],
+                           s["sig"], s["px"], s["N"])
+        ostate = orc.weights_global(d, pR, pT, kIdx=k, nK=2, state=ostate)
+    check_weights(state, ostate, nR, nT)
+
+
+def test_local_phase(orc, stack):
+    s = stack
+    px = dev_pixels(s)
+    nImg, nR, nT = 5, 10, 9
+    rng = np.random.default_rng(11)
+    quat = synth.uniform_quaternions(nImg * nR, rng).reshape(nImg, nR, 4)
+    trans = rng.standard_normal((nImg, nT, 2)) * 2
+    pC = rng.uniform(0.5, 1, nImg)
+    pR = rng.uniform(0.1, 1, (nImg, nR))
+    pT = rng.uniform(0.1, 1, (nImg, nT))
+    wC, wR, wT, base, d = ops.local_phase(T(s["vol"]), T(quat), T(trans), T(pC), T(pR), T(pT),
+                                          T(s["dat"][:nImg]), T(s["ctf"][:nImg]),
+                                          T(s["sig"][:nImg]), px, want_dvp=True)
+    wC, wR, wT, base, d = [x.cpu().numpy() for x in (wC, wR, wT, base, d)]
+    for l in range(nImg):
+        rc, rr, rt, rb, rd = orc.local_phase(s["vol"], s["vdim"], s["pf"], quat[l], trans[l],
+                                             pC[l], pR[l], pT[l], s["dat"][l], s["ctf"][l],
+                                             s["sig"][l], s["px"], s["N"])
+        assert np.max(np.abs(d[l] - rd) / np.abs(rd)) < 1e-5
+        assert abs(base[l] - rb) <= 1e-5 * abs(rb)
+        for a, b in ((wR[l], rr), (wT[l], rt)):
+            m = b >= 1e-4 * b.max()
+            assert np.all(np.abs(a - b)[m] <= 1e-3 * b[m])
+        assert abs(wC[l] - rc) <= 1e-3 * rc
+
+
+def test_resample_bit_exact(orc):
+    rng = np.random.default_rng(5)
+    for nIn, nOut, nImg in ((125, 125, 7), (2000, 125, 3), (151, 9, 4), (9, 9, 6)):
+        w = rng.uniform(0.1, 1, (nImg, nIn))
+        u = (rng.uniform(0, 1, (nImg, nIn)) ** 4).astype(np.float32)
+        u0 = rng.uniform(0, 1.0 / nOut, nImg)
+        anc, wo, imax = ops.resample(T(w), T(u), nOut, T(u0))
+        anc, wo, imax = anc.cpu().numpy(), wo.cpu().numpy(), imax.cpu().numpy()
+        for l in range(nImg):
+            ra, rw, ri = orc.resample(w[l], u[l].astype(np.float64), nOut, u0[l])
+            assert np.array_equal(anc[l], ra)
+            assert np.array_equal(wo[l], rw)
+            assert imax[l] == ri
+
+
+def test_insert3d(orc, stack):
+    s = stack
+    px = dev_pixels(s)
+    nImg, mReco = 4, 6
+    rng = np.random.default_rng(21)
+    quat = synth.uniform_quaternions(nImg * mReco, rng).reshape(nImg, mReco, 4)
+    trans = rng.standard_normal((nImg, mReco, 2)) * 3
+    off = rng.standard_normal((nImg, 2))
+    w = np.full(nImg, 1.0 / mReco, np.float32)
+    hm = ops.HalfMap(s["vdim"], DEV)
+    ops.insert3d(hm, T(s["dat"][:nImg]), T(s["ctf"][:nImg]), T(quat), T(trans), T(off), T(w), px)
+    F, Tm, O, cnt = orc.insert_batch(s["vdim"], s["pf"], s["dat"][:nImg], s["ctf"][:nImg], quat,
+                                     trans, off, w, s["px"], s["N"])
+    gF = hm.F.cpu().numpy().reshape(-1)
+    gT = hm.T.cpu().numpy().reshape(-1)
+    assert np.max(np.abs(gF - F)) <= 1e-5 * np.max(np.abs(F))
+    assert np.max(np.abs(gT - Tm)) <= 1e-5 * np.max(np.abs(Tm))
+    assert np.allclose(hm.O.cpu().numpy(), O, rtol=1e-12, atol=1e-12)
+    assert int(hm.counter.item()) == cnt == nImg * mReco
+
+
+def test_fsc(orc):
+    vdim = 48
+    rng = np.random.default_rng(7)
+    shape = (vdim, vdim, vdim // 2 + 1)
+    A = (rng.standard_normal(shape) + 1j * rng.standard_normal(shape)).astype(np.complex64)
+    B = (A + 0.7 * (rng.standard_normal(shape) + 1j * rng.standard_normal(shape))).astype(np.complex64)
+    got = ops.fsc(T(A), T(B), vdim // 2).cpu().numpy()
+    assert np.max(np.abs(got - orc.fsc(A, B, vdim, vdim // 2))) < 1e-6
+
+
+def test_host_adapters_match_device_ops(orc, stack):
+    """thx_Expect* / thx_InsertFT (Interface.h-shaped, host pointers)."""
+    s = stack
+    px = dev_pixels(s)
+    L = lib()
+    nR, nT, n = len(s["quat"]), len(s["trans"]), s["px"].n
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    traP = np.zeros((nT, n), np.complex64)
+    mat = np.zeros((nR, 9))
+    iCol, iRow = s["px"].iCol.copy(), s["px"].iRow.copy()
+    q = np.ascontiguousarray(s["quat"])
+    tr = np.ascontiguousarray(s["trans"])
+    assert L.thx_ExpectRotran(P(traP), P(tr), P(q), P(mat), P(iCol), P(iRow), nR, nT, s["N"], n) == 0
+    rotP = np.zeros((nR, n), np.complex64)
+    vol = np.ascontiguousarray(s["vol"])
+    assert L.thx_ExpectProject(P(vol), P(rotP), P(mat), P(iCol), P(iRow), nR, s["pf"], 1,
+                               s["vdim"], n) == 0
+    g_rot, g_tra = gpu_tables(orc, s, px)
+    assert np.array_equal(rotP, g_rot.cpu().numpy())
+    assert np.array_equal(traP, g_tra.cpu().numpy())
+    nImg = len(s["dat"])
+    pR = np.full(nR, 1.0 / nR)
+    pT = np.full(nT, 1.0 / nT)
+    wC = np.zeros(nImg, np.float32)
+    wR = np.zeros(nImg * nR, np.float32)
+    wT = np.zeros(nImg * nT, np.float32)
+    base = np.zeros(nImg, np.float32)
+    dat, ctf, sig = (np.ascontiguousarray(s[k]) for k in ("dat", "ctf", "sig"))
+    assert L.thx_ExpectGlobal3D(P(rotP), P(traP), P(dat), P(ctf), P(sig), P(wC), P(wR), P(wT),
+                                P(pR), P(pT), P(base), 0, 1, nR, nT, n, nImg) == 0
+    ref = ops.global_scan(g_rot, g_tra, T(dat), T(ctf), T(sig), T(pR), T(pT), algo=1)
+    assert np.array_equal(wR, ref[1].cpu().numpy().reshape(-1))
+    assert np.array_equal(base, ref[3].cpu().numpy())
+    # InsertFT
+    mReco = 3
+    rng = np.random.default_rng(2)
+    iq = synth.uniform_quaternions(nImg * mReco, rng).reshape(nImg, mReco, 4)
+    it = rng.standard_normal((nImg, mReco, 2))
+    off = np.zeros((nImg, 2))
+    w = np.full(nImg, 1.0 / mReco, np.float32)
+    size = (s["vdim"] // 2 + 1) * s["vdim"] ** 2
+    F = np.zeros(2 * size, np.float32)
+    Tm = np.zeros(size, np.float32)
+    O = np.zeros(3)
+    cnt = np.zeros(1, np.int32)
+    assert L.thx_InsertFT(P(F), P(Tm), P(O), P(cnt), P(dat), P(ctf), P(off), P(w), P(iq), P(it),
+                          P(iCol), P(iRow), s["pf"], n, mReco, s["N"], s["vdim"], nImg) == 0
+    rF, rT, rO, rc = orc.insert_batch(s["vdim"], s["pf"], dat, ctf, iq, it, off, w, s["px"], s["N"])
+    assert np.max(np.abs(F - rF.view(np.float32))) <= 1e-5 * np.max(np.abs(rF.view(np.float32)))
+    assert int(cnt[0]) == rc

@@ -1,0 +1,81 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol the
+header declares, the host-only entry points agree with the oracle, and
+argument validation rejects bad shapes before anything is enqueued."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from thunder_amd import _lib, build
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                      "thunder_amd.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(thx_\w+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    build.build()
+    return _lib.lib()
+
+
+def test_exports_every_declared_symbol(L):
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(L, n), n
+        assert n in _lib.SIGNATURES, f"{n} missing from the ctypes table"
+
+
+def test_abi_version(L):
+    assert L.thx_abi_version() == 1
+
+
+@pytest.mark.parametrize("N,rL,rU", [(64, 0, 30), (256, 1, 24), (256, 1, 126), (200, 1, 19)])
+def test_pixel_set_matches_oracle(L, orc, N, rL, rU):
+    cap = (N // 2 + 1) * N
+    bufs = [np.zeros(cap, np.int32) for _ in range(4)]
+    n = ctypes.c_int()
+    st = L.thx_pixel_set(N, 2, rU, rL, cap, *[b.ctypes.data_as(ctypes.c_void_p) for b in bufs],
+                         ctypes.byref(n))
+    assert st == 0
+    px = orc.pixel_set(N, 2, rU, rL)
+    assert n.value == px.n
+    for a, b in zip(bufs, (px.iCol, px.iRow, px.iSig, px.iPxl)):
+        assert np.array_equal(a[:n.value], b)
+
+
+def test_pixel_set_rejects_radius_past_nyquist(L):
+    n = ctypes.c_int()
+    st = L.thx_pixel_set(64, 2, 40.0, 0.0, 10, None, None, None, None, ctypes.byref(n))
+    assert st == 1
+    assert b"rU" in L.thx_last_error()
+
+
+def test_argument_validation_without_gpu(L):
+    # invalid shapes are rejected before any kernel is enqueued
+    assert L.thx_global_scan(None, 0, None, 5, None, None, None, 1, 10, None, None, 0, 1,
+                             None, None, None, None, 1, None, 0, None) == 1
+    assert L.thx_global_scan(None, 4, None, 5, None, None, None, 1, 10, None, None, 2, 1,
+                             None, None, None, None, 1, None, 0, None) == 1
+    assert L.thx_local_phase(None, 64, 2, None, 0, None, 9, None, None, None, None, None, None,
+                             None, None, 10, 32, 1, None, None, None, None, None, None, 0,
+                             None) == 1
+    assert L.thx_resample(1, 0, None, None, 4, None, None, None, None, None) == 1
+    assert L.thx_fsc(None, None, 31, 8, None, None, 0, None) == 1
+    assert L.thx_ExpectProject(None, None, None, None, None, 1, 2, 1, 64, 10) == 1
+
+
+def test_workspace_queries_are_host_only(L):
+    ws0 = L.thx_global_scan_workspace(100, 2000, 151, 870, 0)
+    ws1 = L.thx_global_scan_workspace(100, 2000, 151, 870, 1)
+    assert ws0 >= 100 * 2000 * 151 * 4
+    assert ws1 > 0
+    assert L.thx_fsc_workspace(64) >= 3 * 64 * 8

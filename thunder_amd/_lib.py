@@ -1,0 +1,75 @@
+"""ctypes binding of libthunder_amd.so (the C-ABI declared in include/thunder_amd.h).
+
+There is no fallback: if the HIP library is missing or fails to load, every
+entry point raises.  Build it with ``python -m thunder_amd.build`` (or
+``__graft_entry__.build()``).
+"""
+import ctypes
+import os
+
+from .build import LIB
+
+_c_int, _c_float, _c_double, _c_size = ctypes.c_int, ctypes.c_float, ctypes.c_double, ctypes.c_size_t
+_p = ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/thunder_amd.h
+SIGNATURES = {
+    "thx_abi_version": (_c_int, []),
+    "thx_last_error": (ctypes.c_char_p, []),
+    "thx_pixel_set": (_c_int, [_c_int, _c_int, _c_float, _c_float, _c_int, _p, _p, _p, _p, _p]),
+    "thx_ctf": (_c_int, [_p, _c_int, _p, _p, _c_int, _c_int, _p, _p]),
+    "thx_trans_table": (_c_int, [_p, _c_int, _p, _p, _c_int, _c_int, _p, _p]),
+    "thx_rotmat": (_c_int, [_p, _c_int, _p, _p]),
+    "thx_project3d": (_c_int, [_p, _c_int, _c_int, _p, _c_int, _p, _p, _c_int, _p, _p]),
+    "thx_dvp": (_c_int, [_p, _c_int, _p, _c_int, _p, _p, _p, _c_int, _c_int, _p, _p]),
+    "thx_global_scan_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
+    "thx_global_scan": (_c_int, [_p, _c_int, _p, _c_int, _p, _p, _p, _c_int, _c_int, _p, _p,
+                                 _c_int, _c_int, _p, _p, _p, _p, _c_int, _p, _c_size, _p]),
+    "thx_local_phase_workspace": (_c_size, [_c_int, _c_int, _c_int]),
+    "thx_local_phase": (_c_int, [_p, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _p, _p,
+                                 _p, _p, _p, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p, _p,
+                                 _c_size, _p]),
+    "thx_resample": (_c_int, [_c_int, _c_int, _p, _p, _c_int, _p, _p, _p, _p, _p]),
+    "thx_insert3d": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_int,
+                              _c_int, _p, _p, _c_int, _c_int, _p]),
+    "thx_fsc_workspace": (_c_size, [_c_int]),
+    "thx_fsc": (_c_int, [_p, _p, _c_int, _c_int, _p, _p, _c_size, _p]),
+    "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int]),
+    "thx_expectation": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _p, _p,
+                                 _p, _p, _p, _p, _c_size, _p]),
+    "thx_ExpectRotran": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
+    "thx_ExpectProject": (_c_int, [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int]),
+    "thx_ExpectGlobal3D": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
+                                    _c_int, _c_int, _c_int, _c_int]),
+    "thx_InsertFT": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
+                              _c_int, _c_int, _c_int, _c_int]),
+}
+
+_lib = None
+
+
+class ThxError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libthunder_amd.so (raises if it is absent: no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        raise ThxError(f"{LIB} is missing: run `python -m thunder_amd.build` "
+                       "(the HIP path has no fallback)")
+    L = ctypes.CDLL(LIB)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(status, what=""):
+    if status != 0:
+        msg = lib().thx_last_error().decode(errors="replace")
+        raise ThxError(f"{what} failed (status {status}): {msg}")

@@ -1,0 +1,170 @@
+// common.h -- shared helpers for the gfx950 kernels and the C-ABI glue.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/thunder_amd.h"
+
+namespace thx {
+
+// Thread-local last-error text behind thx_last_error().
+void set_error(const char* fmt, ...);
+
+// Error convention: every exported entry point returns a THX_* status; the
+// reference's exit(1) on any CUDA error (gpu/config/Device.cuh.in:27-58) is
+// replaced by a status code + message the caller can act on.
+#define THX_CHECK_ARG(cond, ...)                \
+    do {                                        \
+        if (!(cond)) {                          \
+            ::thx::set_error(__VA_ARGS__);      \
+            return THX_ERR_ARG;                 \
+        }                                       \
+    } while (0)
+
+#define THX_HIP(call)                                                          \
+    do {                                                                       \
+        hipError_t e_ = (call);                                                \
+        if (e_ != hipSuccess) {                                                \
+            ::thx::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call,        \
+                             hipGetErrorString(e_));                           \
+            return THX_ERR_HIP;                                                \
+        }                                                                      \
+    } while (0)
+
+#define THX_LAUNCH_CHECK() THX_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(thx_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+// Workspace carving: 256-B aligned sub-buffers of a caller-provided device
+// allocation (no hipMalloc inside launch functions, so callers may capture
+// them into a HIP graph).
+struct Carver {
+    char* base;
+    size_t cap;
+    size_t off = 0;
+    Carver(void* b, size_t c) : base(static_cast<char*>(b)), cap(c) {}
+    template <typename T>
+    T* take(size_t n) {
+        off = (off + 255) & ~size_t(255);
+        T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+        off += n * sizeof(T);
+        return p;
+    }
+    bool ok() const { return off <= cap; }
+};
+
+}  // namespace thx
+
+// ---------------------------------------------------------------- device ---
+#define THX_DEV __device__ __forceinline__
+
+// Negative row / slice indices wrap by +vdim: Volume::iFTHalf
+// (include/Image/Volume.h:567-575).
+THX_DEV int wrap_idx(int v, int n) { return v >= 0 ? v : v + n; }
+
+THX_DEV float2 cmul(float2 a, float2 b)
+{
+    // operator* of include/Complex.h:195-203
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+template <typename T>
+THX_DEV T wave_sum(T v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+THX_DEV float wave_max(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Trilinear Fourier-space gather of Volume::getByInterpolationFT
+// (src/Image/Volume.cpp:314-338): Hermitian fold when x < 0 (conjHalf,
+// include/Image/Volume.h:135-147), floor + 8 weights
+// (WG_TRI_INTERP_LINEAR, include/Functions/Interpolation.h:187-200), taps
+// summed in box order k, j, i (getFTHalf, src/Image/Volume.cpp:491-563).
+THX_DEV float2 interp_ft(const float2* __restrict__ vol, int vdim, float x,
+                         float y, float z)
+{
+    const bool conj = !(x >= 0.f);
+    if (conj) { x = -x; y = -y; z = -z; }
+    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+    const float dx = x - fx, dy = y - fy, dz = z - fz;
+    const float vx[2] = {1.f - dx, dx};
+    const float vy[2] = {1.f - dy, dy};
+    const float vz[2] = {1.f - dz, dz};
+    const int nColFT = vdim / 2 + 1;
+    const int ya = wrap_idx(y0, vdim), yb = wrap_idx(y0 + 1, vdim);
+    const int za = wrap_idx(z0, vdim), zb = wrap_idx(z0 + 1, vdim);
+    const size_t r00 = ((size_t)za * vdim + ya) * nColFT + x0;
+    const size_t r01 = ((size_t)za * vdim + yb) * nColFT + x0;
+    const size_t r10 = ((size_t)zb * vdim + ya) * nColFT + x0;
+    const size_t r11 = ((size_t)zb * vdim + yb) * nColFT + x0;
+    const float2 a0 = vol[r00], a1 = vol[r00 + 1];
+    const float2 b0 = vol[r01], b1 = vol[r01 + 1];
+    const float2 c0 = vol[r10], c1 = vol[r10 + 1];
+    const float2 d0 = vol[r11], d1 = vol[r11 + 1];
+    float re = 0.f, im = 0.f;
+    float w;
+    w = vx[0] * vy[0] * vz[0]; re += a0.x * w; im += a0.y * w;
+    w = vx[1] * vy[0] * vz[0]; re += a1.x * w; im += a1.y * w;
+    w = vx[0] * vy[1] * vz[0]; re += b0.x * w; im += b0.y * w;
+    w = vx[1] * vy[1] * vz[0]; re += b1.x * w; im += b1.y * w;
+    w = vx[0] * vy[0] * vz[1]; re += c0.x * w; im += c0.y * w;
+    w = vx[1] * vy[0] * vz[1]; re += c1.x * w; im += c1.y * w;
+    w = vx[0] * vy[1] * vz[1]; re += d0.x * w; im += d0.y * w;
+    w = vx[1] * vy[1] * vz[1]; re += d1.x * w; im += d1.y * w;
+    return make_float2(re, conj ? -im : im);
+}
+
+// Rotated Fourier coordinate of Projector::project (src/Projector.cpp:
+// 365-368): FP64 R * (iCol*pf, iRow*pf, 0), then cast to FP32.
+THX_DEV void rot_coord(const double* m, int ic, int ir, int pf, float& x,
+                       float& y, float& z)
+{
+    const double nx = (double)(ic * pf), ny = (double)(ir * pf);
+    x = (float)(m[0] * nx + m[3] * ny);
+    y = (float)(m[1] * nx + m[4] * ny);
+    z = (float)(m[2] * nx + m[5] * ny);
+}
+
+// Translation phase exp(-2*pi*i*(iCol*tx + iRow*ty)/N) of translate()
+// (src/Image/ImageFunctions.cpp:233-252).  The phase is formed in FP32 like
+// the reference; the hardware sin/cos take revolutions, so the 2*pi product
+// never has to be rounded.
+THX_DEV float2 phase_shift(int ic, int ir, float rCol, float rRow)
+{
+    const float rev = -(ic * rCol + ir * rRow);
+    const float f = rev - rintf(rev);
+    return make_float2(__builtin_amdgcn_cosf(f), __builtin_amdgcn_sinf(f));
+}
+
+// rotate3D, src/Geometry/Euler.cpp:181-189: R = I + 2 q0 A + 2 A A with
+// A = [[0,-q3,q2],[q3,0,-q1],[-q2,q1,0]], stored column-major.
+THX_DEV void quat_to_mat(const double* q, double* m)
+{
+    const double A[3][3] = {{0, -q[3], q[2]}, {q[3], 0, -q[1]}, {-q[2], q[1], 0}};
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            double aa = 0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) aa += (2 * A[r][k]) * A[k][c];
+            m[c * 3 + r] = (r == c ? 1.0 : 0.0) + (2 * q[0]) * A[r][c] + aa;
+        }
+}
+

@@ -1,0 +1,166 @@
+// geom.hip -- pixel set (a1), CTF (a2), translation table (a4), quaternion ->
+// rotation (a5), and the error / version plumbing of the C-ABI.
+#include <cmath>
+#include <cstdarg>
+#include <cstring>
+
+#include "common.h"
+
+namespace thx {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+}  // namespace thx
+
+extern "C" int thx_abi_version(void) { return THX_ABI_VERSION; }
+extern "C" const char* thx_last_error(void) { return thx::g_err; }
+
+// ---------------------------------------------------------------------- a1
+extern "C" int thx_pixel_set(int idim, int pf, float rU, float rL, int cap,
+                             int* iCol, int* iRow, int* iSig, int* iPxl,
+                             int* nPxl)
+{
+    THX_CHECK_ARG(idim > 0 && pf > 0 && nPxl, "thx_pixel_set: bad idim/pf/nPxl");
+    THX_CHECK_ARG(rU <= idim / 2 - 1,
+                  "thx_pixel_set: rU=%g exceeds idim/2-1 (trilinear taps would leave the volume)",
+                  (double)rU);
+    // Optimiser::allocPreCalIdx, src/Optimiser.cpp:8008-8040.
+    const float rU2 = (float)((double)rU * rU);
+    const float rL2 = (float)((double)rL * rL);
+    const float r = rU + 1;
+    const long nColFT = idim / 2 + 1;
+    int n = 0;
+    for (long j = (long)(-r); j < r; j++)
+        for (long i = 0; i <= r; i++) {
+            if (i == 0 && j < 0) continue;
+            const float u = (float)((double)i * i + (double)j * j);
+            if (u < rU2 && u >= rL2) {
+                const int v = (int)std::rint(std::hypot((double)i, (double)j));
+                if (v < rU && v >= rL) {
+                    if (n >= cap) {
+                        thx::set_error("thx_pixel_set: cap=%d too small", cap);
+                        return THX_ERR_ARG;
+                    }
+                    if (iCol) iCol[n] = (int)i;
+                    if (iRow) iRow[n] = (int)j;
+                    if (iSig) iSig[n] = v;
+                    if (iPxl) iPxl[n] = (int)((j >= 0 ? j : j + idim) * nColFT + i);
+                    n++;
+                }
+            }
+        }
+    *nPxl = n;
+    return THX_OK;
+}
+
+// ---------------------------------------------------------------------- a2
+// One workgroup column per image, pixels across threads.  CTF(RFLOAT*, ...),
+// src/CTF.cpp:113-151; per-image constants are formed exactly as there (FP64
+// wavelength, then RFLOAT).
+__global__ void __launch_bounds__(256) k_ctf(const float* __restrict__ attr,
+                                             const int* __restrict__ iCol,
+                                             const int* __restrict__ iRow,
+                                             int nPxl, int idim,
+                                             float* __restrict__ ctfP)
+{
+    const int l = blockIdx.y;
+    const float* a = attr + 8 * l;
+    const float pixelSize = a[0], voltage = a[1], dU = a[2], dV = a[3];
+    const float theta = a[4], Cs = a[5], ampC = a[6], phaseShift = a[7];
+    const float lambda =
+        (float)(12.2643247 / sqrt((double)voltage * (1 + (double)voltage * 0.978466e-6)));
+    const float w1 = sqrtf(1.f - (float)((double)ampC * ampC));
+    const float w2 = ampC;
+    const float K1 = (float)(M_PI * lambda);
+    const float K2 = (float)(M_PI_2 * Cs * (float)((double)lambda * lambda * lambda));
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nPxl;
+         i += gridDim.x * blockDim.x) {
+        const int ic = iCol[i], ir = iRow[i];
+        const float fa = ic / (pixelSize * idim);
+        const float fb = ir / (pixelSize * idim);
+        const float u = (float)hypot((double)fa, (double)fb);
+        const float angle = (float)(atan2((double)ir, (double)ic) - theta);
+        const float defocus = -(dU + dV + (dU - dV) * cosf(2.f * angle)) / 2.f;
+        const float u2 = (float)((double)u * u);
+        const float u4 = (float)((double)u * u * u * u);
+        const float ki = K1 * defocus * u2 + K2 * u4 - phaseShift;
+        ctfP[(size_t)l * nPxl + i] = -w1 * sinf(ki) + w2 * cosf(ki);
+    }
+}
+
+extern "C" int thx_ctf(const float* attr, int nImg, const int* iCol,
+                       const int* iRow, int nPxl, int idim, float* ctfP,
+                       thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && nPxl >= 0 && idim > 0, "thx_ctf: bad sizes");
+    if (nImg == 0 || nPxl == 0) return THX_OK;
+    THX_CHECK_ARG(nImg <= 65535 * 64, "thx_ctf: nImg too large");
+    dim3 grid(thx::cdiv(nPxl, 256) > 64 ? 64 : thx::cdiv(nPxl, 256), nImg);
+    hipLaunchKernelGGL(k_ctf, grid, dim3(256), 0, thx::as_stream(stream), attr,
+                       iCol, iRow, nPxl, idim, ctfP);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+// ---------------------------------------------------------------------- a4
+__global__ void __launch_bounds__(256) k_trans_table(const double* __restrict__ trans,
+                                                     const int* __restrict__ iCol,
+                                                     const int* __restrict__ iRow,
+                                                     int nPxl, int idim,
+                                                     float2* __restrict__ traP)
+{
+    const int t = blockIdx.y;
+    // translate(): rCol = nTransCol / nCol in RFLOAT (ImageFunctions.cpp:243-244)
+    const float rCol = (float)trans[2 * t] / idim;
+    const float rRow = (float)trans[2 * t + 1] / idim;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nPxl;
+         i += gridDim.x * blockDim.x)
+        traP[(size_t)t * nPxl + i] = phase_shift(iCol[i], iRow[i], rCol, rRow);
+}
+
+extern "C" int thx_trans_table(const double* trans, int nT, const int* iCol,
+                               const int* iRow, int nPxl, int idim,
+                               float* traP, thx_stream_t stream)
+{
+    THX_CHECK_ARG(nT >= 0 && nPxl >= 0 && idim > 0 && nT <= 65535,
+                  "thx_trans_table: bad sizes");
+    if (nT == 0 || nPxl == 0) return THX_OK;
+    dim3 grid(thx::cdiv(nPxl, 256) > 64 ? 64 : thx::cdiv(nPxl, 256), nT);
+    hipLaunchKernelGGL(k_trans_table, grid, dim3(256), 0,
+                       thx::as_stream(stream), trans, iCol, iRow, nPxl, idim,
+                       reinterpret_cast<float2*>(traP));
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+// ---------------------------------------------------------------------- a5
+__global__ void __launch_bounds__(256) k_rotmat(const double* __restrict__ quat,
+                                                int n, double* __restrict__ mat)
+{
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    double q[4] = {quat[4 * r], quat[4 * r + 1], quat[4 * r + 2], quat[4 * r + 3]};
+    double m[9];
+    quat_to_mat(q, m);
+#pragma unroll
+    for (int k = 0; k < 9; k++) mat[9 * (size_t)r + k] = m[k];
+}
+
+extern "C" int thx_rotmat(const double* quat, int n, double* mat,
+                          thx_stream_t stream)
+{
+    THX_CHECK_ARG(n >= 0, "thx_rotmat: bad n");
+    if (n == 0) return THX_OK;
+    hipLaunchKernelGGL(k_rotmat, dim3(thx::cdiv(n, 256)), dim3(256), 0,
+                       thx::as_stream(stream), quat, n, mat);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}

@@ -1,0 +1,122 @@
+"""Optimiser::expectation() / Reconstructor::insert() surface over the C-ABI.
+
+Mirrors the reference call surface for this path (include/Optimiser.h:747-749,
+include/Reconstructor.h:577-664): an ``Expectation`` holds the device-resident
+projectee and the shared global sample set of one round and runs the
+expectation of an image batch through ``thx_expectation`` (C++ driver in
+csrc/optimiser.hip); ``Reconstructor`` inserts posterior samples into a
+device half-map through ``thx_insert3d``.  The half-map reduction across the
+ranks of one hemisphere is an RCCL all-reduce (``halfmap_allreduce``).
+"""
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import ops, synth
+from ._lib import check, lib
+
+INCLUDE_OPTIMISER_H = {
+    "MIN_N_PHASE_PER_ITER_GLOBAL": 10,   # include/Optimiser.h:56
+    "MIN_STD_FACTOR": 1,                 # include/Optimiser.h:73
+}
+
+
+class ExpectCfg(ctypes.Structure):
+    _fields_ = [("idim", ctypes.c_int), ("pf", ctypes.c_int), ("vdim", ctypes.c_int),
+                ("nR", ctypes.c_int), ("nT", ctypes.c_int), ("mLR", ctypes.c_int),
+                ("mLT", ctypes.c_int), ("nPhase", ctypes.c_int), ("algo", ctypes.c_int),
+                ("perturbFactor", ctypes.c_double), ("kMin", ctypes.c_double),
+                ("sMin", ctypes.c_double), ("transS", ctypes.c_double),
+                ("transM", ctypes.c_double), ("seed", ctypes.c_ulonglong)]
+
+
+class Expectation:
+    """One round of the global-search expectation on the current GPU.
+
+    vol: half-complex projectee [vdim, vdim, vdim/2+1] complex64 (device).
+    gset: (quat [nR,4], trans [nT,2], pR [nR], pT [nT]) numpy float64.
+    """
+
+    def __init__(self, vol, px, gset, mLR=125, mLT=9, n_phase=10, perturb=0.5,
+                 trans_s=10.0, trans_search_factor=0.25, algo=1, seed=7):
+        dev = vol.device
+        self.vol, self.px, self.dev = vol, px, dev
+        q, t, pR, pT = gset
+        self.gQuat = torch.as_tensor(np.ascontiguousarray(q), dtype=torch.float64, device=dev)
+        self.gTrans = torch.as_tensor(np.ascontiguousarray(t), dtype=torch.float64, device=dev)
+        self.gPR = torch.as_tensor(np.ascontiguousarray(pR), dtype=torch.float64, device=dev)
+        self.gPT = torch.as_tensor(np.ascontiguousarray(pT), dtype=torch.float64, device=dev)
+        vdim = vol.shape[0]
+        nR, nT = len(q), len(t)
+        scan_min_std_r = nR ** (-1.0 / 3)                    # src/Optimiser.cpp:765-771
+        scan_min_std_t = 1.0 / synth.CHI2_QINV_HALF_2DOF / math.sqrt(trans_search_factor * math.pi)
+        trans_m = trans_s * (-2.0 * math.log(0.05))           # reCentre, TRANS_Q = 0.05
+        self.cfg = ExpectCfg(px.idim, px.pf, vdim, nR, nT, mLR, mLT, n_phase, algo, perturb,
+                             scan_min_std_r ** 2, scan_min_std_t, trans_s, trans_m, seed)
+        self.mLR, self.mLT = mLR, mLT
+
+    def workspace_bytes(self, nImg):
+        return lib().thx_expectation_workspace(ctypes.byref(self.cfg), nImg, self.px.n)
+
+    def run(self, dat, ctf, sig, out=None):
+        """Expectation of one image batch; returns (quat, trans, pR, pT, score) on device."""
+        nImg, nPxl = dat.shape
+        if nPxl != self.px.n:
+            raise ValueError("pixel set / image size mismatch")
+        for name, t, dt in (("dat", dat, torch.complex64), ("ctf", ctf, torch.float32),
+                            ("sigRcp", sig, torch.float32)):
+            ops._req(t, dt, (nImg, nPxl), name)
+        dev = self.dev
+        if out is None:
+            out = (torch.empty(nImg, self.mLR, 4, dtype=torch.float64, device=dev),
+                   torch.empty(nImg, self.mLT, 2, dtype=torch.float64, device=dev),
+                   torch.empty(nImg, self.mLR, dtype=torch.float64, device=dev),
+                   torch.empty(nImg, self.mLT, dtype=torch.float64, device=dev),
+                   torch.empty(nImg, dtype=torch.float32, device=dev))
+        quat, trans, pR, pT, score = out
+        ws = ops.workspace(self.workspace_bytes(nImg), dev)
+        P = ops._ptr
+        check(lib().thx_expectation(ctypes.byref(self.cfg), P(self.vol), P(self.gQuat),
+                                    P(self.gTrans), P(self.gPR), P(self.gPT), P(dat), P(ctf),
+                                    P(sig), P(self.px.d_iCol), P(self.px.d_iRow), nPxl, nImg,
+                                    P(quat), P(trans), P(pR), P(pT), P(score), P(ws), ws.numel(),
+                                    ops._stream(dev)), "thx_expectation")
+        return out
+
+
+class Reconstructor:
+    """Device half-map of one hemisphere: Reconstructor::insertP / insertI
+    (src/Reconstructor.cpp:782-985) over thx_insert3d."""
+
+    def __init__(self, idim, pf, device):
+        self.hm = ops.HalfMap(pf * idim, device)
+        self.pf = pf
+
+    def insert(self, dat, ctf, quat, trans, offS, w, px):
+        return ops.insert3d(self.hm, dat, ctf, quat, trans, offS, w, px)
+
+
+def draw_insert_samples(quat, trans, m_reco, seed=11):
+    """Particle::rand (src/Particle.cpp:2109-2200): mReco uniform draws from the
+    final particle sets of each image -> (quat [nImg,mReco,4], trans [nImg,mReco,2])."""
+    nImg, mR, _ = quat.shape
+    mT = trans.shape[1]
+    g = torch.Generator(device=quat.device).manual_seed(seed)
+    ir = torch.randint(0, mR, (nImg, m_reco), generator=g, device=quat.device)
+    it = torch.randint(0, mT, (nImg, m_reco), generator=g, device=quat.device)
+    q = torch.gather(quat, 1, ir.unsqueeze(-1).expand(-1, -1, 4)).contiguous()
+    t = torch.gather(trans, 1, it.unsqueeze(-1).expand(-1, -1, 2)).contiguous()
+    return q, t
+
+
+def halfmap_allreduce(hm, group=None):
+    """RCCL sum of F, T, O, counter over the ranks of one hemisphere
+    (the ncclAllReduce of gpu/src/cuthunder.cu:5903-5993, counter as int32)."""
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return hm
+    for t in (hm.F, hm.T, hm.O, hm.counter):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return hm

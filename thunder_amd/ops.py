@@ -1,0 +1,265 @@
+"""torch-tensor front end of the C-ABI (include/thunder_amd.h).
+
+PyTorch supplies device memory, the current HIP stream and torch.distributed;
+all arithmetic runs in the hand-written gfx950 kernels of libthunder_amd.so.
+Every function validates shapes / dtypes / devices on the host before a kernel
+is enqueued (a mis-shaped launch must never reach the GPU).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import check, lib
+
+_ws_cache = {}
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _req(t, dtype, shape, name):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a device (cuda/HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+    return t
+
+
+def workspace(nbytes, device):
+    key = torch.device(device)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=key)
+        _ws_cache[key] = buf
+    return buf
+
+
+# ------------------------------------------------------------------- a1
+class PixelSet:
+    """Pixel index set of Optimiser::allocPreCalIdx (src/Optimiser.cpp:7991-8041)."""
+
+    def __init__(self, idim, pf, rU, rL, device=None):
+        cap = (idim // 2 + 1) * idim
+        bufs = [np.zeros(cap, np.int32) for _ in range(4)]
+        n = ctypes.c_int(0)
+        check(lib().thx_pixel_set(idim, pf, float(rU), float(rL), cap,
+                                  *[b.ctypes.data_as(ctypes.c_void_p) for b in bufs],
+                                  ctypes.byref(n)), "thx_pixel_set")
+        n = n.value
+        self.idim, self.pf, self.rU, self.rL, self.n = idim, pf, rU, rL, n
+        self.iCol, self.iRow, self.iSig, self.iPxl = (b[:n].copy() for b in bufs)
+        self.device = device
+        if device is not None:
+            self.d_iCol = torch.from_numpy(self.iCol).to(device)
+            self.d_iRow = torch.from_numpy(self.iRow).to(device)
+
+
+# ------------------------------------------------------------------- a2
+def ctf(attr, px):
+    """attr: [nImg, 8] float32 {pixelSize, voltage, dU, dV, theta, Cs, ampC, phaseShift}."""
+    nImg = attr.shape[0]
+    _req(attr, torch.float32, (nImg, 8), "attr")
+    out = torch.empty(nImg, px.n, dtype=torch.float32, device=attr.device)
+    check(lib().thx_ctf(_ptr(attr), nImg, _ptr(px.d_iCol), _ptr(px.d_iRow), px.n, px.idim,
+                        _ptr(out), _stream(attr.device)), "thx_ctf")
+    return out
+
+
+# ------------------------------------------------------------------- a4
+def trans_table(trans, px):
+    nT = trans.shape[0]
+    _req(trans, torch.float64, (nT, 2), "trans")
+    out = torch.empty(nT, px.n, dtype=torch.complex64, device=trans.device)
+    check(lib().thx_trans_table(_ptr(trans), nT, _ptr(px.d_iCol), _ptr(px.d_iRow), px.n,
+                                px.idim, _ptr(out), _stream(trans.device)), "thx_trans_table")
+    return out
+
+
+# ------------------------------------------------------------------- a5
+def rotmat(quat):
+    n = quat.shape[0]
+    _req(quat, torch.float64, (n, 4), "quat")
+    out = torch.empty(n, 9, dtype=torch.float64, device=quat.device)
+    check(lib().thx_rotmat(_ptr(quat), n, _ptr(out), _stream(quat.device)), "thx_rotmat")
+    return out
+
+
+# ------------------------------------------------------------------- a6
+def _vol_dim(vol):
+    if vol.dim() != 3 or vol.shape[0] != vol.shape[1] or vol.shape[2] != vol.shape[0] // 2 + 1:
+        raise ValueError(f"vol: expected [vdim, vdim, vdim/2+1] half-complex, got {tuple(vol.shape)}")
+    _req(vol, torch.complex64, None, "vol")
+    return vol.shape[0]
+
+
+def project3d(vol, mat, px):
+    vdim = _vol_dim(vol)
+    if px.rU * px.pf >= vdim // 2 - 1:
+        raise ValueError("pixel radius * pf reaches the volume edge")
+    nR = mat.shape[0]
+    _req(mat, torch.float64, (nR, 9), "mat")
+    out = torch.empty(nR, px.n, dtype=torch.complex64, device=vol.device)
+    for r0 in range(0, nR, 65535):
+        nb = min(65535, nR - r0)
+        check(lib().thx_project3d(_ptr(vol), vdim, px.pf, _ptr(mat[r0:r0 + nb]), nb,
+                                  _ptr(px.d_iCol), _ptr(px.d_iRow), px.n, _ptr(out[r0:r0 + nb]),
+                                  _stream(vol.device)), "thx_project3d")
+    return out
+
+
+# ------------------------------------------------------------------- a7
+def _images(dat, ctf_, sig):
+    nImg, nPxl = dat.shape
+    _req(dat, torch.complex64, (nImg, nPxl), "dat")
+    _req(ctf_, torch.float32, (nImg, nPxl), "ctf")
+    _req(sig, torch.float32, (nImg, nPxl), "sigRcp")
+    return nImg, nPxl
+
+
+def dvp(rotP, traP, dat, ctf_, sig):
+    nImg, nPxl = _images(dat, ctf_, sig)
+    nR, nT = rotP.shape[0], traP.shape[0]
+    _req(rotP, torch.complex64, (nR, nPxl), "rotP")
+    _req(traP, torch.complex64, (nT, nPxl), "traP")
+    out = torch.empty(nImg, nR, nT, dtype=torch.float32, device=dat.device)
+    for l0 in range(0, nImg, 65535):
+        nb = min(65535, nImg - l0)
+        check(lib().thx_dvp(_ptr(rotP), nR, _ptr(traP), nT, _ptr(dat[l0:]), _ptr(ctf_[l0:]),
+                            _ptr(sig[l0:]), nb, nPxl, _ptr(out[l0:]), _stream(dat.device)), "thx_dvp")
+    return out
+
+
+# ------------------------------------------------------------- a7 + a8
+def global_scan(rotP, traP, dat, ctf_, sig, pR, pT, kIdx=0, nK=1, state=None, algo=1):
+    """ExpectGlobal3D: returns (wC [nImg,nK], wR [nImg,nK,nR], wT [nImg,nK,nT], baseL [nImg])."""
+    nImg, nPxl = _images(dat, ctf_, sig)
+    nR, nT = rotP.shape[0], traP.shape[0]
+    dev = dat.device
+    _req(rotP, torch.complex64, (nR, nPxl), "rotP")
+    _req(traP, torch.complex64, (nT, nPxl), "traP")
+    _req(pR, torch.float64, (nR,), "pR")
+    _req(pT, torch.float64, (nT,), "pT")
+    if state is None:
+        if kIdx != 0:
+            raise ValueError("kIdx > 0 needs the running state of the earlier classes")
+        state = (torch.zeros(nImg, nK, dtype=torch.float32, device=dev),
+                 torch.zeros(nImg, nK, nR, dtype=torch.float32, device=dev),
+                 torch.zeros(nImg, nK, nT, dtype=torch.float32, device=dev),
+                 torch.full((nImg,), float("nan"), dtype=torch.float32, device=dev))
+    wC, wR, wT, baseL = state
+    _req(wC, torch.float32, (nImg, nK), "wC")
+    _req(wR, torch.float32, (nImg, nK, nR), "wR")
+    _req(wT, torch.float32, (nImg, nK, nT), "wT")
+    _req(baseL, torch.float32, (nImg,), "baseL")
+    nbytes = lib().thx_global_scan_workspace(nImg, nR, nT, nPxl, algo)
+    ws = workspace(nbytes, dev)
+    check(lib().thx_global_scan(_ptr(rotP), nR, _ptr(traP), nT, _ptr(dat), _ptr(ctf_), _ptr(sig),
+                                nImg, nPxl, _ptr(pR), _ptr(pT), kIdx, nK, _ptr(wC), _ptr(wR),
+                                _ptr(wT), _ptr(baseL), algo, _ptr(ws), ws.numel(), _stream(dev)),
+          "thx_global_scan")
+    return wC, wR, wT, baseL
+
+
+# -------------------------------------------------------- a6 + a7 + a9
+def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False):
+    vdim = _vol_dim(vol)
+    nImg, nPxl = _images(dat, ctf_, sig)
+    if nPxl != px.n:
+        raise ValueError("pixel set / image size mismatch")
+    nR, nT = quat.shape[1], trans.shape[1]
+    dev = dat.device
+    _req(quat, torch.float64, (nImg, nR, 4), "quat")
+    _req(trans, torch.float64, (nImg, nT, 2), "trans")
+    _req(pC, torch.float64, (nImg,), "pC")
+    _req(pR, torch.float64, (nImg, nR), "pR")
+    _req(pT, torch.float64, (nImg, nT), "pT")
+    wC = torch.empty(nImg, dtype=torch.float32, device=dev)
+    wR = torch.empty(nImg, nR, dtype=torch.float32, device=dev)
+    wT = torch.empty(nImg, nT, dtype=torch.float32, device=dev)
+    base = torch.empty(nImg, dtype=torch.float32, device=dev)
+    d = torch.empty(nImg, nR, nT, dtype=torch.float32, device=dev) if want_dvp else None
+    ws = workspace(lib().thx_local_phase_workspace(min(nImg, 65535), nR, nT), dev)
+    for l0 in range(0, nImg, 65535):
+        nb = min(65535, nImg - l0)
+        check(lib().thx_local_phase(_ptr(vol), vdim, px.pf, _ptr(quat[l0:]), nR, _ptr(trans[l0:]),
+                                    nT, _ptr(pC[l0:]), _ptr(pR[l0:]), _ptr(pT[l0:]), _ptr(dat[l0:]),
+                                    _ptr(ctf_[l0:]), _ptr(sig[l0:]), _ptr(px.d_iCol),
+                                    _ptr(px.d_iRow), nPxl, px.idim, nb, _ptr(wC[l0:]),
+                                    _ptr(wR[l0:]), _ptr(wT[l0:]), _ptr(base[l0:]),
+                                    _ptr(d[l0:]) if d is not None else None, _ptr(ws),
+                                    ws.numel(), _stream(dev)), "thx_local_phase")
+    return wC, wR, wT, base, d
+
+
+# ------------------------------------------------------------------ a10
+def resample(w, u, n_out, u0):
+    nImg, nIn = w.shape
+    dev = w.device
+    _req(w, torch.float64, (nImg, nIn), "w")
+    _req(u, torch.float32, (nImg, nIn), "u")
+    _req(u0, torch.float64, (nImg,), "u0")
+    anc = torch.empty(nImg, n_out, dtype=torch.int32, device=dev)
+    wout = torch.empty(nImg, n_out, dtype=torch.float64, device=dev)
+    imax = torch.empty(nImg, dtype=torch.int32, device=dev)
+    check(lib().thx_resample(nImg, nIn, _ptr(w), _ptr(u), n_out, _ptr(u0), _ptr(anc), _ptr(wout),
+                             _ptr(imax), _stream(dev)), "thx_resample")
+    return anc, wout, imax
+
+
+# ------------------------------------------------------------------ a12
+class HalfMap:
+    """Device F/T/O/counter accumulators of one Reconstructor (padded box vdim)."""
+
+    def __init__(self, vdim, device):
+        self.vdim = vdim
+        self.F = torch.zeros(vdim, vdim, vdim // 2 + 1, dtype=torch.complex64, device=device)
+        self.T = torch.zeros(vdim, vdim, vdim // 2 + 1, dtype=torch.float32, device=device)
+        self.O = torch.zeros(3, dtype=torch.float64, device=device)
+        self.counter = torch.zeros(1, dtype=torch.int32, device=device)
+
+
+def insert3d(hm, dat, ctf_, quat, trans, offS, w, px):
+    nImg, nPxl = dat.shape
+    _req(dat, torch.complex64, (nImg, nPxl), "dat")
+    _req(ctf_, torch.float32, (nImg, nPxl), "ctf")
+    mReco = quat.shape[1]
+    _req(quat, torch.float64, (nImg, mReco, 4), "quat")
+    _req(trans, torch.float64, (nImg, mReco, 2), "trans")
+    _req(offS, torch.float64, (nImg, 2), "offS")
+    _req(w, torch.float32, (nImg,), "w")
+    if nPxl != px.n:
+        raise ValueError("pixel set / image size mismatch")
+    if px.rU * px.pf >= hm.vdim // 2 - 1:
+        raise ValueError("pixel radius * pf reaches the volume edge")
+    dev = dat.device
+    for l0 in range(0, nImg, 65535):
+        nb = min(65535, nImg - l0)
+        check(lib().thx_insert3d(_ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim,
+                                 px.pf, _ptr(dat[l0:]), _ptr(ctf_[l0:]), _ptr(quat[l0:]),
+                                 _ptr(trans[l0:]), _ptr(offS[l0:]), _ptr(w[l0:]), nb, mReco,
+                                 _ptr(px.d_iCol), _ptr(px.d_iRow), nPxl, px.idim, _stream(dev)),
+              "thx_insert3d")
+    return hm
+
+
+# ------------------------------------------------------------------ a14
+def fsc(A, B, n_shell):
+    vdim = _vol_dim(A)
+    _req(B, torch.complex64, tuple(A.shape), "B")
+    out = torch.empty(n_shell, dtype=torch.float64, device=A.device)
+    ws = workspace(lib().thx_fsc_workspace(n_shell), A.device)
+    check(lib().thx_fsc(_ptr(A), _ptr(B), vdim, n_shell, _ptr(out), _ptr(ws), ws.numel(),
+                        _stream(A.device)), "thx_fsc")
+    return out
