@@ -134,15 +134,27 @@ int thx_global_scan(const float* rotP, int nR, const float* traP, int nT,
  *   quat: nImg x nR x 4, trans: nImg x nT x 2, pC: nImg, pR: nImg x nR,
  *   pT: nImg x nT (double priors, as Particle::wC/wR/wT).
  * Outputs wC[nImg], wR[nImg x nR], wT[nImg x nT], baseL[nImg] (float, like
- * the reference's RFLOAT vec) and, if dvp != NULL, dvp[nImg x nR x nT]. */
+ * the reference's RFLOAT vec) and, if dvp != NULL, dvp[nImg x nR x nT].
+ * volLayout 0: `vol` is the half-complex projectee; 1: `vol` is its
+ * cell-expanded copy from thx_volume_cells (8x the bytes, one aligned 64-B
+ * segment per trilinear gather -- the layout for HBM-bound full-resolution
+ * phases). */
 size_t thx_local_phase_workspace(int nImg, int nR, int nT);
-int thx_local_phase(const float* vol, int vdim, int pf, const double* quat,
+int thx_local_phase(const float* vol, int volLayout, int vdim, int pf,
+                    const double* quat,
                     int nR, const double* trans, int nT, const double* pC,
                     const double* pR, const double* pT, const float* dat,
                     const float* ctf, const float* sigRcp, const int* iCol,
                     const int* iRow, int nPxl, int idim, int nImg, float* wC,
                     float* wR, float* wT, float* baseL, float* dvp,
                     void* workspace, size_t wsBytes, thx_stream_t stream);
+
+/* Cell-expanded copy of a half-complex volume: cells[(k*vdim + j)*(vdim/2+1)
+ * + i] holds the 8 Complex taps v(i+dx, j+dy, k+dz), (dz, dy, dx) in the box
+ * order of getFTHalf (src/Image/Volume.cpp:491-563), rows / slices wrapped,
+ * i + 1 past the half plane zero.  cells: 8 * dimSize Complex. */
+int thx_volume_cells(const float* vol, int vdim, float* cells,
+                     thx_stream_t stream);
 
 /* ----------------------------------------------------------------- a10 ---
  * Systematic resampling of Particle::resample (src/Particle.cpp:1291-1478)

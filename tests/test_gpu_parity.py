@@ -161,6 +161,32 @@ def test_local_phase(orc, stack):
         assert abs(wC[l] - rc) <= 1e-3 * rc
 
 
+def test_local_phase_cells_layout_and_many_rotations(orc, stack):
+    """The cell-expanded projectee gives the same gathers; mR > 128 and
+    mT > 16 exercise the multi-tile grid."""
+    s = stack
+    px = dev_pixels(s)
+    nImg, nR, nT = 2, 150, 20
+    rng = np.random.default_rng(12)
+    quat = synth.uniform_quaternions(nImg * nR, rng).reshape(nImg, nR, 4)
+    trans = rng.standard_normal((nImg, nT, 2)) * 2
+    pC = np.ones(nImg)
+    pR = np.full((nImg, nR), 1.0 / nR)
+    pT = np.full((nImg, nT), 1.0 / nT)
+    vol = T(s["vol"])
+    cells = ops.volume_cells(vol)
+    args = (T(quat), T(trans), T(pC), T(pR), T(pT), T(s["dat"][:nImg]), T(s["ctf"][:nImg]),
+            T(s["sig"][:nImg]), px)
+    a = ops.local_phase(vol, *args, want_dvp=True)
+    b = ops.local_phase(vol, *args, want_dvp=True, cells=cells)
+    assert torch.equal(a[4], b[4])
+    d = a[4].cpu().numpy()
+    for l in range(nImg):
+        *_, rd = orc.local_phase(s["vol"], s["vdim"], s["pf"], quat[l], trans[l], 1.0, pR[l],
+                                 pT[l], s["dat"][l], s["ctf"][l], s["sig"][l], s["px"], s["N"])
+        assert np.max(np.abs(d[l] - rd) / np.abs(rd)) < 1e-5
+
+
 def test_resample_bit_exact(orc):
     rng = np.random.default_rng(5)
     for nIn, nOut, nImg in ((125, 125, 7), (2000, 125, 3), (151, 9, 4), (9, 9, 6)):

@@ -402,7 +402,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                            trans, pR, pT, p.topQ, c.perturbFactor, kMin, sMin,
                            c.transS, c.transM, c.seed, (uint32_t)(2000 + phase));
         THX_LAUNCH_CHECK();
-        THX_RET(thx_local_phase(vol, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT, dat,
+        THX_RET(thx_local_phase(vol, 0, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT, dat,
                                 ctf, sigRcp, iCol, iRow, nPxl, c.idim, nImg, p.wC, p.wR, p.wT,
                                 p.base, nullptr, p.localWs, p.localWsBytes, stream));
         // resample R and T by the phase marginals; ancestors gathered in place

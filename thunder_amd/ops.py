@@ -173,8 +173,21 @@ def global_scan(rotP, traP, dat, ctf_, sig, pR, pT, kIdx=0, nK=1, state=None, al
 
 
 # -------------------------------------------------------- a6 + a7 + a9
-def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False):
+def volume_cells(vol):
+    """Cell-expanded copy (8 taps per voxel, 64 B) for HBM-bound gathers."""
     vdim = _vol_dim(vol)
+    out = torch.empty(vdim, vdim, vdim // 2 + 1, 8, dtype=torch.complex64, device=vol.device)
+    check(lib().thx_volume_cells(_ptr(vol), vdim, _ptr(out), _stream(vol.device)), "thx_volume_cells")
+    return out
+
+
+def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False, cells=None):
+    """cells: optional thx_volume_cells copy of vol (used for the gathers)."""
+    vdim = _vol_dim(vol)
+    layout = 0
+    if cells is not None:
+        _req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
+        layout = 1
     nImg, nPxl = _images(dat, ctf_, sig)
     if nPxl != px.n:
         raise ValueError("pixel set / image size mismatch")
@@ -193,7 +206,7 @@ def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False
     ws = workspace(lib().thx_local_phase_workspace(min(nImg, 65535), nR, nT), dev)
     for l0 in range(0, nImg, 65535):
         nb = min(65535, nImg - l0)
-        check(lib().thx_local_phase(_ptr(vol), vdim, px.pf, _ptr(quat[l0:]), nR, _ptr(trans[l0:]),
+        check(lib().thx_local_phase(_ptr(cells if layout else vol), layout, vdim, px.pf, _ptr(quat[l0:]), nR, _ptr(trans[l0:]),
                                     nT, _ptr(pC[l0:]), _ptr(pR[l0:]), _ptr(pT[l0:]), _ptr(dat[l0:]),
                                     _ptr(ctf_[l0:]), _ptr(sig[l0:]), _ptr(px.d_iCol),
                                     _ptr(px.d_iRow), nPxl, px.idim, nb, _ptr(wC[l0:]),
