@@ -65,7 +65,7 @@ def test_argument_validation_without_gpu(L):
                              None, None, None, None, 1, None, 0, None) == 1
     assert L.thx_global_scan(None, 4, None, 5, None, None, None, 1, 10, None, None, 2, 1,
                              None, None, None, None, 1, None, 0, None) == 1
-    assert L.thx_local_phase(None, 64, 2, None, 0, None, 9, None, None, None, None, None, None,
+    assert L.thx_local_phase(None, 0, 64, 2, None, 0, None, 9, None, None, None, None, None, None,
                              None, None, 10, 32, 1, None, None, None, None, None, None, 0,
                              None) == 1
     assert L.thx_resample(1, 0, None, None, 4, None, None, None, None, None) == 1
