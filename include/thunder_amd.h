@@ -103,7 +103,7 @@ int thx_dvp(const float* rotP, int nR, const float* traP, int nT,
             int nPxl, float* dvp, thx_stream_t stream);
 
 /* ------------------------------------------------------------- a7 + a8 ---
- * Global scan of ExpectGlobal3D (gpu/interface/Interface.h:239-256;
+ * Global scan of ExpectGlobal3D (gpu/interface/Interface.h:221-237;
  * cuthunder::expectGlobal3D, gpu/src/cuthunder.cu:1842-2198): likelihood of
  * every image against every (rotation, translation) sample of class kIdx and
  * the normalised marginals of the CPU online-baseline loop
@@ -232,20 +232,20 @@ int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
  * Reference-shaped host adapters (host pointers, stateless, synchronous).  *
  * ====================================================================== */
 
-/* gpu/interface/Interface.h:222-231 ExpectRotran: traP[nT][npxl] and
+/* gpu/interface/Interface.h:199-208 ExpectRotran: traP[nT][npxl] and
  * rotMat[nR][9] from trans[nT*2] and rot[nR*4]. */
 int thx_ExpectRotran(float* traP, const double* trans, const double* rot,
                      double* rotMat, const int* iCol, const int* iRow, int nR,
                      int nT, int idim, int npxl);
 
-/* gpu/interface/Interface.h:233-242 ExpectProject: rotP[nR][npxl] from the
+/* gpu/interface/Interface.h:210-219 ExpectProject: rotP[nR][npxl] from the
  * half-complex projectee `vol` (vdim box).  interp must be LINEAR_INTERP (1),
  * the only mode the search uses (include/Model.h:90-93). */
 int thx_ExpectProject(const float* vol, float* rotP, const double* rotMat,
                       const int* iCol, const int* iRow, int nR, int pf,
                       int interp, int vdim, int npxl);
 
-/* gpu/interface/Interface.h:244-260 ExpectGlobal3D.  pR[nR], pT[nT]; wC
+/* gpu/interface/Interface.h:221-237 ExpectGlobal3D.  pR[nR], pT[nT]; wC
  * [imgNum*nK], wR[imgNum*nK*nR], wT[imgNum*nK*nT], baseL[imgNum] in/out
  * (kIdx > 0 merges into them). */
 int thx_ExpectGlobal3D(const float* rotP, const float* traP, const float* datP,
@@ -254,10 +254,11 @@ int thx_ExpectGlobal3D(const float* rotP, const float* traP, const float* datP,
                        const double* pT, float* baseL, int kIdx, int nK,
                        int nR, int nT, int npxl, int imgNum);
 
-/* gpu/interface/Interface.h:291-318 InsertFT (K = 1, cSearch off): F3D
+/* gpu/interface/Interface.h:294-318 InsertFT (K = 1, cSearch off): F3D
  * [dimSize*2], T3D[dimSize] (real), O3D[3], counter[1] are read-modify-write
  * host buffers; nR[imgNum*mReco*4], nT[imgNum*mReco*2], offS[imgNum*2],
- * w[imgNum]; iCol/iRow the unpadded pixel set; opf the padding factor.
+ * w[imgNum]; iCol/iRow the Reconstructor's padded pixel set (i*opf, j*opf,
+ * as passed by Reconstructor::insertI, src/Reconstructor.cpp:928-985).
  * The MPI/NCCL hemisphere reduction of the reference call is the caller's
  * (thunder_amd.halfmap_allreduce over RCCL). */
 int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,

@@ -278,8 +278,10 @@ def test_host_adapters_match_device_ops(orc, stack):
     Tm = np.zeros(size, np.float32)
     O = np.zeros(3)
     cnt = np.zeros(1, np.int32)
+    iColPad = (iCol * s["pf"]).astype(np.int32)
+    iRowPad = (iRow * s["pf"]).astype(np.int32)
     assert L.thx_InsertFT(P(F), P(Tm), P(O), P(cnt), P(dat), P(ctf), P(off), P(w), P(iq), P(it),
-                          P(iCol), P(iRow), s["pf"], n, mReco, s["N"], s["vdim"], nImg) == 0
+                          P(iColPad), P(iRowPad), s["pf"], n, mReco, s["N"], s["vdim"], nImg) == 0
     rF, rT, rO, rc = orc.insert_batch(s["vdim"], s["pf"], dat, ctf, iq, it, off, w, s["px"], s["N"])
     assert np.max(np.abs(F - rF.view(np.float32))) <= 1e-5 * np.max(np.abs(rF.view(np.float32)))
     assert int(cnt[0]) == rc

@@ -184,8 +184,20 @@ extern "C" int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
     THX_HIP(hipMemcpy(dW.p, w, sizeof(float) * imgNum, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dQ.p, nR, sizeof(double) * 4 * nS, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dTr.p, nT, sizeof(double) * 2 * nS, hipMemcpyHostToDevice));
-    THX_HIP(hipMemcpy(dIc.p, iCol, sizeof(int) * npxl, hipMemcpyHostToDevice));
-    THX_HIP(hipMemcpy(dIr.p, iRow, sizeof(int) * npxl, hipMemcpyHostToDevice));
+    {
+        // Reconstructor::insertI passes the padded pixel set (_iCol = iCol * pf,
+        // src/Reconstructor.cpp:928-985); the kernels take the unpadded one + pf,
+        // as kernel_Translate does with iColPad / opf (gpu/src/Kernel.cu:2088).
+        std::vector<int> uc(npxl), ur(npxl);
+        for (int i = 0; i < npxl; i++) {
+            THX_CHECK_ARG(iCol[i] % opf == 0 && iRow[i] % opf == 0,
+                          "thx_InsertFT: iCol/iRow must be the padded (x opf) pixel set");
+            uc[i] = iCol[i] / opf;
+            ur[i] = iRow[i] / opf;
+        }
+        THX_HIP(hipMemcpy(dIc.p, uc.data(), sizeof(int) * npxl, hipMemcpyHostToDevice));
+        THX_HIP(hipMemcpy(dIr.p, ur.data(), sizeof(int) * npxl, hipMemcpyHostToDevice));
+    }
     for (int l0 = 0; l0 < imgNum; l0 += 65535) {
         const int nb = imgNum - l0 < 65535 ? imgNum - l0 : 65535;
         THX_RET(thx_insert3d(dF.as<float>(), dT.as<float>(), dO.as<double>(), dC.as<int>(),

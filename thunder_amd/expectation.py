@@ -111,6 +111,28 @@ def draw_insert_samples(quat, trans, m_reco, seed=11):
     return q, t
 
 
+def hemisphere_shard(n_images, world, rank):
+    """Particle indices owned by `rank`: gold-standard hemisphere = rank % 2
+    (odd / even split of src/Parallel.cpp:26-53, images alternating between
+    hemispheres), then one contiguous block per rank inside its hemisphere
+    (Database::split, src/Database.cpp:621-641).  One rank keeps everything."""
+    idx = np.arange(n_images)
+    if world == 1:
+        return idx
+    hemi = rank % 2
+    members = [r for r in range(world) if r % 2 == hemi]
+    idx = idx[hemi::2]
+    k = members.index(rank)
+    per = (len(idx) + len(members) - 1) // len(members)
+    return idx[k * per:(k + 1) * per]
+
+
+def hemisphere_groups(world):
+    """One process group per hemisphere; every rank must call this (collective)."""
+    import torch.distributed as dist
+    return [dist.new_group([r for r in range(world) if r % 2 == h]) for h in (0, 1)]
+
+
 def halfmap_allreduce(hm, group=None):
     """RCCL sum of F, T, O, counter over the ranks of one hemisphere
     (the ncclAllReduce of gpu/src/cuthunder.cu:5903-5993, counter as int32)."""
