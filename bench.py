@@ -32,6 +32,7 @@ from thunder_amd._lib import lib  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3    # MI355X_MICROARCH.md, dense f32 MFMA (= VALU)
 PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E spec
+PEAK_BF16_MFMA_TFLOPS = 2500.0   # MI355X_MICROARCH.md, dense bf16 MFMA
 
 
 def parse():
@@ -85,9 +86,11 @@ def timed_events(fn, reps, stream):
     return s.elapsed_time(e) / reps / 1e3
 
 
-def scan_roofline(vol, px, gset, dat, ctf, sig, reps=3):
+def scan_roofline(vol, px, gset, dat, ctf, sig, algo, reps=3):
     """Average duration of the global-scan launch sequence (HIP events on the
-    launch stream) priced against the FP32 MFMA roof."""
+    launch stream) priced against the matrix-core roof of its dtype:
+    algo 1 = FP32 MFMA (4 flop per image x rotation x translation x pixel),
+    algo 2 = bf16 MFMA, three products per FP32 product (12 bf16 flop)."""
     dev = dat.device
     q, t, pR, pT = gset
     nImg, nR, nT = dat.shape[0], len(q), len(t)
@@ -95,12 +98,14 @@ def scan_roofline(vol, px, gset, dat, ctf, sig, reps=3):
     traP = ops.trans_table(torch.as_tensor(t, device=dev), px)
     pRd, pTd = torch.as_tensor(pR, device=dev), torch.as_tensor(pT, device=dev)
     st = torch.cuda.current_stream(dev)
-    sec = timed_events(lambda: ops.global_scan(rotP, traP, dat, ctf, sig, pRd, pTd, algo=1),
+    sec = timed_events(lambda: ops.global_scan(rotP, traP, dat, ctf, sig, pRd, pTd, algo=algo),
                        reps, st)
     pad = lambda v, m: (v + m - 1) // m * m
-    issued = 4.0 * pad(nImg, 64) * pad(nR, 4) * pad(nT, 32) * pad(px.n, 16)
+    elems = float(pad(nImg, 64)) * pad(nR, 4) * pad(nT, 32) * pad(px.n, 16)
+    issued = (12.0 if algo == 2 else 4.0) * elems
+    peak = PEAK_BF16_MFMA_TFLOPS if algo == 2 else PEAK_FP32_MFMA_TFLOPS
     algorithmic = 15.0 * nImg * nR * nT * px.n      # SURVEY §8(d), direct formulation
-    return sec, issued, algorithmic
+    return sec, issued, algorithmic, peak
 
 
 def local_roofline(vol, N, pf, device, n_img=512, reps=3):
@@ -223,18 +228,20 @@ def main():
     extras = {}
     if not a.no_extras:
         # dominant kernel: the global scan
-        sec, issued, algorithmic = scan_roofline(vol, px, gset, dat[:a.chunk], ctf[:a.chunk],
-                                                 sig[:a.chunk])
+        sec, issued, algorithmic, peak = scan_roofline(vol, px, gset, dat[:a.chunk],
+                                                       ctf[:a.chunk], sig[:a.chunk], a.algo)
+        kname = {1: "k_scan_mfma (fp32 32x32x2)", 2: "k_scan_bf16x3 (bf16 32x32x16, 3-product split)"}
         extras["roofline"] = {"bound": "mfma", "achieved": issued / sec / 1e12,
-                              "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                              "frac": issued / sec / 1e12 / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
-                              "kernel": "global scan (k_scan_mfma + prep + combine)",
-                              "launch_ms": sec * 1e3,
+                              "peak": peak, "unit": "TFLOP/s",
+                              "frac": issued / sec / 1e12 / peak, "traffic": None,
+                              "kernel": f"global scan {kname.get(a.algo, a.algo)} + prep + combine",
+                              "launch_ms": sec * 1e3, "images_per_launch": min(a.chunk, a.images),
                               "algorithmic_equiv_tflops": algorithmic / sec / 1e12,
-                              "note": "achieved = issued FP32-MFMA flops (4 per image x rotation "
-                                      "x translation x pixel after the expansion of |d-cTP|^2); "
+                              "note": "achieved = issued matrix-core flops after the expansion of "
+                                      "|d-cTP|^2 into a GEMM (4 fp32 flop, or 3x4 bf16 flop, per "
+                                      "image x rotation x translation x pixel); "
                                       "algorithmic_equiv uses the direct 15-flop count of SURVEY "
-                                      "8(d) and can exceed the VALU peak"}
+                                      "8(d) and can exceed the FP32 VALU peak"}
         lsec, lbytes, lnpx, lsec_plain = local_roofline(vol, N, pf, dev)
         extras["roofline_local"] = {"bound": "hbm", "achieved": lbytes / lsec / 1e9,
                                     "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -97,7 +97,7 @@ def check_weights(got, ref, nR, nT):
         assert np.allclose(a.sum(-1), b.sum(-1), rtol=1e-4)
 
 
-@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("algo", [0, 1, 2])
 def test_global_scan(orc, stack, algo):
     s = stack
     px = dev_pixels(s)
@@ -113,7 +113,7 @@ def test_global_scan(orc, stack, algo):
     check_weights(got, orc.weights_global(dref, pR, pT), nR, nT)
 
 
-@pytest.mark.parametrize("algo", [0, 1])
+@pytest.mark.parametrize("algo", [0, 1, 2])
 def test_global_scan_two_classes(orc, stack, algo):
     """kIdx > 0 merges into the running baseline (kernel_setBaseLine)."""
     s = stack
