@@ -24,8 +24,8 @@ namespace {
 constexpr int THREADS = 256;
 constexpr int RT = 128;          // rotations per workgroup (8 MFMA M-tiles)
 constexpr int TT = 16;           // translations per workgroup (1 MFMA N-tile)
-constexpr int KC = 16;           // pixels per LDS stage
-constexpr int APITCH = RT + 16;  // LDS row pitch of the A tile (bank spread)
+constexpr int KC = 32;           // pixels per LDS stage
+constexpr int APITCH = KC + 1;   // LDS row pitch (float2) of the [rotation][pixel] tile
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(THREADS) k_local_fused(const float2* __restric
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     __shared__ double sMat[RT][6];
     __shared__ float sTr[TT][2];
-    __shared__ __attribute__((aligned(16))) float sA[KC * 4 * APITCH];   // [px][k][r]
+    __shared__ __attribute__((aligned(16))) float2 sA[RT * APITCH];      // [r][px]
     __shared__ __attribute__((aligned(16))) float sB[KC * 4 * TT];       // [px][k][t]
     __shared__ float sRed[THREADS / 64];
 
@@ -104,17 +104,19 @@ __global__ void __launch_bounds__(THREADS) k_local_fused(const float2* __restric
     const float* S = sig + (size_t)l * nPxl;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     float aConst = 0.f;
-    // gather mapping: lane%16 -> pixel of the chunk, 4 rotations per wave-pass
-    const int gpx = lane & 15, grq = lane >> 4;
-    // B-tile mapping: one (pixel, translation) pair per thread
-    const int bpx = tid / TT, bt = tid % TT;
+    // gather mapping: a half-wave covers 32 consecutive pixels of one rotation
+    // (neighbouring pixels hit neighbouring cells of the same slice)
+    const int gpx = lane & 31, grq = lane >> 5;
     // MFMA mapping: wave wv owns M-tiles 2wv, 2wv+1 (32 rotations)
     const int mm = lane & 15, kk = lane >> 4;
 
     __syncthreads();
     for (int i0 = 0; i0 < nPxl; i0 += KC) {
         // ---- translation / image tile: B[px][0..3][t] = (U, V, b, 0)
-        {
+#pragma unroll
+        for (int u = 0; u < KC * TT / THREADS; u++) {
+            const int q = tid + u * THREADS;
+            const int bpx = q / TT, bt = q % TT;
             const int i = i0 + bpx;
             float U = 0.f, V = 0.f, b = 0.f;
             if (i < nPxl) {
@@ -136,15 +138,15 @@ __global__ void __launch_bounds__(THREADS) k_local_fused(const float2* __restric
             B[2 * TT + bt] = b;
             B[3 * TT + bt] = 0.f;
         }
-        // ---- projection tile: A[px][0..3][r] = (P.re, P.im, |P|^2, 0)
+        // ---- projection tile: A[px][r] = P (complex)
         {
             const int i = i0 + gpx;
             const bool ok = i < nPxl;
             const int ic = ok ? iCol[i] : 0, ir = ok ? iRow[i] : 0;
             const double nx = (double)(ic * pf), ny = (double)(ir * pf);
 #pragma unroll 4
-            for (int p = 0; p < RT / 16; p++) {
-                const int r = wv * (RT / 4) + p * 4 + grq;
+            for (int p = 0; p < RT / 8; p++) {
+                const int r = wv * (RT / 4) + p * 2 + grq;
                 const double* m = sMat[r];
                 const float x = (float)(m[0] * nx + m[3] * ny);
                 const float y = (float)(m[1] * nx + m[4] * ny);
@@ -153,20 +155,18 @@ __global__ void __launch_bounds__(THREADS) k_local_fused(const float2* __restric
                 if (ok)
                     P = CELLS ? interp_cells(reinterpret_cast<const float4*>(vol), vdim, x, y, z)
                               : interp_ft(vol, vdim, x, y, z);
-                float* A = sA + gpx * 4 * APITCH;
-                A[0 * APITCH + r] = P.x;
-                A[1 * APITCH + r] = P.y;
-                A[2 * APITCH + r] = P.x * P.x + P.y * P.y;
-                A[3 * APITCH + r] = 0.f;
+                sA[r * APITCH + gpx] = P;
             }
         }
         __syncthreads();
-        // ---- reduce the chunk on the matrix cores
-#pragma unroll
+        // ---- reduce the chunk on the matrix cores: A row = (P.re, P.im, |P|^2, 0)
+#pragma unroll 8
         for (int px = 0; px < KC; px++) {
             const float bv = sB[(px * 4 + kk) * TT + mm];
-            const float a0 = sA[(px * 4 + kk) * APITCH + wv * 32 + mm];
-            const float a1 = sA[(px * 4 + kk) * APITCH + wv * 32 + 16 + mm];
+            const float2 p0 = sA[(wv * 32 + mm) * APITCH + px];
+            const float2 p1 = sA[(wv * 32 + 16 + mm) * APITCH + px];
+            const float a0 = kk == 0 ? p0.x : kk == 1 ? p0.y : kk == 2 ? p0.x * p0.x + p0.y * p0.y : 0.f;
+            const float a1 = kk == 0 ? p1.x : kk == 1 ? p1.y : kk == 2 ? p1.x * p1.x + p1.y * p1.y : 0.f;
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc1, 0, 0, 0);
         }
