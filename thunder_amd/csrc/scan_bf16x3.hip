@@ -1,22 +1,27 @@
 // scan_bf16x3.hip -- a7 + a8, algo 2: the global scan's cross term on the
 // bf16 matrix cores with a three-product split (bf16x3).
 //
-// Same expansion as algo 1 (scan_mfma.hip):
-//   dvp[l][r][t] = A_l + B[l][r] + sum_i a_li . z_rti,  a = -2 s c d,
-//   z = T_t (.) P_r,  A_l = sum s|d|^2,  B[l][r] = sum s c^2 |P|^2 (FP32).
-// Each FP32 operand is split as x = x_hi + x_lo with x_hi = bf16(x) and
-// x_lo = bf16(x - x_hi), and the dot product is accumulated in FP32 as
-//   a_hi z_hi + a_hi z_lo + a_lo z_hi
-// on v_mfma_f32_32x32x16_bf16 (K = 16 = 8 pixels per instruction).  The
-// dropped a_lo z_lo term and the 16-bit split leave a relative error of
-// ~2^-16 per product; summed over K = 2 nPxl terms of random sign this is
-// ~1e-7 of |dvp| -- the same order as the reference's own sequential FP32
-// sum (tests/test_gpu_parity.py holds it to the same 1e-5 bar as algo 1).
-// Three bf16 MFMAs cost 96 cycles per 8 pixels against 512 for eight FP32
-// 32x32x2 MFMAs, so the matrix work drops ~5x.
+// Same expansion as algo 1 (scan_mfma.hip): with |T| = 1
+//   dvp[l][r][t] = A_l + B[l][r] + X[l][r][t],  A_l = sum s|d|^2,
+//   B[l][r] = sum s c^2 |P_r|^2 (FP32),
+//   X = sum_i Re(a conj(T P)) = sum_i Re(w_lri conj(T_ti)),  w = a conj(P_r),
+//   a = -2 s c d.
+// Regrouped this way, for one rotation X is a GEMM whose B operand is the
+// translation table T -- the same for every rotation and image, split ONCE
+// into bf16 hi/lo planes in the prep -- and whose A operand w = a conj(P_r)
+// is formed per (image tile, rotation) in registers and split there.  Each
+// generated A fragment is reused across all NF translation fragments.
+// FP32 operands x = x_hi + x_lo (x_hi = bf16(x), x_lo = bf16(x - x_hi)) are
+// multiplied as w_hi T_hi + w_hi T_lo + w_lo T_hi with FP32 accumulation on
+// v_mfma_f32_32x32x16_bf16 (K = 16 = 8 pixels per instruction).  The
+// dropped lo*lo term and the 16-bit split leave ~2^-16 relative error per
+// product; summed over K = 2 nPxl terms of random sign that is ~1e-7 of
+// |dvp|, the order of the reference's own sequential FP32 sum
+// (tests/test_gpu_parity.py holds it to the same bar as algo 1).
 //
-// Workgroup = 4 waves = 4 rotations x 64 images; each wave holds 2 image
-// fragments x NF translation fragments (2 NF accumulators of 32x32).
+// Workgroup = 8 waves = 2 image halves x 4 rotations; each wave owns a
+// 32-image x NT_PAD-translation tile of ONE rotation (NF accumulators of
+// 32x32) -- the wave mapping and epilogue of algo 1.
 #include "common.h"
 #include "scan_common.h"
 
@@ -25,11 +30,11 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int KC = 16;          // pixels per LDS stage (2 MFMA k-steps)
+constexpr int KC = 16;            // pixels per LDS stage (2 MFMA k-steps)
 constexpr int IMG_TILE = 64;
 constexpr int ROT_TILE = 4;
-constexpr int THREADS = 256;
-constexpr int AROW = KC * 2 + 8;   // bf16 per image row in LDS (80 B, bank spread)
+constexpr int THREADS = 512;
+constexpr int TROW = KC * 2 + 8;  // bf16 per translation row of the T tile (80 B)
 
 inline int pad_to(int v, int m) { return (v + m - 1) / m * m; }
 
@@ -50,11 +55,11 @@ Dims dims(int nImg, int nR, int nT, int nPxl)
 }
 
 struct WS {
-    __bf16* Ahi;    // [nCk][nImgPad][KC*2]
-    __bf16* Alo;    // [nCk][nImgPad][KC*2]
-    float* Bhat;    // [nPxlPad][nImgPad]
+    float2* Ac;     // [nCk][nImgPad][KC]   a = -2 s c d
+    float* Bc;      // [nCk][nImgPad][KC]   b = s c^2
     float* Aconst;  // [nImgPad]
-    float2* Tt;     // [nPxlPad][nTPad]
+    __bf16* Thi;    // [nCk][nTPad][KC*2]   T split, (re, im) interleaved
+    __bf16* Tlo;
     float2* wRp;    // [nImg][nR]
     float* pM;      // [nRB][nImgPad]
     float* pWT;     // [nRB][nImgPad][nTPad]
@@ -66,11 +71,11 @@ WS carve(void* base, const Dims& d)
 {
     thx::Carver c(base, ~size_t(0));
     WS w;
-    w.Ahi = c.take<__bf16>((size_t)d.nPxlPad * d.nImgPad * 2);
-    w.Alo = c.take<__bf16>((size_t)d.nPxlPad * d.nImgPad * 2);
-    w.Bhat = c.take<float>((size_t)d.nPxlPad * d.nImgPad);
+    w.Ac = c.take<float2>((size_t)d.nPxlPad * d.nImgPad);
+    w.Bc = c.take<float>((size_t)d.nPxlPad * d.nImgPad);
     w.Aconst = c.take<float>(d.nImgPad);
-    w.Tt = c.take<float2>((size_t)d.nPxlPad * d.nTPad);
+    w.Thi = c.take<__bf16>((size_t)d.nPxlPad * d.nTPad * 2);
+    w.Tlo = c.take<__bf16>((size_t)d.nPxlPad * d.nTPad * 2);
     w.wRp = c.take<float2>((size_t)d.nImg * d.nR);
     w.pM = c.take<float>((size_t)d.nRB * d.nImgPad);
     w.pWT = c.take<float>((size_t)d.nRB * d.nImgPad * d.nTPad);
@@ -85,42 +90,38 @@ THX_DEV void split_bf16(float x, __bf16& hi, __bf16& lo)
     lo = (__bf16)(x - (float)hi);
 }
 
-__global__ void __launch_bounds__(256) k_prep_bf(const float2* __restrict__ dat,
-                                                 const float* __restrict__ ctf,
-                                                 const float* __restrict__ sig, int nImg,
-                                                 int nPxl, int nImgPad, int nPxlPad,
-                                                 __bf16* __restrict__ Ahi,
-                                                 __bf16* __restrict__ Alo,
-                                                 float* __restrict__ Bhat)
+// a, b in pixel-chunked image rows; pixel fastest so writes are contiguous
+__global__ void __launch_bounds__(256) k_prep_img(const float2* __restrict__ dat,
+                                                  const float* __restrict__ ctf,
+                                                  const float* __restrict__ sig, int nImg,
+                                                  int nPxl, int nImgPad, int nPxlPad,
+                                                  float2* __restrict__ Ac,
+                                                  float* __restrict__ Bc)
 {
-    // thread per (image, pixel) with pixel fastest: the bf16 writes of one
-    // image row are contiguous
     const long n = (long)nImgPad * nPxlPad;
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
          q += (long)gridDim.x * blockDim.x) {
         const int i = (int)(q % nPxlPad), l = (int)(q / nPxlPad);
-        float ar = 0.f, ai = 0.f, b = 0.f;
+        float2 a = make_float2(0.f, 0.f);
+        float b = 0.f;
         if (l < nImg && i < nPxl) {
             const size_t s = (size_t)l * nPxl + i;
             const float2 d = dat[s];
             const float c = ctf[s], sg = sig[s];
             const float k = -2.f * sg * c;
-            ar = k * d.x;
-            ai = k * d.y;
+            a = make_float2(k * d.x, k * d.y);
             b = sg * c * c;
         }
-        const size_t o = (((size_t)(i / KC) * nImgPad + l) * KC + (i % KC)) * 2;
-        __bf16 h, lo;
-        split_bf16(ar, h, lo); Ahi[o] = h; Alo[o] = lo;
-        split_bf16(ai, h, lo); Ahi[o + 1] = h; Alo[o + 1] = lo;
-        Bhat[(size_t)i * nImgPad + l] = b;
+        const size_t o = ((size_t)(i / KC) * nImgPad + l) * KC + (i % KC);
+        Ac[o] = a;
+        Bc[o] = b;
     }
 }
 
-__global__ void __launch_bounds__(256) k_prep_aconst_bf(const float2* __restrict__ dat,
-                                                        const float* __restrict__ sig,
-                                                        int nImg, int nPxl, int nImgPad,
-                                                        float* __restrict__ Aconst)
+__global__ void __launch_bounds__(256) k_prep_aconst2(const float2* __restrict__ dat,
+                                                      const float* __restrict__ sig, int nImg,
+                                                      int nPxl, int nImgPad,
+                                                      float* __restrict__ Aconst)
 {
     const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -135,17 +136,22 @@ __global__ void __launch_bounds__(256) k_prep_aconst_bf(const float2* __restrict
     if (lane == 0) Aconst[l] = a;
 }
 
-__global__ void __launch_bounds__(256) k_prep_trans_bf(const float2* __restrict__ traP,
-                                                       const double* __restrict__ pT, int nT,
-                                                       int nPxl, int nTPad, int nPxlPad,
-                                                       float2* __restrict__ Tt,
-                                                       float* __restrict__ pTf)
+__global__ void __launch_bounds__(256) k_prep_tsplit(const float2* __restrict__ traP,
+                                                     const double* __restrict__ pT, int nT,
+                                                     int nPxl, int nTPad, int nPxlPad,
+                                                     __bf16* __restrict__ Thi,
+                                                     __bf16* __restrict__ Tlo,
+                                                     float* __restrict__ pTf)
 {
-    const long n = (long)nPxlPad * nTPad;
+    const long n = (long)nTPad * nPxlPad;
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
          q += (long)gridDim.x * blockDim.x) {
-        const int t = (int)(q % nTPad), i = (int)(q / nTPad);
-        Tt[q] = (t < nT && i < nPxl) ? traP[(size_t)t * nPxl + i] : make_float2(0.f, 0.f);
+        const int i = (int)(q % nPxlPad), t = (int)(q / nPxlPad);
+        const float2 v = (t < nT && i < nPxl) ? traP[(size_t)t * nPxl + i] : make_float2(0.f, 0.f);
+        const size_t o = (((size_t)(i / KC) * nTPad + t) * KC + (i % KC)) * 2;
+        __bf16 h, lo;
+        split_bf16(v.x, h, lo); Thi[o] = h; Tlo[o] = lo;
+        split_bf16(v.y, h, lo); Thi[o + 1] = h; Tlo[o + 1] = lo;
         if (i == 0) pTf[t] = t < nT ? (float)pT[t] : 0.f;
     }
 }
@@ -153,74 +159,72 @@ __global__ void __launch_bounds__(256) k_prep_trans_bf(const float2* __restrict_
 template <int NF>
 struct Smem {
     static constexpr int NTP = NF * 32;
-    static constexpr int T_F = KC * NTP * 2;               // floats
-    static constexpr int A_H = IMG_TILE * AROW;            // bf16 per part
-    static constexpr int B_F = KC * IMG_TILE;
-    static constexpr int P_F = ROT_TILE * KC * 2;
-    static constexpr int STAGE_B = T_F * 4 + 2 * A_H * 2 + B_F * 4 + P_F * 4;
-    static constexpr int EPI_B = (4 * 64 + 2 * 4 * 32 + 32 * NTP) * 4;
+    static constexpr int T_H = NTP * TROW;                 // bf16 per hi / lo plane
+    static constexpr int A_F2 = IMG_TILE * KC;             // float2
+    static constexpr int B_F = IMG_TILE * KC;              // float
+    static constexpr int P_F2 = ROT_TILE * KC;             // float2
+    static constexpr int STAGE_B = 2 * T_H * 2 + A_F2 * 8 + B_F * 4 + P_F2 * 8;
+    static constexpr int EPI_B = (8 * 32 + 2 * 4 * 32 + 32 * NTP) * 4;
     static constexpr int TOTAL_B = STAGE_B > EPI_B ? STAGE_B : EPI_B;
+    static constexpr int T16 = NTP * KC * 2 * 2 / 16;      // 16-B pieces per plane
 };
 
 template <int NF>
-__global__ void __launch_bounds__(THREADS, NF <= 5 ? 2 : 1) k_scan_bf16x3(const __bf16* __restrict__ Ahi,
-                                                            const __bf16* __restrict__ Alo,
-                                                            const float* __restrict__ Bhat,
-                                                            const float* __restrict__ Aconst,
-                                                            const float2* __restrict__ Tt,
-                                                            const float2* __restrict__ rotP,
-                                                            const float* __restrict__ pTf,
-                                                            const double* __restrict__ pR,
-                                                            int nImg, int nR, int nT, int nPxl,
-                                                            int nImgPad, int nPxlPad,
-                                                            float2* __restrict__ wRp,
-                                                            float* __restrict__ pM,
-                                                            float* __restrict__ pWT)
+__global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restrict__ Ac,
+                                                         const float* __restrict__ Bc,
+                                                         const float* __restrict__ Aconst,
+                                                         const __bf16* __restrict__ Thi,
+                                                         const __bf16* __restrict__ Tlo,
+                                                         const float2* __restrict__ rotP,
+                                                         const float* __restrict__ pTf,
+                                                         const double* __restrict__ pR,
+                                                         int nImg, int nR, int nT, int nPxl,
+                                                         int nImgPad, int nPxlPad, int nTPad,
+                                                         float2* __restrict__ wRp,
+                                                         float* __restrict__ pM,
+                                                         float* __restrict__ pWT)
 {
     using S = Smem<NF>;
     constexpr int NTP = S::NTP;
     __shared__ __attribute__((aligned(16))) char lds[S::TOTAL_B];
-    float2* sT = reinterpret_cast<float2*>(lds);                              // [KC][NTP]
-    __bf16* sAh = reinterpret_cast<__bf16*>(lds + S::T_F * 4);                 // [64][AROW]
-    __bf16* sAl = sAh + S::A_H;
-    float* sB = reinterpret_cast<float*>(sAl + S::A_H);                        // [KC][64]
-    float2* sP = reinterpret_cast<float2*>(sB + S::B_F);                       // [4][KC]
+    __bf16* sTh = reinterpret_cast<__bf16*>(lds);                   // [NTP][TROW]
+    __bf16* sTl = sTh + S::T_H;
+    float2* sA = reinterpret_cast<float2*>(sTl + S::T_H);           // [64][KC]
+    float* sB = reinterpret_cast<float*>(sA + S::A_F2);             // [64][KC]
+    float2* sP = reinterpret_cast<float2*>(sB + S::B_F);            // [4][KC]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int q = w & 3, hh = w >> 2;        // rotation column, image half
     const int n = lane & 31, h = lane >> 5;
     const int l0 = blockIdx.x * IMG_TILE;
     const int rb = blockIdx.y;
-    const int r = rb * ROT_TILE + w;
+    const int r = rb * ROT_TILE + q;
     const bool rValid = r < nR;
+    const int img = hh * 32 + n;              // image row of this lane's A fragment
 
-    f32x16 acc[2][NF];
+    f32x16 acc[NF];
 #pragma unroll
-    for (int a = 0; a < 2; a++)
+    for (int f = 0; f < NF; f++)
 #pragma unroll
-        for (int f = 0; f < NF; f++)
-#pragma unroll
-            for (int j = 0; j < 16; j++) acc[a][f][j] = 0.f;
+        for (int j = 0; j < 16; j++) acc[f][j] = 0.f;
     float bsum = 0.f;
 
     for (int ck = 0; ck * KC < nPxlPad; ck++) {
         const int i0 = ck * KC;
-        // ---- stage T, A (hi, lo), B, P
+        // ---- stage T hi/lo, a, b, P
         {
-            const float4* gT = reinterpret_cast<const float4*>(Tt + (size_t)i0 * NTP);
-            float4* dT = reinterpret_cast<float4*>(sT);
-            for (int x = tid; x < S::T_F / 4; x += THREADS) dT[x] = gT[x];
-            const float4* gAh = reinterpret_cast<const float4*>(Ahi + ((size_t)ck * nImgPad + l0) * KC * 2);
-            const float4* gAl = reinterpret_cast<const float4*>(Alo + ((size_t)ck * nImgPad + l0) * KC * 2);
-            // 64 rows x 4 float4 (KC*2 bf16 = 64 B)
-            {
-                const int row = tid >> 2, qd = tid & 3;
-                *reinterpret_cast<float4*>(sAh + row * AROW + qd * 8) = gAh[tid];
-                *reinterpret_cast<float4*>(sAl + row * AROW + qd * 8) = gAl[tid];
+            const float4* gh = reinterpret_cast<const float4*>(Thi + (size_t)ck * nTPad * KC * 2);
+            const float4* gl = reinterpret_cast<const float4*>(Tlo + (size_t)ck * nTPad * KC * 2);
+            for (int x = tid; x < S::T16; x += THREADS) {   // 4 pieces of 16 B per row
+                const int row = x >> 2, qd = x & 3;
+                *reinterpret_cast<float4*>(sTh + row * TROW + qd * 8) = gh[x];
+                *reinterpret_cast<float4*>(sTl + row * TROW + qd * 8) = gl[x];
             }
-            {
-                const int kc = tid >> 4, c4 = tid & 15;
-                reinterpret_cast<float4*>(sB)[tid] =
-                    reinterpret_cast<const float4*>(Bhat + (size_t)(i0 + kc) * nImgPad + l0)[c4];
+            const float4* ga = reinterpret_cast<const float4*>(Ac + ((size_t)ck * nImgPad + l0) * KC);
+            reinterpret_cast<float4*>(sA)[tid] = ga[tid];              // 64*16 float2 = 512 float4
+            if (tid < S::B_F / 4) {
+                const float4* gb = reinterpret_cast<const float4*>(Bc + ((size_t)ck * nImgPad + l0) * KC);
+                reinterpret_cast<float4*>(sB)[tid] = gb[tid];
             }
             if (tid < ROT_TILE * KC) {
                 const int qq = tid / KC, kc = tid % KC;
@@ -229,51 +233,46 @@ __global__ void __launch_bounds__(THREADS, NF <= 5 ? 2 : 1) k_scan_bf16x3(const 
             }
         }
         __syncthreads();
-        // bias: lane = image of the 64-image tile
+        if (h == 0) {
 #pragma unroll
-        for (int kc = 0; kc < KC; kc++) {
-            const float2 p = sP[w * KC + kc];
-            bsum += sB[kc * IMG_TILE + lane] * (p.x * p.x + p.y * p.y);
+            for (int kc = 0; kc < KC; kc++) {
+                const float2 p = sP[q * KC + kc];
+                bsum += sB[img * KC + kc] * (p.x * p.x + p.y * p.y);
+            }
         }
 #pragma unroll
         for (int s = 0; s < KC / 8; s++) {
-            bf16x8 ah[2], al[2];
+            // A fragment: w = a conj(P) for pixels 8s + 4h + {0..3}, split
+            bf16x8 wh, wl;
 #pragma unroll
-            for (int a = 0; a < 2; a++) {
-                ah[a] = *reinterpret_cast<const bf16x8*>(sAh + (a * 32 + n) * AROW + 16 * s + 8 * h);
-                al[a] = *reinterpret_cast<const bf16x8*>(sAl + (a * 32 + n) * AROW + 16 * s + 8 * h);
+            for (int qd = 0; qd < 4; qd++) {
+                const int px = 8 * s + 4 * h + qd;
+                const float2 a = sA[img * KC + px];
+                const float2 p = sP[q * KC + px];
+                const float wr = a.x * p.x + a.y * p.y;
+                const float wi = a.y * p.x - a.x * p.y;
+                __bf16 x0, x1;
+                split_bf16(wr, x0, x1); wh[2 * qd] = x0; wl[2 * qd] = x1;
+                split_bf16(wi, x0, x1); wh[2 * qd + 1] = x0; wl[2 * qd + 1] = x1;
             }
-            float2 pv[4];
-#pragma unroll
-            for (int qd = 0; qd < 4; qd++) pv[qd] = sP[w * KC + 8 * s + 4 * h + qd];
 #pragma unroll
             for (int f = 0; f < NF; f++) {
-                bf16x8 bh, bl;
-#pragma unroll
-                for (int qd = 0; qd < 4; qd++) {
-                    const float2 tv = sT[(8 * s + 4 * h + qd) * NTP + f * 32 + n];
-                    const float zr = tv.x * pv[qd].x - tv.y * pv[qd].y;
-                    const float zi = tv.x * pv[qd].y + tv.y * pv[qd].x;
-                    __bf16 x0, x1;
-                    split_bf16(zr, x0, x1); bh[2 * qd] = x0; bl[2 * qd] = x1;
-                    split_bf16(zi, x0, x1); bh[2 * qd + 1] = x0; bl[2 * qd + 1] = x1;
-                }
-#pragma unroll
-                for (int a = 0; a < 2; a++) {
-                    acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bh, acc[a][f], 0, 0, 0);
-                    acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[a], bl, acc[a][f], 0, 0, 0);
-                    acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[a], bh, acc[a][f], 0, 0, 0);
-                }
+                const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
+                const bf16x8 th = *reinterpret_cast<const bf16x8*>(sTh + row);
+                const bf16x8 tl = *reinterpret_cast<const bf16x8*>(sTl + row);
+                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, th, acc[f], 0, 0, 0);
+                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, tl, acc[f], 0, 0, 0);
+                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, th, acc[f], 0, 0, 0);
             }
         }
         __syncthreads();
     }
 
     // ------------------------------------------------------------ epilogue
-    float* sBias = reinterpret_cast<float*>(lds);        // [4 waves][64]
-    float* sMax = sBias + 4 * 64;                        // [2 halves][4][32]
-    float* sWT = sMax + 2 * 4 * 32;                      // [32][NTP]
-    sBias[w * 64 + lane] = bsum;
+    float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][32]
+    float* sMax = sBias + 8 * 32;                      // [2][4][32]
+    float* sWT = sMax + 2 * 4 * 32;                    // [32][NTP]
+    if (h == 0) sBias[w * 32 + n] = bsum;
     __syncthreads();
 
     float pTv[NF];
@@ -282,60 +281,58 @@ __global__ void __launch_bounds__(THREADS, NF <= 5 ? 2 : 1) k_scan_bf16x3(const 
     const float pRr = rValid ? (float)pR[r] : 0.f;
 
 #pragma unroll
-    for (int a = 0; a < 2; a++)
+    for (int j = 0; j < 16; j++) {
+        const int m = (j & 3) + 8 * (j >> 2) + 4 * h;
+        const int l = l0 + hh * 32 + m;
+        const float b = Aconst[l] + sBias[w * 32 + m];
+        float mx = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int m = (j & 3) + 8 * (j >> 2) + 4 * h;
-            const int row = a * 32 + m;
-            const int l = l0 + row;
-            const float b = Aconst[l] + sBias[w * 64 + row];
-            float mx = -INFINITY;
-#pragma unroll
-            for (int f = 0; f < NF; f++) {
-                const float d = acc[a][f][j] + b;
-                acc[a][f][j] = d;
-                if (f * 32 + n < nT) mx = fmaxf(mx, d);
-            }
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-            if (!rValid) mx = -INFINITY;
-            float sR = 0.f;
-#pragma unroll
-            for (int f = 0; f < NF; f++) {
-                const float e = (f * 32 + n < nT && rValid) ? expf(acc[a][f][j] - mx) : 0.f;
-                acc[a][f][j] = e;
-                sR += e * pTv[f];
-            }
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) sR += __shfl_xor(sR, o, 64);
-            if (n == 0) {
-                sMax[(a * 4 + w) * 32 + m] = mx;
-                if (rValid && l < nImg) wRp[(size_t)l * nR + r] = make_float2(mx, sR);
-            }
+        for (int f = 0; f < NF; f++) {
+            const float d = acc[f][j] + b;
+            acc[f][j] = d;
+            if (f * 32 + n < nT) mx = fmaxf(mx, d);
         }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+        if (!rValid) mx = -INFINITY;
+        float sR = 0.f;
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            const float e = (f * 32 + n < nT && rValid) ? expf(acc[f][j] - mx) : 0.f;
+            acc[f][j] = e;
+            sR += e * pTv[f];
+        }
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) sR += __shfl_xor(sR, o, 64);
+        if (n == 0) {
+            sMax[(hh * 4 + q) * 32 + m] = mx;
+            if (rValid && l < nImg) wRp[(size_t)l * nR + r] = make_float2(mx, sR);
+        }
+    }
     __syncthreads();
 
-#pragma unroll
-    for (int a = 0; a < 2; a++) {
+    for (int half = 0; half < 2; half++) {
         for (int x = tid; x < 32 * NTP; x += THREADS) sWT[x] = 0.f;
         __syncthreads();
+        if (hh == half) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int m = (j & 3) + 8 * (j >> 2) + 4 * h;
-            const float M = fmaxf(fmaxf(sMax[(a * 4 + 0) * 32 + m], sMax[(a * 4 + 1) * 32 + m]),
-                                  fmaxf(sMax[(a * 4 + 2) * 32 + m], sMax[(a * 4 + 3) * 32 + m]));
-            const float sc = rValid ? expf(sMax[(a * 4 + w) * 32 + m] - M) * pRr : 0.f;
+            for (int j = 0; j < 16; j++) {
+                const int m = (j & 3) + 8 * (j >> 2) + 4 * h;
+                const float M = fmaxf(fmaxf(sMax[(hh * 4 + 0) * 32 + m], sMax[(hh * 4 + 1) * 32 + m]),
+                                      fmaxf(sMax[(hh * 4 + 2) * 32 + m], sMax[(hh * 4 + 3) * 32 + m]));
+                const float sc = rValid ? expf(sMax[(hh * 4 + q) * 32 + m] - M) * pRr : 0.f;
 #pragma unroll
-            for (int f = 0; f < NF; f++) atomicAdd(&sWT[m * NTP + f * 32 + n], acc[a][f][j] * sc);
+                for (int f = 0; f < NF; f++) atomicAdd(&sWT[m * NTP + f * 32 + n], acc[f][j] * sc);
+            }
         }
         __syncthreads();
         for (int x = tid; x < 32 * NTP; x += THREADS) {
             const int m = x / NTP, t = x % NTP;
-            const int l = l0 + a * 32 + m;
+            const int l = l0 + half * 32 + m;
             pWT[((size_t)rb * nImgPad + l) * NTP + t] = sWT[x];
             if (t == 0) {
-                const float M = fmaxf(fmaxf(sMax[(a * 4 + 0) * 32 + m], sMax[(a * 4 + 1) * 32 + m]),
-                                      fmaxf(sMax[(a * 4 + 2) * 32 + m], sMax[(a * 4 + 3) * 32 + m]));
+                const float M = fmaxf(fmaxf(sMax[(half * 4 + 0) * 32 + m], sMax[(half * 4 + 1) * 32 + m]),
+                                      fmaxf(sMax[(half * 4 + 2) * 32 + m], sMax[(half * 4 + 3) * 32 + m]));
                 pM[(size_t)rb * nImgPad + l] = M;
             }
         }
@@ -393,9 +390,10 @@ template <int NF>
 int launch_main(const WS& ws, const Dims& d, const float* rotP, const double* pR, hipStream_t s)
 {
     dim3 grid(d.nImgPad / IMG_TILE, d.nRB);
-    hipLaunchKernelGGL(k_scan_bf16x3<NF>, grid, dim3(THREADS), 0, s, ws.Ahi, ws.Alo, ws.Bhat,
-                       ws.Aconst, ws.Tt, reinterpret_cast<const float2*>(rotP), ws.pTf, pR,
-                       d.nImg, d.nR, d.nT, d.nPxl, d.nImgPad, d.nPxlPad, ws.wRp, ws.pM, ws.pWT);
+    hipLaunchKernelGGL(k_scan_bf16x3<NF>, grid, dim3(THREADS), 0, s, ws.Ac, ws.Bc, ws.Aconst,
+                       ws.Thi, ws.Tlo, reinterpret_cast<const float2*>(rotP), ws.pTf, pR,
+                       d.nImg, d.nR, d.nT, d.nPxl, d.nImgPad, d.nPxlPad, d.nTPad, ws.wRp, ws.pM,
+                       ws.pWT);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
@@ -420,15 +418,15 @@ int scan_bf16x3(const float* rotP, int nR, const float* traP, int nT, const floa
     const WS ws = carve(workspace, d);
     THX_CHECK_ARG(ws.bytes <= wsBytes, "thx_global_scan(algo=2): workspace too small");
     const float2* dat2 = reinterpret_cast<const float2*>(dat);
-    hipLaunchKernelGGL(k_prep_bf, dim3(2048), dim3(256), 0, s, dat2, ctf, sigRcp, nImg, nPxl,
-                       d.nImgPad, d.nPxlPad, ws.Ahi, ws.Alo, ws.Bhat);
+    hipLaunchKernelGGL(k_prep_img, dim3(2048), dim3(256), 0, s, dat2, ctf, sigRcp, nImg, nPxl,
+                       d.nImgPad, d.nPxlPad, ws.Ac, ws.Bc);
     THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_aconst_bf, dim3(thx::cdiv(d.nImgPad, 4)), dim3(256), 0, s, dat2,
+    hipLaunchKernelGGL(k_prep_aconst2, dim3(thx::cdiv(d.nImgPad, 4)), dim3(256), 0, s, dat2,
                        sigRcp, nImg, nPxl, d.nImgPad, ws.Aconst);
     THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_trans_bf, dim3(512), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_prep_tsplit, dim3(512), dim3(256), 0, s,
                        reinterpret_cast<const float2*>(traP), pT, nT, nPxl, d.nTPad, d.nPxlPad,
-                       ws.Tt, ws.pTf);
+                       ws.Thi, ws.Tlo, ws.pTf);
     THX_LAUNCH_CHECK();
     int st;
     switch (d.nTPad / 32) {

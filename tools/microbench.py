@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmarks for profiling (rocprofv3 target), not the headline bench.
+
+  python tools/microbench.py local  [--box 256 --ru 24 --images 4096 --cells 0]
+  python tools/microbench.py scan   [--algo 2 --images 4096]
+  python tools/microbench.py insert [--images 1024 --mreco 100]
+Prints one JSON line with the per-launch time measured with HIP events.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import make_stack, timed_events  # noqa: E402
+from thunder_amd import expectation as ex  # noqa: E402
+from thunder_amd import ops, synth  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("what", choices=["local", "scan", "insert"])
+    p.add_argument("--box", type=int, default=256)
+    p.add_argument("--ru", type=int, default=24)
+    p.add_argument("--images", type=int, default=4096)
+    p.add_argument("--cells", type=int, default=0)
+    p.add_argument("--algo", type=int, default=2)
+    p.add_argument("--nr", type=int, default=2000)
+    p.add_argument("--mreco", type=int, default=100)
+    p.add_argument("--reps", type=int, default=5)
+    a = p.parse_args()
+    dev = torch.device("cuda", 0)
+    N, pf = a.box, 2
+    vol = synth.projectee(synth.blob_volume(N, seed=1, device=dev), pf)
+    px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, a.ru, 1, a.images, dev, vol=vol)
+    st = torch.cuda.current_stream(dev)
+    rng = np.random.default_rng(3)
+    out = {"what": a.what, "box": N, "rU": a.ru, "nPxl": px.n, "images": a.images}
+    if a.what == "local":
+        mR, mT = 125, 9
+        quat = torch.as_tensor(synth.uniform_quaternions(a.images * mR, rng).reshape(a.images, mR, 4),
+                               device=dev)
+        trans = torch.as_tensor(rng.standard_normal((a.images, mT, 2)), device=dev)
+        pC = torch.ones(a.images, dtype=torch.float64, device=dev)
+        pR = torch.full((a.images, mR), 1.0 / mR, dtype=torch.float64, device=dev)
+        pT = torch.full((a.images, mT), 1.0 / mT, dtype=torch.float64, device=dev)
+        cells = ops.volume_cells(vol) if a.cells else None
+        sec = timed_events(lambda: ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px,
+                                                   cells=cells), a.reps, st)
+        out.update(ms=sec * 1e3, us_per_image_phase=sec / a.images * 1e6,
+                   algo_GBps=a.images * (64.0 * mR * px.n + 16.0 * px.n) / sec / 1e9)
+    elif a.what == "scan":
+        q, t, pR, pT = synth.global_sample_set(a.nr, seed=2)
+        rotP = ops.project3d(vol, ops.rotmat(torch.as_tensor(q, device=dev)), px)
+        traP = ops.trans_table(torch.as_tensor(t, device=dev), px)
+        pRd, pTd = torch.as_tensor(pR, device=dev), torch.as_tensor(pT, device=dev)
+        sec = timed_events(lambda: ops.global_scan(rotP, traP, dat, ctf, sig, pRd, pTd,
+                                                   algo=a.algo), a.reps, st)
+        out.update(ms=sec * 1e3, us_per_image=sec / a.images * 1e6, algo=a.algo)
+    else:
+        rec = ex.Reconstructor(N, pf, dev)
+        quat = torch.as_tensor(synth.uniform_quaternions(a.images * a.mreco, rng).reshape(
+            a.images, a.mreco, 4), device=dev)
+        trans = torch.as_tensor(rng.standard_normal((a.images, a.mreco, 2)), device=dev)
+        offS = torch.zeros(a.images, 2, dtype=torch.float64, device=dev)
+        w = torch.full((a.images,), 1.0 / a.mreco, dtype=torch.float32, device=dev)
+        sec = timed_events(lambda: rec.insert(dat, ctf, quat, trans, offS, w, px), a.reps, st)
+        out.update(ms=sec * 1e3, images_per_s=a.images / sec)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
