@@ -35,6 +35,8 @@ constexpr int IMG_TILE = 64;
 constexpr int ROT_TILE = 4;
 constexpr int THREADS = 512;
 constexpr int TROW = KC * 2 + 8;  // bf16 per translation row of the T tile (80 B)
+constexpr int APITCH = KC + 1;    // float2 per image row of the a tile (odd: conflict-free b64)
+constexpr int BPITCH = KC + 1;    // float per image row of the b tile
 
 inline int pad_to(int v, int m) { return (v + m - 1) / m * m; }
 
@@ -160,8 +162,8 @@ template <int NF>
 struct Smem {
     static constexpr int NTP = NF * 32;
     static constexpr int T_H = NTP * TROW;                 // bf16 per hi / lo plane
-    static constexpr int A_F2 = IMG_TILE * KC;             // float2
-    static constexpr int B_F = IMG_TILE * KC;              // float
+    static constexpr int A_F2 = IMG_TILE * APITCH;         // float2
+    static constexpr int B_F = IMG_TILE * BPITCH;          // float
     static constexpr int P_F2 = ROT_TILE * KC;             // float2
     static constexpr int STAGE_B = 2 * T_H * 2 + A_F2 * 8 + B_F * 4 + P_F2 * 8;
     static constexpr int EPI_B = (8 * 32 + 2 * 4 * 32 + 32 * NTP) * 4;
@@ -209,35 +211,63 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
         for (int j = 0; j < 16; j++) acc[f][j] = 0.f;
     float bsum = 0.f;
 
-    for (int ck = 0; ck * KC < nPxlPad; ck++) {
-        const int i0 = ck * KC;
-        // ---- stage T hi/lo, a, b, P
-        {
-            const float4* gh = reinterpret_cast<const float4*>(Thi + (size_t)ck * nTPad * KC * 2);
-            const float4* gl = reinterpret_cast<const float4*>(Tlo + (size_t)ck * nTPad * KC * 2);
-            for (int x = tid; x < S::T16; x += THREADS) {   // 4 pieces of 16 B per row
-                const int row = x >> 2, qd = x & 3;
-                *reinterpret_cast<float4*>(sTh + row * TROW + qd * 8) = gh[x];
-                *reinterpret_cast<float4*>(sTl + row * TROW + qd * 8) = gl[x];
-            }
-            const float4* ga = reinterpret_cast<const float4*>(Ac + ((size_t)ck * nImgPad + l0) * KC);
-            reinterpret_cast<float4*>(sA)[tid] = ga[tid];              // 64*16 float2 = 512 float4
-            if (tid < S::B_F / 4) {
-                const float4* gb = reinterpret_cast<const float4*>(Bc + ((size_t)ck * nImgPad + l0) * KC);
-                reinterpret_cast<float4*>(sB)[tid] = gb[tid];
-            }
-            if (tid < ROT_TILE * KC) {
-                const int qq = tid / KC, kc = tid % KC;
-                const int rr = rb * ROT_TILE + qq, i = i0 + kc;
-                sP[tid] = (rr < nR && i < nPxl) ? rotP[(size_t)rr * nPxl + i] : make_float2(0.f, 0.f);
+    // register-staged prefetch of one pixel chunk (global -> regs during the
+    // previous chunk's MFMAs, regs -> LDS after the barrier)
+    constexpr int TPER = (S::T16 + THREADS - 1) / THREADS;
+    float4 gTh[TPER], gTl[TPER], gA;
+    float4 gB = make_float4(0.f, 0.f, 0.f, 0.f);
+    float2 gP = make_float2(0.f, 0.f);
+    auto load_chunk = [&](int ck) {
+        const float4* gh = reinterpret_cast<const float4*>(Thi + (size_t)ck * nTPad * KC * 2);
+        const float4* gl = reinterpret_cast<const float4*>(Tlo + (size_t)ck * nTPad * KC * 2);
+#pragma unroll
+        for (int u = 0; u < TPER; u++) {
+            const int x = tid + u * THREADS;
+            if (x < S::T16) { gTh[u] = gh[x]; gTl[u] = gl[x]; }
+        }
+        gA = reinterpret_cast<const float4*>(Ac + ((size_t)ck * nImgPad + l0) * KC)[tid];
+        if (tid < IMG_TILE * KC / 4)
+            gB = reinterpret_cast<const float4*>(Bc + ((size_t)ck * nImgPad + l0) * KC)[tid];
+        if (tid < ROT_TILE * KC) {
+            const int qq = tid / KC, kc = tid % KC;
+            const int rr = rb * ROT_TILE + qq, i = ck * KC + kc;
+            gP = (rr < nR && i < nPxl) ? rotP[(size_t)rr * nPxl + i] : make_float2(0.f, 0.f);
+        }
+    };
+    auto store_chunk = [&]() {
+#pragma unroll
+        for (int u = 0; u < TPER; u++) {
+            const int x = tid + u * THREADS;
+            if (x < S::T16) {                      // KC/4 pieces of 16 B per row
+                const int row = x / (KC / 4), qd = x % (KC / 4);
+                *reinterpret_cast<float4*>(sTh + row * TROW + qd * 8) = gTh[u];
+                *reinterpret_cast<float4*>(sTl + row * TROW + qd * 8) = gTl[u];
             }
         }
+        {                                          // 2 float2 of image row tid / (KC/2)
+            const int row = tid / (KC / 2), c2 = (tid % (KC / 2)) * 2;
+            sA[row * APITCH + c2] = make_float2(gA.x, gA.y);
+            sA[row * APITCH + c2 + 1] = make_float2(gA.z, gA.w);
+        }
+        if (tid < IMG_TILE * KC / 4) {
+            const int row = tid / (KC / 4), c4 = (tid % (KC / 4)) * 4;
+            sB[row * BPITCH + c4] = gB.x; sB[row * BPITCH + c4 + 1] = gB.y;
+            sB[row * BPITCH + c4 + 2] = gB.z; sB[row * BPITCH + c4 + 3] = gB.w;
+        }
+        if (tid < ROT_TILE * KC) sP[tid] = gP;
+    };
+
+    load_chunk(0);
+    for (int ck = 0; ck * KC < nPxlPad; ck++) {
+        __syncthreads();                   // previous chunk consumed
+        store_chunk();
         __syncthreads();
+        if ((ck + 1) * KC < nPxlPad) load_chunk(ck + 1);
         if (h == 0) {
 #pragma unroll
             for (int kc = 0; kc < KC; kc++) {
                 const float2 p = sP[q * KC + kc];
-                bsum += sB[img * KC + kc] * (p.x * p.x + p.y * p.y);
+                bsum += sB[img * BPITCH + kc] * (p.x * p.x + p.y * p.y);
             }
         }
 #pragma unroll
@@ -247,7 +277,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
 #pragma unroll
             for (int qd = 0; qd < 4; qd++) {
                 const int px = 8 * s + 4 * h + qd;
-                const float2 a = sA[img * KC + px];
+                const float2 a = sA[img * APITCH + px];
                 const float2 p = sP[q * KC + px];
                 const float wr = a.x * p.x + a.y * p.y;
                 const float wi = a.y * p.x - a.x * p.y;
@@ -265,8 +295,8 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
                 acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, th, acc[f], 0, 0, 0);
             }
         }
-        __syncthreads();
     }
+    __syncthreads();
 
     // ------------------------------------------------------------ epilogue
     float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][32]
