@@ -10,7 +10,8 @@
 // translation table T -- the same for every rotation and image, split ONCE
 // into bf16 hi/lo planes in the prep -- and whose A operand w = a conj(P_r)
 // is formed per (image tile, rotation) in registers and split there.  Each
-// generated A fragment is reused across all NF translation fragments.
+// generated A fragment is reused across all NF translation fragments, and
+// each T fragment read from LDS feeds both image fragments of the wave.
 // FP32 operands x = x_hi + x_lo (x_hi = bf16(x), x_lo = bf16(x - x_hi)) are
 // multiplied as w_hi T_hi + w_hi T_lo + w_lo T_hi with FP32 accumulation on
 // v_mfma_f32_32x32x16_bf16 (K = 16 = 8 pixels per instruction).  The
@@ -19,9 +20,11 @@
 // |dvp|, the order of the reference's own sequential FP32 sum
 // (tests/test_gpu_parity.py holds it to the same bar as algo 1).
 //
-// Workgroup = 8 waves = 2 image halves x 4 rotations; each wave owns a
-// 32-image x NT_PAD-translation tile of ONE rotation (NF accumulators of
-// 32x32) -- the wave mapping and epilogue of algo 1.
+// Workgroup = 8 waves = 8 rotations x 64 images; each wave owns a
+// 64-image x NT_PAD-translation tile of ONE rotation (2 x NF accumulators
+// of 32x32).  Epilogue: per-(image, rotation) max + wR marginal, then a
+// block-local merge of the 8 rotations into a (max, wT[NT_PAD]) partial per
+// image; k_scan_combine_bf folds the partials of all rotation blocks.
 #include "common.h"
 #include "scan_common.h"
 
@@ -32,7 +35,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int KC = 16;            // pixels per LDS stage (2 MFMA k-steps)
 constexpr int IMG_TILE = 64;
-constexpr int ROT_TILE = 4;
+constexpr int ROT_TILE = 8;
 constexpr int THREADS = 512;
 constexpr int TROW = KC * 2 + 8;  // bf16 per translation row of the T tile (80 B)
 constexpr int APITCH = KC + 1;    // float2 per image row of the a tile (odd: conflict-free b64)
@@ -166,7 +169,7 @@ struct Smem {
     static constexpr int B_F = IMG_TILE * BPITCH;          // float
     static constexpr int P_F2 = ROT_TILE * KC;             // float2
     static constexpr int STAGE_B = 2 * T_H * 2 + A_F2 * 8 + B_F * 4 + P_F2 * 8;
-    static constexpr int EPI_B = (8 * 32 + 2 * 4 * 32 + 32 * NTP) * 4;
+    static constexpr int EPI_B = (ROT_TILE * 64 + ROT_TILE * 64 + 32 * NTP) * 4;
     static constexpr int TOTAL_B = STAGE_B > EPI_B ? STAGE_B : EPI_B;
     static constexpr int T16 = NTP * KC * 2 * 2 / 16;      // 16-B pieces per plane
 };
@@ -191,25 +194,25 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
     __shared__ __attribute__((aligned(16))) char lds[S::TOTAL_B];
     __bf16* sTh = reinterpret_cast<__bf16*>(lds);                   // [NTP][TROW]
     __bf16* sTl = sTh + S::T_H;
-    float2* sA = reinterpret_cast<float2*>(sTl + S::T_H);           // [64][KC]
-    float* sB = reinterpret_cast<float*>(sA + S::A_F2);             // [64][KC]
-    float2* sP = reinterpret_cast<float2*>(sB + S::B_F);            // [4][KC]
+    float2* sA = reinterpret_cast<float2*>(sTl + S::T_H);           // [64][APITCH]
+    float* sB = reinterpret_cast<float*>(sA + S::A_F2);             // [64][BPITCH]
+    float2* sP = reinterpret_cast<float2*>(sB + S::B_F);            // [8][KC]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int q = w & 3, hh = w >> 2;        // rotation column, image half
     const int n = lane & 31, h = lane >> 5;
     const int l0 = blockIdx.x * IMG_TILE;
     const int rb = blockIdx.y;
-    const int r = rb * ROT_TILE + q;
+    const int r = rb * ROT_TILE + w;        // this wave's rotation
     const bool rValid = r < nR;
-    const int img = hh * 32 + n;              // image row of this lane's A fragment
 
-    f32x16 acc[NF];
+    f32x16 acc[2][NF];
 #pragma unroll
-    for (int f = 0; f < NF; f++)
+    for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int j = 0; j < 16; j++) acc[f][j] = 0.f;
-    float bsum = 0.f;
+        for (int f = 0; f < NF; f++)
+#pragma unroll
+            for (int j = 0; j < 16; j++) acc[a][f][j] = 0.f;
+    float bsum = 0.f;                         // bias of image `lane`, rotation r
 
     // register-staged prefetch of one pixel chunk (global -> regs during the
     // previous chunk's MFMAs, regs -> LDS after the barrier)
@@ -263,46 +266,50 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
         store_chunk();
         __syncthreads();
         if ((ck + 1) * KC < nPxlPad) load_chunk(ck + 1);
-        if (h == 0) {
 #pragma unroll
-            for (int kc = 0; kc < KC; kc++) {
-                const float2 p = sP[q * KC + kc];
-                bsum += sB[img * BPITCH + kc] * (p.x * p.x + p.y * p.y);
-            }
+        for (int kc = 0; kc < KC; kc++) {
+            const float2 p = sP[w * KC + kc];
+            bsum += sB[lane * BPITCH + kc] * (p.x * p.x + p.y * p.y);
         }
 #pragma unroll
         for (int s = 0; s < KC / 8; s++) {
-            // A fragment: w = a conj(P) for pixels 8s + 4h + {0..3}, split
-            bf16x8 wh, wl;
+            // A fragments: w = a conj(P_r) for images a*32 + n, pixels 8s+4h+{0..3}
+            bf16x8 wh[2], wl[2];
 #pragma unroll
             for (int qd = 0; qd < 4; qd++) {
                 const int px = 8 * s + 4 * h + qd;
-                const float2 a = sA[img * APITCH + px];
-                const float2 p = sP[q * KC + px];
-                const float wr = a.x * p.x + a.y * p.y;
-                const float wi = a.y * p.x - a.x * p.y;
-                __bf16 x0, x1;
-                split_bf16(wr, x0, x1); wh[2 * qd] = x0; wl[2 * qd] = x1;
-                split_bf16(wi, x0, x1); wh[2 * qd + 1] = x0; wl[2 * qd + 1] = x1;
+                const float2 p = sP[w * KC + px];
+#pragma unroll
+                for (int a = 0; a < 2; a++) {
+                    const float2 av = sA[(a * 32 + n) * APITCH + px];
+                    const float wr = av.x * p.x + av.y * p.y;
+                    const float wi = av.y * p.x - av.x * p.y;
+                    __bf16 x0, x1;
+                    split_bf16(wr, x0, x1); wh[a][2 * qd] = x0; wl[a][2 * qd] = x1;
+                    split_bf16(wi, x0, x1); wh[a][2 * qd + 1] = x0; wl[a][2 * qd + 1] = x1;
+                }
             }
 #pragma unroll
             for (int f = 0; f < NF; f++) {
                 const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
                 const bf16x8 th = *reinterpret_cast<const bf16x8*>(sTh + row);
                 const bf16x8 tl = *reinterpret_cast<const bf16x8*>(sTl + row);
-                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, th, acc[f], 0, 0, 0);
-                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, tl, acc[f], 0, 0, 0);
-                acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, th, acc[f], 0, 0, 0);
+#pragma unroll
+                for (int a = 0; a < 2; a++) {
+                    acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[a], th, acc[a][f], 0, 0, 0);
+                    acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[a], tl, acc[a][f], 0, 0, 0);
+                    acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[a], th, acc[a][f], 0, 0, 0);
+                }
             }
         }
     }
     __syncthreads();
 
     // ------------------------------------------------------------ epilogue
-    float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][32]
-    float* sMax = sBias + 8 * 32;                      // [2][4][32]
-    float* sWT = sMax + 2 * 4 * 32;                    // [32][NTP]
-    if (h == 0) sBias[w * 32 + n] = bsum;
+    float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][64]
+    float* sMax = sBias + ROT_TILE * 64;               // [8 waves][64 rows]
+    float* sWT = sMax + ROT_TILE * 64;                 // [32][NTP]
+    sBias[w * 64 + lane] = bsum;
     __syncthreads();
 
     float pTv[NF];
@@ -311,58 +318,63 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
     const float pRr = rValid ? (float)pR[r] : 0.f;
 
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const int m = (j & 3) + 8 * (j >> 2) + 4 * h;
-        const int l = l0 + hh * 32 + m;
-        const float b = Aconst[l] + sBias[w * 32 + m];
-        float mx = -INFINITY;
+    for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int f = 0; f < NF; f++) {
-            const float d = acc[f][j] + b;
-            acc[f][j] = d;
-            if (f * 32 + n < nT) mx = fmaxf(mx, d);
+        for (int j = 0; j < 16; j++) {
+            const int row = a * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
+            const int l = l0 + row;
+            const float b = Aconst[l] + sBias[w * 64 + row];
+            float mx = -INFINITY;
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                const float d = acc[a][f][j] + b;
+                acc[a][f][j] = d;
+                if (f * 32 + n < nT) mx = fmaxf(mx, d);
+            }
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+            if (!rValid) mx = -INFINITY;
+            float sR = 0.f;
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                const float e = (f * 32 + n < nT && rValid) ? expf(acc[a][f][j] - mx) : 0.f;
+                acc[a][f][j] = e;
+                sR += e * pTv[f];
+            }
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) sR += __shfl_xor(sR, o, 64);
+            if (n == 0) {
+                sMax[w * 64 + row] = mx;
+                if (rValid && l < nImg) wRp[(size_t)l * nR + r] = make_float2(mx, sR);
+            }
         }
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-        if (!rValid) mx = -INFINITY;
-        float sR = 0.f;
-#pragma unroll
-        for (int f = 0; f < NF; f++) {
-            const float e = (f * 32 + n < nT && rValid) ? expf(acc[f][j] - mx) : 0.f;
-            acc[f][j] = e;
-            sR += e * pTv[f];
-        }
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) sR += __shfl_xor(sR, o, 64);
-        if (n == 0) {
-            sMax[(hh * 4 + q) * 32 + m] = mx;
-            if (rValid && l < nImg) wRp[(size_t)l * nR + r] = make_float2(mx, sR);
-        }
-    }
     __syncthreads();
 
-    for (int half = 0; half < 2; half++) {
+#pragma unroll
+    for (int a = 0; a < 2; a++) {          // merge the 8 rotations, 32 image rows at a time
         for (int x = tid; x < 32 * NTP; x += THREADS) sWT[x] = 0.f;
         __syncthreads();
-        if (hh == half) {
 #pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const int m = (j & 3) + 8 * (j >> 2) + 4 * h;
-                const float M = fmaxf(fmaxf(sMax[(hh * 4 + 0) * 32 + m], sMax[(hh * 4 + 1) * 32 + m]),
-                                      fmaxf(sMax[(hh * 4 + 2) * 32 + m], sMax[(hh * 4 + 3) * 32 + m]));
-                const float sc = rValid ? expf(sMax[(hh * 4 + q) * 32 + m] - M) * pRr : 0.f;
+        for (int j = 0; j < 16; j++) {
+            const int m = (j & 3) + 8 * (j >> 2) + 4 * h;
+            const int row = a * 32 + m;
+            float M = sMax[row];
 #pragma unroll
-                for (int f = 0; f < NF; f++) atomicAdd(&sWT[m * NTP + f * 32 + n], acc[f][j] * sc);
-            }
+            for (int k = 1; k < ROT_TILE; k++) M = fmaxf(M, sMax[k * 64 + row]);
+            const float sc = rValid ? expf(sMax[w * 64 + row] - M) * pRr : 0.f;
+#pragma unroll
+            for (int f = 0; f < NF; f++) atomicAdd(&sWT[m * NTP + f * 32 + n], acc[a][f][j] * sc);
         }
         __syncthreads();
         for (int x = tid; x < 32 * NTP; x += THREADS) {
             const int m = x / NTP, t = x % NTP;
-            const int l = l0 + half * 32 + m;
+            const int row = a * 32 + m;
+            const int l = l0 + row;
             pWT[((size_t)rb * nImgPad + l) * NTP + t] = sWT[x];
             if (t == 0) {
-                const float M = fmaxf(fmaxf(sMax[(half * 4 + 0) * 32 + m], sMax[(half * 4 + 1) * 32 + m]),
-                                      fmaxf(sMax[(half * 4 + 2) * 32 + m], sMax[(half * 4 + 3) * 32 + m]));
+                float M = sMax[row];
+#pragma unroll
+                for (int k = 1; k < ROT_TILE; k++) M = fmaxf(M, sMax[k * 64 + row]);
                 pM[(size_t)rb * nImgPad + l] = M;
             }
         }
@@ -432,9 +444,17 @@ int launch_main(const WS& ws, const Dims& d, const float* rotP, const double* pR
 
 namespace thx {
 
+int scan_mfma(const float* rotP, int nR, const float* traP, int nT, const float* dat,
+              const float* ctf, const float* sigRcp, int nImg, int nPxl, const double* pR,
+              const double* pT, int kIdx, int nK, float* wC, float* wR, float* wT,
+              float* baseL, void* workspace, size_t wsBytes, hipStream_t stream);
+size_t scan_mfma_workspace(int nImg, int nR, int nT, int nPxl);
+
 size_t scan_bf16x3_workspace(int nImg, int nR, int nT, int nPxl)
 {
-    return carve(nullptr, dims(nImg, nR, nT, nPxl)).bytes;
+    const Dims d = dims(nImg, nR, nT, nPxl);
+    if (d.nTPad > 160) return scan_mfma_workspace(nImg, nR, nT, nPxl);
+    return carve(nullptr, d).bytes;
 }
 
 int scan_bf16x3(const float* rotP, int nR, const float* traP, int nT, const float* dat,
@@ -443,7 +463,9 @@ int scan_bf16x3(const float* rotP, int nR, const float* traP, int nT, const floa
                 float* baseL, void* workspace, size_t wsBytes, hipStream_t s)
 {
     const Dims d = dims(nImg, nR, nT, nPxl);
-    THX_CHECK_ARG(d.nTPad <= 256, "thx_global_scan(algo=2): nT=%d > 256", nT);
+    if (d.nTPad > 160)   // 2 x NF accumulators no longer fit one wave: FP32 MFMA path
+        return scan_mfma(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx, nK,
+                         wC, wR, wT, baseL, workspace, wsBytes, s);
     THX_CHECK_ARG(d.nRB <= 65535, "thx_global_scan(algo=2): grid too large");
     const WS ws = carve(workspace, d);
     THX_CHECK_ARG(ws.bytes <= wsBytes, "thx_global_scan(algo=2): workspace too small");
@@ -464,10 +486,7 @@ int scan_bf16x3(const float* rotP, int nR, const float* traP, int nT, const floa
         case 2: st = launch_main<2>(ws, d, rotP, pR, s); break;
         case 3: st = launch_main<3>(ws, d, rotP, pR, s); break;
         case 4: st = launch_main<4>(ws, d, rotP, pR, s); break;
-        case 5: st = launch_main<5>(ws, d, rotP, pR, s); break;
-        case 6: st = launch_main<6>(ws, d, rotP, pR, s); break;
-        case 7: st = launch_main<7>(ws, d, rotP, pR, s); break;
-        default: st = launch_main<8>(ws, d, rotP, pR, s); break;
+        default: st = launch_main<5>(ws, d, rotP, pR, s); break;
     }
     if (st != THX_OK) return st;
     hipLaunchKernelGGL(k_scan_combine_bf, dim3(nImg), dim3(256), sizeof(float) * d.nRB, s,
