@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--box", type=int, default=256)
     p.add_argument("--nr", type=int, default=2000)
     p.add_argument("--phases", type=int, default=10)
-    p.add_argument("--algo", type=int, default=1)
+    p.add_argument("--algo", type=int, default=2,
+                   help="global-scan algorithm: 0 direct, 1 FP32 MFMA, 2 bf16x3 MFMA")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-extras", action="store_true", help="skip insert / all-reduce / local roofline")

@@ -40,7 +40,7 @@ class Expectation:
     """
 
     def __init__(self, vol, px, gset, mLR=125, mLT=9, n_phase=10, perturb=0.5,
-                 trans_s=10.0, trans_search_factor=0.25, algo=1, seed=7):
+                 trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7):
         dev = vol.device
         self.vol, self.px, self.dev = vol, px, dev
         q, t, pR, pT = gset
