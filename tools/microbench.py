@@ -31,6 +31,8 @@ def main():
     p.add_argument("--nr", type=int, default=2000)
     p.add_argument("--mreco", type=int, default=100)
     p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--spread", type=float, default=3.0,
+                   help="local: rotation spread (deg) of each image's cloud, 0 = uniform")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     N, pf = a.box, 2
@@ -41,8 +43,18 @@ def main():
     out = {"what": a.what, "box": N, "rU": a.ru, "nPxl": px.n, "images": a.images}
     if a.what == "local":
         mR, mT = 125, 9
-        quat = torch.as_tensor(synth.uniform_quaternions(a.images * mR, rng).reshape(a.images, mR, 4),
-                               device=dev)
+        if a.spread > 0:   # particle clouds: perturbations of one pose per image
+            base = synth.uniform_quaternions(a.images, rng)
+            d = rng.standard_normal((a.images, mR, 4)) * np.radians(a.spread) / 2
+            d[..., 0] = 1.0
+            d /= np.linalg.norm(d, axis=-1, keepdims=True)
+            w0, x0, y0, z0 = [base[:, None, k] for k in range(4)]
+            w1, x1, y1, z1 = [d[..., k] for k in range(4)]
+            q = np.stack([w0 * w1 - x0 * x1 - y0 * y1 - z0 * z1, w0 * x1 + x0 * w1 + y0 * z1 - z0 * y1,
+                          w0 * y1 - x0 * z1 + y0 * w1 + z0 * x1, w0 * z1 + x0 * y1 - y0 * x1 + z0 * w1], -1)
+        else:
+            q = synth.uniform_quaternions(a.images * mR, rng).reshape(a.images, mR, 4)
+        quat = torch.as_tensor(np.ascontiguousarray(q), device=dev)
         trans = torch.as_tensor(rng.standard_normal((a.images, mT, 2)), device=dev)
         pC = torch.ones(a.images, dtype=torch.float64, device=dev)
         pR = torch.full((a.images, mR), 1.0 / mR, dtype=torch.float64, device=dev)
