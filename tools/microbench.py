@@ -31,6 +31,7 @@ def main():
     p.add_argument("--nr", type=int, default=2000)
     p.add_argument("--mreco", type=int, default=100)
     p.add_argument("--reps", type=int, default=5)
+    p.add_argument("--tile", type=int, default=0, help="local: 2D pixel tile order (0 = reference order)")
     p.add_argument("--spread", type=float, default=3.0,
                    help="local: rotation spread (deg) of each image's cloud, 0 = uniform")
     a = p.parse_args()
@@ -60,6 +61,15 @@ def main():
         pR = torch.full((a.images, mR), 1.0 / mR, dtype=torch.float64, device=dev)
         pT = torch.full((a.images, mT), 1.0 / mT, dtype=torch.float64, device=dev)
         cells = ops.volume_cells(vol) if a.cells else None
+        if a.tile > 0:     # pixels in 2D tiles of tile x tile (row-major inside a tile)
+            key = (px.iRow // a.tile + 1000) * 100000 + (px.iCol // a.tile) * 1000 + \
+                  (px.iRow % a.tile) * a.tile + px.iCol % a.tile
+            perm = np.argsort(key, kind="stable")
+            px.iCol, px.iRow = px.iCol[perm].copy(), px.iRow[perm].copy()
+            px.d_iCol = torch.from_numpy(px.iCol).to(dev)
+            px.d_iRow = torch.from_numpy(px.iRow).to(dev)
+            pt = torch.from_numpy(perm).to(dev)
+            dat, ctf, sig = (x[:, pt].contiguous() for x in (dat, ctf, sig))
         sec = timed_events(lambda: ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px,
                                                    cells=cells), a.reps, st)
         out.update(ms=sec * 1e3, us_per_image_phase=sec / a.images * 1e6,
