@@ -225,6 +225,14 @@ def main():
         qt = qtrue[:q0.shape[0]]
         cosang = (q0 * qt).sum(-1).abs().clamp(max=1)
         res["median_pose_error_deg"] = float(torch.rad2deg(2 * torch.acos(cosang)).median())
+        # final particle-cloud spread: angle of every rotation sample to the top one
+        qa = outs[0][0]
+        ca = (qa * qa[:, :1, :]).sum(-1).abs().clamp(max=1)
+        ang = torch.rad2deg(2 * torch.acos(ca))
+        qs = torch.tensor([0.1, 0.5, 0.9], dtype=ang.dtype, device=ang.device)
+        res["cloud_spread_deg"] = {
+            "median_p10_p50_p90": [round(float(v), 2) for v in torch.quantile(ang.median(1).values, qs)],
+            "max_p10_p50_p90": [round(float(v), 2) for v in torch.quantile(ang.max(1).values, qs)]}
 
     extras = {}
     if not a.no_extras:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define THX_ABI_VERSION 1
+#define THX_ABI_VERSION 2
 
 enum {
     THX_OK = 0,
@@ -60,6 +60,17 @@ const char* thx_last_error(void);
  * Outputs (any may be NULL) need `cap` entries; *nPxl receives the count. */
 int thx_pixel_set(int idim, int pf, float rU, float rL, int cap, int* iCol,
                   int* iRow, int* iSig, int* iPxl, int* nPxl);
+
+/* Visiting order of the pixel set for the local phases (no reference
+ * counterpart; the reference walks the set in allocPreCalIdx order): the
+ * set is cut into 4 x 4 squares of (iCol, iRow), squares in serpentine row
+ * order, consecutive partial squares (the disc edge) merged while they fit in
+ * 16 entries, every group padded to 16 with -1.  Each 16-entry group of
+ * `order` is then a compact patch whose slice neighbourhood fits in LDS
+ * (thx_local_phase).  Host function; order: cap ints, *nOrd receives the
+ * length (a multiple of 16; every pixel index appears exactly once). */
+int thx_pixel_tile_order(const int* iCol, const int* iRow, int nPxl, int cap,
+                         int* order, int* nOrd);
 
 /* ------------------------------------------------------------------ a2 ---
  * Per-image CTF over the pixel set: CTF(RFLOAT* dst, ...) (src/CTF.cpp:
@@ -138,14 +149,24 @@ int thx_global_scan(const float* rotP, int nR, const float* traP, int nT,
  * volLayout 0: `vol` is the half-complex projectee; 1: `vol` is its
  * cell-expanded copy from thx_volume_cells (8x the bytes, one aligned 64-B
  * segment per trilinear gather -- the layout for HBM-bound full-resolution
- * phases). */
-size_t thx_local_phase_workspace(int nImg, int nR, int nT);
+ * phases).
+ * pxOrder (device, nOrd ints, may be NULL = set order, nOrd ignored): the
+ * pixel visiting order from thx_pixel_tile_order (-1 entries skipped).
+ * Pixels are taken 16 at a time; when the
+ * Hermitian-folded neighbourhood of a 16-pixel patch under the workgroup's
+ * 128 rotations fits in LDS it is staged there once and the 8 taps of every
+ * sample are read from LDS, otherwise straight from `vol`.  The order only
+ * changes the FP32 summation order over pixels, not which taps are summed.
+ * workspace (required): >= thx_local_phase_workspace(nImg, nR, nT, nVisit)
+ * bytes, nVisit = nOrd with pxOrder, nPxl without. */
+size_t thx_local_phase_workspace(int nImg, int nR, int nT, int nVisit);
 int thx_local_phase(const float* vol, int volLayout, int vdim, int pf,
                     const double* quat,
                     int nR, const double* trans, int nT, const double* pC,
                     const double* pR, const double* pT, const float* dat,
                     const float* ctf, const float* sigRcp, const int* iCol,
-                    const int* iRow, int nPxl, int idim, int nImg, float* wC,
+                    const int* iRow, const int* pxOrder, int nOrd, int nPxl,
+                    int idim, int nImg, float* wC,
                     float* wR, float* wT, float* baseL, float* dvp,
                     void* workspace, size_t wsBytes, thx_stream_t stream);
 
@@ -219,12 +240,15 @@ typedef struct thx_expect_cfg {
     unsigned long long seed;  /* counter-RNG seed */
 } thx_expect_cfg;
 
-size_t thx_expectation_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl);
+/* nOrd: length of pxOrder (<= 0 when pxOrder is NULL). */
+size_t thx_expectation_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl,
+                                 int nOrd);
 int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                     const double* gQuat, const double* gTrans,
                     const double* gPR, const double* gPT, const float* dat,
                     const float* ctf, const float* sigRcp, const int* iCol,
-                    const int* iRow, int nPxl, int nImg, double* quat,
+                    const int* iRow, const int* pxOrder, int nOrd, int nPxl,
+                    int nImg, double* quat,
                     double* trans, double* pR, double* pT, float* score,
                     void* workspace, size_t wsBytes, thx_stream_t stream);
 

@@ -187,6 +187,71 @@ def test_local_phase_cells_layout_and_many_rotations(orc, stack):
         assert np.max(np.abs(d[l] - rd) / np.abs(rd)) < 1e-5
 
 
+def staged_fraction(orc, px, quat, pf, cap=6400):
+    """Host restatement of the kernel's patch-neighbourhood bound: share of
+    (image, patch) stages whose two folded boxes fit in the LDS capacity."""
+    fits = []
+    for q in quat:
+        R = np.stack([orc.rotate3d(x) for x in q])              # column-major 3x3 -> [r, 9]
+        R = R.reshape(-1, 3, 3).transpose(0, 2, 1)              # row-major
+        for g in px.order.reshape(-1, 16):
+            g = g[g >= 0]
+            c = np.array([[a, b, 0.0] for b in (px.iRow[g].min(), px.iRow[g].max())
+                          for a in (px.iCol[g].min(), px.iCol[g].max())]) * pf
+            P = np.einsum("rij,kj->rki", R, c)                 # [r, 4, 3]
+            mn, mx = P.min(1), P.max(1)
+            tot = 0
+            pos, neg = mx[:, 0] >= -1e-3, mn[:, 0] < 1e-3
+            if pos.any():
+                lo = np.floor(np.maximum(mn[pos], [0, -np.inf, -np.inf])).min(0) - 1
+                hi = np.floor(mx[pos]).max(0) + 2
+                lo[0] = max(lo[0], 0)
+                tot += np.prod(hi - lo + 1)
+            if neg.any():
+                lo = np.floor(np.maximum(-mx[neg], [0, -np.inf, -np.inf])).min(0) - 1
+                hi = np.floor(-mn[neg]).max(0) + 2
+                lo[0] = max(lo[0], 0)
+                tot += np.prod(hi - lo + 1)
+            fits.append(tot <= cap)
+    return float(np.mean(fits))
+
+
+@pytest.fixture(scope="module")
+def stack64(orc):
+    return small_stack(orc, N=64, nImg=4, nR=4, nT=3, seed=4)
+
+
+@pytest.mark.parametrize("spread,lo,hi", [(1.0, 0.99, 1.0), (8.0, 0.1, 0.6), (20.0, 0.0, 0.2)])
+def test_local_phase_staged_patches(orc, stack64, spread, lo, hi):
+    """Particle clouds of a few degrees: the tile-ordered kernel stages most
+    16-pixel patch neighbourhoods in LDS, wide clouds fall back to direct
+    gathers; both routes match the oracle and the set-order kernel."""
+    s = stack64
+    px = dev_pixels(s)
+    nImg, nR, nT = 4, 125, 9
+    rng = np.random.default_rng(13)
+    quat = synth.clustered_quaternions(nImg, nR, spread, rng)
+    frac = staged_fraction(orc, px, quat, s["pf"])
+    assert lo <= frac <= hi, frac
+    trans = rng.standard_normal((nImg, nT, 2)) * 2
+    pC = np.ones(nImg)
+    pR = np.full((nImg, nR), 1.0 / nR)
+    pT = np.full((nImg, nT), 1.0 / nT)
+    vol = T(s["vol"])
+    args = (T(quat), T(trans), T(pC), T(pR), T(pT), T(s["dat"][:nImg]), T(s["ctf"][:nImg]),
+            T(s["sig"][:nImg]), px)
+    a = ops.local_phase(vol, *args, want_dvp=True)
+    b = ops.local_phase(vol, *args, want_dvp=True, tiled=False)
+    c = ops.local_phase(vol, *args, want_dvp=True, cells=ops.volume_cells(vol))
+    assert torch.equal(a[4], c[4])
+    da, db = a[4].cpu().numpy(), b[4].cpu().numpy()
+    assert np.max(np.abs(da - db) / np.abs(db)) < 2e-6      # pixel summation order only
+    for l in range(nImg):
+        *_, rd = orc.local_phase(s["vol"], s["vdim"], s["pf"], quat[l], trans[l], 1.0, pR[l],
+                                 pT[l], s["dat"][l], s["ctf"][l], s["sig"][l], s["px"], s["N"])
+        assert np.max(np.abs(da[l] - rd) / np.abs(rd)) < 1e-5
+
+
 def test_resample_bit_exact(orc):
     rng = np.random.default_rng(5)
     for nIn, nOut, nImg in ((125, 125, 7), (2000, 125, 3), (151, 9, 4), (9, 9, 6)):

@@ -35,7 +35,27 @@ def test_exports_every_declared_symbol(L):
 
 
 def test_abi_version(L):
-    assert L.thx_abi_version() == 1
+    assert L.thx_abi_version() == 2
+
+
+def test_pixel_tile_order(L):
+    # every pixel once, 16-entry groups padded with -1, each group a compact patch
+    from thunder_amd import ops
+    for N, rU in ((256, 24), (64, 20), (256, 126)):
+        px = ops.PixelSet(N, 2, rU, 1)
+        o = px.order
+        assert len(o) % 16 == 0 and len(o) < 1.25 * px.n + 16
+        assert sorted(o[o >= 0].tolist()) == list(range(px.n))
+        ext = []
+        for c0 in range(0, len(o), 16):
+            s = o[c0:c0 + 16]
+            s = s[s >= 0]
+            assert len(s) > 0
+            ext.append(max(np.ptp(px.iCol[s]), np.ptp(px.iRow[s])))
+        ext = np.array(ext)
+        assert np.median(ext) <= 3 and np.mean(ext <= 7) > 0.95, (N, rU, np.percentile(ext, 90))
+    st = L.thx_pixel_tile_order(None, None, 4, 0, None, None)
+    assert st == 1
 
 
 @pytest.mark.parametrize("N,rL,rU", [(64, 0, 30), (256, 1, 24), (256, 1, 126), (200, 1, 19)])
@@ -66,8 +86,8 @@ def test_argument_validation_without_gpu(L):
     assert L.thx_global_scan(None, 4, None, 5, None, None, None, 1, 10, None, None, 2, 1,
                              None, None, None, None, 1, None, 0, None) == 1
     assert L.thx_local_phase(None, 0, 64, 2, None, 0, None, 9, None, None, None, None, None, None,
-                             None, None, 10, 32, 1, None, None, None, None, None, None, 0,
-                             None) == 1
+                             None, None, None, 0, 10, 32, 1, None, None, None, None, None, None,
+                             0, None) == 1
     assert L.thx_resample(1, 0, None, None, 4, None, None, None, None, None) == 1
     assert L.thx_fsc(None, None, 31, 8, None, None, 0, None) == 1
     assert L.thx_ExpectProject(None, None, None, None, None, 1, 2, 1, 64, 10) == 1
@@ -79,3 +99,5 @@ def test_workspace_queries_are_host_only(L):
     assert ws0 >= 100 * 2000 * 151 * 4
     assert ws1 > 0
     assert L.thx_fsc_workspace(64) >= 3 * 64 * 8
+    # dvp + one 64-B neighbourhood record per (image, rotation tile, patch)
+    assert L.thx_local_phase_workspace(10, 125, 9, 944) >= 10 * 125 * 9 * 4 + 10 * 59 * 64

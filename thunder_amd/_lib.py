@@ -25,18 +25,20 @@ SIGNATURES = {
     "thx_global_scan_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "thx_global_scan": (_c_int, [_p, _c_int, _p, _c_int, _p, _p, _p, _c_int, _c_int, _p, _p,
                                  _c_int, _c_int, _p, _p, _p, _p, _c_int, _p, _c_size, _p]),
-    "thx_local_phase_workspace": (_c_size, [_c_int, _c_int, _c_int]),
+    "thx_local_phase_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "thx_volume_cells": (_c_int, [_p, _c_int, _p, _p]),
+    "thx_pixel_tile_order": (_c_int, [_p, _p, _c_int, _c_int, _p, _p]),
     "thx_local_phase": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _p, _p,
-                                 _p, _p, _p, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p, _p,
+                                 _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p, _p,
                                  _c_size, _p]),
     "thx_resample": (_c_int, [_c_int, _c_int, _p, _p, _c_int, _p, _p, _p, _p, _p]),
     "thx_insert3d": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_int,
                               _c_int, _p, _p, _c_int, _c_int, _p]),
     "thx_fsc_workspace": (_c_size, [_c_int]),
     "thx_fsc": (_c_int, [_p, _p, _c_int, _c_int, _p, _p, _c_size, _p]),
-    "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int]),
-    "thx_expectation": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _p, _p,
+    "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int, _c_int]),
+    "thx_expectation": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int,
+                                 _p, _p,
                                  _p, _p, _p, _p, _c_size, _p]),
     "thx_ExpectRotran": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
     "thx_ExpectProject": (_c_int, [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int]),

@@ -1,8 +1,10 @@
 // geom.hip -- pixel set (a1), CTF (a2), translation table (a4), quaternion ->
 // rotation (a5), and the error / version plumbing of the C-ABI.
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstring>
+#include <vector>
 
 #include "common.h"
 
@@ -58,6 +60,55 @@ extern "C" int thx_pixel_set(int idim, int pf, float rU, float rL, int cap,
             }
         }
     *nPxl = n;
+    return THX_OK;
+}
+
+extern "C" int thx_pixel_tile_order(const int* iCol, const int* iRow, int nPxl, int cap,
+                                    int* order, int* nOrd)
+{
+    constexpr int TILE = 4, GROUP = TILE * TILE;
+    THX_CHECK_ARG(iCol && iRow && nOrd && nPxl >= 0 && cap >= 0,
+                  "thx_pixel_tile_order: bad arguments");
+    *nOrd = 0;
+    if (nPxl == 0) return THX_OK;
+    int cMin = iCol[0], rMin = iRow[0], cMax = iCol[0];
+    for (int i = 1; i < nPxl; i++) {
+        cMin = std::min(cMin, iCol[i]);
+        cMax = std::max(cMax, iCol[i]);
+        rMin = std::min(rMin, iRow[i]);
+    }
+    const long nTc = (cMax - cMin) / TILE + 1;
+    std::vector<long> key(nPxl);
+    for (int i = 0; i < nPxl; i++) {
+        const long tr = (iRow[i] - rMin) / TILE, tc0 = (iCol[i] - cMin) / TILE;
+        const long tc = (tr & 1) ? nTc - 1 - tc0 : tc0;   // serpentine square rows
+        key[i] = tr * nTc + tc;
+    }
+    std::vector<int> idx(nPxl);
+    for (int i = 0; i < nPxl; i++) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return key[a] < key[b]; });
+    // groups of <= 16: whole squares, consecutive partial squares merged
+    std::vector<int> out;
+    out.reserve(nPxl + GROUP);
+    int fill = 0;
+    for (int a = 0; a < nPxl;) {
+        int b = a;
+        while (b < nPxl && key[idx[b]] == key[idx[a]]) b++;
+        if (fill + (b - a) > GROUP) {
+            out.insert(out.end(), GROUP - fill, -1);
+            fill = 0;
+        }
+        out.insert(out.end(), idx.begin() + a, idx.begin() + b);
+        fill += b - a;
+        a = b;
+    }
+    if (fill) out.insert(out.end(), GROUP - fill, -1);
+    *nOrd = (int)out.size();
+    if (order) {
+        THX_CHECK_ARG((int)out.size() <= cap, "thx_pixel_tile_order: cap=%d < %d", cap,
+                      (int)out.size());
+        std::copy(out.begin(), out.end(), order);
+    }
     return THX_OK;
 }
 

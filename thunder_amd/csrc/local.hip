@@ -11,23 +11,50 @@
 //   s|d - c T P|^2 = s|d|^2 + P.re U_t + P.im V_t + b |P|^2
 //   U_t = Re(Y) T.re + Im(Y) T.im,  V_t = Im(Y) T.re - Re(Y) T.im,
 //   Y = -2 s c d,  b = s c^2,
-// so dvp[r][t] - A_l = sum_i [P.re, P.im, |P|^2, 0]_ri . [U, V, b, 0]_it is a
-// K = 4 nPxl product of a (rotation x 4 nPxl) projection tile and a
-// (4 nPxl x translation) image tile.  The workgroup gathers the projection
-// tile (the HBM-bound part: 8 taps per rotation-pixel), stages it in LDS and
-// reduces it against the translation tile on v_mfma_f32_16x16x4_f32, so no
-// cross-lane reduction and no per-(r,t) VALU loop is left.
+// so dvp[r][t] = A_l + B_r + sum_i [P.re, P.im]_ri . [U, V]_it with the
+// per-rotation bias B_r = sum_i b_i |P_ri|^2: a K = 2 nPxl product of a
+// (rotation x 2 nPxl) projection tile and a (2 nPxl x translation) image tile,
+// reduced on v_mfma_f32_16x16x4_f32 (two pixels per MFMA).
+//
+// The projection tile is the expensive part: 8 trilinear taps per
+// (rotation, pixel).  A particle cloud is a few degrees wide, so the 128
+// rotated copies of a compact 16-pixel patch (thx_pixel_tile_order) land in a
+// small neighbourhood of the projectee.  k_patch_boxes bounds that
+// neighbourhood exactly for every (image, rotation tile, patch): the
+// per-rotation hull of the patch corners, split into the part with x >= 0 and
+// the Hermitian-folded part with x < 0 (two boxes of one shape).
+// k_local_fused streams the patches through a two-barrier software pipeline:
+// while it gathers patch c from LDS the voxels of patch c+1 are in flight from
+// L2/HBM into registers.  A patch whose neighbourhood exceeds the LDS box is
+// gathered straight from `vol`.  Both routes sum the same taps with the same
+// weights in the same order as interp_ft.
+//
+// Thread mapping (8 waves): wave w owns rotations 16w .. 16w+15, lane l works
+// on rotation 16w + (l & 15) -- its rotation matrix lives in registers for the
+// whole launch -- and on pixel 4s + (l >> 4) of step s of a patch.  After a
+// step the (re, im) of the four pixels are regrouped across lane rows with
+// v_permlane16_swap into the A operands of two 16x16x4 MFMAs (k = re, im of
+// two pixels), so the projection tile never goes through LDS.
+#include <climits>
+
 #include "common.h"
 
 namespace {
 
-constexpr int THREADS = 256;
-constexpr int RT = 128;          // rotations per workgroup (8 MFMA M-tiles)
-constexpr int TT = 16;           // translations per workgroup (1 MFMA N-tile)
-constexpr int KC = 32;           // pixels per LDS stage
-constexpr int APITCH = KC + 1;   // LDS row pitch (float2) of the [rotation][pixel] tile
+constexpr int THREADS = 512;
+constexpr int NWAVE = THREADS / 64;
+constexpr int RT = 16 * NWAVE;   // rotations per workgroup (one 16-row M-tile per wave)
+constexpr int TT = 16;           // translations per workgroup (one N-tile)
+constexpr int KC = 16;           // pixels per stage: one patch of the tile order
+constexpr int BOX_CAP = 8192;    // LDS voxels (64 KiB) for a patch neighbourhood
+constexpr int NIT = BOX_CAP / 4 / THREADS;   // 32-B box items in flight per thread
+constexpr int REC = 20;          // ints per patch record
+static_assert(KC * TT <= THREADS, "one (pixel, translation) of the image tile per thread");
+static_assert(BOX_CAP % (4 * THREADS) == 0, "whole prefetch rounds");
+static_assert(KC == 16, "four steps of four pixels");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(8)));
 
 // Cell-expanded projectee (thx_volume_cells): the 8 taps of the trilinear
 // cell with base (x0, y0, z0) are 64 contiguous bytes, so one gather is one
@@ -56,37 +83,307 @@ THX_DEV float2 interp_cells(const float4* __restrict__ cells, int vdim, float x,
     return make_float2(re, conj ? -im : im);
 }
 
+// Patch record (k_patch_boxes -> k_local_fused).  Two boxes of one shape in
+// folded (x >= 0) coordinates, side 0 for samples with x >= 0, side 1 for the
+// folded ones, each stored [z][y][x] in LDS (rows padded to 4 voxels):
+//   [0..2] side-0 origin (x, y, z; rows / slices signed, unwrapped)
+//   [3..5] side-1 origin  [6] row pitch nx  [7] nx*ny  [8] ny
+//   [9] side-0 voxels (= LDS offset of side 1)  [10] total voxels
+//   (> BOX_CAP: the patch is gathered from the volume)
+//   [11] side-0 items (4 voxels = 32 B)  [12] total items
+//   [13] magic(nx / 4)  [14] magic(ny)  (udiv)
+//   [15] / [16] LDS index of voxel (0, 0, 0) for side 0 / 1 (may be negative)
+//   [17], [18] (iCol, iRow) of the patch's first pixel (stand-in for padding)
+struct Rec {
+    int v[REC];
+    THX_DEV bool staged() const { return v[10] <= BOX_CAP; }
+};
+
+THX_DEV Rec load_rec(const int* __restrict__ p)
+{
+    Rec r;
+    const int4* q = reinterpret_cast<const int4*>(p);
+#pragma unroll
+    for (int k = 0; k < REC / 4; k++) {
+        const int4 a = q[k];
+        r.v[4 * k] = a.x; r.v[4 * k + 1] = a.y; r.v[4 * k + 2] = a.z; r.v[4 * k + 3] = a.w;
+    }
+    return r;
+}
+
+// Wave-wide integer min / max: 4 DPP steps inside each row of 16, then the
+// four row results through readlane.  |v| < 2^30.
+THX_DEV int wave_min_i(int v)
+{
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0xb1, 0xf, 0xf, false));   // quad_perm 1032
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x4e, 0xf, 0xf, false));   // quad_perm 2301
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x124, 0xf, 0xf, false));  // row_ror 4
+    v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x128, 0xf, 0xf, false));  // row_ror 8
+    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
+THX_DEV int wave_max_i(int v) { return -wave_min_i(-v); }
+
+// Exact u / d for u * d < 2^32 with m = magic(d) (round-up reciprocal).
+THX_DEV unsigned magic(unsigned d) { return d <= 1 ? 0u : 0xFFFFFFFFu / d + 1u; }
+THX_DEV int udiv(int u, int d, unsigned m) { return d <= 1 ? u : (int)__umulhi((unsigned)u, m); }
+
+constexpr int BIG = 1 << 29;
+
+THX_DEV int patch_pixel(const int* __restrict__ order, int nVisit, int k)
+{
+    return k < nVisit ? (order ? order[k] : k) : -1;
+}
+
+// One wave per (image, rotation tile, patch): the LDS boxes that hold every
+// tap of the patch's samples under the tile's rotations.
+__global__ void __launch_bounds__(256) k_patch_boxes(const double* __restrict__ quat, int nR,
+                                                     const int* __restrict__ iCol,
+                                                     const int* __restrict__ iRow,
+                                                     const int* __restrict__ order,
+                                                     int nVisit, int pf, int vdim, int nImg,
+                                                     int* __restrict__ rec)
+{
+    const int nC = (nVisit + KC - 1) / KC, nRT = (nR + RT - 1) / RT;
+    const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= (long)nImg * nRT * nC) return;
+    const int lane = threadIdx.x & 63;
+    const int c = (int)(w % nC);
+    const long lr = w / nC;
+    const int ry = (int)(lr % nRT), l = (int)(lr / nRT);
+    const int p = lane < KC ? patch_pixel(order, nVisit, c * KC + lane) : -1;
+    const int ic = p >= 0 ? iCol[p] : 0, ir = p >= 0 ? iRow[p] : 0;
+    const int cLo = wave_min_i(p >= 0 ? ic : BIG), cHi = wave_max_i(p >= 0 ? ic : -BIG);
+    const int rLo = wave_min_i(p >= 0 ? ir : BIG), rHi = wave_max_i(p >= 0 ? ir : -BIG);
+    const int ic0 = __builtin_amdgcn_readfirstlane(ic), ir0 = __builtin_amdgcn_readfirstlane(ir);
+    // e[0..5]: side 0 lo xyz, hi xyz; e[6..11]: side 1
+    int e[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) e[k] = (k % 6) < 3 ? BIG : -BIG;
+    if (cLo <= cHi) {
+#pragma unroll
+        for (int h = 0; h < (RT + 63) / 64; h++) {
+            const int r = ry * RT + h * 64 + lane;
+            if (h * 64 + lane >= RT || r >= nR) continue;
+            double q[4], m[9];
+            for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
+            quat_to_mat(q, m);
+            float mn[3] = {INFINITY, INFINITY, INFINITY};
+            float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                float x[3];
+                rot_coord(m, (k & 1) ? cHi : cLo, (k & 2) ? rHi : rLo, pf, x[0], x[1], x[2]);
+#pragma unroll
+                for (int a = 0; a < 3; a++) { mn[a] = fminf(mn[a], x[a]); mx[a] = fmaxf(mx[a], x[a]); }
+            }
+            // every rotated patch point lies in the corner hull; a 1-voxel margin
+            // on each side absorbs the FP32 rounding of the coordinates
+            if (mx[0] >= -1e-3f) {
+                e[0] = min(e[0], (int)floorf(fmaxf(mn[0], 0.f)) - 1);
+                e[1] = min(e[1], (int)floorf(mn[1]) - 1);
+                e[2] = min(e[2], (int)floorf(mn[2]) - 1);
+                e[3] = max(e[3], (int)floorf(mx[0]) + 2);
+                e[4] = max(e[4], (int)floorf(mx[1]) + 2);
+                e[5] = max(e[5], (int)floorf(mx[2]) + 2);
+            }
+            if (mn[0] < 1e-3f) {
+                e[6] = min(e[6], (int)floorf(fmaxf(-mx[0], 0.f)) - 1);
+                e[7] = min(e[7], (int)floorf(-mx[1]) - 1);
+                e[8] = min(e[8], (int)floorf(-mx[2]) - 1);
+                e[9] = max(e[9], (int)floorf(-mn[0]) + 2);
+                e[10] = max(e[10], (int)floorf(-mn[1]) + 2);
+                e[11] = max(e[11], (int)floorf(-mn[2]) + 2);
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 12; k++) e[k] = (k % 6) < 3 ? wave_min_i(e[k]) : wave_max_i(e[k]);
+    if (lane == 0) {
+        const int nColFT = vdim / 2 + 1, half = vdim / 2;
+        int o[REC] = {0};
+        int lo[2][3], n[2][3];
+        bool any[2];
+        for (int s = 0; s < 2; s++) {
+            // clamp into the half volume (rows / slices wrap once at most)
+            lo[s][0] = max(e[6 * s], 0);
+            lo[s][1] = max(e[6 * s + 1], -half);
+            lo[s][2] = max(e[6 * s + 2], -half);
+            n[s][0] = min(e[6 * s + 3], nColFT - 1) - lo[s][0] + 1;
+            n[s][1] = min(e[6 * s + 4], half) - lo[s][1] + 1;
+            n[s][2] = min(e[6 * s + 5], half) - lo[s][2] + 1;
+            any[s] = n[s][0] > 0 && n[s][1] > 0 && n[s][2] > 0;
+        }
+        int nx = 4, ny = 1, nz = 1;
+        for (int s = 0; s < 2; s++)
+            if (any[s]) {
+                nx = max(nx, (n[s][0] + 3) & ~3);   // rows padded to 4 voxels (32 B)
+                ny = max(ny, n[s][1]);
+                nz = max(nz, n[s][2]);
+            }
+        const long nxy = (long)nx * ny, nv = nxy * nz;
+        const long nv0 = any[0] ? nv : 0, nv1 = any[1] ? nv : 0;
+        for (int s = 0; s < 3; s++) { o[s] = lo[0][s]; o[3 + s] = lo[1][s]; }
+        o[6] = nx;
+        o[7] = (int)min(nxy, (long)BIG);
+        o[8] = ny;
+        o[9] = (int)min(nv0, (long)BIG);
+        o[10] = (int)min(nv0 + nv1, (long)BIG);
+        o[11] = (int)min(nv0 / 4, (long)BIG);
+        o[12] = (int)min((nv0 + nv1) / 4, (long)BIG);
+        o[13] = (int)magic((unsigned)nx / 4);
+        o[14] = (int)magic((unsigned)ny);
+        if (nv0 + nv1 <= BOX_CAP) {
+            o[15] = -(lo[0][2] * o[7] + lo[0][1] * nx + lo[0][0]);
+            o[16] = o[9] - (lo[1][2] * o[7] + lo[1][1] * nx + lo[1][0]);
+        }
+        o[17] = ic0;
+        o[18] = ir0;
+        int4* dst = reinterpret_cast<int4*>(rec + w * REC);
+        for (int k = 0; k < REC / 4; k++)
+            dst[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    }
+}
+
+// Pixel of the image tile a staging thread owns: (iCol, iRow), data.
+struct Pix {
+    int p, ic, ir;
+    float2 d;
+    float c, s;
+};
+
+THX_DEV Pix load_pix(int p, const int* __restrict__ iCol, const int* __restrict__ iRow,
+                     const float2* __restrict__ D, const float* __restrict__ C,
+                     const float* __restrict__ S)
+{
+    Pix x{p, 0, 0, make_float2(0.f, 0.f), 0.f, 0.f};
+    if (p >= 0) {
+        x.ic = iCol[p];
+        x.ir = iRow[p];
+        x.d = D[p];
+        x.c = C[p];
+        x.s = S[p];
+    }
+    return x;
+}
+
+// The items (4 consecutive voxels of a box row, 32 B) of a staged patch this
+// thread moves: item it = tid + j THREADS lands at LDS voxel 4 it.
 template <bool CELLS>
-__global__ void __launch_bounds__(THREADS) k_local_fused(const float2* __restrict__ vol,
-                                                         int vdim, int pf,
-                                                         const double* __restrict__ quat,
-                                                         int nR,
-                                                         const double* __restrict__ trans,
-                                                         int nT,
-                                                         const float2* __restrict__ dat,
-                                                         const float* __restrict__ ctf,
-                                                         const float* __restrict__ sig,
-                                                         const int* __restrict__ iCol,
-                                                         const int* __restrict__ iRow,
-                                                         int nPxl, int idim,
-                                                         float* __restrict__ dvp)
+THX_DEV void fetch_box(f32x4 (&pre)[NIT][2], const Rec& b, const float2* __restrict__ vol,
+                       int vdim, int tid)
+{
+    if (!b.staged()) return;
+    const int nColFT = vdim / 2 + 1;
+    const int nq = b.v[6] >> 2, ny = b.v[8];
+#pragma unroll
+    for (int j = 0; j < NIT; j++) {
+        const int it = tid + j * THREADS;
+        if (it < b.v[12]) {
+            const bool s1 = it >= b.v[11];
+            const int u = s1 ? it - b.v[11] : it;
+            const int row = udiv(u, nq, (unsigned)b.v[13]);
+            const int xq = u - row * nq;
+            const int z = udiv(row, ny, (unsigned)b.v[14]);
+            const int y = row - z * ny;
+            const int gx = (s1 ? b.v[3] : b.v[0]) + 4 * xq;
+            const int gy = wrap_idx((s1 ? b.v[4] : b.v[1]) + y, vdim);
+            const int gz = wrap_idx((s1 ? b.v[5] : b.v[2]) + z, vdim);
+            const unsigned g = ((unsigned)gz * vdim + gy) * nColFT + gx;
+            if (!CELLS && gx + 3 < nColFT) {
+                const f32x4u* p = reinterpret_cast<const f32x4u*>(vol + g);
+                const f32x4u lo = p[0], hi = p[1];
+                pre[j][0] = f32x4{lo.x, lo.y, lo.z, lo.w};
+                pre[j][1] = f32x4{hi.x, hi.y, hi.z, hi.w};
+                continue;
+            }
+            float2 e[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                e[k] = make_float2(0.f, 0.f);
+                if (gx + k < nColFT) {
+                    if (CELLS) {
+                        const float4 q = reinterpret_cast<const float4*>(vol)[(size_t)(g + k) * 4];
+                        e[k] = make_float2(q.x, q.y);
+                    } else {
+                        e[k] = vol[g + k];
+                    }
+                }
+            }
+            pre[j][0] = f32x4{e[0].x, e[0].y, e[1].x, e[1].y};
+            pre[j][1] = f32x4{e[2].x, e[2].y, e[3].x, e[3].y};
+        }
+    }
+}
+
+// interp_ft (common.h) with the taps read from the staged boxes.
+THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int nxy, int off0, int off1,
+                          float x, float y, float z)
+{
+    const bool conj = !(x >= 0.f);
+    if (conj) { x = -x; y = -y; z = -z; }
+    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+    const float dx = x - fx, dy = y - fy, dz = z - fz;
+    const float vx[2] = {1.f - dx, dx};
+    const float vy[2] = {1.f - dy, dy};
+    const float vz[2] = {1.f - dz, dz};
+    const int a = z0 * nxy + y0 * nx + x0 + (conj ? off1 : off0);
+    const float2 a0 = box[a], a1 = box[a + 1];
+    const float2 b0 = box[a + nx], b1 = box[a + nx + 1];
+    const float2 c0 = box[a + nxy], c1 = box[a + nxy + 1];
+    const float2 d0 = box[a + nxy + nx], d1 = box[a + nxy + nx + 1];
+    float re, im, w;
+    w = vx[0] * vy[0] * vz[0]; re = a0.x * w; im = a0.y * w;
+    w = vx[1] * vy[0] * vz[0]; re += a1.x * w; im += a1.y * w;
+    w = vx[0] * vy[1] * vz[0]; re += b0.x * w; im += b0.y * w;
+    w = vx[1] * vy[1] * vz[0]; re += b1.x * w; im += b1.y * w;
+    w = vx[0] * vy[0] * vz[1]; re += c0.x * w; im += c0.y * w;
+    w = vx[1] * vy[0] * vz[1]; re += c1.x * w; im += c1.y * w;
+    w = vx[0] * vy[1] * vz[1]; re += d0.x * w; im += d0.y * w;
+    w = vx[1] * vy[1] * vz[1]; re += d1.x * w; im += d1.y * w;
+    return make_float2(re, conj ? -im : im);
+}
+
+template <bool CELLS>
+__global__ void __launch_bounds__(THREADS, 2) k_local_fused(const float2* __restrict__ vol,
+                                                            int vdim, int pf,
+                                                            const double* __restrict__ quat,
+                                                            int nR,
+                                                            const double* __restrict__ trans,
+                                                            int nT,
+                                                            const float2* __restrict__ dat,
+                                                            const float* __restrict__ ctf,
+                                                            const float* __restrict__ sig,
+                                                            const int* __restrict__ iCol,
+                                                            const int* __restrict__ iRow,
+                                                            const int* __restrict__ order,
+                                                            int nVisit, int nPxl, int idim,
+                                                            const int* __restrict__ rec,
+                                                            float* __restrict__ dvp)
 {
     const int l = blockIdx.x, r0 = blockIdx.y * RT, t0 = blockIdx.z * TT;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    __shared__ double sMat[RT][6];
+    const int nRl = min(RT, nR - r0);
+    __shared__ __attribute__((aligned(16))) float2 sBox[BOX_CAP];
+    __shared__ __attribute__((aligned(16))) float sB[KC * 2 * TT];   // [px][U, V][t]
+    __shared__ __attribute__((aligned(16))) double2 sXY[KC];        // (iCol pf, iRow pf)
+    __shared__ float sBq[KC];                                        // b = s c^2
     __shared__ float sTr[TT][2];
-    __shared__ __attribute__((aligned(16))) float2 sA[RT * APITCH];      // [r][px]
-    __shared__ __attribute__((aligned(16))) float sB[KC * 4 * TT];       // [px][k][t]
-    __shared__ float sRed[THREADS / 64];
+    __shared__ float sRed[NWAVE];
+    __shared__ float sBias[RT];
 
-    if (tid < RT) {
-        const int r = r0 + tid;
-        double q[4] = {1, 0, 0, 0};
-        if (r < nR)
-            for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
-        double m[9];
-        quat_to_mat(q, m);
-        for (int k = 0; k < 6; k++) sMat[tid][k] = m[k];
+    // this lane's rotation (rows past nR reuse the tile's first rotation, so
+    // their taps stay inside the staged box; those rows are never stored)
+    const int rl = wv * 16 + (lane & 15);
+    double m[6];
+    {
+        const int r = r0 + (rl < nRl ? rl : 0);
+        double q[4], mm[9];
+        for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
+        quat_to_mat(q, mm);
+        for (int k = 0; k < 6; k++) m[k] = mm[k];
     }
     if (tid < TT) {
         const int t = t0 + tid;
@@ -102,91 +399,122 @@ __global__ void __launch_bounds__(THREADS) k_local_fused(const float2* __restric
     const float2* D = dat + (size_t)l * nPxl;
     const float* C = ctf + (size_t)l * nPxl;
     const float* S = sig + (size_t)l * nPxl;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    float aConst = 0.f;
-    // gather mapping: a half-wave covers 32 consecutive pixels of one rotation
-    // (neighbouring pixels hit neighbouring cells of the same slice)
-    const int gpx = lane & 31, grq = lane >> 5;
-    // MFMA mapping: wave wv owns M-tiles 2wv, 2wv+1 (32 rotations)
-    const int mm = lane & 15, kk = lane >> 4;
+    const int nC = (nVisit + KC - 1) / KC;
+    const int* R = rec + ((size_t)l * gridDim.y + blockIdx.y) * nC * REC;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    float bias = 0.f, aConst = 0.f;
+    // image-tile element staged by threads tid < KC * TT
+    const bool stager = tid < KC * TT;
+    const int bpx = tid / TT, bt = tid % TT;
+    const int g = lane >> 4;       // pixel slot of this lane in a step
+    const int kk = lane >> 4, tc = lane & 15;   // B-operand row / column
+
+    // pipeline prologue: patch 0 data + box, patch 1 order entry + record
+    Pix px = load_pix(stager ? patch_pixel(order, nVisit, bpx) : -1, iCol, iRow, D, C, S);
+    int pNext = stager ? patch_pixel(order, nVisit, KC + bpx) : -1;
+    Rec rc = load_rec(R);
+    Rec rn = nC > 1 ? load_rec(R + REC) : rc;
+    f32x4 pre[NIT][2];
+    fetch_box<CELLS>(pre, rc, vol, vdim, tid);
 
     __syncthreads();
-    for (int i0 = 0; i0 < nPxl; i0 += KC) {
-        // ---- translation / image tile: B[px][0..3][t] = (U, V, b, 0)
+    for (int c = 0; c < nC; c++) {
+        // ---- stage patch c: box voxels, image tile B[px][U, V][t], b, (iCol, iRow) pf
+        if (rc.staged()) {
+            f32x4* box4 = reinterpret_cast<f32x4*>(sBox);
 #pragma unroll
-        for (int u = 0; u < KC * TT / THREADS; u++) {
-            const int q = tid + u * THREADS;
-            const int bpx = q / TT, bt = q % TT;
-            const int i = i0 + bpx;
-            float U = 0.f, V = 0.f, b = 0.f;
-            if (i < nPxl) {
-                const float2 d = D[i];
-                const float c = C[i], s = S[i];
-                const float k2 = -2.f * s * c;
-                const float yr = k2 * d.x, yi = k2 * d.y;
-                if (t0 + bt < nT) {
-                    const float2 T = phase_shift(iCol[i], iRow[i], sTr[bt][0], sTr[bt][1]);
-                    U = yr * T.x + yi * T.y;
-                    V = yi * T.x - yr * T.y;
-                    b = s * c * c;
+            for (int j = 0; j < NIT; j++) {
+                const int it = tid + j * THREADS;
+                if (it < rc.v[12]) {
+                    box4[2 * it] = pre[j][0];
+                    box4[2 * it + 1] = pre[j][1];
                 }
-                if (bt == 0) aConst += s * (d.x * d.x + d.y * d.y);
             }
-            float* B = sB + bpx * 4 * TT;
-            B[0 * TT + bt] = U;
-            B[1 * TT + bt] = V;
-            B[2 * TT + bt] = b;
-            B[3 * TT + bt] = 0.f;
         }
-        // ---- projection tile: A[px][r] = P (complex)
-        {
-            const int i = i0 + gpx;
-            const bool ok = i < nPxl;
-            const int ic = ok ? iCol[i] : 0, ir = ok ? iRow[i] : 0;
-            const double nx = (double)(ic * pf), ny = (double)(ir * pf);
-#pragma unroll 4
-            for (int p = 0; p < RT / 8; p++) {
-                const int r = wv * (RT / 4) + p * 2 + grq;
-                const double* m = sMat[r];
-                const float x = (float)(m[0] * nx + m[3] * ny);
-                const float y = (float)(m[1] * nx + m[4] * ny);
-                const float z = (float)(m[2] * nx + m[5] * ny);
-                float2 P = make_float2(0.f, 0.f);
-                if (ok)
-                    P = CELLS ? interp_cells(reinterpret_cast<const float4*>(vol), vdim, x, y, z)
-                              : interp_ft(vol, vdim, x, y, z);
-                sA[r * APITCH + gpx] = P;
+        if (stager) {
+            float U = 0.f, V = 0.f;
+            const bool ok = px.p >= 0;
+            if (ok && t0 + bt < nT) {
+                const float k2 = -2.f * px.s * px.c;
+                const float yr = k2 * px.d.x, yi = k2 * px.d.y;
+                const float2 T = phase_shift(px.ic, px.ir, sTr[bt][0], sTr[bt][1]);
+                U = yr * T.x + yi * T.y;
+                V = yi * T.x - yr * T.y;
+            }
+            sB[(bpx * 2) * TT + bt] = U;
+            sB[(bpx * 2 + 1) * TT + bt] = V;
+            if (bt == 0) {
+                if (ok) aConst += px.s * (px.d.x * px.d.x + px.d.y * px.d.y);
+                sBq[bpx] = ok ? px.s * px.c * px.c : 0.f;
+                // padding entries sample the patch's first pixel (inside the box)
+                const int ic = ok ? px.ic : rc.v[17], ir = ok ? px.ir : rc.v[18];
+                sXY[bpx] = make_double2((double)(ic * pf), (double)(ir * pf));
             }
         }
         __syncthreads();
-        // ---- reduce the chunk on the matrix cores: A row = (P.re, P.im, |P|^2, 0)
-#pragma unroll 8
-        for (int px = 0; px < KC; px++) {
-            const float bv = sB[(px * 4 + kk) * TT + mm];
-            const float2 p0 = sA[(wv * 32 + mm) * APITCH + px];
-            const float2 p1 = sA[(wv * 32 + 16 + mm) * APITCH + px];
-            const float a0 = kk == 0 ? p0.x : kk == 1 ? p0.y : kk == 2 ? p0.x * p0.x + p0.y * p0.y : 0.f;
-            const float a1 = kk == 0 ? p1.x : kk == 1 ? p1.y : kk == 2 ? p1.x * p1.x + p1.y * p1.y : 0.f;
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc1, 0, 0, 0);
+        // ---- prefetch patch c + 1 (in flight during the gathers below)
+        Rec r2 = rn;
+        if (c + 1 < nC) {
+            if (stager) {
+                px = load_pix(pNext, iCol, iRow, D, C, S);
+                pNext = patch_pixel(order, nVisit, (c + 2) * KC + bpx);
+            }
+            fetch_box<CELLS>(pre, rn, vol, vdim, tid);
+            if (c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
         }
+        // ---- projection samples: this lane's rotation x pixels 4s + g
+        float pre_[4], pim[4];
+        const bool staged = rc.staged();
+        const int nx = rc.v[6], nxy = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const int p = 4 * s + g;
+            const double2 xy = sXY[p];
+            const float x = (float)(m[0] * xy.x + m[3] * xy.y);
+            const float y = (float)(m[1] * xy.x + m[4] * xy.y);
+            const float z = (float)(m[2] * xy.x + m[5] * xy.y);
+            float2 P;
+            if (staged)
+                P = interp_box(sBox, nx, nxy, off0, off1, x, y, z);
+            else
+                P = CELLS ? interp_cells(reinterpret_cast<const float4*>(vol), vdim, x, y, z)
+                          : interp_ft(vol, vdim, x, y, z);
+            pre_[s] = P.x;
+            pim[s] = P.y;
+            bias += sBq[p] * (P.x * P.x + P.y * P.y);
+        }
+        // ---- reduce on the matrix cores: rows (re, im) of pixels 4s, 4s+2 and 4s+1, 4s+3
+#pragma unroll
+        for (int s = 0; s < 4; s++) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(pre_[s]),
+                                                             __float_as_uint(pim[s]), false, false);
+            const float a0 = __uint_as_float(sw[0]), a1 = __uint_as_float(sw[1]);
+            const int q0 = 4 * s + (kk < 2 ? 0 : 2), q1 = 4 * s + (kk < 2 ? 1 : 3);
+            const float b0 = sB[(q0 * 2 + (kk & 1)) * TT + tc];
+            const float b1 = sB[(q1 * 2 + (kk & 1)) * TT + tc];
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc, 0, 0, 0);
+        }
+        rc = rn;
+        rn = r2;
         __syncthreads();
     }
-    // A_l = sum_i s |d|^2 (only the bt == 0 threads accumulated)
+    // A_l = sum_i s |d|^2 (staging threads with bt == 0 accumulated it)
     aConst = wave_sum(aConst);
     if (lane == 0) sRed[wv] = aConst;
+    // B_r: the four pixel slots of a rotation are lanes l, l + 16, l + 32, l + 48
+    bias += __shfl_xor(bias, 16, 64);
+    bias += __shfl_xor(bias, 32, 64);
+    if (lane < 16) sBias[rl] = bias;
     __syncthreads();
-    const float Al = sRed[0] + sRed[1] + sRed[2] + sRed[3];
+    float Al = 0.f;
+    for (int k = 0; k < NWAVE; k++) Al += sRed[k];
     // C layout of 16x16x4: col = lane & 15 (translation), row = 4 (lane >> 4) + j
-    const int t = t0 + (lane & 15);
+    const int t = t0 + tc;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const int ra = r0 + wv * 32 + 4 * (lane >> 4) + j;
-        const int rb = ra + 16;
-        if (t < nT) {
-            if (ra < nR) dvp[((size_t)l * nR + ra) * nT + t] = Al + acc0[j];
-            if (rb < nR) dvp[((size_t)l * nR + rb) * nT + t] = Al + acc1[j];
-        }
+        const int rr = wv * 16 + 4 * kk + j;
+        if (t < nT && rr < nRl) dvp[((size_t)l * nR + r0 + rr) * nT + t] = Al + sBias[rr] + acc[j];
     }
 }
 
@@ -270,6 +598,13 @@ __global__ void __launch_bounds__(256) k_volume_cells(const float2* __restrict__
     }
 }
 
+size_t dvp_bytes(int nImg, int nR, int nT) { return (size_t)nImg * nR * nT * sizeof(float); }
+
+size_t rec_bytes(int nImg, int nR, int nVisit)
+{
+    return (size_t)nImg * thx::cdiv(nR, RT) * thx::cdiv(nVisit, KC) * REC * sizeof(int);
+}
+
 }  // namespace
 
 extern "C" int thx_volume_cells(const float* vol, int vdim, float* cells,
@@ -283,9 +618,9 @@ extern "C" int thx_volume_cells(const float* vol, int vdim, float* cells,
     return THX_OK;
 }
 
-extern "C" size_t thx_local_phase_workspace(int nImg, int nR, int nT)
+extern "C" size_t thx_local_phase_workspace(int nImg, int nR, int nT, int nVisit)
 {
-    return (size_t)nImg * nR * nT * sizeof(float) + 256;
+    return dvp_bytes(nImg, nR, nT) + rec_bytes(nImg, nR, nVisit) + 512;
 }
 
 extern "C" int thx_local_phase(const float* vol, int volLayout, int vdim, int pf,
@@ -293,8 +628,8 @@ extern "C" int thx_local_phase(const float* vol, int volLayout, int vdim, int pf
                                int nT, const double* pC, const double* pR,
                                const double* pT, const float* dat,
                                const float* ctf, const float* sigRcp,
-                               const int* iCol, const int* iRow, int nPxl,
-                               int idim, int nImg, float* wC, float* wR,
+                               const int* iCol, const int* iRow, const int* pxOrder,
+                               int nOrd, int nPxl, int idim, int nImg, float* wC, float* wR,
                                float* wT, float* baseL, float* dvp,
                                void* workspace, size_t wsBytes,
                                thx_stream_t stream)
@@ -304,25 +639,31 @@ extern "C" int thx_local_phase(const float* vol, int volLayout, int vdim, int pf
     THX_CHECK_ARG(volLayout == 0 || volLayout == 1, "thx_local_phase: volLayout must be 0 or 1");
     THX_CHECK_ARG(nImg <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 && (nT + TT - 1) / TT <= 65535,
                   "thx_local_phase: grid too large");
+    THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % KC == 0),
+                  "thx_local_phase: nOrd must be a positive multiple of 16 (thx_pixel_tile_order)");
     if (nImg == 0) return THX_OK;
-    float* d = dvp;
-    if (!d) {
-        THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase_workspace(nImg, nR, nT),
-                      "thx_local_phase: workspace too small");
-        d = static_cast<float*>(workspace);
-    }
+    const int nVisit = pxOrder ? nOrd : nPxl;
+    THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase_workspace(nImg, nR, nT, nVisit),
+                  "thx_local_phase: workspace too small");
+    thx::Carver ws(workspace, wsBytes);
+    float* d = dvp ? dvp : ws.take<float>((size_t)nImg * nR * nT);
+    int* rec = ws.take<int>(rec_bytes(nImg, nR, nVisit) / sizeof(int));
     hipStream_t s = thx::as_stream(stream);
+    const long nWaves = (long)nImg * thx::cdiv(nR, RT) * thx::cdiv(nVisit, KC);
+    hipLaunchKernelGGL(k_patch_boxes, dim3(thx::cdiv(nWaves, 4)), dim3(256), 0, s, quat, nR,
+                       iCol, iRow, pxOrder, nVisit, pf, vdim, nImg, rec);
+    THX_LAUNCH_CHECK();
     dim3 grid(nImg, thx::cdiv(nR, RT), thx::cdiv(nT, TT));
     if (volLayout == 1)
         hipLaunchKernelGGL(k_local_fused<true>, grid, dim3(THREADS), 0, s,
                            reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
-                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, nPxl,
-                           idim, d);
+                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
+                           nVisit, nPxl, idim, rec, d);
     else
         hipLaunchKernelGGL(k_local_fused<false>, grid, dim3(THREADS), 0, s,
                            reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
-                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, nPxl,
-                           idim, d);
+                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
+                           nVisit, nPxl, idim, rec, d);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_local_weights, dim3(nImg), dim3(256), 0, s, d, nR, nT, pC, pR, pT, wC,
                        wR, wT, baseL);

@@ -281,7 +281,7 @@ struct Plan {
     size_t bytes;
 };
 
-Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl)
+Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
 {
     thx::Carver k(base, ~size_t(0));
     Plan p;
@@ -307,7 +307,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl)
     p.wT = k.take<float>((size_t)nImg * c.mLT);
     p.base = k.take<float>(nImg);
     p.pC = k.take<double>(nImg);
-    p.localWsBytes = thx_local_phase_workspace(nImg, c.mLR, c.mLT);
+    p.localWsBytes = thx_local_phase_workspace(nImg, c.mLR, c.mLT, nVisit);
     p.localWs = k.take<char>(p.localWsBytes);
     p.bytes = k.off + 256;
     return p;
@@ -331,10 +331,11 @@ __global__ void k_fill(double* p, long n, double v)
 
 }  // namespace
 
-extern "C" size_t thx_expectation_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl)
+extern "C" size_t thx_expectation_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl,
+                                            int nOrd)
 {
     if (!cfg) return 0;
-    return plan(nullptr, *cfg, nImg, nPxl).bytes;
+    return plan(nullptr, *cfg, nImg, nPxl, nOrd > 0 ? nOrd : nPxl).bytes;
 }
 
 #define THX_RET(call)                  \
@@ -348,7 +349,8 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                                const double* gPR, const double* gPT,
                                const float* dat, const float* ctf,
                                const float* sigRcp, const int* iCol,
-                               const int* iRow, int nPxl, int nImg, double* quat,
+                               const int* iRow, const int* pxOrder, int nOrd, int nPxl, int nImg,
+                               double* quat,
                                double* trans, double* pR, double* pT,
                                float* score, void* workspace, size_t wsBytes,
                                thx_stream_t stream)
@@ -362,7 +364,9 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                   "thx_expectation: bad configuration");
     THX_CHECK_ARG(c.nR <= 65535, "thx_expectation: nR > 65535");
     if (nImg == 0) return THX_OK;
-    const Plan p = plan(workspace, c, nImg, nPxl);
+    THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % 16 == 0),
+                  "thx_expectation: nOrd must be a positive multiple of 16");
+    const Plan p = plan(workspace, c, nImg, nPxl, pxOrder ? nOrd : nPxl);
     THX_CHECK_ARG(workspace && p.bytes <= wsBytes, "thx_expectation: workspace too small");
     hipStream_t s = thx::as_stream(stream);
     const unsigned gImg = thx::cdiv(nImg, 4);
@@ -403,7 +407,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                            c.transS, c.transM, c.seed, (uint32_t)(2000 + phase));
         THX_LAUNCH_CHECK();
         THX_RET(thx_local_phase(vol, 0, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT, dat,
-                                ctf, sigRcp, iCol, iRow, nPxl, c.idim, nImg, p.wC, p.wR, p.wT,
+                                ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, c.idim, nImg, p.wC, p.wR, p.wT,
                                 p.base, nullptr, p.localWs, p.localWsBytes, stream));
         // resample R and T by the phase marginals; ancestors gathered in place
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, c.mLR, pR,

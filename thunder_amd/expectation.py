@@ -58,7 +58,8 @@ class Expectation:
         self.mLR, self.mLT = mLR, mLT
 
     def workspace_bytes(self, nImg):
-        return lib().thx_expectation_workspace(ctypes.byref(self.cfg), nImg, self.px.n)
+        return lib().thx_expectation_workspace(ctypes.byref(self.cfg), nImg, self.px.n,
+                                               len(self.px.order))
 
     def run(self, dat, ctf, sig, out=None):
         """Expectation of one image batch; returns (quat, trans, pR, pT, score) on device."""
@@ -80,7 +81,8 @@ class Expectation:
         P = ops._ptr
         check(lib().thx_expectation(ctypes.byref(self.cfg), P(self.vol), P(self.gQuat),
                                     P(self.gTrans), P(self.gPR), P(self.gPT), P(dat), P(ctf),
-                                    P(sig), P(self.px.d_iCol), P(self.px.d_iRow), nPxl, nImg,
+                                    P(sig), P(self.px.d_iCol), P(self.px.d_iRow),
+                                    P(self.px.d_order), len(self.px.order), nPxl, nImg,
                                     P(quat), P(trans), P(pR), P(pT), P(score), P(ws), ws.numel(),
                                     ops._stream(dev)), "thx_expectation")
         return out

@@ -60,10 +60,28 @@ class PixelSet:
         n = n.value
         self.idim, self.pf, self.rU, self.rL, self.n = idim, pf, rU, rL, n
         self.iCol, self.iRow, self.iSig, self.iPxl = (b[:n].copy() for b in bufs)
+        self.order = tile_order(self.iCol, self.iRow)
         self.device = device
         if device is not None:
             self.d_iCol = torch.from_numpy(self.iCol).to(device)
             self.d_iRow = torch.from_numpy(self.iRow).to(device)
+            self.d_order = torch.from_numpy(self.order).to(device)
+
+
+def tile_order(iCol, iRow):
+    """thx_pixel_tile_order: local-phase visiting order of a pixel set
+    (16-entry patches, -1 = padding)."""
+    iCol = np.ascontiguousarray(iCol, np.int32)
+    iRow = np.ascontiguousarray(iRow, np.int32)
+    n = ctypes.c_int(0)
+    vp = ctypes.c_void_p
+    check(lib().thx_pixel_tile_order(iCol.ctypes.data_as(vp), iRow.ctypes.data_as(vp), len(iCol),
+                                     0, None, ctypes.byref(n)), "thx_pixel_tile_order")
+    order = np.zeros(n.value, np.int32)
+    check(lib().thx_pixel_tile_order(iCol.ctypes.data_as(vp), iRow.ctypes.data_as(vp), len(iCol),
+                                     len(order), order.ctypes.data_as(vp), ctypes.byref(n)),
+          "thx_pixel_tile_order")
+    return order
 
 
 # ------------------------------------------------------------------- a2
@@ -181,8 +199,10 @@ def volume_cells(vol):
     return out
 
 
-def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False, cells=None):
-    """cells: optional thx_volume_cells copy of vol (used for the gathers)."""
+def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False, cells=None,
+                tiled=True):
+    """cells: optional thx_volume_cells copy of vol (used for the gathers).
+    tiled: visit pixels in px.order (LDS-staged neighbourhoods) instead of set order."""
     vdim = _vol_dim(vol)
     layout = 0
     if cells is not None:
@@ -203,13 +223,15 @@ def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False
     wT = torch.empty(nImg, nT, dtype=torch.float32, device=dev)
     base = torch.empty(nImg, dtype=torch.float32, device=dev)
     d = torch.empty(nImg, nR, nT, dtype=torch.float32, device=dev) if want_dvp else None
-    ws = workspace(lib().thx_local_phase_workspace(min(nImg, 65535), nR, nT), dev)
+    ws = workspace(lib().thx_local_phase_workspace(min(nImg, 65535), nR, nT,
+                                                   len(px.order) if tiled else nPxl), dev)
     for l0 in range(0, nImg, 65535):
         nb = min(65535, nImg - l0)
         check(lib().thx_local_phase(_ptr(cells if layout else vol), layout, vdim, px.pf, _ptr(quat[l0:]), nR, _ptr(trans[l0:]),
                                     nT, _ptr(pC[l0:]), _ptr(pR[l0:]), _ptr(pT[l0:]), _ptr(dat[l0:]),
                                     _ptr(ctf_[l0:]), _ptr(sig[l0:]), _ptr(px.d_iCol),
-                                    _ptr(px.d_iRow), nPxl, px.idim, nb, _ptr(wC[l0:]),
+                                    _ptr(px.d_iRow), _ptr(px.d_order) if tiled else None,
+                                    len(px.order), nPxl, px.idim, nb, _ptr(wC[l0:]),
                                     _ptr(wR[l0:]), _ptr(wT[l0:]), _ptr(base[l0:]),
                                     _ptr(d[l0:]) if d is not None else None, _ptr(ws),
                                     ws.numel(), _stream(dev)), "thx_local_phase")

@@ -58,6 +58,20 @@ def uniform_quaternions(n, rng):
     return q
 
 
+def clustered_quaternions(n_img, n_r, spread_deg, rng):
+    """Particle clouds [n_img, n_r, 4]: every image's rotations are small
+    perturbations (per-axis std ~ spread_deg) of one uniform pose."""
+    base = uniform_quaternions(n_img, rng)
+    d = rng.standard_normal((n_img, n_r, 4)) * np.radians(spread_deg) / 2
+    d[..., 0] = 1.0
+    d /= np.linalg.norm(d, axis=-1, keepdims=True)
+    w0, x0, y0, z0 = [base[:, None, k] for k in range(4)]
+    w1, x1, y1, z1 = [d[..., k] for k in range(4)]
+    return np.ascontiguousarray(np.stack(
+        [w0 * w1 - x0 * x1 - y0 * y1 - z0 * z1, w0 * x1 + x0 * w1 + y0 * z1 - z0 * y1,
+         w0 * y1 - x0 * z1 + y0 * w1 + z0 * x1, w0 * z1 + x0 * y1 - y0 * x1 + z0 * w1], -1))
+
+
 def global_sample_set(nR, trans_s=10.0, trans_search_factor=0.25, seed=2):
     """(quat [nR,4], trans [nT,2], pR [nR], pT [nT]) of Particle::reset for 3D, C1."""
     rng = np.random.default_rng(seed)

@@ -31,7 +31,8 @@ def main():
     p.add_argument("--nr", type=int, default=2000)
     p.add_argument("--mreco", type=int, default=100)
     p.add_argument("--reps", type=int, default=5)
-    p.add_argument("--tile", type=int, default=0, help="local: 2D pixel tile order (0 = reference order)")
+    p.add_argument("--tiled", type=int, default=1,
+                   help="local: 1 = tile visiting order (LDS-staged patches), 0 = set order")
     p.add_argument("--spread", type=float, default=3.0,
                    help="local: rotation spread (deg) of each image's cloud, 0 = uniform")
     a = p.parse_args()
@@ -45,14 +46,7 @@ def main():
     if a.what == "local":
         mR, mT = 125, 9
         if a.spread > 0:   # particle clouds: perturbations of one pose per image
-            base = synth.uniform_quaternions(a.images, rng)
-            d = rng.standard_normal((a.images, mR, 4)) * np.radians(a.spread) / 2
-            d[..., 0] = 1.0
-            d /= np.linalg.norm(d, axis=-1, keepdims=True)
-            w0, x0, y0, z0 = [base[:, None, k] for k in range(4)]
-            w1, x1, y1, z1 = [d[..., k] for k in range(4)]
-            q = np.stack([w0 * w1 - x0 * x1 - y0 * y1 - z0 * z1, w0 * x1 + x0 * w1 + y0 * z1 - z0 * y1,
-                          w0 * y1 - x0 * z1 + y0 * w1 + z0 * x1, w0 * z1 + x0 * y1 - y0 * x1 + z0 * w1], -1)
+            q = synth.clustered_quaternions(a.images, mR, a.spread, rng)
         else:
             q = synth.uniform_quaternions(a.images * mR, rng).reshape(a.images, mR, 4)
         quat = torch.as_tensor(np.ascontiguousarray(q), device=dev)
@@ -61,17 +55,8 @@ def main():
         pR = torch.full((a.images, mR), 1.0 / mR, dtype=torch.float64, device=dev)
         pT = torch.full((a.images, mT), 1.0 / mT, dtype=torch.float64, device=dev)
         cells = ops.volume_cells(vol) if a.cells else None
-        if a.tile > 0:     # pixels in 2D tiles of tile x tile (row-major inside a tile)
-            key = (px.iRow // a.tile + 1000) * 100000 + (px.iCol // a.tile) * 1000 + \
-                  (px.iRow % a.tile) * a.tile + px.iCol % a.tile
-            perm = np.argsort(key, kind="stable")
-            px.iCol, px.iRow = px.iCol[perm].copy(), px.iRow[perm].copy()
-            px.d_iCol = torch.from_numpy(px.iCol).to(dev)
-            px.d_iRow = torch.from_numpy(px.iRow).to(dev)
-            pt = torch.from_numpy(perm).to(dev)
-            dat, ctf, sig = (x[:, pt].contiguous() for x in (dat, ctf, sig))
         sec = timed_events(lambda: ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px,
-                                                   cells=cells), a.reps, st)
+                                                   cells=cells, tiled=bool(a.tiled)), a.reps, st)
         out.update(ms=sec * 1e3, us_per_image_phase=sec / a.images * 1e6,
                    algo_GBps=a.images * (64.0 * mR * px.n + 16.0 * px.n) / sec / 1e9)
     elif a.what == "scan":
