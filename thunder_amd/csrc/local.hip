@@ -87,10 +87,10 @@ THX_DEV float2 interp_cells(const float4* __restrict__ cells, int vdim, float x,
 // folded (x >= 0) coordinates, side 0 for samples with x >= 0, side 1 for the
 // folded ones, each stored [z][y][x] in LDS (rows padded to 4 voxels):
 //   [0..2] side-0 origin (x, y, z; rows / slices signed, unwrapped)
-//   [3..5] side-1 origin  [6] row pitch nx  [7] nx*ny  [8] ny
+//   [3..5] side-1 origin  [6] row pitch nx  [7] slice pitch sp  [8] ny
 //   [9] side-0 voxels (= LDS offset of side 1)  [10] total voxels
 //   (> BOX_CAP: the patch is gathered from the volume)
-//   [11] side-0 items (4 voxels = 32 B)  [12] total items
+//   [11] side-0 items (4 voxels = 32 B of a row)  [12] total items
 //   [13] magic(nx / 4)  [14] magic(ny)  (udiv)
 //   [15] / [16] LDS index of voxel (0, 0, 0) for side 0 / 1 (may be negative)
 //   [17], [18] (iCol, iRow) of the patch's first pixel (stand-in for padding)
@@ -222,16 +222,24 @@ __global__ void __launch_bounds__(256) k_patch_boxes(const double* __restrict__ 
                 ny = max(ny, n[s][1]);
                 nz = max(nz, n[s][2]);
             }
-        const long nxy = (long)nx * ny, nv = nxy * nz;
+        // LDS bank spread: the 16 lanes of a ds_read2_b64 group read 8-B voxels
+        // whose index mod 16 picks the bank pair; a row pitch of 4 x odd and a
+        // slice pitch = 2 mod 16 keep the neighbouring rows / slices that the
+        // 16 rotations of one pixel touch on different banks
+        if ((nx / 4) % 2 == 0) nx += 4;
+        long sp = (long)nx * ny;
+        sp += ((2 - sp % 16) + 16) % 16;
+        const long nv = sp * nz;
         const long nv0 = any[0] ? nv : 0, nv1 = any[1] ? nv : 0;
+        const long ni = (long)(nx / 4) * ny * nz;
         for (int s = 0; s < 3; s++) { o[s] = lo[0][s]; o[3 + s] = lo[1][s]; }
         o[6] = nx;
-        o[7] = (int)min(nxy, (long)BIG);
+        o[7] = (int)min(sp, (long)BIG);
         o[8] = ny;
         o[9] = (int)min(nv0, (long)BIG);
         o[10] = (int)min(nv0 + nv1, (long)BIG);
-        o[11] = (int)min(nv0 / 4, (long)BIG);
-        o[12] = (int)min((nv0 + nv1) / 4, (long)BIG);
+        o[11] = (int)min(any[0] ? ni : 0, (long)BIG);
+        o[12] = (int)min((any[0] ? ni : 0) + (any[1] ? ni : 0), (long)BIG);
         o[13] = (int)magic((unsigned)nx / 4);
         o[14] = (int)magic((unsigned)ny);
         if (nv0 + nv1 <= BOX_CAP) {
@@ -269,10 +277,10 @@ THX_DEV Pix load_pix(int p, const int* __restrict__ iCol, const int* __restrict_
 }
 
 // The items (4 consecutive voxels of a box row, 32 B) of a staged patch this
-// thread moves: item it = tid + j THREADS lands at LDS voxel 4 it.
+// thread moves: item it = tid + j THREADS, LDS voxel dst[j].
 template <bool CELLS>
-THX_DEV void fetch_box(f32x4 (&pre)[NIT][2], const Rec& b, const float2* __restrict__ vol,
-                       int vdim, int tid)
+THX_DEV void fetch_box(f32x4 (&pre)[NIT][2], int (&dst)[NIT], const Rec& b,
+                       const float2* __restrict__ vol, int vdim, int tid)
 {
     if (!b.staged()) return;
     const int nColFT = vdim / 2 + 1;
@@ -287,6 +295,7 @@ THX_DEV void fetch_box(f32x4 (&pre)[NIT][2], const Rec& b, const float2* __restr
             const int xq = u - row * nq;
             const int z = udiv(row, ny, (unsigned)b.v[14]);
             const int y = row - z * ny;
+            dst[j] = (s1 ? b.v[9] : 0) + z * b.v[7] + y * b.v[6] + 4 * xq;
             const int gx = (s1 ? b.v[3] : b.v[0]) + 4 * xq;
             const int gy = wrap_idx((s1 ? b.v[4] : b.v[1]) + y, vdim);
             const int gz = wrap_idx((s1 ? b.v[5] : b.v[2]) + z, vdim);
@@ -317,8 +326,13 @@ THX_DEV void fetch_box(f32x4 (&pre)[NIT][2], const Rec& b, const float2* __restr
     }
 }
 
-// interp_ft (common.h) with the taps read from the staged boxes.
-THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int nxy, int off0, int off1,
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Trilinear gather of getByInterpolationFT (the taps and weights of
+// interp_ft, common.h) from the staged boxes, on packed FP32: the weights are
+// vx (vy vz) and (re, im) accumulates with v_pk_fma_f32 -- fused, so it can
+// differ from interp_ft in the last bits.
+THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int sp, int off0, int off1,
                           float x, float y, float z)
 {
     const bool conj = !(x >= 0.f);
@@ -326,24 +340,25 @@ THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int nxy, int o
     const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
     const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
     const float dx = x - fx, dy = y - fy, dz = z - fz;
-    const float vx[2] = {1.f - dx, dx};
-    const float vy[2] = {1.f - dy, dy};
-    const float vz[2] = {1.f - dz, dz};
-    const int a = z0 * nxy + y0 * nx + x0 + (conj ? off1 : off0);
-    const float2 a0 = box[a], a1 = box[a + 1];
-    const float2 b0 = box[a + nx], b1 = box[a + nx + 1];
-    const float2 c0 = box[a + nxy], c1 = box[a + nxy + 1];
-    const float2 d0 = box[a + nxy + nx], d1 = box[a + nxy + nx + 1];
-    float re, im, w;
-    w = vx[0] * vy[0] * vz[0]; re = a0.x * w; im = a0.y * w;
-    w = vx[1] * vy[0] * vz[0]; re += a1.x * w; im += a1.y * w;
-    w = vx[0] * vy[1] * vz[0]; re += b0.x * w; im += b0.y * w;
-    w = vx[1] * vy[1] * vz[0]; re += b1.x * w; im += b1.y * w;
-    w = vx[0] * vy[0] * vz[1]; re += c0.x * w; im += c0.y * w;
-    w = vx[1] * vy[0] * vz[1]; re += c1.x * w; im += c1.y * w;
-    w = vx[0] * vy[1] * vz[1]; re += d0.x * w; im += d0.y * w;
-    w = vx[1] * vy[1] * vz[1]; re += d1.x * w; im += d1.y * w;
-    return make_float2(re, conj ? -im : im);
+    const f32x2 vx = {1.f - dx, dx};
+    const float vy0 = 1.f - dy, vz0 = 1.f - dz;
+    const int a = z0 * sp + y0 * nx + x0 + (conj ? off1 : off0);
+    const f32x2* bx = reinterpret_cast<const f32x2*>(box);
+    const f32x2 a0 = bx[a], a1 = bx[a + 1];
+    const f32x2 b0 = bx[a + nx], b1 = bx[a + nx + 1];
+    const f32x2 c0 = bx[a + sp], c1 = bx[a + sp + 1];
+    const f32x2 d0 = bx[a + sp + nx], d1 = bx[a + sp + nx + 1];
+    const f32x2 w00 = vx * (vy0 * vz0), w10 = vx * (dy * vz0);
+    const f32x2 w01 = vx * (vy0 * dz), w11 = vx * (dy * dz);
+    f32x2 s = a0 * w00.x;
+    s = __builtin_elementwise_fma(a1, (f32x2)w00.y, s);
+    s = __builtin_elementwise_fma(b0, (f32x2)w10.x, s);
+    s = __builtin_elementwise_fma(b1, (f32x2)w10.y, s);
+    s = __builtin_elementwise_fma(c0, (f32x2)w01.x, s);
+    s = __builtin_elementwise_fma(c1, (f32x2)w01.y, s);
+    s = __builtin_elementwise_fma(d0, (f32x2)w11.x, s);
+    s = __builtin_elementwise_fma(d1, (f32x2)w11.y, s);
+    return make_float2(s.x, conj ? -s.y : s.y);
 }
 
 template <bool CELLS>
@@ -415,7 +430,8 @@ __global__ void __launch_bounds__(THREADS, 2) k_local_fused(const float2* __rest
     Rec rc = load_rec(R);
     Rec rn = nC > 1 ? load_rec(R + REC) : rc;
     f32x4 pre[NIT][2];
-    fetch_box<CELLS>(pre, rc, vol, vdim, tid);
+    int dst[NIT];
+    fetch_box<CELLS>(pre, dst, rc, vol, vdim, tid);
 
     __syncthreads();
     for (int c = 0; c < nC; c++) {
@@ -426,8 +442,8 @@ __global__ void __launch_bounds__(THREADS, 2) k_local_fused(const float2* __rest
             for (int j = 0; j < NIT; j++) {
                 const int it = tid + j * THREADS;
                 if (it < rc.v[12]) {
-                    box4[2 * it] = pre[j][0];
-                    box4[2 * it + 1] = pre[j][1];
+                    box4[dst[j] / 2] = pre[j][0];
+                    box4[dst[j] / 2 + 1] = pre[j][1];
                 }
             }
         }
@@ -459,13 +475,13 @@ __global__ void __launch_bounds__(THREADS, 2) k_local_fused(const float2* __rest
                 px = load_pix(pNext, iCol, iRow, D, C, S);
                 pNext = patch_pixel(order, nVisit, (c + 2) * KC + bpx);
             }
-            fetch_box<CELLS>(pre, rn, vol, vdim, tid);
+            fetch_box<CELLS>(pre, dst, rn, vol, vdim, tid);
             if (c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
         }
         // ---- projection samples: this lane's rotation x pixels 4s + g
         float pre_[4], pim[4];
         const bool staged = rc.staged();
-        const int nx = rc.v[6], nxy = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
+        const int nx = rc.v[6], sp = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
 #pragma unroll
         for (int s = 0; s < 4; s++) {
             const int p = 4 * s + g;
@@ -475,7 +491,7 @@ __global__ void __launch_bounds__(THREADS, 2) k_local_fused(const float2* __rest
             const float z = (float)(m[2] * xy.x + m[5] * xy.y);
             float2 P;
             if (staged)
-                P = interp_box(sBox, nx, nxy, off0, off1, x, y, z);
+                P = interp_box(sBox, nx, sp, off0, off1, x, y, z);
             else
                 P = CELLS ? interp_cells(reinterpret_cast<const float4*>(vol), vdim, x, y, z)
                           : interp_ft(vol, vdim, x, y, z);
