@@ -136,121 +136,154 @@ THX_DEV int patch_pixel(const int* __restrict__ order, int nVisit, int k)
     return k < nVisit ? (order ? order[k] : k) : -1;
 }
 
-// One wave per (image, rotation tile, patch): the LDS boxes that hold every
-// tap of the patch's samples under the tile's rotations.
-__global__ void __launch_bounds__(256) k_patch_boxes(const double* __restrict__ quat, int nR,
-                                                     const int* __restrict__ iCol,
-                                                     const int* __restrict__ iRow,
-                                                     const int* __restrict__ order,
-                                                     int nVisit, int pf, int vdim, int nImg,
-                                                     int* __restrict__ rec)
+// The patch record from the folded-box bounds e (side 0 lo xyz, hi xyz; side 1).
+THX_DEV void store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __restrict__ out)
 {
-    const int nC = (nVisit + KC - 1) / KC, nRT = (nR + RT - 1) / RT;
-    const long w = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (w >= (long)nImg * nRT * nC) return;
-    const int lane = threadIdx.x & 63;
-    const int c = (int)(w % nC);
-    const long lr = w / nC;
-    const int ry = (int)(lr % nRT), l = (int)(lr / nRT);
-    const int p = lane < KC ? patch_pixel(order, nVisit, c * KC + lane) : -1;
-    const int ic = p >= 0 ? iCol[p] : 0, ir = p >= 0 ? iRow[p] : 0;
-    const int cLo = wave_min_i(p >= 0 ? ic : BIG), cHi = wave_max_i(p >= 0 ? ic : -BIG);
-    const int rLo = wave_min_i(p >= 0 ? ir : BIG), rHi = wave_max_i(p >= 0 ? ir : -BIG);
-    const int ic0 = __builtin_amdgcn_readfirstlane(ic), ir0 = __builtin_amdgcn_readfirstlane(ir);
-    // e[0..5]: side 0 lo xyz, hi xyz; e[6..11]: side 1
-    int e[12];
-#pragma unroll
-    for (int k = 0; k < 12; k++) e[k] = (k % 6) < 3 ? BIG : -BIG;
-    if (cLo <= cHi) {
-#pragma unroll
-        for (int h = 0; h < (RT + 63) / 64; h++) {
-            const int r = ry * RT + h * 64 + lane;
-            if (h * 64 + lane >= RT || r >= nR) continue;
-            double q[4], m[9];
-            for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
-            quat_to_mat(q, m);
-            float mn[3] = {INFINITY, INFINITY, INFINITY};
-            float mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                float x[3];
-                rot_coord(m, (k & 1) ? cHi : cLo, (k & 2) ? rHi : rLo, pf, x[0], x[1], x[2]);
-#pragma unroll
-                for (int a = 0; a < 3; a++) { mn[a] = fminf(mn[a], x[a]); mx[a] = fmaxf(mx[a], x[a]); }
-            }
-            // every rotated patch point lies in the corner hull; a 1-voxel margin
-            // on each side absorbs the FP32 rounding of the coordinates
-            if (mx[0] >= -1e-3f) {
-                e[0] = min(e[0], (int)floorf(fmaxf(mn[0], 0.f)) - 1);
-                e[1] = min(e[1], (int)floorf(mn[1]) - 1);
-                e[2] = min(e[2], (int)floorf(mn[2]) - 1);
-                e[3] = max(e[3], (int)floorf(mx[0]) + 2);
-                e[4] = max(e[4], (int)floorf(mx[1]) + 2);
-                e[5] = max(e[5], (int)floorf(mx[2]) + 2);
-            }
-            if (mn[0] < 1e-3f) {
-                e[6] = min(e[6], (int)floorf(fmaxf(-mx[0], 0.f)) - 1);
-                e[7] = min(e[7], (int)floorf(-mx[1]) - 1);
-                e[8] = min(e[8], (int)floorf(-mx[2]) - 1);
-                e[9] = max(e[9], (int)floorf(-mn[0]) + 2);
-                e[10] = max(e[10], (int)floorf(-mn[1]) + 2);
-                e[11] = max(e[11], (int)floorf(-mn[2]) + 2);
-            }
-        }
+    const int nColFT = vdim / 2 + 1, half = vdim / 2;
+    int o[REC] = {0};
+    int lo[2][3], n[2][3];
+    bool any[2];
+    for (int s = 0; s < 2; s++) {
+        // clamp into the half volume (rows / slices wrap once at most)
+        lo[s][0] = max(e[6 * s], 0);
+        lo[s][1] = max(e[6 * s + 1], -half);
+        lo[s][2] = max(e[6 * s + 2], -half);
+        n[s][0] = min(e[6 * s + 3], nColFT - 1) - lo[s][0] + 1;
+        n[s][1] = min(e[6 * s + 4], half) - lo[s][1] + 1;
+        n[s][2] = min(e[6 * s + 5], half) - lo[s][2] + 1;
+        any[s] = n[s][0] > 0 && n[s][1] > 0 && n[s][2] > 0;
     }
+    int nx = 4, ny = 1, nz = 1;
+    for (int s = 0; s < 2; s++)
+        if (any[s]) {
+            nx = max(nx, (n[s][0] + 3) & ~3);   // rows padded to 4 voxels (32 B)
+            ny = max(ny, n[s][1]);
+            nz = max(nz, n[s][2]);
+        }
+    // LDS bank spread: the 16 lanes of a ds_read2_b64 group read 8-B voxels
+    // whose index mod 16 picks the bank pair; a row pitch of 4 x odd and a
+    // slice pitch = 2 mod 16 keep the neighbouring rows / slices that the 16
+    // rotations of one pixel touch on different banks
+    if ((nx / 4) % 2 == 0) nx += 4;
+    long sp = (long)nx * ny;
+    sp += ((2 - sp % 16) + 16) % 16;
+    const long nv = sp * nz;
+    const long nv0 = any[0] ? nv : 0, nv1 = any[1] ? nv : 0;
+    const long ni = (long)(nx / 4) * ny * nz;
+    for (int s = 0; s < 3; s++) { o[s] = lo[0][s]; o[3 + s] = lo[1][s]; }
+    o[6] = nx;
+    o[7] = (int)min(sp, (long)BIG);
+    o[8] = ny;
+    o[9] = (int)min(nv0, (long)BIG);
+    o[10] = (int)min(nv0 + nv1, (long)BIG);
+    o[11] = (int)min(any[0] ? ni : 0, (long)BIG);
+    o[12] = (int)min((any[0] ? ni : 0) + (any[1] ? ni : 0), (long)BIG);
+    o[13] = (int)magic((unsigned)nx / 4);
+    o[14] = (int)magic((unsigned)ny);
+    if (nv0 + nv1 <= BOX_CAP) {
+        o[15] = -(lo[0][2] * o[7] + lo[0][1] * nx + lo[0][0]);
+        o[16] = o[9] - (lo[1][2] * o[7] + lo[1][1] * nx + lo[1][0]);
+    }
+    o[17] = ic0;
+    o[18] = ir0;
+    int4* dst = reinterpret_cast<int4*>(out);
+    for (int k = 0; k < REC / 4; k++)
+        dst[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+}
+
+// One workgroup per (image, rotation tile), one lane per patch, the tile's
+// rotations split over the 4 waves: the LDS boxes that hold every tap of the
+// patch's samples under the tile's rotations.  The matrices sit in LDS and
+// are read as broadcasts; per rotation and axis the extremes of the rotated
+// patch rectangle are its corners picked by the signs of the two matrix
+// entries.  The waves' partial bounds meet in LDS.
+constexpr int PB_WAVES = 4;
+
+__global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __restrict__ quat,
+                                                               int nR,
+                                                               const int* __restrict__ iCol,
+                                                               const int* __restrict__ iRow,
+                                                               const int* __restrict__ order,
+                                                               int nVisit, int pf, int vdim,
+                                                               int* __restrict__ rec)
+{
+    __shared__ float sM[RT][6];
+    __shared__ int sE[PB_WAVES][12][64];
+    const int nC = (nVisit + KC - 1) / KC, nRT = (nR + RT - 1) / RT;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ry = blockIdx.x % nRT, l = blockIdx.x / nRT;
+    const int nRl = min(RT, nR - ry * RT);
+    for (int k = threadIdx.x; k < nRl; k += 64 * PB_WAVES) {
+        double q[4], m[9];
+        for (int a = 0; a < 4; a++) q[a] = quat[((size_t)l * nR + ry * RT + k) * 4 + a];
+        quat_to_mat(q, m);
+        for (int a = 0; a < 6; a++) sM[k][a] = (float)m[a];
+    }
+    __syncthreads();
+    const int rPer = (nRl + PB_WAVES - 1) / PB_WAVES;
+    const int rBeg = wv * rPer, rEnd = min(nRl, rBeg + rPer);
+    for (int c0 = 0; c0 < nC; c0 += 64) {
+        const int c = c0 + lane;
+        int cLo = BIG, cHi = -BIG, rLo = BIG, rHi = -BIG, ic0 = 0, ir0 = 0;
+        int pk[KC];
 #pragma unroll
-    for (int k = 0; k < 12; k++) e[k] = (k % 6) < 3 ? wave_min_i(e[k]) : wave_max_i(e[k]);
-    if (lane == 0) {
-        const int nColFT = vdim / 2 + 1, half = vdim / 2;
-        int o[REC] = {0};
-        int lo[2][3], n[2][3];
-        bool any[2];
-        for (int s = 0; s < 2; s++) {
-            // clamp into the half volume (rows / slices wrap once at most)
-            lo[s][0] = max(e[6 * s], 0);
-            lo[s][1] = max(e[6 * s + 1], -half);
-            lo[s][2] = max(e[6 * s + 2], -half);
-            n[s][0] = min(e[6 * s + 3], nColFT - 1) - lo[s][0] + 1;
-            n[s][1] = min(e[6 * s + 4], half) - lo[s][1] + 1;
-            n[s][2] = min(e[6 * s + 5], half) - lo[s][2] + 1;
-            any[s] = n[s][0] > 0 && n[s][1] > 0 && n[s][2] > 0;
-        }
-        int nx = 4, ny = 1, nz = 1;
-        for (int s = 0; s < 2; s++)
-            if (any[s]) {
-                nx = max(nx, (n[s][0] + 3) & ~3);   // rows padded to 4 voxels (32 B)
-                ny = max(ny, n[s][1]);
-                nz = max(nz, n[s][2]);
+        for (int k = 0; k < KC; k++) pk[k] = patch_pixel(order, nVisit, c * KC + k);
+#pragma unroll
+        for (int k = KC - 1; k >= 0; k--) {
+            const int ic = iCol[max(pk[k], 0)], ir = iRow[max(pk[k], 0)];   // loads in flight together
+            if (pk[k] >= 0) {
+                cLo = min(cLo, ic); cHi = max(cHi, ic);
+                rLo = min(rLo, ir); rHi = max(rHi, ir);
+                ic0 = ic; ir0 = ir;          // ends on the patch's first pixel
             }
-        // LDS bank spread: the 16 lanes of a ds_read2_b64 group read 8-B voxels
-        // whose index mod 16 picks the bank pair; a row pitch of 4 x odd and a
-        // slice pitch = 2 mod 16 keep the neighbouring rows / slices that the
-        // 16 rotations of one pixel touch on different banks
-        if ((nx / 4) % 2 == 0) nx += 4;
-        long sp = (long)nx * ny;
-        sp += ((2 - sp % 16) + 16) % 16;
-        const long nv = sp * nz;
-        const long nv0 = any[0] ? nv : 0, nv1 = any[1] ? nv : 0;
-        const long ni = (long)(nx / 4) * ny * nz;
-        for (int s = 0; s < 3; s++) { o[s] = lo[0][s]; o[3 + s] = lo[1][s]; }
-        o[6] = nx;
-        o[7] = (int)min(sp, (long)BIG);
-        o[8] = ny;
-        o[9] = (int)min(nv0, (long)BIG);
-        o[10] = (int)min(nv0 + nv1, (long)BIG);
-        o[11] = (int)min(any[0] ? ni : 0, (long)BIG);
-        o[12] = (int)min((any[0] ? ni : 0) + (any[1] ? ni : 0), (long)BIG);
-        o[13] = (int)magic((unsigned)nx / 4);
-        o[14] = (int)magic((unsigned)ny);
-        if (nv0 + nv1 <= BOX_CAP) {
-            o[15] = -(lo[0][2] * o[7] + lo[0][1] * nx + lo[0][0]);
-            o[16] = o[9] - (lo[1][2] * o[7] + lo[1][1] * nx + lo[1][0]);
         }
-        o[17] = ic0;
-        o[18] = ir0;
-        int4* dst = reinterpret_cast<int4*>(rec + w * REC);
-        for (int k = 0; k < REC / 4; k++)
-            dst[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+        int e[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) e[k] = (k % 6) < 3 ? BIG : -BIG;
+        if (cLo <= cHi) {
+            const float X0 = (float)(cLo * pf), X1 = (float)(cHi * pf);
+            const float Y0 = (float)(rLo * pf), Y1 = (float)(rHi * pf);
+            for (int r = rBeg; r < rEnd; r++) {
+                const float* m = sM[r];
+                float mn[3], mx[3];
+#pragma unroll
+                for (int a = 0; a < 3; a++) {
+                    const float u = m[a], v = m[a + 3];
+                    mn[a] = u * (u >= 0 ? X0 : X1) + v * (v >= 0 ? Y0 : Y1);
+                    mx[a] = u * (u >= 0 ? X1 : X0) + v * (v >= 0 ? Y1 : Y0);
+                }
+                // every rotated patch point lies in the corner hull; the bounds
+                // are FP32 (|error| < 1e-4 voxel against the FP64-then-rounded
+                // sample coordinates) and a 1-voxel margin on each side absorbs it
+                if (mx[0] >= -1e-3f) {
+                    e[0] = min(e[0], (int)floorf(fmaxf(mn[0], 0.f)) - 1);
+                    e[1] = min(e[1], (int)floorf(mn[1]) - 1);
+                    e[2] = min(e[2], (int)floorf(mn[2]) - 1);
+                    e[3] = max(e[3], (int)floorf(mx[0]) + 2);
+                    e[4] = max(e[4], (int)floorf(mx[1]) + 2);
+                    e[5] = max(e[5], (int)floorf(mx[2]) + 2);
+                }
+                if (mn[0] < 1e-3f) {
+                    e[6] = min(e[6], (int)floorf(fmaxf(-mx[0], 0.f)) - 1);
+                    e[7] = min(e[7], (int)floorf(-mx[1]) - 1);
+                    e[8] = min(e[8], (int)floorf(-mx[2]) - 1);
+                    e[9] = max(e[9], (int)floorf(-mn[0]) + 2);
+                    e[10] = max(e[10], (int)floorf(-mn[1]) + 2);
+                    e[11] = max(e[11], (int)floorf(-mn[2]) + 2);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 12; k++) sE[wv][k][lane] = e[k];
+        __syncthreads();
+        if (wv == 0 && c < nC) {
+            for (int w = 1; w < PB_WAVES; w++)
+#pragma unroll
+                for (int k = 0; k < 12; k++)
+                    e[k] = (k % 6) < 3 ? min(e[k], sE[w][k][lane]) : max(e[k], sE[w][k][lane]);
+            store_rec(e, ic0, ir0, vdim, rec + (((size_t)l * nRT + ry) * nC + c) * REC);
+        }
+        __syncthreads();
     }
 }
 
@@ -342,7 +375,8 @@ THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int sp, int of
     const float dx = x - fx, dy = y - fy, dz = z - fz;
     const f32x2 vx = {1.f - dx, dx};
     const float vy0 = 1.f - dy, vz0 = 1.f - dz;
-    const int a = z0 * sp + y0 * nx + x0 + (conj ? off1 : off0);
+    // |coordinates| < 2^23: 24-bit multiplies (full rate) for the LDS index
+    const int a = __mul24(z0, sp) + __mul24(y0, nx) + x0 + (conj ? off1 : off0);
     const f32x2* bx = reinterpret_cast<const f32x2*>(box);
     const f32x2 a0 = bx[a], a1 = bx[a + 1];
     const f32x2 b0 = bx[a + nx], b1 = bx[a + nx + 1];
@@ -362,7 +396,9 @@ THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int sp, int of
 }
 
 template <bool CELLS>
-__global__ void __launch_bounds__(THREADS, 2) k_local_fused(const float2* __restrict__ vol,
+// two workgroups per CU (LDS-bound): 4 waves per SIMD, 128 VGPRs
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4)))
+k_local_fused(const float2* __restrict__ vol,
                                                             int vdim, int pf,
                                                             const double* __restrict__ quat,
                                                             int nR,
@@ -479,37 +515,39 @@ __global__ void __launch_bounds__(THREADS, 2) k_local_fused(const float2* __rest
             if (c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
         }
         // ---- projection samples: this lane's rotation x pixels 4s + g
-        float pre_[4], pim[4];
-        const bool staged = rc.staged();
-        const int nx = rc.v[6], sp = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const int p = 4 * s + g;
-            const double2 xy = sXY[p];
-            const float x = (float)(m[0] * xy.x + m[3] * xy.y);
-            const float y = (float)(m[1] * xy.x + m[4] * xy.y);
-            const float z = (float)(m[2] * xy.x + m[5] * xy.y);
-            float2 P;
-            if (staged)
-                P = interp_box(sBox, nx, sp, off0, off1, x, y, z);
-            else
-                P = CELLS ? interp_cells(reinterpret_cast<const float4*>(vol), vdim, x, y, z)
-                          : interp_ft(vol, vdim, x, y, z);
-            pre_[s] = P.x;
-            pim[s] = P.y;
-            bias += sBq[p] * (P.x * P.x + P.y * P.y);
-        }
-        // ---- reduce on the matrix cores: rows (re, im) of pixels 4s, 4s+2 and 4s+1, 4s+3
-#pragma unroll
-        for (int s = 0; s < 4; s++) {
-            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(pre_[s]),
-                                                             __float_as_uint(pim[s]), false, false);
-            const float a0 = __uint_as_float(sw[0]), a1 = __uint_as_float(sw[1]);
-            const int q0 = 4 * s + (kk < 2 ? 0 : 2), q1 = 4 * s + (kk < 2 ? 1 : 3);
+        // one step: the sample's bias term, then (re, im) of pixels 4s, 4s+2 and
+        // 4s+1, 4s+3 regrouped into two MFMA A operands against [U, V]
+        auto reduce_step = [&](int s, float2 P) {
+            bias += sBq[4 * s + g] * (P.x * P.x + P.y * P.y);
+            const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(P.x),
+                                                             __float_as_uint(P.y), false, false);
+            const int q0 = 4 * s + (kk < 2 ? 0 : 2), q1 = q0 + 1;
             const float b0 = sB[(q0 * 2 + (kk & 1)) * TT + tc];
             const float b1 = sB[(q1 * 2 + (kk & 1)) * TT + tc];
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[0]), b0, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[1]), b1, acc, 0, 0, 0);
+        };
+        if (rc.staged()) {
+            const int nx = rc.v[6], sp = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const double2 xy = sXY[4 * s + g];
+                const float x = (float)(m[0] * xy.x + m[3] * xy.y);
+                const float y = (float)(m[1] * xy.x + m[4] * xy.y);
+                const float z = (float)(m[2] * xy.x + m[5] * xy.y);
+                reduce_step(s, interp_box(sBox, nx, sp, off0, off1, x, y, z));
+            }
+        } else {
+#pragma unroll 2
+            for (int s = 0; s < 4; s++) {
+                const double2 xy = sXY[4 * s + g];
+                const float x = (float)(m[0] * xy.x + m[3] * xy.y);
+                const float y = (float)(m[1] * xy.x + m[4] * xy.y);
+                const float z = (float)(m[2] * xy.x + m[5] * xy.y);
+                reduce_step(s, CELLS ? interp_cells(reinterpret_cast<const float4*>(vol), vdim,
+                                                    x, y, z)
+                                     : interp_ft(vol, vdim, x, y, z));
+            }
         }
         rc = rn;
         rn = r2;
@@ -653,7 +691,8 @@ extern "C" int thx_local_phase(const float* vol, int volLayout, int vdim, int pf
     THX_CHECK_ARG(nR > 0 && nT > 0 && nPxl > 0 && nImg >= 0 && vdim > 0 && pf > 0,
                   "thx_local_phase: bad sizes");
     THX_CHECK_ARG(volLayout == 0 || volLayout == 1, "thx_local_phase: volLayout must be 0 or 1");
-    THX_CHECK_ARG(nImg <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 && (nT + TT - 1) / TT <= 65535,
+    THX_CHECK_ARG((long)nImg * ((nR + RT - 1) / RT) <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 &&
+                      (nT + TT - 1) / TT <= 65535,
                   "thx_local_phase: grid too large");
     THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % KC == 0),
                   "thx_local_phase: nOrd must be a positive multiple of 16 (thx_pixel_tile_order)");
@@ -665,9 +704,8 @@ extern "C" int thx_local_phase(const float* vol, int volLayout, int vdim, int pf
     float* d = dvp ? dvp : ws.take<float>((size_t)nImg * nR * nT);
     int* rec = ws.take<int>(rec_bytes(nImg, nR, nVisit) / sizeof(int));
     hipStream_t s = thx::as_stream(stream);
-    const long nWaves = (long)nImg * thx::cdiv(nR, RT) * thx::cdiv(nVisit, KC);
-    hipLaunchKernelGGL(k_patch_boxes, dim3(thx::cdiv(nWaves, 4)), dim3(256), 0, s, quat, nR,
-                       iCol, iRow, pxOrder, nVisit, pf, vdim, nImg, rec);
+    hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * thx::cdiv(nR, RT)), dim3(64 * PB_WAVES),
+                       0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec);
     THX_LAUNCH_CHECK();
     dim3 grid(nImg, thx::cdiv(nR, RT), thx::cdiv(nT, TT));
     if (volLayout == 1)
