@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, headline bench, kernel-trace profile and HBM
+# PMC passes of the bench.  Run on the GPU box from the repo root:
+#   tools/gpu_round.sh TAG [tests|bench|prof|pmc ...]   (default: all four)
+# Every step has its own time limit; the first failure ends the script.
+set -e
+tag=$1; shift
+steps=${*:-tests bench prof pmc}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$tag
+mkdir -p $O
+export TMPDIR=/tmp
+for s in $steps; do
+  case $s in
+    tests)
+      (cd $R && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 \
+          --timeout-method thread > $O/tests.log 2>&1) ;;
+    bench)
+      (cd $R && timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err) ;;
+    prof)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d $O/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline \
+          > $O/prof.json 2> $O/prof.err) ;;
+    pmc)
+      # HBM bytes: FETCH_SIZE and WRITE_SIZE need separate passes (TCC slots)
+      i=0
+      for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+        i=$((i+1))
+        (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv \
+            --kernel-include-regex "k_scan|k_local|k_patch|k_insert|k_prep" \
+            -d $O/pmc$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline \
+            > $O/pmc$i.log 2>&1)
+      done ;;
+  esac
+done
