@@ -254,22 +254,24 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
                 }
                 // every rotated patch point lies in the corner hull; the bounds
                 // are FP32 (|error| < 1e-4 voxel against the FP64-then-rounded
-                // sample coordinates) and a 1-voxel margin on each side absorbs it
-                if (mx[0] >= -1e-3f) {
-                    e[0] = min(e[0], (int)floorf(fmaxf(mn[0], 0.f)) - 1);
-                    e[1] = min(e[1], (int)floorf(mn[1]) - 1);
-                    e[2] = min(e[2], (int)floorf(mn[2]) - 1);
-                    e[3] = max(e[3], (int)floorf(mx[0]) + 2);
-                    e[4] = max(e[4], (int)floorf(mx[1]) + 2);
-                    e[5] = max(e[5], (int)floorf(mx[2]) + 2);
+                // sample coordinates), widened by EPS before the floor; a cell
+                // spans floor(c) .. floor(c) + 1
+                constexpr float EPS = 1e-3f;
+                if (mx[0] >= -EPS) {
+                    e[0] = min(e[0], (int)floorf(fmaxf(mn[0] - EPS, 0.f)));
+                    e[1] = min(e[1], (int)floorf(mn[1] - EPS));
+                    e[2] = min(e[2], (int)floorf(mn[2] - EPS));
+                    e[3] = max(e[3], (int)floorf(mx[0] + EPS) + 1);
+                    e[4] = max(e[4], (int)floorf(mx[1] + EPS) + 1);
+                    e[5] = max(e[5], (int)floorf(mx[2] + EPS) + 1);
                 }
-                if (mn[0] < 1e-3f) {
-                    e[6] = min(e[6], (int)floorf(fmaxf(-mx[0], 0.f)) - 1);
-                    e[7] = min(e[7], (int)floorf(-mx[1]) - 1);
-                    e[8] = min(e[8], (int)floorf(-mx[2]) - 1);
-                    e[9] = max(e[9], (int)floorf(-mn[0]) + 2);
-                    e[10] = max(e[10], (int)floorf(-mn[1]) + 2);
-                    e[11] = max(e[11], (int)floorf(-mn[2]) + 2);
+                if (mn[0] < EPS) {
+                    e[6] = min(e[6], (int)floorf(fmaxf(-mx[0] - EPS, 0.f)));
+                    e[7] = min(e[7], (int)floorf(-mx[1] - EPS));
+                    e[8] = min(e[8], (int)floorf(-mx[2] - EPS));
+                    e[9] = max(e[9], (int)floorf(-mn[0] + EPS) + 1);
+                    e[10] = max(e[10], (int)floorf(-mn[1] + EPS) + 1);
+                    e[11] = max(e[11], (int)floorf(-mn[2] + EPS) + 1);
                 }
             }
         }

@@ -20,6 +20,32 @@ from thunder_amd import expectation as ex  # noqa: E402
 from thunder_amd import ops, synth  # noqa: E402
 
 
+def box_stats(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px, rec_ints=20, rt=128, kc=16):
+    """Patch-box voxel counts from the records k_patch_boxes leaves at the
+    start of the workspace (dvp passed explicitly, so the records come first)."""
+    from thunder_amd.ops import _ptr, _stream, workspace
+    from thunder_amd._lib import check, lib
+    nImg, nR, nT = quat.shape[0], quat.shape[1], trans.shape[1]
+    dev = dat.device
+    d = torch.empty(nImg, nR, nT, dtype=torch.float32, device=dev)
+    w = [torch.empty(nImg, *s, dtype=torch.float32, device=dev) for s in ((), (nR,), (nT,), ())]
+    ws = workspace(lib().thx_local_phase_workspace(nImg, nR, nT, len(px.order)), dev)
+    ws.zero_()
+    check(lib().thx_local_phase(_ptr(vol), 0, vol.shape[0], px.pf, _ptr(quat), nR, _ptr(trans), nT,
+                                _ptr(pC), _ptr(pR), _ptr(pT), _ptr(dat), _ptr(ctf), _ptr(sig),
+                                _ptr(px.d_iCol), _ptr(px.d_iRow), _ptr(px.d_order), len(px.order),
+                                px.n, px.idim, nImg, _ptr(w[0]), _ptr(w[1]), _ptr(w[2]), _ptr(w[3]),
+                                _ptr(d), _ptr(ws), ws.numel(), _stream(dev)), "thx_local_phase")
+    torch.cuda.synchronize()
+    nC = (len(px.order) + kc - 1) // kc
+    nRT = (nR + rt - 1) // rt
+    rec = ws.view(torch.int32)[:nImg * nRT * nC * rec_ints].view(nImg, nRT, nC, rec_ints)
+    tot = rec[..., 10].double().flatten()
+    q = torch.tensor([0.1, 0.5, 0.9], dtype=torch.float64, device=dev)
+    return {"box_voxels_p10_p50_p90": [int(v) for v in torch.quantile(tot, q)],
+            "staged_frac": {str(c): float((tot <= c).double().mean()) for c in (4096, 8192, 16384, 32768)}}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("what", choices=["local", "scan", "insert"])
@@ -33,6 +59,8 @@ def main():
     p.add_argument("--reps", type=int, default=5)
     p.add_argument("--tiled", type=int, default=1,
                    help="local: 1 = tile visiting order (LDS-staged patches), 0 = set order")
+    p.add_argument("--stats", type=int, default=0,
+                   help="local: report patch-box sizes (voxels per LDS neighbourhood)")
     p.add_argument("--spread", type=float, default=3.0,
                    help="local: rotation spread (deg) of each image's cloud, 0 = uniform")
     a = p.parse_args()
@@ -57,6 +85,8 @@ def main():
         cells = ops.volume_cells(vol) if a.cells else None
         sec = timed_events(lambda: ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px,
                                                    cells=cells, tiled=bool(a.tiled)), a.reps, st)
+        if a.stats:
+            out.update(box_stats(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px))
         out.update(ms=sec * 1e3, us_per_image_phase=sec / a.images * 1e6,
                    algo_GBps=a.images * (64.0 * mR * px.n + 16.0 * px.n) / sec / 1e9)
     elif a.what == "scan":
