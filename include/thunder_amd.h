@@ -126,7 +126,10 @@ int thx_dvp(const float* rotP, int nR, const float* traP, int nT,
  * kIdx == 0 initialises wC/wR/wT/baseL; kIdx > 0 merges, rescaling earlier
  * classes when the baseline rises (kernel_setBaseLine, Kernel.cu:1096-1128).
  * algo: 0 = direct per-pixel formulation, materialised dvp;
- *       1 = fused MFMA formulation (default).
+ *       1 = fused FP32 MFMA formulation;
+ *       2 = bf16 MFMA, three-product split (bf16x3);
+ *       3 = fp16 MFMA, two-product split of w against an fp16 T (fp16x2);
+ *       2 and 3 fall back to 1 when nT > 160.
  * workspace: >= thx_global_scan_workspace(...) bytes of device memory. */
 size_t thx_global_scan_workspace(int nImg, int nR, int nT, int nPxl, int algo);
 int thx_global_scan(const float* rotP, int nR, const float* traP, int nT,

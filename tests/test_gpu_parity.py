@@ -84,20 +84,27 @@ def test_dvp_direct(orc, stack):
     assert np.max(np.abs(d - ref) / np.abs(ref)) < 1e-5
 
 
-def check_weights(got, ref, nR, nT):
+def check_weights(got, ref, nR, nT, rtol_base=1e-5, rtol_w=1e-3):
     wC, wR, wT, base = [x.cpu().numpy() for x in got]
     rC, rR, rT, rb = ref
-    assert np.allclose(base, rb, rtol=1e-5, atol=0)
+    assert np.allclose(base, rb, rtol=rtol_base, atol=0)
     rR = rR.reshape(wR.shape)
     rT = rT.reshape(wT.shape)
     rC = rC.reshape(wC.shape)
     for a, b in ((wR, rR), (wT, rT), (wC, rC)):
         m = b >= 1e-4 * b.max(axis=-1, keepdims=True)
-        assert np.all(np.abs(a - b)[m] <= 1e-3 * b[m]), np.max(np.abs(a - b)[m] / b[m])
-        assert np.allclose(a.sum(-1), b.sum(-1), rtol=1e-4)
+        assert np.all(np.abs(a - b)[m] <= rtol_w * b[m]), np.max(np.abs(a - b)[m] / b[m])
+        assert np.allclose(a.sum(-1), b.sum(-1), rtol=min(1e-4 * rtol_w / 1e-3, 1e-2))
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2])
+def scan_tol(algo):
+    """fp16x2 (algo 3) rounds the translation table to fp16: its log-likelihoods
+    hold the north-star bar (1e-4 relative), marginals 1 %; algos 0-2 hold
+    1e-5 / 1e-3."""
+    return dict(rtol_base=1e-4, rtol_w=1e-2) if algo == 3 else {}
+
+
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_global_scan(orc, stack, algo):
     s = stack
     px = dev_pixels(s)
@@ -110,10 +117,10 @@ def test_global_scan(orc, stack, algo):
                           algo=algo)
     dref = orc.dvp_global(s["vol"], s["vdim"], s["pf"], s["quat"], s["trans"], s["dat"],
                           s["ctf"], s["sig"], s["px"], s["N"])
-    check_weights(got, orc.weights_global(dref, pR, pT), nR, nT)
+    check_weights(got, orc.weights_global(dref, pR, pT), nR, nT, **scan_tol(algo))
 
 
-@pytest.mark.parametrize("algo", [0, 1, 2])
+@pytest.mark.parametrize("algo", [0, 1, 2, 3])
 def test_global_scan_two_classes(orc, stack, algo):
     """kIdx > 0 merges into the running baseline (kernel_setBaseLine)."""
     s = stack
@@ -132,7 +139,7 @@ def test_global_scan_two_classes(orc, stack, algo):
         d = orc.dvp_global(v, s["vdim"], s["pf"], s["quat"], s["trans"], s["dat"], s["ctf"],
                            s["sig"], s["px"], s["N"])
         ostate = orc.weights_global(d, pR, pT, kIdx=k, nK=2, state=ostate)
-    check_weights(state, ostate, nR, nT)
+    check_weights(state, ostate, nR, nT, **scan_tol(algo))
 
 
 def test_local_phase(orc, stack):

@@ -143,14 +143,19 @@ int scan_bf16x3(const float* rotP, int nR, const float* traP, int nT,
                 int nImg, int nPxl, const double* pR, const double* pT, int kIdx,
                 int nK, float* wC, float* wR, float* wT, float* baseL,
                 void* workspace, size_t wsBytes, hipStream_t stream);
-size_t scan_bf16x3_workspace(int nImg, int nR, int nT, int nPxl);
+int scan_f16x2(const float* rotP, int nR, const float* traP, int nT,
+               const float* dat, const float* ctf, const float* sigRcp,
+               int nImg, int nPxl, const double* pR, const double* pT, int kIdx,
+               int nK, float* wC, float* wR, float* wT, float* baseL,
+               void* workspace, size_t wsBytes, hipStream_t stream);
+size_t scan_split_workspace(int nImg, int nR, int nT, int nPxl);
 }  // namespace thx
 
 extern "C" size_t thx_global_scan_workspace(int nImg, int nR, int nT, int nPxl,
                                             int algo)
 {
     if (algo == 1) return thx::scan_mfma_workspace(nImg, nR, nT, nPxl);
-    if (algo == 2) return thx::scan_bf16x3_workspace(nImg, nR, nT, nPxl);
+    if (algo == 2 || algo == 3) return thx::scan_split_workspace(nImg, nR, nT, nPxl);
     thx::Carver c(nullptr, 0);
     c.take<float>((size_t)nImg * nR * nT);
     return c.off + 256;
@@ -169,7 +174,7 @@ extern "C" int thx_global_scan(const float* rotP, int nR, const float* traP,
                   nT, nImg, nPxl);
     THX_CHECK_ARG(nK >= 1 && kIdx >= 0 && kIdx < nK,
                   "thx_global_scan: bad kIdx=%d nK=%d", kIdx, nK);
-    THX_CHECK_ARG(algo >= 0 && algo <= 2, "thx_global_scan: algo must be 0, 1 or 2");
+    THX_CHECK_ARG(algo >= 0 && algo <= 3, "thx_global_scan: algo must be 0, 1, 2 or 3");
     THX_CHECK_ARG(wsBytes >= thx_global_scan_workspace(nImg, nR, nT, nPxl, algo),
                   "thx_global_scan: workspace too small");
     if (nImg == 0) return THX_OK;
@@ -182,6 +187,10 @@ extern "C" int thx_global_scan(const float* rotP, int nR, const float* traP,
         return thx::scan_bf16x3(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl,
                                 pR, pT, kIdx, nK, wC, wR, wT, baseL, workspace,
                                 wsBytes, s);
+    if (algo == 3)
+        return thx::scan_f16x2(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl,
+                               pR, pT, kIdx, nK, wC, wR, wT, baseL, workspace,
+                               wsBytes, s);
     thx::Carver c(workspace, wsBytes);
     float* dvp = c.take<float>((size_t)nImg * nR * nT);
     for (int l0 = 0; l0 < nImg; l0 += 65535) {

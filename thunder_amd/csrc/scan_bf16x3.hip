@@ -1,50 +1,62 @@
-// scan_bf16x3.hip -- a7 + a8, algo 2: the global scan's cross term on the
-// bf16 matrix cores with a three-product split (bf16x3).
+// scan_bf16x3.hip -- a7 + a8 on 16-bit matrix cores: the global scan's cross
+// term with FP32 operands split into 16-bit pieces.
+//   algo 2 (BF16X3): bf16 hi/lo of both operands, three products
+//                    (hi hi + hi lo + lo hi), ~2^-16 relative per product;
+//   algo 3 (F16X2):  fp16 hi/lo of the generated operand w, the translation
+//                    table T (|T| = 1) as ONE fp16 plane, two products
+//                    (w_hi T + w_lo T): 2/3 of the matrix work, error set by
+//                    the fp16 rounding of T (<= 2^-12 per component).
 //
 // Same expansion as algo 1 (scan_mfma.hip): with |T| = 1
 //   dvp[l][r][t] = A_l + B[l][r] + X[l][r][t],  A_l = sum s|d|^2,
-//   B[l][r] = sum s c^2 |P_r|^2 (FP32),
+//   B[l][r] = sum s c^2 |P_r|^2 (FP32, its own small GEMM: k_scan_bias),
 //   X = sum_i Re(a conj(T P)) = sum_i Re(w_lri conj(T_ti)),  w = a conj(P_r),
 //   a = -2 s c d.
-// Regrouped this way, for one rotation X is a GEMM whose B operand is the
-// translation table T -- the same for every rotation and image, split ONCE
-// into bf16 hi/lo planes in the prep -- and whose A operand w = a conj(P_r)
-// is formed per (image tile, rotation) in registers and split there.  Each
-// generated A fragment is reused across all NF translation fragments, and
-// each T fragment read from LDS feeds both image fragments of the wave.
-// FP32 operands x = x_hi + x_lo (x_hi = bf16(x), x_lo = bf16(x - x_hi)) are
-// multiplied as w_hi T_hi + w_hi T_lo + w_lo T_hi with FP32 accumulation on
-// v_mfma_f32_32x32x16_bf16 (K = 16 = 8 pixels per instruction).  The
-// dropped lo*lo term and the 16-bit split leave ~2^-16 relative error per
-// product; summed over K = 2 nPxl terms of random sign that is ~1e-7 of
-// |dvp|, the order of the reference's own sequential FP32 sum
-// (tests/test_gpu_parity.py holds it to the same bar as algo 1).
+// For one rotation X is a GEMM whose B operand is the translation table T --
+// the same for every rotation and image, split ONCE in the prep -- and whose A
+// operand w = a conj(P_r) is formed per (image tile, rotation) in registers
+// and split there.  Each generated A fragment is reused across all NF
+// translation fragments, and each T fragment read from LDS feeds both image
+// fragments of the wave.  The fp16 form needs range: a is pre-scaled per
+// image by an exact power of two 2^e_l so that max |w| <= 2^14, and X is
+// scaled back by 2^-e_l in the epilogue (exact).
 //
 // Workgroup = 8 waves = 8 rotations x 64 images; each wave owns a
 // 64-image x NT_PAD-translation tile of ONE rotation (2 x NF accumulators
-// of 32x32).  Epilogue: per-(image, rotation) max + wR marginal, then a
-// block-local merge of the 8 rotations into a (max, wT[NT_PAD]) partial per
-// image; k_scan_combine_bf folds the partials of all rotation blocks.
+// of 32x32).  Per 16-pixel chunk a wave reads its a / P operands with four
+// ds_read_b128 and the T fragments with NF (fp16) or 2 NF (bf16) more.
+// Epilogue: per-(image, rotation) max + wR marginal, then a block-local merge
+// of the 8 rotations into a (max, wT[NT_PAD]) partial per image;
+// k_scan_combine_bf folds the partials of all rotation blocks.
 #include "common.h"
 #include "scan_common.h"
 
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+enum Mode { BF16X3 = 0, F16X2 = 1 };
+
+template <int MODE> struct Elt;
+template <> struct Elt<BF16X3> { typedef __bf16 T; typedef bf16x8 V; };
+template <> struct Elt<F16X2> { typedef _Float16 T; typedef f16x8 V; };
 
 constexpr int KC = 16;            // pixels per LDS stage (2 MFMA k-steps)
 constexpr int IMG_TILE = 64;
 constexpr int ROT_TILE = 8;
 constexpr int THREADS = 512;
-constexpr int TROW = KC * 2 + 8;  // bf16 per translation row of the T tile (80 B)
-constexpr int APITCH = KC + 1;    // float2 per image row of the a tile (odd: conflict-free b64)
-constexpr int BPITCH = KC + 1;    // float per image row of the b tile
+constexpr int TROW = KC * 2 + 8;  // 16-bit elements per translation row of the T tile (80 B)
+constexpr int APITCH = KC + 2;    // float2 per image row of the a tile (144 B: aligned, conflict-free b128)
+constexpr int PMAX_BLOCKS = 256;
+constexpr float WMAX = 16384.f;   // fp16 range budget of the scaled w
 
 inline int pad_to(int v, int m) { return (v + m - 1) / m * m; }
 
 struct Dims {
-    int nImg, nR, nT, nPxl, nImgPad, nPxlPad, nTPad, nRB, nCk;
+    int nImg, nR, nT, nPxl, nImgPad, nPxlPad, nTPad, nRB, nCk, nRBias;
 };
 
 Dims dims(int nImg, int nR, int nT, int nPxl)
@@ -56,15 +68,20 @@ Dims dims(int nImg, int nR, int nT, int nPxl)
     d.nTPad = pad_to(nT, 32);
     d.nRB = (nR + ROT_TILE - 1) / ROT_TILE;
     d.nCk = d.nPxlPad / KC;
+    d.nRBias = pad_to(nR, 64);
     return d;
 }
 
 struct WS {
-    float2* Ac;     // [nCk][nImgPad][KC]   a = -2 s c d
+    float2* Ac;     // [nCk][nImgPad][KC]   a = -2 s c d (x 2^e_l for F16X2)
     float* Bc;      // [nCk][nImgPad][KC]   b = s c^2
     float* Aconst;  // [nImgPad]
-    __bf16* Thi;    // [nCk][nTPad][KC*2]   T split, (re, im) interleaved
-    __bf16* Tlo;
+    float* amax;    // [nImgPad]   max_i |a.re| + |a.im|
+    float* scale;   // [nImgPad]   2^e_l
+    float* pmaxB;   // [PMAX_BLOCKS]
+    float* bias;    // [nImgPad][nRBias]  B[l][r]
+    uint16_t* Thi;  // [nCk][nTPad][KC*2]   T split, (re, im) interleaved
+    uint16_t* Tlo;
     float2* wRp;    // [nImg][nR]
     float* pM;      // [nRB][nImgPad]
     float* pWT;     // [nRB][nImgPad][nTPad]
@@ -79,8 +96,12 @@ WS carve(void* base, const Dims& d)
     w.Ac = c.take<float2>((size_t)d.nPxlPad * d.nImgPad);
     w.Bc = c.take<float>((size_t)d.nPxlPad * d.nImgPad);
     w.Aconst = c.take<float>(d.nImgPad);
-    w.Thi = c.take<__bf16>((size_t)d.nPxlPad * d.nTPad * 2);
-    w.Tlo = c.take<__bf16>((size_t)d.nPxlPad * d.nTPad * 2);
+    w.amax = c.take<float>(d.nImgPad);
+    w.scale = c.take<float>(d.nImgPad);
+    w.pmaxB = c.take<float>(PMAX_BLOCKS);
+    w.bias = c.take<float>((size_t)d.nImgPad * d.nRBias);
+    w.Thi = c.take<uint16_t>((size_t)d.nPxlPad * d.nTPad * 2);
+    w.Tlo = c.take<uint16_t>((size_t)d.nPxlPad * d.nTPad * 2);
     w.wRp = c.take<float2>((size_t)d.nImg * d.nR);
     w.pM = c.take<float>((size_t)d.nRB * d.nImgPad);
     w.pWT = c.take<float>((size_t)d.nRB * d.nImgPad * d.nTPad);
@@ -89,16 +110,89 @@ WS carve(void* base, const Dims& d)
     return w;
 }
 
-THX_DEV void split_bf16(float x, __bf16& hi, __bf16& lo)
+template <typename H>
+THX_DEV void split16(float x, H& hi, H& lo)
 {
-    hi = (__bf16)x;
-    lo = (__bf16)(x - (float)hi);
+    hi = (H)x;
+    lo = (H)(x - (float)hi);
 }
 
-// a, b in pixel-chunked image rows; pixel fastest so writes are contiguous
+// Per image: A_l = sum s|d|^2 and max |a| (a = -2 s c d) for the fp16 scale.
+__global__ void __launch_bounds__(256) k_prep_aconst(const float2* __restrict__ dat,
+                                                     const float* __restrict__ ctf,
+                                                     const float* __restrict__ sig, int nImg,
+                                                     int nPxl, int nImgPad,
+                                                     float* __restrict__ Aconst,
+                                                     float* __restrict__ amax)
+{
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (l >= nImgPad) return;
+    float a = 0.f, m = 0.f;
+    if (l < nImg)
+        for (int i = lane; i < nPxl; i += 64) {
+            const size_t s = (size_t)l * nPxl + i;
+            const float2 d = dat[s];
+            const float sg = sig[s];
+            a += sg * (d.x * d.x + d.y * d.y);
+            const float k = -2.f * sg * ctf[s];
+            m = fmaxf(m, fabsf(k * d.x) + fabsf(k * d.y));
+        }
+    a = wave_sum(a);
+    m = wave_max(m);
+    if (lane == 0) {
+        Aconst[l] = a;
+        amax[l] = m;
+    }
+}
+
+// Block maxima of |P.re| + |P.im| over the shared projections.
+__global__ void __launch_bounds__(256) k_prep_pmax(const float2* __restrict__ rotP, long n,
+                                                   float* __restrict__ pmaxB)
+{
+    __shared__ float sm[4];
+    float m = 0.f;
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
+         q += (long)gridDim.x * blockDim.x) {
+        const float2 p = rotP[q];
+        m = fmaxf(m, fabsf(p.x) + fabsf(p.y));
+    }
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) pmaxB[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+}
+
+// scale_l = 2^e_l with max |w| = amax_l pmax 2^e_l <= WMAX (F16X2), 1 (BF16X3).
+__global__ void __launch_bounds__(256) k_prep_scale(const float* __restrict__ amax,
+                                                    const float* __restrict__ pmaxB, int nImgPad,
+                                                    int fp16, float* __restrict__ scale)
+{
+    __shared__ float sP;
+    if (threadIdx.x < 64) {
+        float m = 0.f;
+        for (int b = threadIdx.x; b < PMAX_BLOCKS; b += 64) m = fmaxf(m, pmaxB[b]);
+        m = wave_max(m);
+        if (threadIdx.x == 0) sP = m;
+    }
+    __syncthreads();
+    for (int l = blockIdx.x * blockDim.x + threadIdx.x; l < nImgPad; l += gridDim.x * blockDim.x) {
+        float s = 1.f;
+        const float wm = amax[l] * sP;
+        if (fp16 && wm > 0.f && wm == wm) {
+            int e;
+            frexpf(WMAX / wm, &e);                 // WMAX / wm = f 2^e, f in [0.5, 1)
+            s = ldexpf(1.f, max(-100, min(100, e - 1)));
+        }
+        scale[l] = s;
+    }
+}
+
+// a (scaled), b in pixel-chunked image rows; pixel fastest so writes are contiguous
 __global__ void __launch_bounds__(256) k_prep_img(const float2* __restrict__ dat,
                                                   const float* __restrict__ ctf,
-                                                  const float* __restrict__ sig, int nImg,
+                                                  const float* __restrict__ sig,
+                                                  const float* __restrict__ scale, int nImg,
                                                   int nPxl, int nImgPad, int nPxlPad,
                                                   float2* __restrict__ Ac,
                                                   float* __restrict__ Bc)
@@ -114,7 +208,8 @@ __global__ void __launch_bounds__(256) k_prep_img(const float2* __restrict__ dat
             const float2 d = dat[s];
             const float c = ctf[s], sg = sig[s];
             const float k = -2.f * sg * c;
-            a = make_float2(k * d.x, k * d.y);
+            const float sc = scale[l];
+            a = make_float2((k * d.x) * sc, (k * d.y) * sc);
             b = sg * c * c;
         }
         const size_t o = ((size_t)(i / KC) * nImgPad + l) * KC + (i % KC);
@@ -123,80 +218,118 @@ __global__ void __launch_bounds__(256) k_prep_img(const float2* __restrict__ dat
     }
 }
 
-__global__ void __launch_bounds__(256) k_prep_aconst2(const float2* __restrict__ dat,
-                                                      const float* __restrict__ sig, int nImg,
-                                                      int nPxl, int nImgPad,
-                                                      float* __restrict__ Aconst)
-{
-    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (l >= nImgPad) return;
-    float a = 0.f;
-    if (l < nImg)
-        for (int i = lane; i < nPxl; i += 64) {
-            const float2 d = dat[(size_t)l * nPxl + i];
-            a += sig[(size_t)l * nPxl + i] * (d.x * d.x + d.y * d.y);
-        }
-    a = wave_sum(a);
-    if (lane == 0) Aconst[l] = a;
-}
-
+template <int MODE>
 __global__ void __launch_bounds__(256) k_prep_tsplit(const float2* __restrict__ traP,
                                                      const double* __restrict__ pT, int nT,
                                                      int nPxl, int nTPad, int nPxlPad,
-                                                     __bf16* __restrict__ Thi,
-                                                     __bf16* __restrict__ Tlo,
+                                                     uint16_t* __restrict__ Thi,
+                                                     uint16_t* __restrict__ Tlo,
                                                      float* __restrict__ pTf)
 {
+    typedef typename Elt<MODE>::T H;
     const long n = (long)nTPad * nPxlPad;
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
          q += (long)gridDim.x * blockDim.x) {
         const int i = (int)(q % nPxlPad), t = (int)(q / nPxlPad);
         const float2 v = (t < nT && i < nPxl) ? traP[(size_t)t * nPxl + i] : make_float2(0.f, 0.f);
         const size_t o = (((size_t)(i / KC) * nTPad + t) * KC + (i % KC)) * 2;
-        __bf16 h, lo;
-        split_bf16(v.x, h, lo); Thi[o] = h; Tlo[o] = lo;
-        split_bf16(v.y, h, lo); Thi[o + 1] = h; Tlo[o + 1] = lo;
+        H h, lo;
+        split16(v.x, h, lo);
+        Thi[o] = __builtin_bit_cast(uint16_t, h);
+        Tlo[o] = __builtin_bit_cast(uint16_t, lo);
+        split16(v.y, h, lo);
+        Thi[o + 1] = __builtin_bit_cast(uint16_t, h);
+        Tlo[o + 1] = __builtin_bit_cast(uint16_t, lo);
         if (i == 0) pTf[t] = t < nT ? (float)pT[t] : 0.f;
     }
 }
 
-template <int NF>
+// B[l][r] = sum_i b_li |P_ri|^2 as an FP32 GEMM on v_mfma_f32_32x32x2_f32:
+// workgroup = 64 images x 64 rotations, 4 waves of 32 x 32, 16-pixel chunks.
+__global__ void __launch_bounds__(256) k_scan_bias(const float* __restrict__ Bc,
+                                                   const float2* __restrict__ rotP, int nR,
+                                                   int nPxl, int nImgPad, int nCk, int nRBias,
+                                                   float* __restrict__ bias)
+{
+    __shared__ float sA[64][KC + 1];
+    __shared__ float sB[64][KC + 1];
+    const int l0 = blockIdx.x * 64, r0 = blockIdx.y * 64;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wi = w & 1, wr = w >> 1, n = lane & 31, h = lane >> 5;
+    f32x16 acc;
+#pragma unroll
+    for (int j = 0; j < 16; j++) acc[j] = 0.f;
+    for (int ck = 0; ck < nCk; ck++) {
+        {
+            const float4 a = reinterpret_cast<const float4*>(Bc + ((size_t)ck * nImgPad + l0) * KC)[tid];
+            const int row = tid / 4, c4 = (tid % 4) * 4;
+            sA[row][c4] = a.x; sA[row][c4 + 1] = a.y; sA[row][c4 + 2] = a.z; sA[row][c4 + 3] = a.w;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int x = tid + u * 256, rr = x / KC, kc = x % KC;
+            const int r = r0 + rr, i = ck * KC + kc;
+            float p2 = 0.f;
+            if (r < nR && i < nPxl) {
+                const float2 p = rotP[(size_t)r * nPxl + i];
+                p2 = p.x * p.x + p.y * p.y;
+            }
+            sB[rr][kc] = p2;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k2 = 0; k2 < KC / 2; k2++)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sA[32 * wi + n][2 * k2 + h],
+                                                       sB[32 * wr + n][2 * k2 + h], acc, 0, 0, 0);
+        __syncthreads();
+    }
+    // C layout: col = n (rotation), row = (j & 3) + 8 (j >> 2) + 4 h (image)
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        const int row = (j & 3) + 8 * (j >> 2) + 4 * h;
+        bias[(size_t)(l0 + 32 * wi + row) * nRBias + r0 + 32 * wr + n] = acc[j];
+    }
+}
+
+template <int MODE, int NF>
 struct Smem {
     static constexpr int NTP = NF * 32;
-    static constexpr int T_H = NTP * TROW;                 // bf16 per hi / lo plane
+    static constexpr int NPLANE = MODE == BF16X3 ? 2 : 1;
+    static constexpr int T_H = NTP * TROW;                 // 16-bit elements per plane
     static constexpr int A_F2 = IMG_TILE * APITCH;         // float2
-    static constexpr int B_F = IMG_TILE * BPITCH;          // float
     static constexpr int P_F2 = ROT_TILE * KC;             // float2
-    static constexpr int STAGE_B = 2 * T_H * 2 + A_F2 * 8 + B_F * 4 + P_F2 * 8;
-    static constexpr int EPI_B = (ROT_TILE * 64 + ROT_TILE * 64 + 32 * NTP) * 4;
+    static constexpr int STAGE_B = NPLANE * T_H * 2 + A_F2 * 8 + P_F2 * 8;
+    static constexpr int EPI_B = (ROT_TILE * 64 * 3 + 32 * NTP) * 4;
     static constexpr int TOTAL_B = STAGE_B > EPI_B ? STAGE_B : EPI_B;
     static constexpr int T16 = NTP * KC * 2 * 2 / 16;      // 16-B pieces per plane
 };
 
-template <int NF>
-__global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restrict__ Ac,
-                                                         const float* __restrict__ Bc,
-                                                         const float* __restrict__ Aconst,
-                                                         const __bf16* __restrict__ Thi,
-                                                         const __bf16* __restrict__ Tlo,
-                                                         const float2* __restrict__ rotP,
-                                                         const float* __restrict__ pTf,
-                                                         const double* __restrict__ pR,
-                                                         int nImg, int nR, int nT, int nPxl,
-                                                         int nImgPad, int nPxlPad, int nTPad,
-                                                         float2* __restrict__ wRp,
-                                                         float* __restrict__ pM,
-                                                         float* __restrict__ pWT)
+template <int MODE, int NF>
+__global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict__ Ac,
+                                                        const float* __restrict__ Aconst,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ bias,
+                                                        const uint16_t* __restrict__ Thi,
+                                                        const uint16_t* __restrict__ Tlo,
+                                                        const float2* __restrict__ rotP,
+                                                        const float* __restrict__ pTf,
+                                                        const double* __restrict__ pR,
+                                                        int nImg, int nR, int nT, int nPxl,
+                                                        int nImgPad, int nPxlPad, int nTPad,
+                                                        int nRBias,
+                                                        float2* __restrict__ wRp,
+                                                        float* __restrict__ pM,
+                                                        float* __restrict__ pWT)
 {
-    using S = Smem<NF>;
+    typedef typename Elt<MODE>::T H;
+    typedef typename Elt<MODE>::V HV;
+    using S = Smem<MODE, NF>;
     constexpr int NTP = S::NTP;
     __shared__ __attribute__((aligned(16))) char lds[S::TOTAL_B];
-    __bf16* sTh = reinterpret_cast<__bf16*>(lds);                   // [NTP][TROW]
-    __bf16* sTl = sTh + S::T_H;
-    float2* sA = reinterpret_cast<float2*>(sTl + S::T_H);           // [64][APITCH]
-    float* sB = reinterpret_cast<float*>(sA + S::A_F2);             // [64][BPITCH]
-    float2* sP = reinterpret_cast<float2*>(sB + S::B_F);            // [8][KC]
+    uint16_t* sTh = reinterpret_cast<uint16_t*>(lds);               // [NTP][TROW]
+    uint16_t* sTl = sTh + S::T_H;                                   // BF16X3 only
+    float2* sA = reinterpret_cast<float2*>(sTh + S::NPLANE * S::T_H);   // [64][APITCH]
+    float2* sP = sA + S::A_F2;                                      // [8][KC]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n = lane & 31, h = lane >> 5;
@@ -212,13 +345,11 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
         for (int f = 0; f < NF; f++)
 #pragma unroll
             for (int j = 0; j < 16; j++) acc[a][f][j] = 0.f;
-    float bsum = 0.f;                         // bias of image `lane`, rotation r
 
     // register-staged prefetch of one pixel chunk (global -> regs during the
     // previous chunk's MFMAs, regs -> LDS after the barrier)
     constexpr int TPER = (S::T16 + THREADS - 1) / THREADS;
     float4 gTh[TPER], gTl[TPER], gA;
-    float4 gB = make_float4(0.f, 0.f, 0.f, 0.f);
     float2 gP = make_float2(0.f, 0.f);
     auto load_chunk = [&](int ck) {
         const float4* gh = reinterpret_cast<const float4*>(Thi + (size_t)ck * nTPad * KC * 2);
@@ -226,11 +357,12 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
 #pragma unroll
         for (int u = 0; u < TPER; u++) {
             const int x = tid + u * THREADS;
-            if (x < S::T16) { gTh[u] = gh[x]; gTl[u] = gl[x]; }
+            if (x < S::T16) {
+                gTh[u] = gh[x];
+                if (MODE == BF16X3) gTl[u] = gl[x];
+            }
         }
         gA = reinterpret_cast<const float4*>(Ac + ((size_t)ck * nImgPad + l0) * KC)[tid];
-        if (tid < IMG_TILE * KC / 4)
-            gB = reinterpret_cast<const float4*>(Bc + ((size_t)ck * nImgPad + l0) * KC)[tid];
         if (tid < ROT_TILE * KC) {
             const int qq = tid / KC, kc = tid % KC;
             const int rr = rb * ROT_TILE + qq, i = ck * KC + kc;
@@ -244,18 +376,12 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
             if (x < S::T16) {                      // KC/4 pieces of 16 B per row
                 const int row = x / (KC / 4), qd = x % (KC / 4);
                 *reinterpret_cast<float4*>(sTh + row * TROW + qd * 8) = gTh[u];
-                *reinterpret_cast<float4*>(sTl + row * TROW + qd * 8) = gTl[u];
+                if (MODE == BF16X3) *reinterpret_cast<float4*>(sTl + row * TROW + qd * 8) = gTl[u];
             }
         }
         {                                          // 2 float2 of image row tid / (KC/2)
             const int row = tid / (KC / 2), c2 = (tid % (KC / 2)) * 2;
-            sA[row * APITCH + c2] = make_float2(gA.x, gA.y);
-            sA[row * APITCH + c2 + 1] = make_float2(gA.z, gA.w);
-        }
-        if (tid < IMG_TILE * KC / 4) {
-            const int row = tid / (KC / 4), c4 = (tid % (KC / 4)) * 4;
-            sB[row * BPITCH + c4] = gB.x; sB[row * BPITCH + c4 + 1] = gB.y;
-            sB[row * BPITCH + c4 + 2] = gB.z; sB[row * BPITCH + c4 + 3] = gB.w;
+            *reinterpret_cast<float4*>(sA + row * APITCH + c2) = gA;
         }
         if (tid < ROT_TILE * KC) sP[tid] = gP;
     };
@@ -267,38 +393,58 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
         __syncthreads();
         if ((ck + 1) * KC < nPxlPad) load_chunk(ck + 1);
 #pragma unroll
-        for (int kc = 0; kc < KC; kc++) {
-            const float2 p = sP[w * KC + kc];
-            bsum += sB[lane * BPITCH + kc] * (p.x * p.x + p.y * p.y);
-        }
-#pragma unroll
         for (int s = 0; s < KC / 8; s++) {
             // A fragments: w = a conj(P_r) for images a*32 + n, pixels 8s+4h+{0..3}
-            bf16x8 wh[2], wl[2];
+            const int px0 = 8 * s + 4 * h;
+            const f32x4v p01 = *reinterpret_cast<const f32x4v*>(sP + w * KC + px0);
+            const f32x4v p23 = *reinterpret_cast<const f32x4v*>(sP + w * KC + px0 + 2);
+            const float pr[4] = {p01.x, p01.z, p23.x, p23.z};
+            const float pi[4] = {p01.y, p01.w, p23.y, p23.w};
+            // w fragments of image half a (hi, lo split in registers)
+            auto make_w = [&](int a, HV& wh, HV& wl) {
+                const float2* rowA = sA + (a * 32 + n) * APITCH + px0;
+                const f32x4v a01 = *reinterpret_cast<const f32x4v*>(rowA);
+                const f32x4v a23 = *reinterpret_cast<const f32x4v*>(rowA + 2);
+                const float ar[4] = {a01.x, a01.z, a23.x, a23.z};
+                const float ai[4] = {a01.y, a01.w, a23.y, a23.w};
 #pragma unroll
-            for (int qd = 0; qd < 4; qd++) {
-                const int px = 8 * s + 4 * h + qd;
-                const float2 p = sP[w * KC + px];
-#pragma unroll
-                for (int a = 0; a < 2; a++) {
-                    const float2 av = sA[(a * 32 + n) * APITCH + px];
-                    const float wr = av.x * p.x + av.y * p.y;
-                    const float wi = av.y * p.x - av.x * p.y;
-                    __bf16 x0, x1;
-                    split_bf16(wr, x0, x1); wh[a][2 * qd] = x0; wl[a][2 * qd] = x1;
-                    split_bf16(wi, x0, x1); wh[a][2 * qd + 1] = x0; wl[a][2 * qd + 1] = x1;
+                for (int qd = 0; qd < 4; qd++) {
+                    const float wr = ar[qd] * pr[qd] + ai[qd] * pi[qd];
+                    const float wi = ai[qd] * pr[qd] - ar[qd] * pi[qd];
+                    H x0, x1;
+                    split16(wr, x0, x1); wh[2 * qd] = x0; wl[2 * qd] = x1;
+                    split16(wi, x0, x1); wh[2 * qd + 1] = x0; wl[2 * qd + 1] = x1;
                 }
-            }
-#pragma unroll
-            for (int f = 0; f < NF; f++) {
-                const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
-                const bf16x8 th = *reinterpret_cast<const bf16x8*>(sTh + row);
-                const bf16x8 tl = *reinterpret_cast<const bf16x8*>(sTl + row);
+            };
+            if constexpr (MODE == BF16X3) {
+                // one image half at a time (register budget of the three products)
 #pragma unroll
                 for (int a = 0; a < 2; a++) {
-                    acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[a], th, acc[a][f], 0, 0, 0);
-                    acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[a], tl, acc[a][f], 0, 0, 0);
-                    acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[a], th, acc[a][f], 0, 0, 0);
+                    HV wh, wl;
+                    make_w(a, wh, wl);
+#pragma unroll
+                    for (int f = 0; f < NF; f++) {
+                        const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
+                        const HV th = *reinterpret_cast<const HV*>(sTh + row);
+                        const HV tl = *reinterpret_cast<const HV*>(sTl + row);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, th, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, tl, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, th, acc[a][f], 0, 0, 0);
+                    }
+                }
+            } else {
+                HV wh[2], wl[2];
+                make_w(0, wh[0], wl[0]);
+                make_w(1, wh[1], wl[1]);
+#pragma unroll
+                for (int f = 0; f < NF; f++) {
+                    const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
+                    const HV th = *reinterpret_cast<const HV*>(sTh + row);
+#pragma unroll
+                    for (int a = 0; a < 2; a++) {
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[a], th, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl[a], th, acc[a][f], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -306,10 +452,12 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
     __syncthreads();
 
     // ------------------------------------------------------------ epilogue
-    float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][64]
-    float* sMax = sBias + ROT_TILE * 64;               // [8 waves][64 rows]
+    float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][64]  A_l + B[l][r]
+    float* sInv = sBias + ROT_TILE * 64;               // [64]           2^-e_l
+    float* sMax = sInv + ROT_TILE * 64;                // [8 waves][64 rows]
     float* sWT = sMax + ROT_TILE * 64;                 // [32][NTP]
-    sBias[w * 64 + lane] = bsum;
+    sBias[w * 64 + lane] = Aconst[l0 + lane] + (rValid ? bias[(size_t)(l0 + lane) * nRBias + r] : 0.f);
+    if (w == 0) sInv[lane] = 1.f / scale[l0 + lane];
     __syncthreads();
 
     float pTv[NF];
@@ -323,11 +471,11 @@ __global__ void __launch_bounds__(THREADS) k_scan_bf16x3(const float2* __restric
         for (int j = 0; j < 16; j++) {
             const int row = a * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
             const int l = l0 + row;
-            const float b = Aconst[l] + sBias[w * 64 + row];
+            const float b = sBias[w * 64 + row], inv = sInv[row];
             float mx = -INFINITY;
 #pragma unroll
             for (int f = 0; f < NF; f++) {
-                const float d = acc[a][f][j] + b;
+                const float d = acc[a][f][j] * inv + b;
                 acc[a][f][j] = d;
                 if (f * 32 + n < nT) mx = fmaxf(mx, d);
             }
@@ -428,14 +576,61 @@ __global__ void __launch_bounds__(256) k_scan_combine_bf(const float2* __restric
     if (threadIdx.x == 0) wC[(size_t)l * nK + kIdx] = (float)(sd[0] + sd[1] + sd[2] + sd[3]);
 }
 
-template <int NF>
+template <int MODE, int NF>
 int launch_main(const WS& ws, const Dims& d, const float* rotP, const double* pR, hipStream_t s)
 {
     dim3 grid(d.nImgPad / IMG_TILE, d.nRB);
-    hipLaunchKernelGGL(k_scan_bf16x3<NF>, grid, dim3(THREADS), 0, s, ws.Ac, ws.Bc, ws.Aconst,
-                       ws.Thi, ws.Tlo, reinterpret_cast<const float2*>(rotP), ws.pTf, pR,
-                       d.nImg, d.nR, d.nT, d.nPxl, d.nImgPad, d.nPxlPad, d.nTPad, ws.wRp, ws.pM,
-                       ws.pWT);
+    hipLaunchKernelGGL((k_scan_split<MODE, NF>), grid, dim3(THREADS), 0, s, ws.Ac, ws.Aconst,
+                       ws.scale, ws.bias, ws.Thi, ws.Tlo, reinterpret_cast<const float2*>(rotP),
+                       ws.pTf, pR, d.nImg, d.nR, d.nT, d.nPxl, d.nImgPad, d.nPxlPad, d.nTPad,
+                       d.nRBias, ws.wRp, ws.pM, ws.pWT);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+template <int MODE>
+int scan_split(const float* rotP, int nR, const float* traP, int nT, const float* dat,
+               const float* ctf, const float* sigRcp, int nImg, int nPxl, const double* pR,
+               const double* pT, int kIdx, int nK, float* wC, float* wR, float* wT,
+               float* baseL, void* workspace, size_t wsBytes, hipStream_t s)
+{
+    const Dims d = dims(nImg, nR, nT, nPxl);
+    THX_CHECK_ARG(d.nRB <= 65535 && d.nRBias / 64 <= 65535, "thx_global_scan: grid too large");
+    const WS ws = carve(workspace, d);
+    THX_CHECK_ARG(ws.bytes <= wsBytes, "thx_global_scan: workspace too small");
+    const float2* dat2 = reinterpret_cast<const float2*>(dat);
+    const float2* rot2 = reinterpret_cast<const float2*>(rotP);
+    hipLaunchKernelGGL(k_prep_aconst, dim3(thx::cdiv(d.nImgPad, 4)), dim3(256), 0, s, dat2, ctf,
+                       sigRcp, nImg, nPxl, d.nImgPad, ws.Aconst, ws.amax);
+    THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_prep_pmax, dim3(PMAX_BLOCKS), dim3(256), 0, s, rot2, (long)nR * nPxl,
+                       ws.pmaxB);
+    THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_prep_scale, dim3(thx::cdiv(d.nImgPad, 256)), dim3(256), 0, s, ws.amax,
+                       ws.pmaxB, d.nImgPad, MODE == F16X2 ? 1 : 0, ws.scale);
+    THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_prep_img, dim3(2048), dim3(256), 0, s, dat2, ctf, sigRcp, ws.scale, nImg,
+                       nPxl, d.nImgPad, d.nPxlPad, ws.Ac, ws.Bc);
+    THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_prep_tsplit<MODE>, dim3(512), dim3(256), 0, s,
+                       reinterpret_cast<const float2*>(traP), pT, nT, nPxl, d.nTPad, d.nPxlPad,
+                       ws.Thi, ws.Tlo, ws.pTf);
+    THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_scan_bias, dim3(d.nImgPad / 64, d.nRBias / 64), dim3(256), 0, s, ws.Bc,
+                       rot2, nR, nPxl, d.nImgPad, d.nCk, d.nRBias, ws.bias);
+    THX_LAUNCH_CHECK();
+    int st;
+    switch (d.nTPad / 32) {
+        case 1: st = launch_main<MODE, 1>(ws, d, rotP, pR, s); break;
+        case 2: st = launch_main<MODE, 2>(ws, d, rotP, pR, s); break;
+        case 3: st = launch_main<MODE, 3>(ws, d, rotP, pR, s); break;
+        case 4: st = launch_main<MODE, 4>(ws, d, rotP, pR, s); break;
+        default: st = launch_main<MODE, 5>(ws, d, rotP, pR, s); break;
+    }
+    if (st != THX_OK) return st;
+    hipLaunchKernelGGL(k_scan_combine_bf, dim3(nImg), dim3(256), sizeof(float) * d.nRB, s,
+                       ws.wRp, ws.pM, ws.pWT, pR, nR, nT, d.nTPad, d.nRB, d.nImgPad, kIdx, nK,
+                       wC, wR, wT, baseL);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
@@ -450,7 +645,8 @@ int scan_mfma(const float* rotP, int nR, const float* traP, int nT, const float*
               float* baseL, void* workspace, size_t wsBytes, hipStream_t stream);
 size_t scan_mfma_workspace(int nImg, int nR, int nT, int nPxl);
 
-size_t scan_bf16x3_workspace(int nImg, int nR, int nT, int nPxl)
+// nT > 160: 2 x NF accumulators no longer fit one wave -- FP32 MFMA path (algo 1)
+size_t scan_split_workspace(int nImg, int nR, int nT, int nPxl)
 {
     const Dims d = dims(nImg, nR, nT, nPxl);
     if (d.nTPad > 160) return scan_mfma_workspace(nImg, nR, nT, nPxl);
@@ -462,38 +658,23 @@ int scan_bf16x3(const float* rotP, int nR, const float* traP, int nT, const floa
                 const double* pT, int kIdx, int nK, float* wC, float* wR, float* wT,
                 float* baseL, void* workspace, size_t wsBytes, hipStream_t s)
 {
-    const Dims d = dims(nImg, nR, nT, nPxl);
-    if (d.nTPad > 160)   // 2 x NF accumulators no longer fit one wave: FP32 MFMA path
+    if (pad_to(nT, 32) > 160)
         return scan_mfma(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx, nK,
                          wC, wR, wT, baseL, workspace, wsBytes, s);
-    THX_CHECK_ARG(d.nRB <= 65535, "thx_global_scan(algo=2): grid too large");
-    const WS ws = carve(workspace, d);
-    THX_CHECK_ARG(ws.bytes <= wsBytes, "thx_global_scan(algo=2): workspace too small");
-    const float2* dat2 = reinterpret_cast<const float2*>(dat);
-    hipLaunchKernelGGL(k_prep_img, dim3(2048), dim3(256), 0, s, dat2, ctf, sigRcp, nImg, nPxl,
-                       d.nImgPad, d.nPxlPad, ws.Ac, ws.Bc);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_aconst2, dim3(thx::cdiv(d.nImgPad, 4)), dim3(256), 0, s, dat2,
-                       sigRcp, nImg, nPxl, d.nImgPad, ws.Aconst);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_tsplit, dim3(512), dim3(256), 0, s,
-                       reinterpret_cast<const float2*>(traP), pT, nT, nPxl, d.nTPad, d.nPxlPad,
-                       ws.Thi, ws.Tlo, ws.pTf);
-    THX_LAUNCH_CHECK();
-    int st;
-    switch (d.nTPad / 32) {
-        case 1: st = launch_main<1>(ws, d, rotP, pR, s); break;
-        case 2: st = launch_main<2>(ws, d, rotP, pR, s); break;
-        case 3: st = launch_main<3>(ws, d, rotP, pR, s); break;
-        case 4: st = launch_main<4>(ws, d, rotP, pR, s); break;
-        default: st = launch_main<5>(ws, d, rotP, pR, s); break;
-    }
-    if (st != THX_OK) return st;
-    hipLaunchKernelGGL(k_scan_combine_bf, dim3(nImg), dim3(256), sizeof(float) * d.nRB, s,
-                       ws.wRp, ws.pM, ws.pWT, pR, nR, nT, d.nTPad, d.nRB, d.nImgPad, kIdx, nK,
-                       wC, wR, wT, baseL);
-    THX_LAUNCH_CHECK();
-    return THX_OK;
+    return scan_split<BF16X3>(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx,
+                              nK, wC, wR, wT, baseL, workspace, wsBytes, s);
+}
+
+int scan_f16x2(const float* rotP, int nR, const float* traP, int nT, const float* dat,
+               const float* ctf, const float* sigRcp, int nImg, int nPxl, const double* pR,
+               const double* pT, int kIdx, int nK, float* wC, float* wR, float* wT,
+               float* baseL, void* workspace, size_t wsBytes, hipStream_t s)
+{
+    if (pad_to(nT, 32) > 160)
+        return scan_mfma(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx, nK,
+                         wC, wR, wT, baseL, workspace, wsBytes, s);
+    return scan_split<F16X2>(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx,
+                             nK, wC, wR, wT, baseL, workspace, wsBytes, s);
 }
 
 }  // namespace thx
