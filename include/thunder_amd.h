@@ -211,6 +211,22 @@ int thx_insert3d(float* F, float* T, double* O, int* counter, int vdim,
                  const float* w, int nImg, int mReco, const int* iCol,
                  const int* iRow, int nPxl, int idim, thx_stream_t stream);
 
+/* Same insert, pixels visited in thx_pixel_tile_order patches (pxOrder:
+ * device, nOrd ints): per (image, patch) the samples are accumulated in an
+ * LDS copy of the patch's neighbourhood (the local phase's patch boxes) and
+ * flushed row by row, so the memory-side atomics run on contiguous rows
+ * instead of one row per lane.  Values and coordinates as thx_insert3d; the
+ * FP32 summation order differs.  workspace: >= thx_insert3d_workspace bytes
+ * of device memory. */
+size_t thx_insert3d_workspace(int nImg, int mReco, int nOrd);
+int thx_insert3d_tiled(float* F, float* T, double* O, int* counter, int vdim,
+                       int pf, const float* dat, const float* ctf,
+                       const double* quat, const double* trans,
+                       const double* offS, const float* w, int nImg, int mReco,
+                       const int* iCol, const int* iRow, const int* pxOrder,
+                       int nOrd, int nPxl, int idim, void* workspace,
+                       size_t wsBytes, thx_stream_t stream);
+
 /* ----------------------------------------------------------------- a14 ---
  * Fourier shell correlation FSC(vec&, const Volume& A, const Volume& B)
  * (src/Functions/Spectrum.cpp:302-337) of two half-complex volumes of real

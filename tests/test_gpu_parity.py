@@ -274,17 +274,26 @@ def test_resample_bit_exact(orc):
             assert imax[l] == ri
 
 
-def test_insert3d(orc, stack):
+@pytest.mark.parametrize("tiled,spread,mReco", [(False, 0.0, 6), (True, 0.0, 6), (True, 2.0, 100),
+                                                (True, 8.0, 150)])
+def test_insert3d(orc, stack, tiled, spread, mReco):
+    """spread 0: uniform samples (patch boxes overflow -> direct scatter);
+    spread 2 deg: a posterior cloud, every patch accumulated in LDS;
+    mReco 150 > 128: two sample tiles per image."""
     s = stack
     px = dev_pixels(s)
-    nImg, mReco = 4, 6
+    nImg = 4
     rng = np.random.default_rng(21)
-    quat = synth.uniform_quaternions(nImg * mReco, rng).reshape(nImg, mReco, 4)
+    if spread > 0:
+        quat = synth.clustered_quaternions(nImg, mReco, spread, rng)
+    else:
+        quat = synth.uniform_quaternions(nImg * mReco, rng).reshape(nImg, mReco, 4)
     trans = rng.standard_normal((nImg, mReco, 2)) * 3
     off = rng.standard_normal((nImg, 2))
     w = np.full(nImg, 1.0 / mReco, np.float32)
     hm = ops.HalfMap(s["vdim"], DEV)
-    ops.insert3d(hm, T(s["dat"][:nImg]), T(s["ctf"][:nImg]), T(quat), T(trans), T(off), T(w), px)
+    ops.insert3d(hm, T(s["dat"][:nImg]), T(s["ctf"][:nImg]), T(quat), T(trans), T(off), T(w), px,
+                 tiled=tiled)
     F, Tm, O, cnt = orc.insert_batch(s["vdim"], s["pf"], s["dat"][:nImg], s["ctf"][:nImg], quat,
                                      trans, off, w, s["px"], s["N"])
     gF = hm.F.cpu().numpy().reshape(-1)

@@ -34,6 +34,9 @@ SIGNATURES = {
     "thx_resample": (_c_int, [_c_int, _c_int, _p, _p, _c_int, _p, _p, _p, _p, _p]),
     "thx_insert3d": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_int,
                               _c_int, _p, _p, _c_int, _c_int, _p]),
+    "thx_insert3d_workspace": (_c_size, [_c_int, _c_int, _c_int]),
+    "thx_insert3d_tiled": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_int,
+                                    _c_int, _p, _p, _p, _c_int, _c_int, _c_int, _p, _c_size, _p]),
     "thx_fsc_workspace": (_c_size, [_c_int]),
     "thx_fsc": (_c_int, [_p, _p, _c_int, _c_int, _p, _p, _c_size, _p]),
     "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int, _c_int]),

@@ -38,6 +38,7 @@
 #include <climits>
 
 #include "common.h"
+#include "patch.h"
 
 namespace {
 
@@ -45,10 +46,11 @@ constexpr int THREADS = 512;
 constexpr int NWAVE = THREADS / 64;
 constexpr int RT = 16 * NWAVE;   // rotations per workgroup (one 16-row M-tile per wave)
 constexpr int TT = 16;           // translations per workgroup (one N-tile)
-constexpr int KC = 16;           // pixels per stage: one patch of the tile order
-constexpr int BOX_CAP = 8192;    // LDS voxels (64 KiB) for a patch neighbourhood
+constexpr int KC = thx::PATCH_KC;          // pixels per stage: one patch of the tile order
+constexpr int BOX_CAP = thx::PATCH_BOX_CAP; // LDS voxels (64 KiB) for a patch neighbourhood
 constexpr int NIT = BOX_CAP / 4 / THREADS;   // 32-B box items in flight per thread
-constexpr int REC = 20;          // ints per patch record
+constexpr int REC = thx::PATCH_REC;         // ints per patch record
+static_assert(RT == thx::PATCH_RT, "one record tile per workgroup");
 static_assert(KC * TT <= THREADS, "one (pixel, translation) of the image tile per thread");
 static_assert(BOX_CAP % (4 * THREADS) == 0, "whole prefetch rounds");
 static_assert(KC == 16, "four steps of four pixels");
@@ -83,17 +85,7 @@ THX_DEV float2 interp_cells(const float4* __restrict__ cells, int vdim, float x,
     return make_float2(re, conj ? -im : im);
 }
 
-// Patch record (k_patch_boxes -> k_local_fused).  Two boxes of one shape in
-// folded (x >= 0) coordinates, side 0 for samples with x >= 0, side 1 for the
-// folded ones, each stored [z][y][x] in LDS (rows padded to 4 voxels):
-//   [0..2] side-0 origin (x, y, z; rows / slices signed, unwrapped)
-//   [3..5] side-1 origin  [6] row pitch nx  [7] slice pitch sp  [8] ny
-//   [9] side-0 voxels (= LDS offset of side 1)  [10] total voxels
-//   (> BOX_CAP: the patch is gathered from the volume)
-//   [11] side-0 items (4 voxels = 32 B of a row)  [12] total items
-//   [13] magic(nx / 4)  [14] magic(ny)  (udiv)
-//   [15] / [16] LDS index of voxel (0, 0, 0) for side 0 / 1 (may be negative)
-//   [17], [18] (iCol, iRow) of the patch's first pixel (stand-in for padding)
+// Patch record (k_patch_boxes -> k_local_fused): layout in patch.h.
 struct Rec {
     int v[REC];
     THX_DEV bool staged() const { return v[10] <= BOX_CAP; }
@@ -130,11 +122,6 @@ THX_DEV unsigned magic(unsigned d) { return d <= 1 ? 0u : 0xFFFFFFFFu / d + 1u; 
 THX_DEV int udiv(int u, int d, unsigned m) { return d <= 1 ? u : (int)__umulhi((unsigned)u, m); }
 
 constexpr int BIG = 1 << 29;
-
-THX_DEV int patch_pixel(const int* __restrict__ order, int nVisit, int k)
-{
-    return k < nVisit ? (order ? order[k] : k) : -1;
-}
 
 // The patch record from the folded-box bounds e (side 0 lo xyz, hi xyz; side 1).
 THX_DEV void store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __restrict__ out)
@@ -662,6 +649,22 @@ size_t rec_bytes(int nImg, int nR, int nVisit)
 }
 
 }  // namespace
+
+namespace thx {
+
+size_t patch_rec_bytes(int nImg, int nR, int nVisit) { return rec_bytes(nImg, nR, nVisit); }
+
+int launch_patch_boxes(const double* quat, int nR, const int* iCol, const int* iRow,
+                       const int* order, int nVisit, int pf, int vdim, int nImg, int* rec,
+                       hipStream_t s)
+{
+    hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * cdiv(nR, RT)), dim3(64 * PB_WAVES), 0,
+                       s, quat, nR, iCol, iRow, order, nVisit, pf, vdim, rec);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+}  // namespace thx
 
 extern "C" int thx_volume_cells(const float* vol, int vdim, float* cells,
                                 thx_stream_t stream)

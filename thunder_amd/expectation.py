@@ -96,8 +96,8 @@ class Reconstructor:
         self.hm = ops.HalfMap(pf * idim, device)
         self.pf = pf
 
-    def insert(self, dat, ctf, quat, trans, offS, w, px):
-        return ops.insert3d(self.hm, dat, ctf, quat, trans, offS, w, px)
+    def insert(self, dat, ctf, quat, trans, offS, w, px, tiled=True):
+        return ops.insert3d(self.hm, dat, ctf, quat, trans, offS, w, px, tiled=tiled)
 
 
 def draw_insert_samples(quat, trans, m_reco, seed=11):

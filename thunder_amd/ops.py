@@ -265,7 +265,9 @@ class HalfMap:
         self.counter = torch.zeros(1, dtype=torch.int32, device=device)
 
 
-def insert3d(hm, dat, ctf_, quat, trans, offS, w, px):
+def insert3d(hm, dat, ctf_, quat, trans, offS, w, px, tiled=True):
+    """tiled: LDS-accumulated patches (thx_insert3d_tiled) instead of one
+    memory-side atomic per tap (thx_insert3d)."""
     nImg, nPxl = dat.shape
     _req(dat, torch.complex64, (nImg, nPxl), "dat")
     _req(ctf_, torch.float32, (nImg, nPxl), "ctf")
@@ -279,8 +281,18 @@ def insert3d(hm, dat, ctf_, quat, trans, offS, w, px):
     if px.rU * px.pf >= hm.vdim // 2 - 1:
         raise ValueError("pixel radius * pf reaches the volume edge")
     dev = dat.device
+    if tiled:
+        ws = workspace(lib().thx_insert3d_workspace(min(nImg, 65535), mReco, len(px.order)), dev)
     for l0 in range(0, nImg, 65535):
         nb = min(65535, nImg - l0)
+        if tiled:
+            check(lib().thx_insert3d_tiled(
+                _ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim, px.pf,
+                _ptr(dat[l0:]), _ptr(ctf_[l0:]), _ptr(quat[l0:]), _ptr(trans[l0:]), _ptr(offS[l0:]),
+                _ptr(w[l0:]), nb, mReco, _ptr(px.d_iCol), _ptr(px.d_iRow), _ptr(px.d_order),
+                len(px.order), nPxl, px.idim, _ptr(ws), ws.numel(), _stream(dev)),
+                "thx_insert3d_tiled")
+            continue
         check(lib().thx_insert3d(_ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim,
                                  px.pf, _ptr(dat[l0:]), _ptr(ctf_[l0:]), _ptr(quat[l0:]),
                                  _ptr(trans[l0:]), _ptr(offS[l0:]), _ptr(w[l0:]), nb, mReco,

@@ -99,12 +99,16 @@ def main():
         out.update(ms=sec * 1e3, us_per_image=sec / a.images * 1e6, algo=a.algo)
     else:
         rec = ex.Reconstructor(N, pf, dev)
-        quat = torch.as_tensor(synth.uniform_quaternions(a.images * a.mreco, rng).reshape(
-            a.images, a.mreco, 4), device=dev)
+        if a.spread > 0:   # posterior samples: a cloud around one pose per image
+            q = synth.clustered_quaternions(a.images, a.mreco, a.spread, rng)
+        else:
+            q = synth.uniform_quaternions(a.images * a.mreco, rng).reshape(a.images, a.mreco, 4)
+        quat = torch.as_tensor(np.ascontiguousarray(q), device=dev)
         trans = torch.as_tensor(rng.standard_normal((a.images, a.mreco, 2)), device=dev)
         offS = torch.zeros(a.images, 2, dtype=torch.float64, device=dev)
         w = torch.full((a.images,), 1.0 / a.mreco, dtype=torch.float32, device=dev)
-        sec = timed_events(lambda: rec.insert(dat, ctf, quat, trans, offS, w, px), a.reps, st)
+        sec = timed_events(lambda: rec.insert(dat, ctf, quat, trans, offS, w, px, tiled=bool(a.tiled)),
+                           a.reps, st)
         out.update(ms=sec * 1e3, images_per_s=a.images / sec)
     print(json.dumps(out), flush=True)
 
