@@ -76,6 +76,18 @@ def make_stack(N, pf, rU, rL, n_img, device, seed=5, snr=0.05, vol=None):
     return px, dat, ctf, sigRcp, qtrue, ttrue
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the roofline launch sequences, measured by the
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench (tools/gpu_round.sh
+    pmc -> tools/traffic.py -> profiles/rNN_traffic.json, the newest round)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files:
+        return {}, None
+    with open(files[-1]) as f:
+        return json.load(f), os.path.relpath(files[-1], ROOT)
+
+
 def timed_events(fn, reps, stream):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
@@ -235,14 +247,23 @@ def main():
             "max_p10_p50_p90": [round(float(v), 2) for v in torch.quantile(ang.max(1).values, qs)]}
 
     extras = {}
+    traffic, traffic_src = pmc_traffic()
+
+    def launch_traffic(key, ok):
+        t = traffic.get(key) if ok else None
+        return (t["traffic_bytes"], f"{traffic_src}: {key}") if t else (None, None)
+
     if not a.no_extras:
         # dominant kernel: the global scan
         sec, issued, algorithmic, peak = scan_roofline(vol, px, gset, dat[:a.chunk],
                                                        ctf[:a.chunk], sig[:a.chunk], a.algo)
-        kname = {1: "k_scan_mfma (fp32 32x32x2)", 2: "k_scan_bf16x3 (bf16 32x32x16, 3-product split)"}
+        kname = {1: "k_scan_mfma (fp32 32x32x2)", 2: "k_scan_split<BF16X3> (bf16 32x32x16, 3-product split)"}
+        tr, tr_src = launch_traffic("scan_4096", a.algo == 2 and min(a.chunk, a.images) == 4096
+                                    and a.nr == 2000 and N == 256)
         extras["roofline"] = {"bound": "mfma", "achieved": issued / sec / 1e12,
                               "peak": peak, "unit": "TFLOP/s",
-                              "frac": issued / sec / 1e12 / peak, "traffic": None,
+                              "frac": issued / sec / 1e12 / peak, "traffic": tr,
+                              "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
                               "kernel": f"global scan {kname.get(a.algo, a.algo)} + prep + combine",
                               "launch_ms": sec * 1e3, "images_per_launch": min(a.chunk, a.images),
                               "algorithmic_equiv_tflops": algorithmic / sec / 1e12,
@@ -252,9 +273,13 @@ def main():
                                       "algorithmic_equiv uses the direct 15-flop count of SURVEY "
                                       "8(d) and can exceed the FP32 VALU peak"}
         lsec, lbytes, lnpx, lsec_plain = local_roofline(vol, N, pf, dev)
+        tr, tr_src = launch_traffic("local_fullres_512", N == 256)
         extras["roofline_local"] = {"bound": "hbm", "achieved": lbytes / lsec / 1e9,
                                     "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                    "frac": lbytes / lsec / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                                    "frac": lbytes / lsec / 1e9 / PEAK_HBM_GBS, "traffic": tr,
+                                    "traffic_unit": "bytes per launch (HBM, PMC)",
+                                    "traffic_source": tr_src,
+                                    "algorithmic_bytes": lbytes,
                                     "kernel": f"local phase full-res (nPxl={lnpx}, 125x9, 512 "
                                               "images, cell-expanded projectee)",
                                     "launch_ms": lsec * 1e3,

@@ -63,10 +63,11 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB):
-        raise ThxError(f"{LIB} is missing: run `python -m thunder_amd.build` "
+    path = os.environ.get("THX_LIB", LIB)   # override: A/B builds in tools/microbench.py
+    if not os.path.exists(path):
+        raise ThxError(f"{path} is missing: run `python -m thunder_amd.build` "
                        "(the HIP path has no fallback)")
-    L = ctypes.CDLL(LIB)
+    L = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(L, name)
         fn.restype = res

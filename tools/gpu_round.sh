@@ -30,6 +30,7 @@ for s in $steps; do
             --kernel-include-regex "k_scan|k_local|k_patch|k_insert|k_prep" \
             -d $O/pmc$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline \
             > $O/pmc$i.log 2>&1)
-      done ;;
+      done
+      python3 $R/tools/traffic.py $O $O/traffic.json > /dev/null ;;
   esac
 done

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch of the two roofline kernels, from the rocprofv3 PMC
+passes of tools/gpu_round.sh (pmc1 = FETCH_SIZE, pmc2 = WRITE_SIZE, both run
+on `bench.py --steps 1 --warmup 0`).
+
+A "launch" is the whole launch sequence the bench times with HIP events:
+  scan  : k_prep_aconst .. k_scan_combine_bf of one thx_global_scan call whose
+          k_scan_split grid is the 4096-image grid (bench.scan_roofline);
+  local : k_patch_boxes .. k_local_weights of one thx_local_phase call that runs
+          k_local_fused<true> (bench.local_roofline, full resolution, 512 images).
+Bytes: FETCH_SIZE x 1024 x 2 (FETCH_SIZE is in KiB and reads half of a wide
+read on gfx950) + WRITE_SIZE x 1024 -- MI355X_MICROARCH.md, HBM section.
+
+  python tools/traffic.py gpurun_out/TAG profiles/rNN_traffic.json
+"""
+import csv
+import json
+import os
+import re
+import sys
+
+
+def dispatches(path, counter):
+    rows = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            d = int(r["Dispatch_Id"])
+            name = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"])
+            e = rows.setdefault(d, [name, int(r["Grid_Size"]), 0.0])
+            e[2] += float(r["Counter_Value"])
+    return [rows[d] for d in sorted(rows)]
+
+
+def groups(disp, start, end):
+    out, cur = [], None
+    for name, grid, val in disp:
+        if start in name:
+            cur = []
+        if cur is not None:
+            cur.append((name, grid, val))
+            if end in name:
+                out.append(cur)
+                cur = None
+    return out
+
+
+def summarise(rd, wr, start, end, pick):
+    gr = [g for g in groups(rd, start, end) if pick(g)]
+    gw = [g for g in groups(wr, start, end) if pick(g)]
+    if not gr or not gw:
+        return None
+    r = sum(sum(v for _, _, v in g) for g in gr) / len(gr) * 1024 * 2
+    w = sum(sum(v for _, _, v in g) for g in gw) / len(gw) * 1024
+    return {"read_bytes": r, "write_bytes": w, "traffic_bytes": r + w, "launches": len(gr),
+            "kernels": [n.split("(")[0] for n, _, _ in gr[-1]]}
+
+
+def main():
+    tag, out = sys.argv[1], sys.argv[2]
+    rd = dispatches(os.path.join(tag, "pmc1", "run_counter_collection.csv"), "FETCH_SIZE")
+    wr = dispatches(os.path.join(tag, "pmc2", "run_counter_collection.csv"), "WRITE_SIZE")
+    scan_grid = (4096 // 64) * 250 * 512          # k_scan_split grid at 4096 images, nR 2000
+    res = {
+        "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({tag}), "
+                  "FETCH_SIZE x2 on gfx950",
+        "scan_4096": summarise(rd, wr, "k_prep_aconst", "k_scan_combine_bf",
+                               lambda g: any("k_scan_split" in n and gr == scan_grid
+                                             for n, gr, _ in g)),
+        "local_fullres_512": summarise(rd, wr, "k_patch_boxes", "k_local_weights",
+                                       lambda g: any("k_local_fused<true>" in n for n, _, _ in g)),
+    }
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
