@@ -33,6 +33,7 @@ from thunder_amd._lib import lib  # noqa: E402
 PEAK_FP32_MFMA_TFLOPS = 157.3    # MI355X_MICROARCH.md, dense f32 MFMA (= VALU)
 PEAK_HBM_GBS = 8000.0            # MI355X_MICROARCH.md, HBM3E spec
 PEAK_BF16_MFMA_TFLOPS = 2500.0   # MI355X_MICROARCH.md, dense bf16 MFMA
+ROOF_IMAGES = 4096               # images per global-scan launch in the roofline measurement
 
 
 def parse():
@@ -41,7 +42,9 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--images", type=int, default=12500, help="particle images per GPU per step")
-    p.add_argument("--chunk", type=int, default=4096, help="images per expectation launch")
+    p.add_argument("--chunk", type=int, default=0,
+                   help="images per expectation launch (0: the whole batch in one launch; "
+                        "288 GB of HBM holds the workspaces of all 12500)")
     p.add_argument("--box", type=int, default=256)
     p.add_argument("--nr", type=int, default=2000)
     p.add_argument("--phases", type=int, default=10)
@@ -201,7 +204,8 @@ def main():
     px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, rL, a.images, dev, seed=5 + 101 * rank,
                                                  vol=vol)
     e = ex.Expectation(vol, px, gset, n_phase=a.phases, algo=a.algo, seed=7 + rank)
-    chunks = [(l0, min(a.images, l0 + a.chunk)) for l0 in range(0, a.images, a.chunk)]
+    chunk = a.chunk or a.images
+    chunks = [(l0, min(a.images, l0 + chunk)) for l0 in range(0, a.images, chunk)]
     outs = [None] * len(chunks)
 
     def step():
@@ -255,17 +259,18 @@ def main():
 
     if not a.no_extras:
         # dominant kernel: the global scan
-        sec, issued, algorithmic, peak = scan_roofline(vol, px, gset, dat[:a.chunk],
-                                                       ctf[:a.chunk], sig[:a.chunk], a.algo)
+        nRoof = min(ROOF_IMAGES, a.images)
+        sec, issued, algorithmic, peak = scan_roofline(vol, px, gset, dat[:nRoof],
+                                                       ctf[:nRoof], sig[:nRoof], a.algo)
         kname = {1: "k_scan_mfma (fp32 32x32x2)", 2: "k_scan_split<BF16X3> (bf16 32x32x16, 3-product split)"}
-        tr, tr_src = launch_traffic("scan_4096", a.algo == 2 and min(a.chunk, a.images) == 4096
+        tr, tr_src = launch_traffic("scan_4096", a.algo == 2 and nRoof == 4096
                                     and a.nr == 2000 and N == 256)
         extras["roofline"] = {"bound": "mfma", "achieved": issued / sec / 1e12,
                               "peak": peak, "unit": "TFLOP/s",
                               "frac": issued / sec / 1e12 / peak, "traffic": tr,
                               "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
                               "kernel": f"global scan {kname.get(a.algo, a.algo)} + prep + combine",
-                              "launch_ms": sec * 1e3, "images_per_launch": min(a.chunk, a.images),
+                              "launch_ms": sec * 1e3, "images_per_launch": nRoof,
                               "algorithmic_equiv_tflops": algorithmic / sec / 1e12,
                               "note": "achieved = issued matrix-core flops after the expansion of "
                                       "|d-cTP|^2 into a GEMM (4 fp32 flop, or 3x4 bf16 flop, per "
