@@ -100,6 +100,15 @@ class Reconstructor:
         return ops.insert3d(self.hm, dat, ctf, quat, trans, offS, w, px, tiled=tiled)
 
 
+def cloud_mode(quat):
+    """Medoid of each image's rotation cloud [nImg, m, 4] (max sum of squared
+    cosines to the other particles).  Systematic resampling leaves particles
+    in ancestor order, so index 0 is not the top particle; this is the
+    estimate of Particle::rank1st without the weights."""
+    c = torch.einsum("lik,ljk->lij", quat, quat) ** 2
+    return quat[torch.arange(quat.shape[0], device=quat.device), c.sum(-1).argmax(-1)]
+
+
 def draw_insert_samples(quat, trans, m_reco, seed=11):
     """Particle::rand (src/Particle.cpp:2109-2200): mReco uniform draws from the
     final particle sets of each image -> (quat [nImg,mReco,4], trans [nImg,mReco,2])."""
