@@ -192,6 +192,24 @@ int thx_resample(int nImg, int nIn, const double* w, const float* u,
                  int nOut, const double* u0, int* ancestor, double* wOut,
                  int* iMax, thx_stream_t stream);
 
+/* Particle statistics of the particle filter, one image per wave, nImg at a
+ * time (device pointers; FP64 particles, FP32 marginals):
+ * thx_pf_calvari -- Particle::calVari, 3D (src/Particle.cpp:1004-1121):
+ *   k[3 l + j-1] = max(kFloor, A(j,j)/A(0,0)) of inferACG
+ *   (src/Geometry/DirectionalStat.cpp:93-222) on the cloud de-meaned by its
+ *   ACG principal axis; sd[2 l + c] = max(sFloor, gsl_stats_sd(t_c)).
+ *   quat: nImg x mR x 4, trans: nImg x mT x 2.
+ * thx_pf_balance_rot -- Particle::balanceWeight(PAR_R), 3D
+ *   (src/Particle.cpp:2330-2340): pR = 1/pdfACG(q, inferACG(Q)), normalised.
+ * thx_pf_peak -- Particle::setPeakFactor(PAR_R) (src/Particle.cpp:1920-1925,
+ *   when setFactor) and keepHalfHeightPeak (:1964-1984) on u in place:
+ *   u: nImg rows of n floats at stride ldu, peak: nImg doubles (out / in). */
+int thx_pf_calvari(int nImg, int mR, const double* quat, int mT, const double* trans,
+                   double kFloor, double sFloor, double* k, double* sd, thx_stream_t stream);
+int thx_pf_balance_rot(int nImg, int mR, const double* quat, double* pR, thx_stream_t stream);
+int thx_pf_peak(int nImg, int n, float* u, int ldu, double* peak, int setFactor,
+                thx_stream_t stream);
+
 /* ----------------------------------------------------------------- a12 ---
  * Weighted trilinear Fourier-space back-projection of the CPU insert loop
  * (src/Optimiser.cpp:7036-7241 -> Reconstructor::insertP, src/Reconstructor.
@@ -254,7 +272,10 @@ typedef struct thx_expect_cfg {
     int nPhase;               /* local phases after the scan (10) */
     int algo;                 /* global-scan algorithm (thx_global_scan) */
     double perturbFactor;     /* perturbFactorSGlobal (0.5) */
-    double kMin, sMin;        /* scan floors: (mS^-1/3)^2, 1/chi2Qinv(.5,2)/sqrt(tsf pi) */
+    double kMin, sMin;        /* reseed floors of k1..k3 and s0, s1 (src/Optimiser.cpp:1033-1079,
+                                 OPTIMISER_SCAN_SET_MIN_STD_WITH_PERTURB):
+                                 (mS^-1/3 / perturbFactor)^2 and
+                                 1/chi2Qinv(.5,2)/sqrt(tsf pi) / perturbFactor */
     double transS, transM;    /* translation prior width, reCentre radius */
     unsigned long long seed;  /* counter-RNG seed */
 } thx_expect_cfg;

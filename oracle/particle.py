@@ -1,0 +1,92 @@
+"""numpy restatement of the deterministic particle-filter statistics (a10).
+
+TEST INFRASTRUCTURE ONLY (tests/ import it; the product path never does).
+Parity unpinned: the reference ships no fixtures for these functions; each
+function restates the reference source it cites, and tests/test_oracle.py
+pins the closed-form cases (an exact ACG sample's scatter, rank-1 clouds).
+"""
+import numpy as np
+
+PEAK_FACTOR_MAX, PEAK_FACTOR_MIN, PEAK_FACTOR_BASE = 0.5, 1e-3, 2   # include/Particle.h:52-57
+PERTURB_K_MAX = 1.0                                                  # include/Particle.h:64
+
+
+def qmul(a, b):
+    """quaternion_mul (src/Geometry/Euler.cpp), Hamilton product, rows."""
+    a, b = np.atleast_2d(a), np.atleast_2d(b)
+    w = a[:, 0] * b[:, 0] - a[:, 1] * b[:, 1] - a[:, 2] * b[:, 2] - a[:, 3] * b[:, 3]
+    x = a[:, 0] * b[:, 1] + a[:, 1] * b[:, 0] + a[:, 2] * b[:, 3] - a[:, 3] * b[:, 2]
+    y = a[:, 0] * b[:, 2] - a[:, 1] * b[:, 3] + a[:, 2] * b[:, 0] + a[:, 3] * b[:, 1]
+    z = a[:, 0] * b[:, 3] + a[:, 1] * b[:, 2] - a[:, 2] * b[:, 1] + a[:, 3] * b[:, 0]
+    return np.stack([w, x, y, z], axis=1)
+
+
+def conj(q):
+    return q * np.array([1.0, -1.0, -1.0, -1.0])
+
+
+def infer_acg(Q):
+    """inferACG(dmat44&, const dmat4&), src/Geometry/DirectionalStat.cpp:93-145:
+    Tyler's fixed point B = 4/nf sum q q^T / (q^T A^-1 q), from B = I, while
+    sum|A - B| > 1e-3; returns the last A.  A NaN criterion (a singular A on a
+    degenerate cloud) ends the loop like the reference's `while`."""
+    B = np.eye(4)
+    while True:
+        A = B
+        with np.errstate(all="ignore"):
+            Ai = np.linalg.inv(A) if np.all(np.isfinite(A)) and abs(np.linalg.det(A)) > 0 else \
+                np.full((4, 4), np.nan)
+            u = np.einsum("ij,jk,ik->i", Q, Ai, Q)
+            B = np.einsum("ij,ik->jk", Q / u[:, None], Q)
+            nf = np.sum(1.0 / u)
+            B = B * (4.0 / nf)
+        crit = np.abs(A - B).sum()
+        if not crit > 1e-3:
+            return A
+
+
+def principal_axis(A):
+    """Eigenvector of the largest eigenvalue (inferACG(dvec4&, ...),
+    DirectionalStat.cpp:224-251), unit norm; sign free."""
+    w, V = np.linalg.eigh(A)
+    return V[:, np.argmax(w)]
+
+
+def cal_vari_rot(Q):
+    """Particle::calVari(PAR_R), 3D, PARTICLE_ROT_MEAN_USING_STAT_CAL_VARI
+    (src/Particle.cpp:1011-1098): de-mean by the ACG principal axis, then
+    k_j = A(j, j) / A(0, 0) of inferACG on the de-meaned cloud (:184-222)."""
+    mean = principal_axis(infer_acg(Q))
+    A = infer_acg(qmul(conj(mean)[None, :], Q))
+    return A[1, 1] / A[0, 0], A[2, 2] / A[0, 0], A[3, 3] / A[0, 0]
+
+
+def cal_vari_trans(T):
+    """Particle::calVari(PAR_T) (src/Particle.cpp:1101-1121): gsl_stats_sd."""
+    return float(np.std(T[:, 0], ddof=1)), float(np.std(T[:, 1], ddof=1))
+
+
+def pdf_acg(x, A):
+    """pdfACG (DirectionalStat.cpp:19-24): det(A)^-1/2 (x^T A^-1 x)^-2."""
+    Ai = np.linalg.inv(A)
+    return np.linalg.det(A) ** -0.5 * np.einsum("ij,jk,ik->i", x, Ai, x) ** -2
+
+
+def balance_rot(Q):
+    """Particle::balanceWeight(PAR_R), 3D (src/Particle.cpp:2330-2340):
+    w_i = 1 / pdfACG(q_i, inferACG(Q)); returned normalised to sum 1."""
+    w = 1.0 / pdf_acg(Q, infer_acg(Q))
+    return w / w.sum()
+
+
+def peak_factor_rot(u):
+    """Particle::setPeakFactor(PAR_R), 3D (src/Particle.cpp:1920-1925)."""
+    s = np.sort(np.asarray(u, np.float64))[::-1]
+    return max(PEAK_FACTOR_MIN, min(PEAK_FACTOR_MAX, s[len(s) // PEAK_FACTOR_BASE ** 3] / s[0]))
+
+
+def keep_half_height(u, peak):
+    """Particle::keepHalfHeightPeak (src/Particle.cpp:1964-1984)."""
+    u = np.asarray(u, np.float64)
+    hh = u.max() * peak
+    return np.where(u < hh, 0.0, u - hh)

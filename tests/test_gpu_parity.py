@@ -366,3 +366,36 @@ def test_host_adapters_match_device_ops(orc, stack):
     rF, rT, rO, rc = orc.insert_batch(s["vdim"], s["pf"], dat, ctf, iq, it, off, w, s["px"], s["N"])
     assert np.max(np.abs(F - rF.view(np.float32))) <= 1e-5 * np.max(np.abs(rF.view(np.float32)))
     assert int(cnt[0]) == rc
+
+
+@pytest.mark.parametrize("spread", [0.0, 2.0, 10.0, 40.0])
+def test_particle_statistics_match_oracle(spread):
+    """calVari (ACG spreads of the de-meaned cloud, translation sd),
+    balanceWeight(PAR_R) priors and the peak factor / keepHalfHeightPeak of
+    the device particle filter against oracle/particle.py (spread 0: the
+    degenerate, all-equal cloud of a sharp reseed)."""
+    from oracle import particle as op
+    rng = np.random.default_rng(int(spread * 10) + 3)
+    nImg, mR, mT = 6, 125, 9
+    if spread > 0:
+        quat = synth.clustered_quaternions(nImg, mR, spread, rng)
+    else:
+        quat = np.repeat(synth.uniform_quaternions(nImg, rng)[:, None, :], mR, axis=1)
+    trans = rng.standard_normal((nImg, mT, 2)) * 2
+    k, sd = ops.pf_calvari(T(quat), T(trans), 1e-4, 0.1)
+    k, sd = k.cpu().numpy(), sd.cpu().numpy()
+    for l in range(nImg):
+        rk = np.maximum(1e-4, op.cal_vari_rot(quat[l]))
+        assert np.allclose(k[l], rk, rtol=1e-6, atol=1e-12), (k[l], rk)
+        assert np.allclose(sd[l], np.maximum(0.1, op.cal_vari_trans(trans[l])), rtol=1e-12)
+    if spread > 0:
+        pR = ops.pf_balance_rot(T(quat)).cpu().numpy()
+        for l in range(nImg):
+            assert np.allclose(pR[l], op.balance_rot(quat[l]), rtol=1e-6)
+    u = rng.exponential(1.0, (nImg, 2000)).astype(np.float32) ** 4
+    ud, peak = ops.pf_peak(T(u).clone())
+    ud, peak = ud.cpu().numpy(), peak.cpu().numpy()
+    for l in range(nImg):
+        rp = op.peak_factor_rot(u[l])
+        assert peak[l] == pytest.approx(rp, rel=1e-7)
+        assert np.allclose(ud[l], op.keep_half_height(u[l], rp), rtol=1e-6, atol=1e-6 * u[l].max())

@@ -267,3 +267,45 @@ def test_insert_batch_recentre_and_direction(orc):
             Oref += -(R @ np.array([*(t[l, m] - off[l]), 0.0]))
     assert np.allclose(O, Oref, atol=1e-12)
     assert np.sum(T) > 0 and np.isfinite(F).all()
+
+
+# ---------------------------------------------------------------- a10 stats
+def test_infer_acg_recovers_the_acg_matrix():
+    """Tyler's fixed point on n samples of ACG(S) estimates S up to scale
+    (trace 4 by construction of the iteration)."""
+    from oracle import particle as op
+    rng = np.random.default_rng(41)
+    S = np.diag([1.0, 0.3, 0.1, 0.05])
+    x = rng.standard_normal((20000, 4)) @ np.sqrt(S)
+    Q = x / np.linalg.norm(x, axis=1, keepdims=True)
+    A = op.infer_acg(Q)
+    assert abs(np.trace(A) - 4.0) < 1e-9
+    assert np.allclose(A, S * 4 / np.trace(S), atol=0.03)
+    k = op.cal_vari_rot(Q)
+    assert np.allclose(k, [0.3, 0.1, 0.05], rtol=0.1)
+
+
+def test_calvari_of_a_degenerate_cloud():
+    """All particles equal (a resampled sharp posterior): the reference's loop
+    leaves with A = 4 q q^T after the singular inverse turns the criterion to
+    NaN, and the de-meaned spreads are 0 (the scan floors then apply)."""
+    from oracle import particle as op
+    q = np.array([0.5, 0.5, -0.5, 0.5])
+    Q = np.tile(q, (125, 1))
+    assert np.allclose(op.infer_acg(Q), 4 * np.outer(q, q))
+    assert np.allclose(op.cal_vari_rot(Q), 0.0)
+
+
+def test_balance_and_peak_closed_forms():
+    from oracle import particle as op
+    rng = np.random.default_rng(42)
+    x = rng.standard_normal((4000, 4))
+    Q = x / np.linalg.norm(x, axis=1, keepdims=True)
+    w = op.balance_rot(Q)                 # near-uniform cloud: A ~ I, pdf ~ 1
+    assert np.allclose(w * len(w), 1.0, atol=0.2)
+    u = np.arange(1, 17, dtype=np.float64)             # 16 values: u_(16/8) = 14
+    assert op.peak_factor_rot(u) == 0.5                # 14/16 clamped to 0.5
+    u2 = np.array([100.0] + [1.0] * 15)
+    pk = op.peak_factor_rot(u2)
+    assert pk == 0.01
+    assert np.allclose(op.keep_half_height(u2, pk), [99.0] + [0.0] * 15)

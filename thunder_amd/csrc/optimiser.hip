@@ -4,9 +4,11 @@
 // no CTF search:
 //
 //   global scan (a4-a8) -> reseed every particle from the scan marginals
-//   (resample nR -> mLR, nT -> mLT; src/Optimiser.cpp:1930-2131) -> nPhase
-//   particle-filter phases, each: perturb (R, T) -> fused projection +
-//   likelihood + marginals (a6+a7+a9) -> calVari -> resample (a10).
+//   (keepHalfHeightPeak, resample nR -> mLR, nT -> mLT, calVari with the scan
+//   floors; src/Optimiser.cpp:1966-2079) -> nPhase particle-filter phases,
+//   each: perturb + balanceWeight (R, T) -> fused projection + likelihood +
+//   marginals (a6+a7+a9) -> keepHalfHeightPeak (R) -> calVari -> resample
+//   (a10; src/Optimiser.cpp:1183-1500).
 //
 // The reference leaves the particle filter on the host and round-trips to the
 // GPU once per image per phase (gpu/src/cuthunder.cu:2675-3140 with a stream
@@ -14,13 +16,13 @@
 // host only enqueues kernels (nothing synchronises, so the sequence can be
 // captured into a HIP graph).
 //
-// Simplifications of Particle (documented in DESIGN.md, row f3 of SURVEY §8):
-// the rotation perturbation uses the particle's top rotation as the ACG mean
-// and a diagonal ACG spread estimated from the de-meaned cloud (instead of the
-// fixed-point inferACG), the rotation prior after perturbation is uniform
-// (instead of 1/pdfACG), and the support is not shuffled before systematic
-// resampling.  Sampling is counter-based (Philox4x32-10), so a run is
-// reproducible for a given seed.
+// The particle statistics follow Particle / DirectionalStat with the
+// reference's Config.h switches: ACG means and spreads by inferACG's fixed
+// point, 1/pdfACG rotation priors, the 3D peak factor.  Not replicated: the
+// support shuffle before systematic resampling (it only decorrelates the
+// stratified draw from the particle order) and the generator: sampling is
+// counter-based (Philox4x32-10), so a run is reproducible for a given seed,
+// where the reference draws from an urandom-seeded GSL mt19937.
 #include "common.h"
 
 namespace {
@@ -74,6 +76,230 @@ THX_DEV void qmul(const double* a, const double* b, double* o)
     const double y = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
     const double z = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
     o[0] = w; o[1] = x; o[2] = y; o[3] = z;
+}
+
+// ------------------------------------------------- particle statistics (a10)
+// Angular central Gaussian estimates of src/Geometry/DirectionalStat.cpp on
+// one wave per image: lanes stride over the particles, every lane holds the
+// 4x4 matrices (FP64) and repeats the tiny dense algebra.
+
+// Inverse of a 4x4 matrix by cofactors; det == 0 or a non-finite input gives
+// NaNs (the reference's Eigen inverse of a singular A does too).
+THX_DEV double inv4(const double* m, double* o)
+{
+    o[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    o[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    o[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    o[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    o[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    o[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    o[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    o[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    o[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    o[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    o[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    o[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    o[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    o[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    o[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    o[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    const double det = m[0] * o[0] + m[1] * o[4] + m[2] * o[8] + m[3] * o[12];
+    const double r = det != 0.0 ? 1.0 / det : __builtin_nan("");
+    for (int k = 0; k < 16; k++) o[k] *= r;
+    return det;
+}
+
+THX_DEV double quad4(const double* q, const double* M)
+{
+    double s = 0.0;
+    for (int j = 0; j < 4; j++)
+        for (int k = 0; k < 4; k++) s += q[j] * M[4 * j + k] * q[k];
+    return s;
+}
+
+// inferACG(dmat44&, const dmat4&), DirectionalStat.cpp:93-145: Tyler's fixed
+// point B = 4/nf sum q q^T / (q^T A^-1 q) from B = I while sum|A - B| > 1e-3
+// (a NaN criterion ends the loop, as in the reference's `while`); returns the
+// last A.  Particle q_i is read as pre q_i (pre = conj(mean) de-means).
+THX_DEV void infer_acg(const double* Q, int m, const double* pre, int lane, double* A)
+{
+    double B[16];
+    for (int k = 0; k < 16; k++) B[k] = (k % 5 == 0) ? 1.0 : 0.0;
+    for (int it = 0; it < 256; it++) {
+        for (int k = 0; k < 16; k++) A[k] = B[k];
+        double Ai[16];
+        inv4(A, Ai);
+        double b[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nf = 0.0;
+        for (int i = lane; i < m; i += 64) {
+            double q[4];
+            if (pre) qmul(pre, Q + 4 * i, q);
+            else for (int k = 0; k < 4; k++) q[k] = Q[4 * i + k];
+            const double r = 1.0 / quad4(q, Ai);
+            int t = 0;
+            for (int j = 0; j < 4; j++)
+                for (int k = j; k < 4; k++) b[t++] += q[j] * q[k] * r;
+            nf += r;
+        }
+        for (int t = 0; t < 10; t++) b[t] = wave_sum(b[t]);
+        nf = wave_sum(nf);
+        int t = 0;
+        for (int j = 0; j < 4; j++)
+            for (int k = j; k < 4; k++, t++) B[4 * j + k] = B[4 * k + j] = b[t] * (4.0 / nf);
+        double crit = 0.0;
+        for (int k = 0; k < 16; k++) crit += fabs(A[k] - B[k]);
+        if (!(crit > 1e-3)) return;
+    }
+}
+
+// Unit eigenvector of the largest eigenvalue of a symmetric 4x4 (cyclic
+// Jacobi), the mean of inferACG(dvec4&, ...), DirectionalStat.cpp:224-251.
+THX_DEV void principal_axis(const double* A0, double* v)
+{
+    double a[16], V[16];
+    for (int k = 0; k < 16; k++) { a[k] = A0[k]; V[k] = (k % 5 == 0) ? 1.0 : 0.0; }
+    for (int sweep = 0; sweep < 32; sweep++) {
+        double off = 0.0, dia = 0.0;
+        for (int p = 0; p < 4; p++)
+            for (int q = 0; q < 4; q++) (p == q ? dia : off) += a[4 * p + q] * a[4 * p + q];
+        if (!(off > 1e-30 * dia)) break;
+        for (int p = 0; p < 3; p++)
+            for (int q = p + 1; q < 4; q++) {
+                const double apq = a[4 * p + q];
+                if (apq == 0.0) continue;
+                const double th = (a[4 * q + q] - a[4 * p + p]) / (2.0 * apq);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 4; k++) {      // a <- a J
+                    const double x = a[4 * k + p], y = a[4 * k + q];
+                    a[4 * k + p] = c * x - s * y;
+                    a[4 * k + q] = s * x + c * y;
+                }
+                for (int k = 0; k < 4; k++) {      // a <- J^T a
+                    const double x = a[4 * p + k], y = a[4 * q + k];
+                    a[4 * p + k] = c * x - s * y;
+                    a[4 * q + k] = s * x + c * y;
+                }
+                for (int k = 0; k < 4; k++) {      // V <- V J
+                    const double x = V[4 * k + p], y = V[4 * k + q];
+                    V[4 * k + p] = c * x - s * y;
+                    V[4 * k + q] = s * x + c * y;
+                }
+            }
+    }
+    int best = 0;
+    for (int k = 1; k < 4; k++)
+        if (a[5 * k] > a[5 * best]) best = k;
+    double n = 0.0;
+    for (int k = 0; k < 4; k++) n += V[4 * k + best] * V[4 * k + best];
+    n = sqrt(n);
+    for (int k = 0; k < 4; k++) v[k] = V[4 * k + best] / n;
+}
+
+// Particle::calVari (src/Particle.cpp:1004-1121), 3D: R -- de-mean by the
+// ACG principal axis (PARTICLE_ROT_MEAN_USING_STAT_CAL_VARI), k_j =
+// A(j, j) / A(0, 0) of inferACG on the de-meaned cloud (:184-222), floored at
+// kFloor; T -- sample standard deviations (gsl_stats_sd), floored at sFloor
+// (the reseed floors of src/Optimiser.cpp:1033-1079).
+__global__ void __launch_bounds__(256) k_pf_calvari(int nImg, int mR, const double* __restrict__ quat,
+                                                    int mT, const double* __restrict__ trans,
+                                                    double kFloor, double sFloor,
+                                                    double* __restrict__ kOut,
+                                                    double* __restrict__ sOut)
+{
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (l >= nImg) return;
+    const double* Q = quat + (size_t)l * mR * 4;
+    double A[16], mean[4], cm[4];
+    infer_acg(Q, mR, nullptr, lane, A);
+    principal_axis(A, mean);
+    cm[0] = mean[0]; cm[1] = -mean[1]; cm[2] = -mean[2]; cm[3] = -mean[3];
+    infer_acg(Q, mR, cm, lane, A);
+    const double* Tr = trans + (size_t)l * mT * 2;
+    double sx = 0, sy = 0;
+    for (int i = lane; i < mT; i += 64) { sx += Tr[2 * i]; sy += Tr[2 * i + 1]; }
+    sx = wave_sum(sx) / mT; sy = wave_sum(sy) / mT;
+    double vx = 0, vy = 0;
+    for (int i = lane; i < mT; i += 64) {
+        vx += (Tr[2 * i] - sx) * (Tr[2 * i] - sx);
+        vy += (Tr[2 * i + 1] - sy) * (Tr[2 * i + 1] - sy);
+    }
+    vx = wave_sum(vx); vy = wave_sum(vy);
+    if (lane == 0) {
+        for (int j = 1; j < 4; j++) kOut[3 * l + j - 1] = fmax(kFloor, A[5 * j] / A[0]);
+        sOut[2 * l] = fmax(sFloor, mT > 1 ? sqrt(vx / (mT - 1)) : 0.0);
+        sOut[2 * l + 1] = fmax(sFloor, mT > 1 ? sqrt(vy / (mT - 1)) : 0.0);
+    }
+}
+
+// Particle::balanceWeight(PAR_R), 3D (src/Particle.cpp:2330-2340):
+// w_i = 1 / pdfACG(q_i, inferACG(Q)), pdfACG = det(A)^-1/2 (q^T A^-1 q)^-2
+// (DirectionalStat.cpp:19-24), normalised to sum 1 (the scale cancels in
+// resample's w u / sum).
+THX_DEV void balance_rot(const double* Q, int m, int lane, double* w)
+{
+    double A[16], Ai[16];
+    infer_acg(Q, m, nullptr, lane, A);
+    const double det = inv4(A, Ai);
+    const double sd = sqrt(det);
+    double tot = 0.0;
+    for (int i = lane; i < m; i += 64) {
+        const double u = quad4(Q + 4 * i, Ai);
+        const double x = sd * u * u;
+        w[i] = x;
+        tot += x;
+    }
+    tot = wave_sum(tot);
+    for (int i = lane; i < m; i += 64) w[i] /= tot;
+}
+
+// Particle::setPeakFactor(PAR_R), 3D (src/Particle.cpp:1920-1925) when
+// setFactor: peak = clamp(u_(n/8) / u_max, 1e-3, 0.5) with u_(k) the k-th
+// largest (0-based); then keepHalfHeightPeak (:1964-1984) in place:
+// u <- u < hh ? 0 : u - hh, hh = u_max peak.  u >= 0, so the k-th largest is
+// found by a bisection over the ordered float bit patterns.
+__global__ void __launch_bounds__(256) k_pf_peak(int nImg, int n, float* __restrict__ u, int ldu,
+                                                 double* __restrict__ peak, int setFactor)
+{
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (l >= nImg) return;
+    float* ul = u + (size_t)l * ldu;
+    float mx = 0.f;
+    for (int i = lane; i < n; i += 64) mx = fmaxf(mx, ul[i]);
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    double pk;
+    if (setFactor) {
+        const int k = n / 8;
+        // largest bit pattern v with count(u >= v) >= k + 1
+        uint32_t lo = 0, hi = __float_as_uint(mx);
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo + 1) / 2;
+            int c = 0;
+            for (int i = lane; i < n; i += 64) c += __float_as_uint(ul[i]) >= mid;
+            for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+            if (c >= k + 1) lo = mid; else hi = mid - 1;
+        }
+        const double r = mx > 0.f ? (double)__uint_as_float(lo) / (double)mx : 0.0;
+        pk = fmax(1e-3, fmin(0.5, r));
+        if (lane == 0) peak[l] = pk;
+    } else {
+        pk = peak[l];
+    }
+    const double hh = (double)mx * pk;
+    for (int i = lane; i < n; i += 64) {
+        const double v = ul[i];
+        ul[i] = v < hh ? 0.f : (float)(v - hh);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pf_balance_rot(int nImg, int mR,
+                                                        const double* __restrict__ quat,
+                                                        double* __restrict__ pR)
+{
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (l >= nImg) return;
+    balance_rot(quat + (size_t)l * mR * 4, mR, threadIdx.x & 63, pR + (size_t)l * mR);
 }
 
 // --------------------------------------------------------------- resample
@@ -166,23 +392,23 @@ __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
     }
 }
 
-// calVari + perturb + balanceWeight for one image per wave.
-//   R: de-mean by the top rotation, k_j = <q_j^2> / <q_0^2> (the diagonal of
-//      inferACG's A, src/Particle.cpp:1004-1098 / DirectionalStat.cpp:184-222),
-//      floored at kMin; perturb r_i <- top d_i top^-1 r_i with
+// Particle::perturb + balanceWeight for one image per wave
+// (src/Particle.cpp:1149-1289, 2309-2375), with k / s from k_pf_calvari:
+//   R: mean = ACG principal axis of the current cloud
+//      (PARTICLE_ROT_MEAN_USING_STAT_PERTURB), r_i <- mean d_i mean^-1 r_i with
 //      d ~ ACG(diag(1, pf^2 min(1,k1), pf^2 min(1,k2), pf^2 min(1,k3)))
-//      (Particle::perturb, src/Particle.cpp:1176-1230).
-//   T: s_c = sd(t_c) floored at sMin, t_i += pf * N(0, s) (src/Particle.cpp:
-//      1232-1262), reCentre beyond transM (:2473-2495), pT = 1/pdf normalised
-//      (balanceWeight, :2340-2375).
+//      (sampleACG: normalised N(0, diag)), then pR = 1 / pdfACG on the
+//      perturbed cloud (balanceWeight(PAR_R)).
+//   T: t_i += pf N(0, s) (:1232-1262), reCentre beyond transM (:2473-2495),
+//      pT = 1/pdf normalised (balanceWeight(PAR_T), :2342-2375).
 __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
                                                     double* __restrict__ quat,
                                                     double* __restrict__ trans,
                                                     double* __restrict__ pR,
                                                     double* __restrict__ pT,
-                                                    const double* __restrict__ topQ,
-                                                    double pf, double kMin, double sMin,
-                                                    double transS, double transM,
+                                                    const double* __restrict__ kIn,
+                                                    const double* __restrict__ sIn,
+                                                    double pf, double transS, double transM,
                                                     uint64_t seed, uint32_t stream)
 {
     const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -193,46 +419,33 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
     Philox rng(seed, (uint32_t)l, stream, (uint32_t)lane);
 
     // ---- rotation
-    double top[4], topc[4];
-    for (int k = 0; k < 4; k++) top[k] = topQ[4 * l + k];
-    topc[0] = top[0]; topc[1] = -top[1]; topc[2] = -top[2]; topc[3] = -top[3];
-    double m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-    for (int i = lane; i < mR; i += 64) {
-        double d[4];
-        qmul(topc, Q + 4 * i, d);
-        m0 += d[0] * d[0]; m1 += d[1] * d[1]; m2 += d[2] * d[2]; m3 += d[3] * d[3];
-    }
-    m0 = wave_sum(m0); m1 = wave_sum(m1); m2 = wave_sum(m2); m3 = wave_sum(m3);
-    const double k1 = fmin(1.0, fmax(kMin, m1 / m0));
-    const double k2 = fmin(1.0, fmax(kMin, m2 / m0));
-    const double k3 = fmin(1.0, fmax(kMin, m3 / m0));
-    const double sd1 = pf * sqrt(k1), sd2 = pf * sqrt(k2), sd3 = pf * sqrt(k3);
+    double A[16], mean[4], cm[4];
+    infer_acg(Q, mR, nullptr, lane, A);
+    principal_axis(A, mean);
+    cm[0] = mean[0]; cm[1] = -mean[1]; cm[2] = -mean[2]; cm[3] = -mean[3];
+    const double sd1 = pf * sqrt(fmin(1.0, kIn[3 * l]));       // PERTURB_K_MAX = 1
+    const double sd2 = pf * sqrt(fmin(1.0, kIn[3 * l + 1]));
+    const double sd3 = pf * sqrt(fmin(1.0, kIn[3 * l + 2]));
     for (int i = lane; i < mR; i += 64) {
         const double2 g0 = rng.gauss2(), g1 = rng.gauss2();
         double d[4] = {g0.x, g0.y * sd1, g1.x * sd2, g1.y * sd3};
         const double nn = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]);
         for (int k = 0; k < 4; k++) d[k] /= nn;
         double a[4], b[4], c[4];
-        qmul(topc, Q + 4 * i, a);      // conj(mean) * r
+        qmul(cm, Q + 4 * i, a);        // conj(mean) * r
         qmul(d, a, b);                 // pert * .
-        qmul(top, b, c);               // mean * .
+        qmul(mean, b, c);              // mean * .
         const double cn = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2] + c[3] * c[3]);
         for (int k = 0; k < 4; k++) Q[4 * i + k] = c[k] / cn;
-        pR[(size_t)l * mR + i] = 1.0 / mR;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    balance_rot(Q, mR, lane, pR + (size_t)l * mR);
 
     // ---- translation
-    double sx = 0, sy = 0;
-    for (int i = lane; i < mT; i += 64) { sx += Tr[2 * i]; sy += Tr[2 * i + 1]; }
-    sx = wave_sum(sx) / mT; sy = wave_sum(sy) / mT;
-    double vx = 0, vy = 0;
-    for (int i = lane; i < mT; i += 64) {
-        vx += (Tr[2 * i] - sx) * (Tr[2 * i] - sx);
-        vy += (Tr[2 * i + 1] - sy) * (Tr[2 * i + 1] - sy);
-    }
-    vx = wave_sum(vx); vy = wave_sum(vy);
-    const double s0 = fmax(sMin, mT > 1 ? sqrt(vx / (mT - 1)) : 0.0);
-    const double s1 = fmax(sMin, mT > 1 ? sqrt(vy / (mT - 1)) : 0.0);
+    const double s0 = sIn[2 * l], s1 = sIn[2 * l + 1];
+    double sx, sy, vx, vy;
     for (int i = lane; i < mT; i += 64) {
         const double2 g = rng.gauss2();
         double x = Tr[2 * i] + g.x * s0 * pf, y = Tr[2 * i + 1] + g.y * s1 * pf;
@@ -275,7 +488,8 @@ struct Plan {
     float* gWC; float* gWR; float* gWT; float* gBase;
     void* scanWs; size_t scanWsBytes;
     int* anc; double* cdf; int* topR; int* topT;
-    double* tmpQ; double* tmpT; double* topQ;
+    double* tmpQ; double* tmpT;
+    double* kv; double* sv; double* peakR;   // calVari k1..k3, s0 s1; setPeakFactor(R)
     float* wC; float* wR; float* wT; float* base; double* pC;
     void* localWs; size_t localWsBytes;
     size_t bytes;
@@ -301,7 +515,9 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     p.topT = k.take<int>(nImg);
     p.tmpQ = k.take<double>((size_t)nImg * c.mLR * 4);
     p.tmpT = k.take<double>((size_t)nImg * c.mLT * 2);
-    p.topQ = k.take<double>((size_t)nImg * 4);
+    p.kv = k.take<double>((size_t)nImg * 3);
+    p.sv = k.take<double>((size_t)nImg * 2);
+    p.peakR = k.take<double>(nImg);
     p.wC = k.take<float>(nImg);
     p.wR = k.take<float>((size_t)nImg * c.mLR);
     p.wT = k.take<float>((size_t)nImg * c.mLT);
@@ -313,16 +529,6 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     return p;
 }
 
-// topQ[l] = src[l (or shared)][top[l]] -- Particle::_topR after calRank1st
-__global__ void k_top_copy(int nImg, const double* __restrict__ src, long lds,
-                           const int* __restrict__ top, double* __restrict__ topQ)
-{
-    const int q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= nImg * 4) return;
-    const int l = q / 4, k = q % 4;
-    topQ[q] = src[(size_t)l * lds + (size_t)top[l] * 4 + k];
-}
-
 __global__ void k_fill(double* p, long n, double v)
 {
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x)
@@ -330,6 +536,43 @@ __global__ void k_fill(double* p, long n, double v)
 }
 
 }  // namespace
+
+extern "C" int thx_pf_calvari(int nImg, int mR, const double* quat, int mT, const double* trans,
+                              double kFloor, double sFloor, double* k, double* sd,
+                              thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && mR > 0 && mT > 0, "thx_pf_calvari: bad sizes");
+    THX_CHECK_ARG(nImg == 0 || (quat && trans && k && sd), "thx_pf_calvari: null argument");
+    if (nImg == 0) return THX_OK;
+    hipLaunchKernelGGL(k_pf_calvari, dim3(thx::cdiv(nImg, 4)), dim3(256), 0,
+                       thx::as_stream(stream), nImg, mR, quat, mT, trans, kFloor, sFloor, k, sd);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" int thx_pf_balance_rot(int nImg, int mR, const double* quat, double* pR,
+                                  thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && mR > 0, "thx_pf_balance_rot: bad sizes");
+    THX_CHECK_ARG(nImg == 0 || (quat && pR), "thx_pf_balance_rot: null argument");
+    if (nImg == 0) return THX_OK;
+    hipLaunchKernelGGL(k_pf_balance_rot, dim3(thx::cdiv(nImg, 4)), dim3(256), 0,
+                       thx::as_stream(stream), nImg, mR, quat, pR);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" int thx_pf_peak(int nImg, int n, float* u, int ldu, double* peak, int setFactor,
+                           thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && n > 0 && ldu >= n, "thx_pf_peak: bad sizes");
+    THX_CHECK_ARG(nImg == 0 || (u && peak), "thx_pf_peak: null argument");
+    if (nImg == 0) return THX_OK;
+    hipLaunchKernelGGL(k_pf_peak, dim3(thx::cdiv(nImg, 4)), dim3(256), 0,
+                       thx::as_stream(stream), nImg, n, u, ldu, peak, setFactor);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
 
 extern "C" size_t thx_expectation_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl,
                                             int nOrd)
@@ -379,15 +622,16 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                             gPT, 0, 1, p.gWC, p.gWR, p.gWT, p.gBase, c.algo, p.scanWs,
                             p.scanWsBytes, stream));
 
-    // ---- reseed from the scan marginals (src/Optimiser.cpp:1930-2131)
+    // ---- reseed from the scan marginals (src/Optimiser.cpp:1966-2079):
+    // setPeakFactor + keepHalfHeightPeak (R), resample R and T, calVari with
+    // the scan floors (OPTIMISER_SCAN_SET_MIN_STD_WITH_PERTURB)
+    hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.nR, p.gWR, c.nR, p.peakR, 1);
+    THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nR, c.mLR, gPR, 0,
                        p.gWR, c.nR, c.seed, 1000u, p.anc, pR, p.topR, p.cdf);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, gQuat, 0L, c.nR,
                        p.anc, quat);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg, gQuat,
-                       0L, p.topR, p.topQ);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nT, c.mLT, gPT, 0,
                        p.gWT, c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf);
@@ -395,20 +639,29 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, gTrans, 0L, c.nT,
                        p.anc, trans);
     THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_pf_calvari, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT, trans,
+                       c.kMin, c.sMin, p.kv, p.sv);
+    THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, s, p.pC, (long)nImg, 1.0);
     THX_LAUNCH_CHECK();
 
-    // ---- particle-filter phases (src/Optimiser.cpp:1183-1616)
+    // ---- particle-filter phases (src/Optimiser.cpp:1183-1500): perturb +
+    // balanceWeight, likelihood + marginals, keepHalfHeightPeak (R),
+    // calRank1st, calVari (pre-resample cloud), resample
     for (int phase = 1; phase <= c.nPhase; phase++) {
-        const double kMin = phase == 1 ? c.kMin : 1e-8;
-        const double sMin = phase == 1 ? c.sMin : 1e-6;
         hipLaunchKernelGGL(k_pf_perturb, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
-                           trans, pR, pT, p.topQ, c.perturbFactor, kMin, sMin,
-                           c.transS, c.transM, c.seed, (uint32_t)(2000 + phase));
+                           trans, pR, pT, p.kv, p.sv, c.perturbFactor, c.transS, c.transM,
+                           c.seed, (uint32_t)(2000 + phase));
         THX_LAUNCH_CHECK();
         THX_RET(thx_local_phase(vol, 0, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT, dat,
                                 ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, c.idim, nImg, p.wC, p.wR, p.wT,
                                 p.base, nullptr, p.localWs, p.localWsBytes, stream));
+        hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
+                           p.peakR, 0);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_pf_calvari, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT,
+                           trans, 0.0, 0.0, p.kv, p.sv);
+        THX_LAUNCH_CHECK();
         // resample R and T by the phase marginals; ancestors gathered in place
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, c.mLR, pR,
                            c.mLR, p.wR, c.mLR, c.seed, (uint32_t)(3000 + phase), p.anc, pR,
@@ -418,9 +671,6 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                                hipMemcpyDeviceToDevice, s));
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, p.tmpQ,
                            (long)c.mLR * 4, c.mLR, p.anc, quat);
-        THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg,
-                           p.tmpQ, (long)c.mLR * 4, p.topR, p.topQ);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLT, c.mLT, pT,
                            c.mLT, p.wT, c.mLT, c.seed, (uint32_t)(4000 + phase), p.anc, pT,

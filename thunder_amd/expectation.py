@@ -53,8 +53,12 @@ class Expectation:
         scan_min_std_r = nR ** (-1.0 / 3)                    # src/Optimiser.cpp:765-771
         scan_min_std_t = 1.0 / synth.CHI2_QINV_HALF_2DOF / math.sqrt(trans_search_factor * math.pi)
         trans_m = trans_s * (-2.0 * math.log(0.05))           # reCentre, TRANS_Q = 0.05
+        # reseed floors with OPTIMISER_SCAN_SET_MIN_STD_WITH_PERTURB (include/Config.h:224,
+        # src/Optimiser.cpp:1033-1079); MIN_STD_FACTOR = 1
+        k_floor = (scan_min_std_r / perturb) ** 2
+        s_floor = scan_min_std_t / perturb
         self.cfg = ExpectCfg(px.idim, px.pf, vdim, nR, nT, mLR, mLT, n_phase, algo, perturb,
-                             scan_min_std_r ** 2, scan_min_std_t, trans_s, trans_m, seed)
+                             k_floor, s_floor, trans_s, trans_m, seed)
         self.mLR, self.mLT = mLR, mLT
 
     def workspace_bytes(self, nImg):

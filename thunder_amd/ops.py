@@ -310,3 +310,42 @@ def fsc(A, B, n_shell):
     check(lib().thx_fsc(_ptr(A), _ptr(B), vdim, n_shell, _ptr(out), _ptr(ws), ws.numel(),
                         _stream(A.device)), "thx_fsc")
     return out
+
+
+def pf_calvari(quat, trans, k_floor=0.0, s_floor=0.0):
+    """thx_pf_calvari: per-image ACG spreads (k1, k2, k3) and translation
+    standard deviations (s0, s1) of particle clouds quat [nImg, mR, 4],
+    trans [nImg, mT, 2] (float64, device)."""
+    nImg, mR = quat.shape[:2]
+    mT = trans.shape[1]
+    _req(quat, torch.float64, (nImg, mR, 4), "quat")
+    _req(trans, torch.float64, (nImg, mT, 2), "trans")
+    k = torch.empty(nImg, 3, dtype=torch.float64, device=quat.device)
+    sd = torch.empty(nImg, 2, dtype=torch.float64, device=quat.device)
+    check(lib().thx_pf_calvari(nImg, mR, _ptr(quat), mT, _ptr(trans), k_floor, s_floor, _ptr(k),
+                               _ptr(sd), _stream(quat.device)), "thx_pf_calvari")
+    return k, sd
+
+
+def pf_balance_rot(quat):
+    """thx_pf_balance_rot: normalised 1/pdfACG rotation priors [nImg, mR]."""
+    nImg, mR = quat.shape[:2]
+    _req(quat, torch.float64, (nImg, mR, 4), "quat")
+    pR = torch.empty(nImg, mR, dtype=torch.float64, device=quat.device)
+    check(lib().thx_pf_balance_rot(nImg, mR, _ptr(quat), _ptr(pR), _stream(quat.device)),
+          "thx_pf_balance_rot")
+    return pR
+
+
+def pf_peak(u, peak=None):
+    """thx_pf_peak: keepHalfHeightPeak on marginals u [nImg, n] float32 (in
+    place); sets the 3D peak factor first when ``peak`` is None.  Returns
+    (u, peak)."""
+    nImg, n = u.shape
+    _req(u, torch.float32, (nImg, n), "u")
+    set_factor = peak is None
+    if set_factor:
+        peak = torch.empty(nImg, dtype=torch.float64, device=u.device)
+    check(lib().thx_pf_peak(nImg, n, _ptr(u), n, _ptr(peak), int(set_factor), _stream(u.device)),
+          "thx_pf_peak")
+    return u, peak
