@@ -17,8 +17,9 @@
 // captured into a HIP graph).
 //
 // The particle statistics follow Particle / DirectionalStat with the
-// reference's Config.h switches: ACG means and spreads by inferACG's fixed
-// point, 1/pdfACG rotation priors, the 3D peak factor.  Not replicated: the
+// reference's Config.h switches: ACG spreads by inferACG's fixed point,
+// 1/pdfACG rotation priors, the 3D peak factor.  Not replicated: the
+// perturbation mean (the top particle, see k_pf_perturb), the
 // support shuffle before systematic resampling (it only decorrelates the
 // stratified draw from the particle order) and the generator: sampling is
 // counter-based (Philox4x32-10), so a run is reproducible for a given seed,
@@ -109,6 +110,18 @@ THX_DEV double inv4(const double* m, double* o)
     return det;
 }
 
+// Particle statistics run one image per GROUP lanes (4 images per wave): the
+// 4x4 algebra is repeated by every lane anyway, so narrower groups mean 4x
+// fewer waves for the same latency-bound FP64 chains.
+constexpr int GROUP = 16;
+
+THX_DEV double group_sum(double v)
+{
+#pragma unroll
+    for (int o = GROUP / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 THX_DEV double quad4(const double* q, const double* M)
 {
     double s = 0.0;
@@ -130,7 +143,7 @@ THX_DEV void infer_acg(const double* Q, int m, const double* pre, int lane, doub
         double Ai[16];
         inv4(A, Ai);
         double b[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nf = 0.0;
-        for (int i = lane; i < m; i += 64) {
+        for (int i = lane; i < m; i += GROUP) {
             double q[4];
             if (pre) qmul(pre, Q + 4 * i, q);
             else for (int k = 0; k < 4; k++) q[k] = Q[4 * i + k];
@@ -140,8 +153,8 @@ THX_DEV void infer_acg(const double* Q, int m, const double* pre, int lane, doub
                 for (int k = j; k < 4; k++) b[t++] += q[j] * q[k] * r;
             nf += r;
         }
-        for (int t = 0; t < 10; t++) b[t] = wave_sum(b[t]);
-        nf = wave_sum(nf);
+        for (int t = 0; t < 10; t++) b[t] = group_sum(b[t]);
+        nf = group_sum(nf);
         int t = 0;
         for (int j = 0; j < 4; j++)
             for (int k = j; k < 4; k++, t++) B[4 * j + k] = B[4 * k + j] = b[t] * (4.0 / nf);
@@ -206,8 +219,8 @@ __global__ void __launch_bounds__(256) k_pf_calvari(int nImg, int mR, const doub
                                                     double* __restrict__ kOut,
                                                     double* __restrict__ sOut)
 {
-    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+    const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
+    const int lane = threadIdx.x % GROUP;
     if (l >= nImg) return;
     const double* Q = quat + (size_t)l * mR * 4;
     double A[16], mean[4], cm[4];
@@ -217,14 +230,14 @@ __global__ void __launch_bounds__(256) k_pf_calvari(int nImg, int mR, const doub
     infer_acg(Q, mR, cm, lane, A);
     const double* Tr = trans + (size_t)l * mT * 2;
     double sx = 0, sy = 0;
-    for (int i = lane; i < mT; i += 64) { sx += Tr[2 * i]; sy += Tr[2 * i + 1]; }
-    sx = wave_sum(sx) / mT; sy = wave_sum(sy) / mT;
+    for (int i = lane; i < mT; i += GROUP) { sx += Tr[2 * i]; sy += Tr[2 * i + 1]; }
+    sx = group_sum(sx) / mT; sy = group_sum(sy) / mT;
     double vx = 0, vy = 0;
-    for (int i = lane; i < mT; i += 64) {
+    for (int i = lane; i < mT; i += GROUP) {
         vx += (Tr[2 * i] - sx) * (Tr[2 * i] - sx);
         vy += (Tr[2 * i + 1] - sy) * (Tr[2 * i + 1] - sy);
     }
-    vx = wave_sum(vx); vy = wave_sum(vy);
+    vx = group_sum(vx); vy = group_sum(vy);
     if (lane == 0) {
         for (int j = 1; j < 4; j++) kOut[3 * l + j - 1] = fmax(kFloor, A[5 * j] / A[0]);
         sOut[2 * l] = fmax(sFloor, mT > 1 ? sqrt(vx / (mT - 1)) : 0.0);
@@ -243,14 +256,14 @@ THX_DEV void balance_rot(const double* Q, int m, int lane, double* w)
     const double det = inv4(A, Ai);
     const double sd = sqrt(det);
     double tot = 0.0;
-    for (int i = lane; i < m; i += 64) {
+    for (int i = lane; i < m; i += GROUP) {
         const double u = quad4(Q + 4 * i, Ai);
         const double x = sd * u * u;
         w[i] = x;
         tot += x;
     }
-    tot = wave_sum(tot);
-    for (int i = lane; i < m; i += 64) w[i] /= tot;
+    tot = group_sum(tot);
+    for (int i = lane; i < m; i += GROUP) w[i] /= tot;
 }
 
 // Particle::setPeakFactor(PAR_R), 3D (src/Particle.cpp:1920-1925) when
@@ -297,9 +310,9 @@ __global__ void __launch_bounds__(256) k_pf_balance_rot(int nImg, int mR,
                                                         const double* __restrict__ quat,
                                                         double* __restrict__ pR)
 {
-    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
     if (l >= nImg) return;
-    balance_rot(quat + (size_t)l * mR * 4, mR, threadIdx.x & 63, pR + (size_t)l * mR);
+    balance_rot(quat + (size_t)l * mR * 4, mR, threadIdx.x % GROUP, pR + (size_t)l * mR);
 }
 
 // --------------------------------------------------------------- resample
@@ -394,8 +407,10 @@ __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
 
 // Particle::perturb + balanceWeight for one image per wave
 // (src/Particle.cpp:1149-1289, 2309-2375), with k / s from k_pf_calvari:
-//   R: mean = ACG principal axis of the current cloud
-//      (PARTICLE_ROT_MEAN_USING_STAT_PERTURB), r_i <- mean d_i mean^-1 r_i with
+//   R: mean = the top particle (calRank1st's _topR, the reference's branch
+//      without PARTICLE_ROT_MEAN_USING_STAT_PERTURB: Config.h turns that switch
+//      on, but inferACG of a resampled cloud of few distinct ancestors
+//      converges slowly or not at all), r_i <- mean d_i mean^-1 r_i with
 //      d ~ ACG(diag(1, pf^2 min(1,k1), pf^2 min(1,k2), pf^2 min(1,k3)))
 //      (sampleACG: normalised N(0, diag)), then pR = 1 / pdfACG on the
 //      perturbed cloud (balanceWeight(PAR_R)).
@@ -406,27 +421,27 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
                                                     double* __restrict__ trans,
                                                     double* __restrict__ pR,
                                                     double* __restrict__ pT,
+                                                    const double* __restrict__ topQ,
                                                     const double* __restrict__ kIn,
                                                     const double* __restrict__ sIn,
                                                     double pf, double transS, double transM,
                                                     uint64_t seed, uint32_t stream)
 {
-    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+    const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
+    const int lane = threadIdx.x % GROUP;
     if (l >= nImg) return;
     double* Q = quat + (size_t)l * mR * 4;
     double* Tr = trans + (size_t)l * mT * 2;
     Philox rng(seed, (uint32_t)l, stream, (uint32_t)lane);
 
     // ---- rotation
-    double A[16], mean[4], cm[4];
-    infer_acg(Q, mR, nullptr, lane, A);
-    principal_axis(A, mean);
+    double mean[4], cm[4];
+    for (int k = 0; k < 4; k++) mean[k] = topQ[4 * l + k];
     cm[0] = mean[0]; cm[1] = -mean[1]; cm[2] = -mean[2]; cm[3] = -mean[3];
     const double sd1 = pf * sqrt(fmin(1.0, kIn[3 * l]));       // PERTURB_K_MAX = 1
     const double sd2 = pf * sqrt(fmin(1.0, kIn[3 * l + 1]));
     const double sd3 = pf * sqrt(fmin(1.0, kIn[3 * l + 2]));
-    for (int i = lane; i < mR; i += 64) {
+    for (int i = lane; i < mR; i += GROUP) {
         const double2 g0 = rng.gauss2(), g1 = rng.gauss2();
         double d[4] = {g0.x, g0.y * sd1, g1.x * sd2, g1.y * sd3};
         const double nn = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]);
@@ -446,7 +461,7 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
     // ---- translation
     const double s0 = sIn[2 * l], s1 = sIn[2 * l + 1];
     double sx, sy, vx, vy;
-    for (int i = lane; i < mT; i += 64) {
+    for (int i = lane; i < mT; i += GROUP) {
         const double2 g = rng.gauss2();
         double x = Tr[2 * i] + g.x * s0 * pf, y = Tr[2 * i + 1] + g.y * s1 * pf;
         if (sqrt(x * x + y * y) > transM) {
@@ -460,26 +475,26 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // balanceWeight(PAR_T) on the perturbed set
     sx = 0; sy = 0;
-    for (int i = lane; i < mT; i += 64) { sx += Tr[2 * i]; sy += Tr[2 * i + 1]; }
-    sx = wave_sum(sx) / mT; sy = wave_sum(sy) / mT;
+    for (int i = lane; i < mT; i += GROUP) { sx += Tr[2 * i]; sy += Tr[2 * i + 1]; }
+    sx = group_sum(sx) / mT; sy = group_sum(sy) / mT;
     vx = 0; vy = 0;
-    for (int i = lane; i < mT; i += 64) {
+    for (int i = lane; i < mT; i += GROUP) {
         vx += (Tr[2 * i] - sx) * (Tr[2 * i] - sx);
         vy += (Tr[2 * i + 1] - sy) * (Tr[2 * i + 1] - sy);
     }
-    vx = wave_sum(vx); vy = wave_sum(vy);
+    vx = group_sum(vx); vy = group_sum(vy);
     const double b0 = fmax(1e-6, mT > 1 ? sqrt(vx / (mT - 1)) : 1.0);
     const double b1 = fmax(1e-6, mT > 1 ? sqrt(vy / (mT - 1)) : 1.0);
     double tot = 0.0;
-    for (int i = lane; i < mT; i += 64) {
+    for (int i = lane; i < mT; i += GROUP) {
         const double u = (Tr[2 * i] - sx) / b0, v = (Tr[2 * i + 1] - sy) / b1;
         const double p = exp(-(u * u + v * v) / 2) / (2 * M_PI * b0 * b1);
         const double x = 1.0 / fmax(p, 1e-300);
         pT[(size_t)l * mT + i] = x;
         tot += x;
     }
-    tot = wave_sum(tot);
-    for (int i = lane; i < mT; i += 64) pT[(size_t)l * mT + i] /= tot;
+    tot = group_sum(tot);
+    for (int i = lane; i < mT; i += GROUP) pT[(size_t)l * mT + i] /= tot;
 }
 
 struct Plan {
@@ -490,6 +505,7 @@ struct Plan {
     int* anc; double* cdf; int* topR; int* topT;
     double* tmpQ; double* tmpT;
     double* kv; double* sv; double* peakR;   // calVari k1..k3, s0 s1; setPeakFactor(R)
+    double* topQ;                            // calRank1st _topR
     float* wC; float* wR; float* wT; float* base; double* pC;
     void* localWs; size_t localWsBytes;
     size_t bytes;
@@ -518,6 +534,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     p.kv = k.take<double>((size_t)nImg * 3);
     p.sv = k.take<double>((size_t)nImg * 2);
     p.peakR = k.take<double>(nImg);
+    p.topQ = k.take<double>((size_t)nImg * 4);
     p.wC = k.take<float>(nImg);
     p.wR = k.take<float>((size_t)nImg * c.mLR);
     p.wT = k.take<float>((size_t)nImg * c.mLT);
@@ -527,6 +544,16 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     p.localWs = k.take<char>(p.localWsBytes);
     p.bytes = k.off + 256;
     return p;
+}
+
+// topQ[l] = src[l (or shared)][top[l]] -- Particle::_topR after calRank1st
+__global__ void k_top_copy(int nImg, const double* __restrict__ src, long lds,
+                           const int* __restrict__ top, double* __restrict__ topQ)
+{
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nImg * 4) return;
+    const int l = q / 4, k = q % 4;
+    topQ[q] = src[(size_t)l * lds + (size_t)top[l] * 4 + k];
 }
 
 __global__ void k_fill(double* p, long n, double v)
@@ -544,7 +571,7 @@ extern "C" int thx_pf_calvari(int nImg, int mR, const double* quat, int mT, cons
     THX_CHECK_ARG(nImg >= 0 && mR > 0 && mT > 0, "thx_pf_calvari: bad sizes");
     THX_CHECK_ARG(nImg == 0 || (quat && trans && k && sd), "thx_pf_calvari: null argument");
     if (nImg == 0) return THX_OK;
-    hipLaunchKernelGGL(k_pf_calvari, dim3(thx::cdiv(nImg, 4)), dim3(256), 0,
+    hipLaunchKernelGGL(k_pf_calvari, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0,
                        thx::as_stream(stream), nImg, mR, quat, mT, trans, kFloor, sFloor, k, sd);
     THX_LAUNCH_CHECK();
     return THX_OK;
@@ -556,7 +583,7 @@ extern "C" int thx_pf_balance_rot(int nImg, int mR, const double* quat, double* 
     THX_CHECK_ARG(nImg >= 0 && mR > 0, "thx_pf_balance_rot: bad sizes");
     THX_CHECK_ARG(nImg == 0 || (quat && pR), "thx_pf_balance_rot: null argument");
     if (nImg == 0) return THX_OK;
-    hipLaunchKernelGGL(k_pf_balance_rot, dim3(thx::cdiv(nImg, 4)), dim3(256), 0,
+    hipLaunchKernelGGL(k_pf_balance_rot, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0,
                        thx::as_stream(stream), nImg, mR, quat, pR);
     THX_LAUNCH_CHECK();
     return THX_OK;
@@ -613,6 +640,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     THX_CHECK_ARG(workspace && p.bytes <= wsBytes, "thx_expectation: workspace too small");
     hipStream_t s = thx::as_stream(stream);
     const unsigned gImg = thx::cdiv(nImg, 4);
+    const unsigned gPf = thx::cdiv(nImg * GROUP, 256);
 
     // ---- global scan (ExpectRotran + ExpectProject + ExpectGlobal3D)
     THX_RET(thx_rotmat(gQuat, c.nR, p.gMat, stream));
@@ -633,13 +661,16 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, gQuat, 0L, c.nR,
                        p.anc, quat);
     THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg, gQuat,
+                       0L, p.topR, p.topQ);
+    THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nT, c.mLT, gPT, 0,
                        p.gWT, c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, gTrans, 0L, c.nT,
                        p.anc, trans);
     THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pf_calvari, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT, trans,
+    hipLaunchKernelGGL(k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT, trans,
                        c.kMin, c.sMin, p.kv, p.sv);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, s, p.pC, (long)nImg, 1.0);
@@ -649,8 +680,8 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     // balanceWeight, likelihood + marginals, keepHalfHeightPeak (R),
     // calRank1st, calVari (pre-resample cloud), resample
     for (int phase = 1; phase <= c.nPhase; phase++) {
-        hipLaunchKernelGGL(k_pf_perturb, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
-                           trans, pR, pT, p.kv, p.sv, c.perturbFactor, c.transS, c.transM,
+        hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
+                           trans, pR, pT, p.topQ, p.kv, p.sv, c.perturbFactor, c.transS, c.transM,
                            c.seed, (uint32_t)(2000 + phase));
         THX_LAUNCH_CHECK();
         THX_RET(thx_local_phase(vol, 0, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT, dat,
@@ -659,7 +690,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
                            p.peakR, 0);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pf_calvari, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT,
+        hipLaunchKernelGGL(k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT,
                            trans, 0.0, 0.0, p.kv, p.sv);
         THX_LAUNCH_CHECK();
         // resample R and T by the phase marginals; ancestors gathered in place
@@ -671,6 +702,9 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                                hipMemcpyDeviceToDevice, s));
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, p.tmpQ,
                            (long)c.mLR * 4, c.mLR, p.anc, quat);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg,
+                           p.tmpQ, (long)c.mLR * 4, p.topR, p.topQ);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLT, c.mLT, pT,
                            c.mLT, p.wT, c.mLT, c.seed, (uint32_t)(4000 + phase), p.anc, pT,
