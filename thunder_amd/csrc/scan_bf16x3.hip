@@ -44,7 +44,11 @@ template <int MODE> struct Elt;
 template <> struct Elt<BF16X3> { typedef __bf16 T; typedef bf16x8 V; };
 template <> struct Elt<F16X2> { typedef _Float16 T; typedef f16x8 V; };
 
-constexpr int KC = 16;            // pixels per LDS stage (2 MFMA k-steps)
+#ifndef SCAN_KC
+#define SCAN_KC 16
+#endif
+constexpr int KC = SCAN_KC;       // pixels per LDS stage (KC / 8 MFMA k-steps)
+static_assert(KC % 16 == 0, "whole float4 rows per thread in the stagers");
 constexpr int IMG_TILE = 64;
 constexpr int ROT_TILE = 8;
 constexpr int THREADS = 512;
@@ -260,13 +264,15 @@ __global__ void __launch_bounds__(256) k_scan_bias(const float* __restrict__ Bc,
 #pragma unroll
     for (int j = 0; j < 16; j++) acc[j] = 0.f;
     for (int ck = 0; ck < nCk; ck++) {
-        {
-            const float4 a = reinterpret_cast<const float4*>(Bc + ((size_t)ck * nImgPad + l0) * KC)[tid];
-            const int row = tid / 4, c4 = (tid % 4) * 4;
+#pragma unroll
+        for (int v = 0; v < KC / 16; v++) {
+            const int x = tid + v * 256;
+            const float4 a = reinterpret_cast<const float4*>(Bc + ((size_t)ck * nImgPad + l0) * KC)[x];
+            const int row = x / (KC / 4), c4 = (x % (KC / 4)) * 4;
             sA[row][c4] = a.x; sA[row][c4 + 1] = a.y; sA[row][c4 + 2] = a.z; sA[row][c4 + 3] = a.w;
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < KC / 4; u++) {
             const int x = tid + u * 256, rr = x / KC, kc = x % KC;
             const int r = r0 + rr, i = ck * KC + kc;
             float p2 = 0.f;
@@ -349,7 +355,8 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
     // register-staged prefetch of one pixel chunk (global -> regs during the
     // previous chunk's MFMAs, regs -> LDS after the barrier)
     constexpr int TPER = (S::T16 + THREADS - 1) / THREADS;
-    float4 gTh[TPER], gTl[TPER], gA;
+    constexpr int APER = KC / 16;            // float4 of the a tile per thread
+    float4 gTh[TPER], gTl[TPER], gA[APER];
     float2 gP = make_float2(0.f, 0.f);
     auto load_chunk = [&](int ck) {
         const float4* gh = reinterpret_cast<const float4*>(Thi + (size_t)ck * nTPad * KC * 2);
@@ -362,7 +369,9 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
                 if (MODE == BF16X3) gTl[u] = gl[x];
             }
         }
-        gA = reinterpret_cast<const float4*>(Ac + ((size_t)ck * nImgPad + l0) * KC)[tid];
+#pragma unroll
+        for (int v = 0; v < APER; v++)
+            gA[v] = reinterpret_cast<const float4*>(Ac + ((size_t)ck * nImgPad + l0) * KC)[tid + v * THREADS];
         if (tid < ROT_TILE * KC) {
             const int qq = tid / KC, kc = tid % KC;
             const int rr = rb * ROT_TILE + qq, i = ck * KC + kc;
@@ -379,9 +388,11 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
                 if (MODE == BF16X3) *reinterpret_cast<float4*>(sTl + row * TROW + qd * 8) = gTl[u];
             }
         }
-        {                                          // 2 float2 of image row tid / (KC/2)
-            const int row = tid / (KC / 2), c2 = (tid % (KC / 2)) * 2;
-            *reinterpret_cast<float4*>(sA + row * APITCH + c2) = gA;
+#pragma unroll
+        for (int v = 0; v < APER; v++) {           // 2 float2 of image row x / (KC/2)
+            const int x = tid + v * THREADS;
+            const int row = x / (KC / 2), c2 = (x % (KC / 2)) * 2;
+            *reinterpret_cast<float4*>(sA + row * APITCH + c2) = gA[v];
         }
         if (tid < ROT_TILE * KC) sP[tid] = gP;
     };
