@@ -322,7 +322,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
                                                         const double* __restrict__ pR,
                                                         int nImg, int nR, int nT, int nPxl,
                                                         int nImgPad, int nPxlPad, int nTPad,
-                                                        int nRBias,
+                                                        int nRBias, int nIT,
                                                         float2* __restrict__ wRp,
                                                         float* __restrict__ pM,
                                                         float* __restrict__ pWT)
@@ -339,8 +339,17 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n = lane & 31, h = lane >> 5;
-    const int l0 = blockIdx.x * IMG_TILE;
-    const int rb = blockIdx.y;
+    // XCD-aware order: workgroup b runs on XCD b % 8, and every XCD walks its
+    // own contiguous range of (image tile, rotation block) pairs, image-major,
+    // so the 64-image a tile of a tile stays in that XCD's L2 for all its
+    // rotation blocks (the translation table is shared by all)
+    const int nB = nIT * ((nR + ROT_TILE - 1) / ROT_TILE);
+    const int per = (nB + 7) / 8;
+    const int pq = (blockIdx.x % 8) * per + blockIdx.x / 8;
+    if (pq >= nB) return;
+    const int nRBk = (nR + ROT_TILE - 1) / ROT_TILE;
+    const int l0 = (pq / nRBk) * IMG_TILE;
+    const int rb = pq % nRBk;
     const int r = rb * ROT_TILE + w;        // this wave's rotation
     const bool rValid = r < nR;
 
@@ -590,11 +599,12 @@ __global__ void __launch_bounds__(256) k_scan_combine_bf(const float2* __restric
 template <int MODE, int NF>
 int launch_main(const WS& ws, const Dims& d, const float* rotP, const double* pR, hipStream_t s)
 {
-    dim3 grid(d.nImgPad / IMG_TILE, d.nRB);
+    const int nIT = d.nImgPad / IMG_TILE;
+    dim3 grid((unsigned)(8 * thx::cdiv(nIT * d.nRB, 8)));
     hipLaunchKernelGGL((k_scan_split<MODE, NF>), grid, dim3(THREADS), 0, s, ws.Ac, ws.Aconst,
                        ws.scale, ws.bias, ws.Thi, ws.Tlo, reinterpret_cast<const float2*>(rotP),
                        ws.pTf, pR, d.nImg, d.nR, d.nT, d.nPxl, d.nImgPad, d.nPxlPad, d.nTPad,
-                       d.nRBias, ws.wRp, ws.pM, ws.pWT);
+                       d.nRBias, nIT, ws.wRp, ws.pM, ws.pWT);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
