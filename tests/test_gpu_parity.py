@@ -399,3 +399,28 @@ def test_particle_statistics_match_oracle(spread):
         rp = op.peak_factor_rot(u[l])
         assert peak[l] == pytest.approx(rp, rel=1e-7)
         assert np.allclose(ud[l], op.keep_half_height(u[l], rp), rtol=1e-6, atol=1e-6 * u[l].max())
+
+
+def test_empty_batches(orc, stack):
+    """Zero images through every batch entry point: no launch, empty results
+    (the reference loops over an empty image set)."""
+    s = stack
+    px = dev_pixels(s)
+    rotP, traP = gpu_tables(orc, s, px)
+    nR, nT = len(s["quat"]), len(s["trans"])
+    e_dat = torch.empty(0, px.n, dtype=torch.complex64, device=DEV)
+    e_f = torch.empty(0, px.n, dtype=torch.float32, device=DEV)
+    for algo in (0, 1, 2, 3):
+        wC, wR, wT, base = ops.global_scan(rotP, traP, e_dat, e_f, e_f,
+                                           T(np.full(nR, 1.0 / nR)), T(np.full(nT, 1.0 / nT)),
+                                           algo=algo)
+        assert wR.shape == (0, 1, nR) and base.shape == (0,)
+    q = torch.empty(0, 5, 4, dtype=torch.float64, device=DEV)
+    t = torch.empty(0, 3, 2, dtype=torch.float64, device=DEV)
+    one = lambda *sh: torch.ones(*sh, dtype=torch.float64, device=DEV)
+    out = ops.local_phase(T(s["vol"]), q, t, one(0), one(0, 5), one(0, 3), e_dat, e_f, e_f, px,
+                          want_dvp=True)
+    assert out[4].shape == (0, 5, 3)
+    k, sd = ops.pf_calvari(q, t)
+    assert k.shape == (0, 3) and sd.shape == (0, 2)
+    torch.cuda.synchronize()

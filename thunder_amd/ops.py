@@ -160,8 +160,9 @@ def dvp(rotP, traP, dat, ctf_, sig):
 
 
 # ------------------------------------------------------------- a7 + a8
-def global_scan(rotP, traP, dat, ctf_, sig, pR, pT, kIdx=0, nK=1, state=None, algo=1):
-    """ExpectGlobal3D: returns (wC [nImg,nK], wR [nImg,nK,nR], wT [nImg,nK,nT], baseL [nImg])."""
+def global_scan(rotP, traP, dat, ctf_, sig, pR, pT, kIdx=0, nK=1, state=None, algo=2):
+    """ExpectGlobal3D: returns (wC [nImg,nK], wR [nImg,nK,nR], wT [nImg,nK,nT], baseL [nImg]).
+    algo: 0 direct, 1 FP32 MFMA, 2 bf16x3 MFMA (default, as the expectation driver), 3 fp16x2."""
     nImg, nPxl = _images(dat, ctf_, sig)
     nR, nT = rotP.shape[0], traP.shape[0]
     dev = dat.device
