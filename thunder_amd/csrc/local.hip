@@ -384,6 +384,66 @@ THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int sp, int of
     return make_float2(s.x, conj ? -s.y : s.y);
 }
 
+#ifndef THX_LOCAL_SORT
+#define THX_LOCAL_SORT 1
+#endif
+
+// 3D Morton code of three 10-bit coordinates.
+THX_DEV unsigned morton3(unsigned x, unsigned y, unsigned z)
+{
+    auto spread = [](unsigned v) {
+        v &= 0x3ffu;
+        v = (v | (v << 16)) & 0x030000ffu;
+        v = (v | (v << 8)) & 0x0300f00fu;
+        v = (v | (v << 4)) & 0x030c30c3u;
+        v = (v | (v << 2)) & 0x09249249u;
+        return v;
+    };
+    return spread(x) | (spread(y) << 1) | (spread(z) << 2);
+}
+
+// Lane slot -> rotation of the tile.  A particle cloud arrives in resampling
+// order (copies of one ancestor adjacent, ancestors in no spatial order), so
+// the 16 rotations a wave gathers for one pixel can land anywhere in the
+// cloud.  Ranking the tile's rotations by the Morton code of their vector
+// part relative to the tile's first rotation (10 bits per axis, 0.22 deg)
+// gives each wave a compact group of rotations: its 16 lanes then read
+// neighbouring voxels (shared cache lines on the L2 gathers, spread banks on
+// the LDS taps).  Per-rotation arithmetic is unchanged, only which lane does
+// it; rows past nRl keep key ~0u and sort last.
+THX_DEV void rotation_slots(const double* __restrict__ q4, int nRl, int tid,
+                            unsigned* __restrict__ sKey, int* __restrict__ sPerm)
+{
+    if (tid < RT) {
+        unsigned key = ~0u;
+        if (THX_LOCAL_SORT && tid < nRl) {
+            const double a0 = q4[0], a1 = -q4[1], a2 = -q4[2], a3 = -q4[3];   // conj(q_0)
+            const double* b = q4 + 4 * tid;
+            double w = a0 * b[0] - a1 * b[1] - a2 * b[2] - a3 * b[3];
+            double x = a0 * b[1] + a1 * b[0] + a2 * b[3] - a3 * b[2];
+            double y = a0 * b[2] - a1 * b[3] + a2 * b[0] + a3 * b[1];
+            double z = a0 * b[3] + a1 * b[2] - a2 * b[1] + a3 * b[0];
+            if (w < 0.0) { x = -x; y = -y; z = -z; }
+            auto qz = [](double v) { return (unsigned)min(1023.0, max(0.0, (v + 1.0) * 512.0)); };
+            key = morton3(qz(x), qz(y), qz(z)) ;
+        } else if (tid < nRl) {
+            key = (unsigned)tid;
+        }
+        sKey[tid] = key;
+    }
+    __syncthreads();
+    if (tid < RT) {
+        const unsigned k = sKey[tid];
+        int rank = 0;
+        for (int j = 0; j < RT; j++) {
+            const unsigned kj = sKey[j];
+            rank += (kj < k) || (kj == k && j < tid);
+        }
+        sPerm[rank] = tid;
+    }
+    __syncthreads();
+}
+
 template <bool CELLS>
 // two workgroups per CU (LDS-bound): 4 waves per SIMD, 128 VGPRs
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4)))
@@ -413,13 +473,17 @@ k_local_fused(const float2* __restrict__ vol,
     __shared__ float sTr[TT][2];
     __shared__ float sRed[NWAVE];
     __shared__ float sBias[RT];
+    __shared__ unsigned sKey[RT];
+    __shared__ int sPerm[RT];   // lane slot -> rotation of the tile
 
+    rotation_slots(quat + ((size_t)l * nR + r0) * 4, nRl, tid, sKey, sPerm);
     // this lane's rotation (rows past nR reuse the tile's first rotation, so
     // their taps stay inside the staged box; those rows are never stored)
     const int rl = wv * 16 + (lane & 15);
     double m[6];
     {
-        const int r = r0 + (rl < nRl ? rl : 0);
+        const int rp = sPerm[rl];
+        const int r = r0 + (rp < nRl ? rp : 0);
         double q[4], mm[9];
         for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
         quat_to_mat(q, mm);
@@ -557,7 +621,8 @@ k_local_fused(const float2* __restrict__ vol,
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const int rr = wv * 16 + 4 * kk + j;
-        if (t < nT && rr < nRl) dvp[((size_t)l * nR + r0 + rr) * nT + t] = Al + sBias[rr] + acc[j];
+        if (t < nT && rr < nRl)
+            dvp[((size_t)l * nR + r0 + sPerm[rr]) * nT + t] = Al + sBias[rr] + acc[j];
     }
 }
 
