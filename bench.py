@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--phases", type=int, default=10)
     p.add_argument("--algo", type=int, default=2,
                    help="global-scan algorithm: 0 direct, 1 FP32 MFMA, 2 bf16x3 MFMA")
+    p.add_argument("--shuffle", type=int, default=1,
+                   help="1: shuffle the support before resampling (Particle::resample)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-extras", action="store_true", help="skip insert / all-reduce / local roofline")
@@ -203,7 +205,8 @@ def main():
     gset = synth.global_sample_set(a.nr, seed=2)
     px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, rL, a.images, dev, seed=5 + 101 * rank,
                                                  vol=vol)
-    e = ex.Expectation(vol, px, gset, n_phase=a.phases, algo=a.algo, seed=7 + rank)
+    e = ex.Expectation(vol, px, gset, n_phase=a.phases, algo=a.algo, seed=7 + rank,
+                       shuffle=bool(a.shuffle))
     chunk = a.chunk or a.images
     chunks = [(l0, min(a.images, l0 + chunk)) for l0 in range(0, a.images, chunk)]
     outs = [None] * len(chunks)

@@ -278,6 +278,9 @@ typedef struct thx_expect_cfg {
                                  1/chi2Qinv(.5,2)/sqrt(tsf pi) / perturbFactor */
     double transS, transM;    /* translation prior width, reCentre radius */
     unsigned long long seed;  /* counter-RNG seed */
+    int shuffle;              /* 1: shuffle the support before every resampling, as
+                                 Particle::resample does (src/Particle.cpp:1298,
+                                 2202-2300); 0: resample in support order */
 } thx_expect_cfg;
 
 /* nOrd: length of pxOrder (<= 0 when pxOrder is NULL). */

@@ -62,13 +62,25 @@ def test_scan_mode_is_the_generating_grid_pose(grid_stack):
     assert np.mean(tt == s["it"]) >= 0.95, (tt, s["it"])
 
 
-@pytest.fixture(scope="module")
-def driver(grid_stack):
+# shuffle: the support is shuffled before every resampling, as
+# Particle::resample does (src/Particle.cpp:1298, 2202-2300); ordered: the
+# support is resampled in its stored order
+@pytest.fixture(scope="module", params=[True, False], ids=["shuffle", "ordered"])
+def driver(grid_stack, request):
     s = grid_stack
-    e = ex.Expectation(s["vol"], s["px"], s["gset"], n_phase=10, seed=5)
+    e = ex.Expectation(s["vol"], s["px"], s["gset"], n_phase=10, seed=5, shuffle=request.param)
     out = [x.clone() for x in e.run(s["dat"], s["ctf"], s["sig"])]
     again = e.run(s["dat"], s["ctf"], s["sig"])
-    return dict(out=out, again=again)
+    return dict(out=out, again=again, shuffle=request.param)
+
+
+def test_shuffle_changes_the_draw(grid_stack):
+    """Same seed, shuffle on / off: the resampled supports differ (the shuffle
+    is applied), both are valid particle clouds (checked above)."""
+    s = grid_stack
+    outs = [ex.Expectation(s["vol"], s["px"], s["gset"], n_phase=2, seed=5, shuffle=f)
+            .run(s["dat"], s["ctf"], s["sig"])[0].clone() for f in (True, False)]
+    assert not torch.equal(outs[0], outs[1])
 
 
 def test_particle_filter_stays_on_the_pose(grid_stack, driver):

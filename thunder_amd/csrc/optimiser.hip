@@ -326,7 +326,8 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
                                                      int* __restrict__ anc,
                                                      double* __restrict__ wOut,
                                                      int* __restrict__ top,
-                                                     double* __restrict__ cdfWs)
+                                                     double* __restrict__ cdfWs,
+                                                     int* __restrict__ permWs)
 {
     const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -334,10 +335,38 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
     const double* wl = w + (size_t)l * ldw;
     const float* ul = u + (size_t)l * ldu;
     double* cdf = cdfWs + (size_t)l * nIn;
+    // Particle::shuffle before resampling (src/Particle.cpp:1298, 2202-2300):
+    // a Fisher-Yates permutation of the support (gsl_ran_shuffle), drawn from
+    // the counter RNG by lane 0; position i of the shuffled support holds
+    // element pm[i], so the CDF, the top particle (iMax, first maximum in
+    // shuffled order) and the systematic draw all run in shuffled order.
+    int* pm = permWs ? permWs + (size_t)l * nIn : nullptr;
+    if (pm) {
+        for (int i = lane; i < nIn; i += 64) pm[i] = i;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane == 0) {
+            Philox sh(seed, (uint32_t)l, stream, 0x5f1e);
+            uint4 v = make_uint4(0, 0, 0, 0);
+            for (int i = nIn - 1, k = 0; i > 0; i--, k = (k + 1) & 3) {
+                if (k == 0) v = sh.next();
+                const uint32_t x = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+                const int j = (int)(((uint64_t)x * (uint64_t)(i + 1)) >> 32);   // U{0..i}
+                const int a = pm[i], b = pm[j];
+                pm[i] = b;
+                pm[j] = a;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    auto at = [&](int i) { return pm ? pm[i] : i; };
     float bv = -INFINITY;
     int bi = 0x7fffffff;
     for (int i = lane; i < nIn; i += 64) {
-        const float v = ul[i];
+        const float v = ul[at(i)];
         if (v > bv || (v == bv && i < bi)) { bv = v; bi = i; }
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -345,15 +374,15 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
         const int oi = __shfl_xor(bi, o, 64);
         if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
     }
-    if (top && lane == 0) top[l] = bi;
+    if (top && lane == 0) top[l] = at(bi);
     // CDF by a wave prefix scan in FP64
     double tot = 0.0;
-    for (int i = lane; i < nIn; i += 64) tot += wl[i] * (double)ul[i];
+    for (int i = lane; i < nIn; i += 64) tot += wl[at(i)] * (double)ul[at(i)];
     tot = wave_sum(tot);
     double carry = 0.0;
     for (int b = 0; b < nIn; b += 64) {
         const int i = b + lane;
-        double v = i < nIn ? wl[i] * (double)ul[i] / tot : 0.0;
+        double v = i < nIn ? wl[at(i)] * (double)ul[at(i)] / tot : 0.0;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const double y = __shfl_up(v, o, 64);
@@ -376,8 +405,9 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
             const int mid = (lo + hi) >> 1;
             if (uj > cdf[mid]) lo = mid + 1; else hi = mid;
         }
-        const float ua = ul[lo];
-        anc[(size_t)l * nOut + j] = lo;
+        const int src = at(lo);
+        const float ua = ul[src];
+        anc[(size_t)l * nOut + j] = src;
         const double x = ua > 0.f ? 1.0 / (double)ua : 0.0;
         wOut[(size_t)l * nOut + j] = x;
         s += x;
@@ -502,7 +532,7 @@ struct Plan {
     float* rotP; double* gMat; float* traP;
     float* gWC; float* gWR; float* gWT; float* gBase;
     void* scanWs; size_t scanWsBytes;
-    int* anc; double* cdf; int* topR; int* topT;
+    int* anc; double* cdf; int* perm; int* topR; int* topT;
     double* tmpQ; double* tmpT;
     double* kv; double* sv; double* peakR;   // calVari k1..k3, s0 s1; setPeakFactor(R)
     double* topQ;                            // calRank1st _topR
@@ -527,6 +557,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     p.scanWs = k.take<char>(p.scanWsBytes);
     p.anc = k.take<int>((size_t)nImg * (c.mLR > c.mLT ? c.mLR : c.mLT));
     p.cdf = k.take<double>((size_t)nImg * (nMax > c.mLR ? nMax : c.mLR));
+    p.perm = k.take<int>((size_t)nImg * (nMax > c.mLR ? nMax : c.mLR));
     p.topR = k.take<int>(nImg);
     p.topT = k.take<int>(nImg);
     p.tmpQ = k.take<double>((size_t)nImg * c.mLR * 4);
@@ -656,7 +687,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.nR, p.gWR, c.nR, p.peakR, 1);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nR, c.mLR, gPR, 0,
-                       p.gWR, c.nR, c.seed, 1000u, p.anc, pR, p.topR, p.cdf);
+                       p.gWR, c.nR, c.seed, 1000u, p.anc, pR, p.topR, p.cdf, c.shuffle ? p.perm : nullptr);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, gQuat, 0L, c.nR,
                        p.anc, quat);
@@ -665,7 +696,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                        0L, p.topR, p.topQ);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nT, c.mLT, gPT, 0,
-                       p.gWT, c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf);
+                       p.gWT, c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf, c.shuffle ? p.perm : nullptr);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, gTrans, 0L, c.nT,
                        p.anc, trans);
@@ -696,7 +727,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         // resample R and T by the phase marginals; ancestors gathered in place
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, c.mLR, pR,
                            c.mLR, p.wR, c.mLR, c.seed, (uint32_t)(3000 + phase), p.anc, pR,
-                           p.topR, p.cdf);
+                           p.topR, p.cdf, c.shuffle ? p.perm : nullptr);
         THX_LAUNCH_CHECK();
         THX_HIP(hipMemcpyAsync(p.tmpQ, quat, sizeof(double) * nImg * c.mLR * 4,
                                hipMemcpyDeviceToDevice, s));
@@ -708,7 +739,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLT, c.mLT, pT,
                            c.mLT, p.wT, c.mLT, c.seed, (uint32_t)(4000 + phase), p.anc, pT,
-                           p.topT, p.cdf);
+                           p.topT, p.cdf, c.shuffle ? p.perm : nullptr);
         THX_LAUNCH_CHECK();
         THX_HIP(hipMemcpyAsync(p.tmpT, trans, sizeof(double) * nImg * c.mLT * 2,
                                hipMemcpyDeviceToDevice, s));

@@ -29,7 +29,8 @@ class ExpectCfg(ctypes.Structure):
                 ("mLT", ctypes.c_int), ("nPhase", ctypes.c_int), ("algo", ctypes.c_int),
                 ("perturbFactor", ctypes.c_double), ("kMin", ctypes.c_double),
                 ("sMin", ctypes.c_double), ("transS", ctypes.c_double),
-                ("transM", ctypes.c_double), ("seed", ctypes.c_ulonglong)]
+                ("transM", ctypes.c_double), ("seed", ctypes.c_ulonglong),
+                ("shuffle", ctypes.c_int)]
 
 
 class Expectation:
@@ -40,7 +41,7 @@ class Expectation:
     """
 
     def __init__(self, vol, px, gset, mLR=125, mLT=9, n_phase=10, perturb=0.5,
-                 trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7):
+                 trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7, shuffle=True):
         dev = vol.device
         self.vol, self.px, self.dev = vol, px, dev
         q, t, pR, pT = gset
@@ -58,7 +59,7 @@ class Expectation:
         k_floor = (scan_min_std_r / perturb) ** 2
         s_floor = scan_min_std_t / perturb
         self.cfg = ExpectCfg(px.idim, px.pf, vdim, nR, nT, mLR, mLT, n_phase, algo, perturb,
-                             k_floor, s_floor, trans_s, trans_m, seed)
+                             k_floor, s_floor, trans_s, trans_m, seed, int(bool(shuffle)))
         self.mLR, self.mLT = mLR, mLT
 
     def workspace_bytes(self, nImg):
