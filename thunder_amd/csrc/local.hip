@@ -384,6 +384,9 @@ THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int sp, int of
     return make_float2(s.x, conj ? -s.y : s.y);
 }
 
+#ifndef THX_SKIP_PAD
+#define THX_SKIP_PAD 1
+#endif
 #ifndef THX_LOCAL_SORT
 #define THX_LOCAL_SORT 1
 #endif
@@ -470,6 +473,7 @@ k_local_fused(const float2* __restrict__ vol,
     __shared__ __attribute__((aligned(16))) float sB[KC * 2 * TT];   // [px][U, V][t]
     __shared__ __attribute__((aligned(16))) double2 sXY[KC];        // (iCol pf, iRow pf)
     __shared__ float sBq[KC];                                        // b = s c^2
+    __shared__ int sValid[KC];                                       // 0: padding entry
     __shared__ float sTr[TT][2];
     __shared__ float sRed[NWAVE];
     __shared__ float sBias[RT];
@@ -551,6 +555,7 @@ k_local_fused(const float2* __restrict__ vol,
             if (bt == 0) {
                 if (ok) aConst += px.s * (px.d.x * px.d.x + px.d.y * px.d.y);
                 sBq[bpx] = ok ? px.s * px.c * px.c : 0.f;
+                sValid[bpx] = ok;
                 // padding entries sample the patch's first pixel (inside the box)
                 const int ic = ok ? px.ic : rc.v[17], ir = ok ? px.ir : rc.v[18];
                 sXY[bpx] = make_double2((double)(ic * pf), (double)(ir * pf));
@@ -580,10 +585,17 @@ k_local_fused(const float2* __restrict__ vol,
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[0]), b0, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[1]), b1, acc, 0, 0, 0);
         };
+        // a step whose four pixels are all padding adds exactly zero (U = V = b
+        // = 0): skipped, wave-uniformly
+        auto pad_step = [&](int s) {
+            return THX_SKIP_PAD &&
+                   !(sValid[4 * s] | sValid[4 * s + 1] | sValid[4 * s + 2] | sValid[4 * s + 3]);
+        };
         if (rc.staged()) {
             const int nx = rc.v[6], sp = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
 #pragma unroll
             for (int s = 0; s < 4; s++) {
+                if (pad_step(s)) continue;
                 const double2 xy = sXY[4 * s + g];
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
@@ -593,6 +605,7 @@ k_local_fused(const float2* __restrict__ vol,
         } else {
 #pragma unroll 2
             for (int s = 0; s < 4; s++) {
+                if (pad_step(s)) continue;
                 const double2 xy = sXY[4 * s + g];
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
