@@ -361,16 +361,31 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
             // ones only with index N - 1, i.e. when there is no padding
             kk[i] = i < nIn ? (ib == 32 ? 0u : (x << ib)) | (uint32_t)i : 0xFFFFFFFFu;
         }
+        // one stage: the N/2 disjoint pairs (i, i + j), four per lane loaded
+        // before any is compared and stored (a quarter of the LDS round trips
+        // of pair-at-a-time, at 8 VGPRs)
+        constexpr int PPL = 4;
         for (int k = 2; k <= N; k <<= 1)
             for (int j = k >> 1; j > 0; j >>= 1) {
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                for (int i = lane; i < N; i += 64) {
-                    const int o = i ^ j;
-                    if (o > i) {
-                        const uint32_t x = kk[i], y = kk[o];
-                        if ((x > y) == ((i & k) == 0)) { kk[i] = y; kk[o] = x; }
+                for (int p0 = 0; p0 < (N >> 1); p0 += 64 * PPL) {
+                    uint32_t x[PPL], y[PPL];
+#pragma unroll
+                    for (int u = 0; u < PPL; u++) {
+                        const int p = p0 + lane + 64 * u;
+                        const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+                        if (p < (N >> 1)) { x[u] = kk[i]; y[u] = kk[i + j]; }
+                    }
+#pragma unroll
+                    for (int u = 0; u < PPL; u++) {
+                        const int p = p0 + lane + 64 * u;
+                        const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+                        if (p < (N >> 1) && (x[u] > y[u]) == ((i & k) == 0)) {
+                            kk[i] = y[u];
+                            kk[i + j] = x[u];
+                        }
                     }
                 }
             }
