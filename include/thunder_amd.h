@@ -192,6 +192,25 @@ int thx_resample(int nImg, int nIn, const double* w, const float* u,
                  int nOut, const double* u0, int* ancestor, double* wOut,
                  int* iMax, thx_stream_t stream);
 
+/* The expectation driver's resampling step (k_pf_resample, used by
+ * thx_expectation): Particle::resample (src/Particle.cpp:1291-1478) for nImg
+ * images at once, one wave per image -- shuffle(pt) first when `shuffle`
+ * (src/Particle.cpp:1298, 2202-2300; a uniform permutation from the counter
+ * RNG keyed by (seed, image, stream_id)), then iMax = first maximum of u in
+ * shuffled order, the CDF of w*u in shuffled order and the systematic draw
+ * u_j = u0 + j/nOut, u0 ~ U(0, 1/nOut).  Outputs are element indices of the
+ * unshuffled support.  w: nImg rows at stride ldw (0 = one row shared by all
+ * images), u: float rows at stride ldu; w and wOut may alias (ldw == nOut ==
+ * nIn).  perm (optional, nImg x nIn): the permutation, position i of the
+ * shuffled support holds element perm[i]; u0 (optional, nImg): the draws.
+ * workspace: >= thx_pf_resample_workspace(nImg, nIn) bytes. */
+size_t thx_pf_resample_workspace(int nImg, int nIn);
+int thx_pf_resample(int nImg, int nIn, int nOut, const double* w, int ldw,
+                    const float* u, int ldu, unsigned long long seed,
+                    unsigned stream_id, int shuffle, int* anc, double* wOut,
+                    int* iMax, int* perm, double* u0, void* workspace,
+                    size_t wsBytes, thx_stream_t stream);
+
 /* Particle statistics of the particle filter, one image per wave, nImg at a
  * time (device pointers; FP64 particles, FP32 marginals):
  * thx_pf_calvari -- Particle::calVari, 3D (src/Particle.cpp:1004-1121):

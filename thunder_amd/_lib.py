@@ -32,6 +32,9 @@ SIGNATURES = {
                                  _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p, _p,
                                  _c_size, _p]),
     "thx_resample": (_c_int, [_c_int, _c_int, _p, _p, _c_int, _p, _p, _p, _p, _p]),
+    "thx_pf_resample_workspace": (_c_size, [_c_int, _c_int]),
+    "thx_pf_resample": (_c_int, [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, ctypes.c_ulonglong,
+                                 ctypes.c_uint, _c_int, _p, _p, _p, _p, _p, _p, _c_size, _p]),
     "thx_pf_calvari": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _c_double, _c_double, _p, _p, _p]),
     "thx_pf_balance_rot": (_c_int, [_c_int, _c_int, _p, _p, _p]),
     "thx_pf_peak": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _c_int, _p]),

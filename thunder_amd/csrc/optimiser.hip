@@ -18,12 +18,11 @@
 //
 // The particle statistics follow Particle / DirectionalStat with the
 // reference's Config.h switches: ACG spreads by inferACG's fixed point,
-// 1/pdfACG rotation priors, the 3D peak factor.  Not replicated: the
-// perturbation mean (the top particle, see k_pf_perturb), the
-// support shuffle before systematic resampling (it only decorrelates the
-// stratified draw from the particle order) and the generator: sampling is
-// counter-based (Philox4x32-10), so a run is reproducible for a given seed,
-// where the reference draws from an urandom-seeded GSL mt19937.
+// 1/pdfACG rotation priors, the 3D peak factor, the support shuffle before
+// every systematic resampling (a bitonic sort of counter-RNG keys, see
+// k_pf_resample).  Not replicated: the generator -- sampling is counter-based
+// (Philox4x32-10), so a run is reproducible for a given seed, where the
+// reference draws from an urandom-seeded GSL mt19937.
 #include "common.h"
 
 namespace {
@@ -318,16 +317,22 @@ __global__ void __launch_bounds__(256) k_pf_balance_rot(int nImg, int mR,
 // --------------------------------------------------------------- resample
 // One wave per image: systematic resampling (src/Particle.cpp:1343-1383) of
 // (w, u) -> ancestors and 1/u priors; w may be shared by all images (ldw = 0).
-// u0 ~ U(0, 1/nOut) is drawn from the counter RNG.
+// u0 ~ U(0, 1/nOut) is drawn from the counter RNG.  w and wOut may alias (the
+// in-phase resamples overwrite the priors in place: every read of w comes
+// before the barrier that precedes the first store to wOut), so neither is
+// __restrict__.  permOut / u0Out (optional) expose the support permutation
+// and the draw for thx_pf_resample's parity tests.
 __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut,
-                                                     const double* __restrict__ w, int ldw,
+                                                     const double* w, int ldw,
                                                      const float* __restrict__ u, int ldu,
                                                      uint64_t seed, uint32_t stream,
                                                      int* __restrict__ anc,
-                                                     double* __restrict__ wOut,
+                                                     double* wOut,
                                                      int* __restrict__ top,
                                                      double* __restrict__ cdfWs,
-                                                     int* __restrict__ permWs)
+                                                     int* __restrict__ permWs,
+                                                     int* __restrict__ permOut,
+                                                     double* __restrict__ u0Out)
 {
     const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -340,15 +345,18 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
     // i of the shuffled support holds element pm[i], so the CDF, the top
     // particle (iMax, first maximum in shuffled order) and the systematic
     // draw all run in shuffled order.  Up to 2048 entries the wave sorts
-    // (random bits | index) keys with a bitonic network in LDS -- all 64 lanes
-    // work, and the index bits make the keys distinct, so the sorted indices
-    // are a permutation (a one-lane Fisher-Yates took 1.4 ms per 12 500-image
-    // call at 2000 entries, a rank count 7 ms).  Larger supports fall back to
-    // Fisher-Yates by lane 0 in global memory.
-    __shared__ __attribute__((aligned(16))) uint32_t sKey[4][2048];
+    // 64-bit (32 random bits | index) keys with a bitonic network in LDS --
+    // all 64 lanes work; the index half makes the keys distinct, so the sorted
+    // indices are a permutation, and two entries tie on their random halves
+    // (and keep their index order) with probability ~nIn^2 / 2^33 per shuffle
+    // (a one-lane Fisher-Yates took 1.4 ms per 12 500-image call at 2000
+    // entries, a rank count 7 ms).  Larger supports fall back to Fisher-Yates
+    // by lane 0 in global memory.
+    constexpr int KMAX = 2048;
+    __shared__ __attribute__((aligned(16))) uint64_t sKey[4][KMAX];
     int* pm = permWs ? permWs + (size_t)l * nIn : nullptr;
-    if (pm && nIn <= 2048) {
-        uint32_t* kk = sKey[threadIdx.x >> 6];
+    if (pm && nIn <= KMAX) {
+        uint64_t* kk = sKey[threadIdx.x >> 6];
         int ib = 0;
         while ((1 << ib) < nIn) ib++;
         const int N = 1 << ib;
@@ -357,13 +365,13 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
         for (int i = lane, k = 0; i < N; i += 64, k = (k + 1) & 3) {
             if (k == 0) v = sh.next();
             const uint32_t x = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-            // padding (i >= nIn) is all ones and sorts last: a real key is all
-            // ones only with index N - 1, i.e. when there is no padding
-            kk[i] = i < nIn ? (ib == 32 ? 0u : (x << ib)) | (uint32_t)i : 0xFFFFFFFFu;
+            // padding (i >= nIn) is all ones and sorts last: a real key has an
+            // index half < 2048
+            kk[i] = i < nIn ? ((uint64_t)x << 32) | (uint64_t)i : ~0ull;
         }
         // one stage: the N/2 disjoint pairs (i, i + j), four per lane loaded
         // before any is compared and stored (a quarter of the LDS round trips
-        // of pair-at-a-time, at 8 VGPRs)
+        // of pair-at-a-time)
         constexpr int PPL = 4;
         for (int k = 2; k <= N; k <<= 1)
             for (int j = k >> 1; j > 0; j >>= 1) {
@@ -371,7 +379,7 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 for (int p0 = 0; p0 < (N >> 1); p0 += 64 * PPL) {
-                    uint32_t x[PPL], y[PPL];
+                    uint64_t x[PPL], y[PPL];
 #pragma unroll
                     for (int u = 0; u < PPL; u++) {
                         const int p = p0 + lane + 64 * u;
@@ -389,11 +397,28 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
                     }
                 }
             }
+        // compact the index halves into the first 4 nIn bytes of the same LDS
+        // row: every lane holds its (<= 32) indices in registers across the
+        // barrier, so no word is overwritten before it has been read
+        uint32_t idx[KMAX / 64];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int i = lane; i < nIn; i += 64) kk[i] &= (uint32_t)(N - 1);
-        pm = reinterpret_cast<int*>(kk);
+#pragma unroll
+        for (int q = 0; q < KMAX / 64; q++) {
+            const int i = lane + 64 * q;
+            idx[q] = i < nIn ? (uint32_t)kk[i] : 0u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        uint32_t* k32 = reinterpret_cast<uint32_t*>(kk);
+#pragma unroll
+        for (int q = 0; q < KMAX / 64; q++) {
+            const int i = lane + 64 * q;
+            if (i < nIn) k32[i] = idx[q];
+        }
+        pm = reinterpret_cast<int*>(k32);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -419,6 +444,8 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
     auto at = [&](int i) { return pm ? pm[i] : i; };
+    if (permOut)
+        for (int i = lane; i < nIn; i += 64) permOut[(size_t)l * nIn + i] = at(i);
     float bv = -INFINITY;
     int bi = 0x7fffffff;
     for (int i = lane; i < nIn; i += 64) {
@@ -453,6 +480,7 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
     const double last = carry;
     Philox rng(seed, (uint32_t)l, stream, 0x5e5a);
     const double u0 = rng.uniform() / nOut;
+    if (u0Out && lane == 0) u0Out[l] = u0;
     double s = 0.0;
     for (int j = lane; j < nOut; j += 64) {
         const double uj = (u0 + j * 1.0 / nOut) * last;
@@ -601,7 +629,9 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
 {
     thx::Carver k(base, ~size_t(0));
     Plan p;
-    const int nMax = c.nR > c.nT ? c.nR : c.nT;
+    int nMax = c.nR > c.nT ? c.nR : c.nT;           // every resampled support size
+    if (c.mLR > nMax) nMax = c.mLR;
+    if (c.mLT > nMax) nMax = c.mLT;
     p.rotP = k.take<float>((size_t)2 * c.nR * nPxl);
     p.gMat = k.take<double>((size_t)9 * c.nR);
     p.traP = k.take<float>((size_t)2 * c.nT * nPxl);
@@ -612,8 +642,8 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     p.scanWsBytes = thx_global_scan_workspace(nImg, c.nR, c.nT, nPxl, c.algo);
     p.scanWs = k.take<char>(p.scanWsBytes);
     p.anc = k.take<int>((size_t)nImg * (c.mLR > c.mLT ? c.mLR : c.mLT));
-    p.cdf = k.take<double>((size_t)nImg * (nMax > c.mLR ? nMax : c.mLR));
-    p.perm = k.take<int>((size_t)nImg * (nMax > c.mLR ? nMax : c.mLR));
+    p.cdf = k.take<double>((size_t)nImg * nMax);
+    p.perm = k.take<int>((size_t)nImg * nMax);
     p.topR = k.take<int>(nImg);
     p.topT = k.take<int>(nImg);
     p.tmpQ = k.take<double>((size_t)nImg * c.mLR * 4);
@@ -688,6 +718,36 @@ extern "C" int thx_pf_peak(int nImg, int n, float* u, int ldu, double* peak, int
     return THX_OK;
 }
 
+extern "C" size_t thx_pf_resample_workspace(int nImg, int nIn)
+{
+    if (nImg <= 0 || nIn <= 0) return 256;
+    thx::Carver k(nullptr, ~size_t(0));
+    k.take<double>((size_t)nImg * nIn);
+    k.take<int>((size_t)nImg * nIn);
+    return k.off + 256;
+}
+
+extern "C" int thx_pf_resample(int nImg, int nIn, int nOut, const double* w, int ldw,
+                               const float* u, int ldu, unsigned long long seed,
+                               unsigned stream_id, int shuffle, int* anc, double* wOut,
+                               int* iMax, int* perm, double* u0, void* workspace,
+                               size_t wsBytes, thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && nIn > 0 && nOut > 0 && (ldw == 0 || ldw >= nIn) && ldu >= nIn,
+                  "thx_pf_resample: bad sizes");
+    THX_CHECK_ARG(nImg == 0 || (w && u && anc && wOut && workspace), "thx_pf_resample: null argument");
+    if (nImg == 0) return THX_OK;
+    THX_CHECK_ARG(wsBytes >= thx_pf_resample_workspace(nImg, nIn), "thx_pf_resample: workspace too small");
+    thx::Carver k(workspace, wsBytes);
+    double* cdf = k.take<double>((size_t)nImg * nIn);
+    int* pw = k.take<int>((size_t)nImg * nIn);
+    hipLaunchKernelGGL(k_pf_resample, dim3(thx::cdiv(nImg, 4)), dim3(256), 0, thx::as_stream(stream),
+                       nImg, nIn, nOut, w, ldw, u, ldu, (uint64_t)seed, (uint32_t)stream_id, anc,
+                       wOut, iMax, cdf, shuffle ? pw : nullptr, perm, u0);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 extern "C" size_t thx_expectation_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl,
                                             int nOrd)
 {
@@ -743,7 +803,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.nR, p.gWR, c.nR, p.peakR, 1);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nR, c.mLR, gPR, 0,
-                       p.gWR, c.nR, c.seed, 1000u, p.anc, pR, p.topR, p.cdf, c.shuffle ? p.perm : nullptr);
+                       p.gWR, c.nR, c.seed, 1000u, p.anc, pR, p.topR, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, gQuat, 0L, c.nR,
                        p.anc, quat);
@@ -752,7 +812,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                        0L, p.topR, p.topQ);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nT, c.mLT, gPT, 0,
-                       p.gWT, c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf, c.shuffle ? p.perm : nullptr);
+                       p.gWT, c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, gTrans, 0L, c.nT,
                        p.anc, trans);
@@ -783,7 +843,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         // resample R and T by the phase marginals; ancestors gathered in place
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, c.mLR, pR,
                            c.mLR, p.wR, c.mLR, c.seed, (uint32_t)(3000 + phase), p.anc, pR,
-                           p.topR, p.cdf, c.shuffle ? p.perm : nullptr);
+                           p.topR, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr);
         THX_LAUNCH_CHECK();
         THX_HIP(hipMemcpyAsync(p.tmpQ, quat, sizeof(double) * nImg * c.mLR * 4,
                                hipMemcpyDeviceToDevice, s));
@@ -795,7 +855,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLT, c.mLT, pT,
                            c.mLT, p.wT, c.mLT, c.seed, (uint32_t)(4000 + phase), p.anc, pT,
-                           p.topT, p.cdf, c.shuffle ? p.perm : nullptr);
+                           p.topT, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr);
         THX_LAUNCH_CHECK();
         THX_HIP(hipMemcpyAsync(p.tmpT, trans, sizeof(double) * nImg * c.mLT * 2,
                                hipMemcpyDeviceToDevice, s));

@@ -313,6 +313,27 @@ def fsc(A, B, n_shell):
     return out
 
 
+def pf_resample(w, u, n_out, seed, stream_id=0, shuffle=True):
+    """thx_pf_resample (the driver's resampling kernel): w [nImg, nIn] float64
+    (or [nIn], shared), u [nImg, nIn] float32 -> (ancestors [nImg, n_out],
+    priors [nImg, n_out], iMax [nImg], perm [nImg, nIn], u0 [nImg])."""
+    nImg, nIn = u.shape
+    dev = u.device
+    _req(u, torch.float32, (nImg, nIn), "u")
+    ldw = 0 if w.dim() == 1 else nIn
+    _req(w, torch.float64, (nIn,) if ldw == 0 else (nImg, nIn), "w")
+    anc = torch.empty(nImg, n_out, dtype=torch.int32, device=dev)
+    wout = torch.empty(nImg, n_out, dtype=torch.float64, device=dev)
+    imax = torch.empty(nImg, dtype=torch.int32, device=dev)
+    perm = torch.empty(nImg, nIn, dtype=torch.int32, device=dev)
+    u0 = torch.empty(nImg, dtype=torch.float64, device=dev)
+    ws = workspace(lib().thx_pf_resample_workspace(nImg, nIn), dev)
+    check(lib().thx_pf_resample(nImg, nIn, n_out, _ptr(w), ldw, _ptr(u), nIn, seed, stream_id,
+                                int(bool(shuffle)), _ptr(anc), _ptr(wout), _ptr(imax), _ptr(perm),
+                                _ptr(u0), _ptr(ws), ws.numel(), _stream(dev)), "thx_pf_resample")
+    return anc, wout, imax, perm, u0
+
+
 def pf_calvari(quat, trans, k_floor=0.0, s_floor=0.0):
     """thx_pf_calvari: per-image ACG spreads (k1, k2, k3) and translation
     standard deviations (s0, s1) of particle clouds quat [nImg, mR, 4],
