@@ -52,6 +52,12 @@ def parse():
                    help="global-scan algorithm: 0 direct, 1 FP32 MFMA, 2 bf16x3 MFMA")
     p.add_argument("--shuffle", type=int, default=1,
                    help="1: shuffle the support before resampling (Particle::resample)")
+    p.add_argument("--perturb-mean", default="acg", choices=["acg", "top"],
+                   help="acg: inferACG mean of the cloud (the reference's compiled switch "
+                        "PARTICLE_ROT_MEAN_USING_STAT_PERTURB); top: the top particle")
+    p.add_argument("--acg-iters", type=int, default=100, help="inferACG fixed-point iteration cap")
+    p.add_argument("--large-first", type=int, default=0,
+                   help="1: OPTIMISER_GLOBAL_PERTURB_LARGE (off in the reference's Config.h)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-extras", action="store_true", help="skip insert / all-reduce / local roofline")
@@ -206,7 +212,8 @@ def main():
     px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, rL, a.images, dev, seed=5 + 101 * rank,
                                                  vol=vol)
     e = ex.Expectation(vol, px, gset, n_phase=a.phases, algo=a.algo, seed=7 + rank,
-                       shuffle=bool(a.shuffle))
+                       shuffle=bool(a.shuffle), perturb_mean=a.perturb_mean, acg_iters=a.acg_iters,
+                       large_first=bool(a.large_first))
     chunk = a.chunk or a.images
     chunks = [(l0, min(a.images, l0 + chunk)) for l0 in range(0, a.images, chunk)]
     outs = [None] * len(chunks)

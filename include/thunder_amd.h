@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define THX_ABI_VERSION 2
+#define THX_ABI_VERSION 3
 
 enum {
     THX_OK = 0,
@@ -173,6 +173,30 @@ int thx_local_phase(const float* vol, int volLayout, int vdim, int pf,
                     float* wR, float* wT, float* baseL, float* dvp,
                     void* workspace, size_t wsBytes, thx_stream_t stream);
 
+/* Image selection for the same phase (the expectation driver's own use, and
+ * a C++ host's): `active` / `nActive` (device; both or neither) restrict the
+ * launch to images active[0 .. *nActive) -- the grid is sized by nImg and
+ * slots past the count exit at once, so the host never reads the count -- and
+ * `cls` (device, nImg, may be NULL) makes image l project class cls[l]'s
+ * volume, vol + cls[l] * volStride float2 elements (K-class classification:
+ * the phases run on the class the reseed drew, src/Optimiser.cpp:1957-1965).
+ * Per-image arrays keep their nImg-row layout. */
+typedef struct thx_local_sel {
+    const int* active;
+    const int* nActive;
+    const int* cls;
+    long long volStride;
+} thx_local_sel;
+int thx_local_phase_sel(const thx_local_sel* sel, const float* vol, int volLayout,
+                        int vdim, int pf, const double* quat, int nR,
+                        const double* trans, int nT, const double* pC,
+                        const double* pR, const double* pT, const float* dat,
+                        const float* ctf, const float* sigRcp, const int* iCol,
+                        const int* iRow, const int* pxOrder, int nOrd, int nPxl,
+                        int idim, int nImg, float* wC, float* wR, float* wT,
+                        float* baseL, float* dvp, void* workspace, size_t wsBytes,
+                        thx_stream_t stream);
+
 /* Cell-expanded copy of a half-complex volume: cells[(k*vdim + j)*(vdim/2+1)
  * + i] holds the 8 Complex taps v(i+dx, j+dy, k+dz), (dz, dy, dx) in the box
  * order of getFTHalf (src/Image/Volume.cpp:491-563), rows / slices wrapped,
@@ -276,21 +300,42 @@ int thx_fsc(const float* A, const float* B, int vdim, int nShell, double* fsc,
 
 /* ------------------------------------------------- a3..a11 expectation ---
  * Device-resident Optimiser::expectationG (src/Optimiser.cpp:1684-3403) for
- * one image batch, K = 1, 3D, no CTF search: global scan over the shared
- * sample set (gQuat[nR*4], gTrans[nT*2], priors gPR[nR], gPT[nT]; a3), reseed
- * of every particle from the scan marginals (src/Optimiser.cpp:1930-2131),
- * then nPhase particle-filter phases (perturb -> fused projection +
- * likelihood + marginals -> calVari -> resample; src/Optimiser.cpp:
- * 1183-1616).  Outputs the particle sets quat[nImg*mLR*4], trans[nImg*mLT*2]
- * with priors pR[nImg*mLR], pT[nImg*mLT] and score[nImg] (last baseline).
- * Host code only enqueues work on `stream`; nothing synchronises. */
+ * one image batch, 3D, no CTF search.
+ *
+ * searchType 0 (SEARCH_TYPE_GLOBAL): global scan of every class k < nK over
+ * the shared sample set (gQuat[nR*4], gTrans[nT*2], priors gPR[nR], gPT[nT];
+ * a3) with the running baseline across classes (src/Optimiser.cpp:834-894);
+ * reseed (src/Optimiser.cpp:1930-2131): class marginals -> PEAK_FACTOR_C
+ * keepHalfHeightPeak -> resample(K, PAR_C) -> rand(cls), then the drawn
+ * class's rotation / translation marginals -> setPeakFactor +
+ * keepHalfHeightPeak -> resample to mLR / mLT -> calVari with the scan floors;
+ * then particle-filter phases 1, 2, ... on the drawn class's volume.
+ * searchType 1 (SEARCH_TYPE_LOCAL): no scan; the phases 0, 1, ... start from
+ * the caller's particle state (quat, trans, pR, pT and, for nK > 1, cls) --
+ * phase 0 perturbs by perturbFactorL, the rest by perturbFactor.
+ * Each phase (src/Optimiser.cpp:1183-1616, GPU twin :2422-2750): perturb +
+ * balanceWeight -> fused projection + likelihood + marginals ->
+ * keepHalfHeightPeak(R) -> calRank1st -> calVari -> resample R and T.
+ * converge 0: exactly nPhase phases.  converge 1: the per-image stopping rule
+ * of OPTIMISER_COMPRESS_CRITERIA -- from phase minPhase on, an image stops
+ * after the first phase in which neither variR = (k1 k2 k3)^(1/6) nor
+ * variT = s0 s1 fell below 0.95 (PARTICLE_FILTER_DECREASE_FACTOR) of its
+ * smallest value so far (N_PHASE_WITH_NO_VARI_DECREASE = 1), at the latest
+ * after phase maxPhase - 1; stopped images drop out of every later launch
+ * (an active-image list).  In this mode the host reads the active count once
+ * per phase (a 4-byte copy + stream sync), so it is not graph-capturable;
+ * converge 0 enqueues only.
+ * Outputs the particle sets quat[nImg*mLR*4], trans[nImg*mLT*2] with priors
+ * pR[nImg*mLR], pT[nImg*mLT], score[nImg] (last baseline), and optionally
+ * cls[nImg] (the drawn class; input for searchType 1, nK > 1) and
+ * nPhaseOut[nImg] (phases run; the reference's _nP). */
 typedef struct thx_expect_cfg {
     int idim, pf, vdim;       /* image box, padding factor, vdim = pf*idim */
     int nR, nT;               /* global sample set sizes */
     int mLR, mLT;             /* particle-filter set sizes (125, 9) */
-    int nPhase;               /* local phases after the scan (10) */
+    int nPhase;               /* phases when converge == 0 (10) */
     int algo;                 /* global-scan algorithm (thx_global_scan) */
-    double perturbFactor;     /* perturbFactorSGlobal (0.5) */
+    double perturbFactor;     /* perturbFactorSGlobal / perturbFactorSLocal (0.5) */
     double kMin, sMin;        /* reseed floors of k1..k3 and s0, s1 (src/Optimiser.cpp:1033-1079,
                                  OPTIMISER_SCAN_SET_MIN_STD_WITH_PERTURB):
                                  (mS^-1/3 / perturbFactor)^2 and
@@ -300,6 +345,20 @@ typedef struct thx_expect_cfg {
     int shuffle;              /* 1: shuffle the support before every resampling, as
                                  Particle::resample does (src/Particle.cpp:1298,
                                  2202-2300); 0: resample in support order */
+    /* ABI 3 */
+    int nK;                   /* classes; vol holds nK projectees of dimSize Complex back to back */
+    int searchType;           /* 0 global, 1 local */
+    int converge;             /* 0 fixed nPhase, 1 vari-decrease stopping rule */
+    int minPhase, maxPhase;   /* MIN_N_PHASE_PER_ITER_GLOBAL / _LOCAL (10 / 3), MAX_N_PHASE_PER_ITER (100) */
+    int perturbMean;          /* 0: top particle; 1: inferACG mean of the cloud
+                                 (PARTICLE_ROT_MEAN_USING_STAT_PERTURB, include/Config.h:79) */
+    int acgIters;             /* iteration cap of inferACG's fixed point (the reference loops
+                                 until sum|A - B| <= 1e-3 without a cap) */
+    double perturbFactorL;    /* perturbFactorL (2): phase 0 of a local search; also phase 1 of a
+                                 global search when largeFirst */
+    int largeFirst;           /* OPTIMISER_GLOBAL_PERTURB_LARGE (off in include/Config.h, so 0 is
+                                 the reference): 1 perturbs the first global phase by
+                                 perturbFactorL (src/Optimiser.cpp:1185-1186, 2424-2425) */
 } thx_expect_cfg;
 
 /* nOrd: length of pxOrder (<= 0 when pxOrder is NULL). */
@@ -312,6 +371,7 @@ int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                     const int* iRow, const int* pxOrder, int nOrd, int nPxl,
                     int nImg, double* quat,
                     double* trans, double* pR, double* pT, float* score,
+                    int* cls, int* nPhaseOut,
                     void* workspace, size_t wsBytes, thx_stream_t stream);
 
 /* ====================================================================== *

@@ -176,7 +176,7 @@ def test_c2_expectation_recovers_grid_poses(c2):
     sigl = ctf * ops.project3d(c2["vol"], ops.rotmat(qtrue), px) * ops.trans_table(ttrue, px)
     dat, sig = synth.noisy_images(sigl, px.iSig, N // 2 + 1, snr=20.0, seed=43)
     e = ex.Expectation(c2["vol"], px, gset, n_phase=10, seed=3)
-    quat, trans, pRo, pTo, score = e.run(dat, ctf, sig)
+    quat, trans, pRo, pTo, score = e.run(dat, ctf, sig)[:5]
     c = (ex.cloud_mode(quat) * qtrue).sum(-1).abs().clamp(max=1)
     err = torch.rad2deg(2 * torch.acos(c))
     assert float(err.median()) < 2.0 and float((err > 10).double().mean()) <= 0.05

@@ -84,7 +84,7 @@ def test_shuffle_changes_the_draw(grid_stack):
 
 
 def test_particle_filter_stays_on_the_pose(grid_stack, driver):
-    quat, trans, pR, pT, score = driver["out"]
+    quat, trans, pR, pT, score = driver["out"][:5]
     err = angle_deg(ex.cloud_mode(quat), grid_stack["qtrue"])
     assert float(err.median()) < 2.0 and float((err > 10).double().mean()) <= 0.05, err
     terr = (trans - grid_stack["ttrue"][:, None, :]).norm(dim=-1).median(dim=1).values
@@ -92,7 +92,7 @@ def test_particle_filter_stays_on_the_pose(grid_stack, driver):
 
 
 def test_particle_state_is_well_formed(driver):
-    quat, trans, pR, pT, score = driver["out"]
+    quat, trans, pR, pT, score = driver["out"][:5]
     assert torch.isfinite(quat).all() and torch.isfinite(trans).all()
     assert torch.allclose(quat.norm(dim=-1), torch.ones_like(quat[..., 0]), atol=1e-9)
     for w in (pR, pT):

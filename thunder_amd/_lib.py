@@ -47,8 +47,10 @@ SIGNATURES = {
     "thx_fsc": (_c_int, [_p, _p, _c_int, _c_int, _p, _p, _c_size, _p]),
     "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int, _c_int]),
     "thx_expectation": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int,
-                                 _p, _p,
-                                 _p, _p, _p, _p, _c_size, _p]),
+                                 _p, _p, _p, _p, _p, _p, _p, _p, _c_size, _p]),
+    "thx_local_phase_sel": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
+                                     _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p,
+                                     _p, _p, _p, _c_size, _p]),
     "thx_ExpectRotran": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
     "thx_ExpectProject": (_c_int, [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int]),
     "thx_ExpectGlobal3D": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,

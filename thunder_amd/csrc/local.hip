@@ -192,13 +192,20 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
                                                                const int* __restrict__ iRow,
                                                                const int* __restrict__ order,
                                                                int nVisit, int pf, int vdim,
-                                                               int* __restrict__ rec)
+                                                               int* __restrict__ rec,
+                                                               const int* __restrict__ act,
+                                                               const int* __restrict__ nAct)
 {
     __shared__ float sM[RT][6];
     __shared__ int sE[PB_WAVES][12][64];
     const int nC = (nVisit + KC - 1) / KC, nRT = (nR + RT - 1) / RT;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int ry = blockIdx.x % nRT, l = blockIdx.x / nRT;
+    const int ry = blockIdx.x % nRT;
+    int l = blockIdx.x / nRT;
+    if (act) {                     // active-image list: slots past the count exit
+        if (l >= *nAct) return;
+        l = act[l];
+    }
     const int nRl = min(RT, nR - ry * RT);
     for (int k = threadIdx.x; k < nRl; k += 64 * PB_WAVES) {
         double q[4], m[9];
@@ -464,9 +471,20 @@ k_local_fused(const float2* __restrict__ vol,
                                                             const int* __restrict__ order,
                                                             int nVisit, int nPxl, int idim,
                                                             const int* __restrict__ rec,
-                                                            float* __restrict__ dvp)
+                                                            float* __restrict__ dvp,
+                                                            const int* __restrict__ act,
+                                                            const int* __restrict__ nAct,
+                                                            const int* __restrict__ cls,
+                                                            long volStride)
 {
-    const int l = blockIdx.x, r0 = blockIdx.y * RT, t0 = blockIdx.z * TT;
+    int l = blockIdx.x;
+    if (act) {
+        if (l >= *nAct) return;
+        l = act[l];
+    }
+    // classification: image l projects its own class's volume
+    if (cls) vol += (size_t)cls[l] * volStride;
+    const int r0 = blockIdx.y * RT, t0 = blockIdx.z * TT;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nRl = min(RT, nR - r0);
     __shared__ __attribute__((aligned(16))) float2 sBox[BOX_CAP];
@@ -650,9 +668,15 @@ __global__ void __launch_bounds__(256) k_local_weights(const float* __restrict__
                                                        float* __restrict__ wC,
                                                        float* __restrict__ wR,
                                                        float* __restrict__ wT,
-                                                       float* __restrict__ baseL)
+                                                       float* __restrict__ baseL,
+                                                       const int* __restrict__ act,
+                                                       const int* __restrict__ nAct)
 {
-    const int l = blockIdx.x;
+    int l = blockIdx.x;
+    if (act) {
+        if (l >= *nAct) return;
+        l = act[l];
+    }
     const float* Dl = dvp + (size_t)l * nR * nT;
     const double* pRl = pR + (size_t)l * nR;
     const double* pTl = pT + (size_t)l * nT;
@@ -737,7 +761,7 @@ int launch_patch_boxes(const double* quat, int nR, const int* iCol, const int* i
                        hipStream_t s)
 {
     hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * cdiv(nR, RT)), dim3(64 * PB_WAVES), 0,
-                       s, quat, nR, iCol, iRow, order, nVisit, pf, vdim, rec);
+                       s, quat, nR, iCol, iRow, order, nVisit, pf, vdim, rec, nullptr, nullptr);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
@@ -760,6 +784,57 @@ extern "C" size_t thx_local_phase_workspace(int nImg, int nR, int nT, int nVisit
     return dvp_bytes(nImg, nR, nT) + rec_bytes(nImg, nR, nVisit) + 512;
 }
 
+static int local_phase_impl(const thx_local_sel* sel, const float* vol, int volLayout, int vdim,
+                            int pf, const double* quat, int nR, const double* trans, int nT,
+                            const double* pC, const double* pR, const double* pT, const float* dat,
+                            const float* ctf, const float* sigRcp, const int* iCol, const int* iRow,
+                            const int* pxOrder, int nOrd, int nPxl, int idim, int nImg, float* wC,
+                            float* wR, float* wT, float* baseL, float* dvp, void* workspace,
+                            size_t wsBytes, thx_stream_t stream)
+{
+    THX_CHECK_ARG(nR > 0 && nT > 0 && nPxl > 0 && nImg >= 0 && vdim > 0 && pf > 0,
+                  "thx_local_phase: bad sizes");
+    THX_CHECK_ARG(volLayout == 0 || volLayout == 1, "thx_local_phase: volLayout must be 0 or 1");
+    THX_CHECK_ARG((long)nImg * ((nR + RT - 1) / RT) <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 &&
+                      (nT + TT - 1) / TT <= 65535,
+                  "thx_local_phase: grid too large");
+    THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % KC == 0),
+                  "thx_local_phase: nOrd must be a positive multiple of 16 (thx_pixel_tile_order)");
+    const int* act = sel ? sel->active : nullptr;
+    const int* nAct = sel ? sel->nActive : nullptr;
+    const int* cls = sel ? sel->cls : nullptr;
+    THX_CHECK_ARG(!act == !nAct, "thx_local_phase_sel: active and nActive go together");
+    THX_CHECK_ARG(!cls || (sel->volStride > 0), "thx_local_phase_sel: cls needs a volStride");
+    if (nImg == 0) return THX_OK;
+    const int nVisit = pxOrder ? nOrd : nPxl;
+    THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase_workspace(nImg, nR, nT, nVisit),
+                  "thx_local_phase: workspace too small");
+    thx::Carver ws(workspace, wsBytes);
+    float* d = dvp ? dvp : ws.take<float>((size_t)nImg * nR * nT);
+    int* rec = ws.take<int>(rec_bytes(nImg, nR, nVisit) / sizeof(int));
+    hipStream_t s = thx::as_stream(stream);
+    hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * thx::cdiv(nR, RT)), dim3(64 * PB_WAVES),
+                       0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct);
+    THX_LAUNCH_CHECK();
+    dim3 grid(nImg, thx::cdiv(nR, RT), thx::cdiv(nT, TT));
+    const long vs = cls ? (long)sel->volStride : 0L;
+    if (volLayout == 1)
+        hipLaunchKernelGGL(k_local_fused<true>, grid, dim3(THREADS), 0, s,
+                           reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
+                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
+                           nVisit, nPxl, idim, rec, d, act, nAct, cls, vs);
+    else
+        hipLaunchKernelGGL(k_local_fused<false>, grid, dim3(THREADS), 0, s,
+                           reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
+                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
+                           nVisit, nPxl, idim, rec, d, act, nAct, cls, vs);
+    THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_local_weights, dim3(nImg), dim3(256), 0, s, d, nR, nT, pC, pR, pT, wC,
+                       wR, wT, baseL, act, nAct);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 extern "C" int thx_local_phase(const float* vol, int volLayout, int vdim, int pf,
                                const double* quat, int nR, const double* trans,
                                int nT, const double* pC, const double* pR,
@@ -771,39 +846,22 @@ extern "C" int thx_local_phase(const float* vol, int volLayout, int vdim, int pf
                                void* workspace, size_t wsBytes,
                                thx_stream_t stream)
 {
-    THX_CHECK_ARG(nR > 0 && nT > 0 && nPxl > 0 && nImg >= 0 && vdim > 0 && pf > 0,
-                  "thx_local_phase: bad sizes");
-    THX_CHECK_ARG(volLayout == 0 || volLayout == 1, "thx_local_phase: volLayout must be 0 or 1");
-    THX_CHECK_ARG((long)nImg * ((nR + RT - 1) / RT) <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 &&
-                      (nT + TT - 1) / TT <= 65535,
-                  "thx_local_phase: grid too large");
-    THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % KC == 0),
-                  "thx_local_phase: nOrd must be a positive multiple of 16 (thx_pixel_tile_order)");
-    if (nImg == 0) return THX_OK;
-    const int nVisit = pxOrder ? nOrd : nPxl;
-    THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase_workspace(nImg, nR, nT, nVisit),
-                  "thx_local_phase: workspace too small");
-    thx::Carver ws(workspace, wsBytes);
-    float* d = dvp ? dvp : ws.take<float>((size_t)nImg * nR * nT);
-    int* rec = ws.take<int>(rec_bytes(nImg, nR, nVisit) / sizeof(int));
-    hipStream_t s = thx::as_stream(stream);
-    hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * thx::cdiv(nR, RT)), dim3(64 * PB_WAVES),
-                       0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec);
-    THX_LAUNCH_CHECK();
-    dim3 grid(nImg, thx::cdiv(nR, RT), thx::cdiv(nT, TT));
-    if (volLayout == 1)
-        hipLaunchKernelGGL(k_local_fused<true>, grid, dim3(THREADS), 0, s,
-                           reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
-                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
-                           nVisit, nPxl, idim, rec, d);
-    else
-        hipLaunchKernelGGL(k_local_fused<false>, grid, dim3(THREADS), 0, s,
-                           reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
-                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
-                           nVisit, nPxl, idim, rec, d);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_local_weights, dim3(nImg), dim3(256), 0, s, d, nR, nT, pC, pR, pT, wC,
-                       wR, wT, baseL);
-    THX_LAUNCH_CHECK();
-    return THX_OK;
+    return local_phase_impl(nullptr, vol, volLayout, vdim, pf, quat, nR, trans, nT, pC, pR, pT,
+                            dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg, wC, wR,
+                            wT, baseL, dvp, workspace, wsBytes, stream);
+}
+
+extern "C" int thx_local_phase_sel(const thx_local_sel* sel, const float* vol, int volLayout,
+                                   int vdim, int pf, const double* quat, int nR,
+                                   const double* trans, int nT, const double* pC,
+                                   const double* pR, const double* pT, const float* dat,
+                                   const float* ctf, const float* sigRcp, const int* iCol,
+                                   const int* iRow, const int* pxOrder, int nOrd, int nPxl,
+                                   int idim, int nImg, float* wC, float* wR, float* wT,
+                                   float* baseL, float* dvp, void* workspace, size_t wsBytes,
+                                   thx_stream_t stream)
+{
+    return local_phase_impl(sel, vol, volLayout, vdim, pf, quat, nR, trans, nT, pC, pR, pT, dat,
+                            ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg, wC, wR, wT,
+                            baseL, dvp, workspace, wsBytes, stream);
 }

@@ -133,11 +133,12 @@ THX_DEV double quad4(const double* q, const double* M)
 // point B = 4/nf sum q q^T / (q^T A^-1 q) from B = I while sum|A - B| > 1e-3
 // (a NaN criterion ends the loop, as in the reference's `while`); returns the
 // last A.  Particle q_i is read as pre q_i (pre = conj(mean) de-means).
-THX_DEV void infer_acg(const double* Q, int m, const double* pre, int lane, double* A)
+THX_DEV int infer_acg(const double* Q, int m, const double* pre, int lane, double* A,
+                      int maxIt = 256)
 {
     double B[16];
     for (int k = 0; k < 16; k++) B[k] = (k % 5 == 0) ? 1.0 : 0.0;
-    for (int it = 0; it < 256; it++) {
+    for (int it = 0; it < maxIt; it++) {
         for (int k = 0; k < 16; k++) A[k] = B[k];
         double Ai[16];
         inv4(A, Ai);
@@ -159,8 +160,9 @@ THX_DEV void infer_acg(const double* Q, int m, const double* pre, int lane, doub
             for (int k = j; k < 4; k++, t++) B[4 * j + k] = B[4 * k + j] = b[t] * (4.0 / nf);
         double crit = 0.0;
         for (int k = 0; k < 16; k++) crit += fabs(A[k] - B[k]);
-        if (!(crit > 1e-3)) return;
+        if (!(crit > 1e-3)) return it + 1;
     }
+    return maxIt;
 }
 
 // Unit eigenvector of the largest eigenvalue of a symmetric 4x4 (cyclic
@@ -216,11 +218,12 @@ __global__ void __launch_bounds__(256) k_pf_calvari(int nImg, int mR, const doub
                                                     int mT, const double* __restrict__ trans,
                                                     double kFloor, double sFloor,
                                                     double* __restrict__ kOut,
-                                                    double* __restrict__ sOut)
+                                                    double* __restrict__ sOut,
+                                                    const int* __restrict__ done = nullptr)
 {
     const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
     const int lane = threadIdx.x % GROUP;
-    if (l >= nImg) return;
+    if (l >= nImg || (done && done[l])) return;
     const double* Q = quat + (size_t)l * mR * 4;
     double A[16], mean[4], cm[4];
     infer_acg(Q, mR, nullptr, lane, A);
@@ -271,12 +274,14 @@ THX_DEV void balance_rot(const double* Q, int m, int lane, double* w)
 // u <- u < hh ? 0 : u - hh, hh = u_max peak.  u >= 0, so the k-th largest is
 // found by a bisection over the ordered float bit patterns.
 __global__ void __launch_bounds__(256) k_pf_peak(int nImg, int n, float* __restrict__ u, int ldu,
-                                                 double* __restrict__ peak, int setFactor)
+                                                 double* __restrict__ peak, int setFactor,
+                                                 const int* __restrict__ cls = nullptr, int ldc = 0,
+                                                 const int* __restrict__ done = nullptr)
 {
     const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (l >= nImg) return;
-    float* ul = u + (size_t)l * ldu;
+    if (l >= nImg || (done && done[l])) return;
+    float* ul = u + (size_t)l * ldu + (cls ? (size_t)cls[l] * ldc : 0);
     float mx = 0.f;
     for (int i = lane; i < n; i += 64) mx = fmaxf(mx, ul[i]);
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -332,13 +337,16 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
                                                      double* __restrict__ cdfWs,
                                                      int* __restrict__ permWs,
                                                      int* __restrict__ permOut,
-                                                     double* __restrict__ u0Out)
+                                                     double* __restrict__ u0Out,
+                                                     const int* __restrict__ cls = nullptr,
+                                                     int ldc = 0,
+                                                     const int* __restrict__ done = nullptr)
 {
     const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (l >= nImg) return;
+    if (l >= nImg || (done && done[l])) return;
     const double* wl = w + (size_t)l * ldw;
-    const float* ul = u + (size_t)l * ldu;
+    const float* ul = u + (size_t)l * ldu + (cls ? (size_t)cls[l] * ldc : 0);
     double* cdf = cdfWs + (size_t)l * nIn;
     // Particle::shuffle before resampling (src/Particle.cpp:1298, 2202-2300):
     // a uniform random permutation of the support (gsl_ran_shuffle); position
@@ -457,6 +465,7 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
         const int oi = __shfl_xor(bi, o, 64);
         if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
     }
+    if (bi >= nIn) bi = 0;   // every u NaN: no comparison held (keep the index in range)
     if (top && lane == 0) top[l] = at(bi);
     // CDF by a wave prefix scan in FP64
     double tot = 0.0;
@@ -505,7 +514,8 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
 __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
                                                 const double* __restrict__ src, long lds,
                                                 int nIn, const int* __restrict__ anc,
-                                                double* __restrict__ dst)
+                                                double* __restrict__ dst,
+                                                const int* __restrict__ done = nullptr)
 {
     const long n = (long)nImg * nOut * width;
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
@@ -513,23 +523,28 @@ __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
         const int c = (int)(q % width);
         const long lj = q / width;
         const int l = (int)(lj / nOut);
+        if (done && done[l]) continue;
         const int a = anc[lj];
         dst[q] = src[(size_t)l * lds + (size_t)a * width + c];
         (void)nIn;
     }
 }
 
-// Particle::perturb + balanceWeight for one image per wave
+// Particle::perturb + balanceWeight for one image per GROUP lanes
 // (src/Particle.cpp:1149-1289, 2309-2375), with k / s from k_pf_calvari:
-//   R: mean = the top particle (calRank1st's _topR, the reference's branch
-//      without PARTICLE_ROT_MEAN_USING_STAT_PERTURB: Config.h turns that switch
-//      on, but inferACG of a resampled cloud of few distinct ancestors
-//      converges slowly or not at all), r_i <- mean d_i mean^-1 r_i with
+//   R: mean = inferACG(mean, _r) of the current (resampled) cloud -- the
+//      reference's compiled switch PARTICLE_ROT_MEAN_USING_STAT_PERTURB
+//      (include/Config.h:79): Tyler's fixed point from B = I until
+//      sum|A - B| <= 1e-3 (DirectionalStat.cpp:93-145), here capped at
+//      acgIters iterations, then the principal axis (:224-251) -- when
+//      meanMode == 1; the top particle (calRank1st's _topR, the branch without
+//      the switch) when meanMode == 0.  r_i <- mean d_i mean^-1 r_i with
 //      d ~ ACG(diag(1, pf^2 min(1,k1), pf^2 min(1,k2), pf^2 min(1,k3)))
 //      (sampleACG: normalised N(0, diag)), then pR = 1 / pdfACG on the
 //      perturbed cloud (balanceWeight(PAR_R)).
 //   T: t_i += pf N(0, s) (:1232-1262), reCentre beyond transM (:2473-2495),
 //      pT = 1/pdf normalised (balanceWeight(PAR_T), :2342-2375).
+// itOut (optional): inferACG iterations of the mean per image.
 __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
                                                     double* __restrict__ quat,
                                                     double* __restrict__ trans,
@@ -539,18 +554,28 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
                                                     const double* __restrict__ kIn,
                                                     const double* __restrict__ sIn,
                                                     double pf, double transS, double transM,
-                                                    uint64_t seed, uint32_t stream)
+                                                    uint64_t seed, uint32_t stream,
+                                                    int meanMode, int acgIters,
+                                                    const int* __restrict__ done,
+                                                    int* __restrict__ itOut)
 {
     const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
     const int lane = threadIdx.x % GROUP;
-    if (l >= nImg) return;
+    if (l >= nImg || (done && done[l])) return;
     double* Q = quat + (size_t)l * mR * 4;
     double* Tr = trans + (size_t)l * mT * 2;
     Philox rng(seed, (uint32_t)l, stream, (uint32_t)lane);
 
     // ---- rotation
     double mean[4], cm[4];
-    for (int k = 0; k < 4; k++) mean[k] = topQ[4 * l + k];
+    if (meanMode == 1) {
+        double A[16];
+        const int it = infer_acg(Q, mR, nullptr, lane, A, acgIters);
+        principal_axis(A, mean);
+        if (itOut && lane == 0) itOut[l] = it;
+    } else {
+        for (int k = 0; k < 4; k++) mean[k] = topQ[4 * l + k];
+    }
     cm[0] = mean[0]; cm[1] = -mean[1]; cm[2] = -mean[2]; cm[3] = -mean[3];
     const double sd1 = pf * sqrt(fmin(1.0, kIn[3 * l]));       // PERTURB_K_MAX = 1
     const double sd2 = pf * sqrt(fmin(1.0, kIn[3 * l + 1]));
@@ -611,6 +636,125 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
     for (int i = lane; i < mT; i += GROUP) pT[(size_t)l * mT + i] /= tot;
 }
 
+// Reseed of the class for K > 1 (src/Optimiser.cpp:1933-1965), one thread
+// per image: u_c = wC[l][c] -> keepHalfHeightPeak(PAR_C) with the fixed
+// PEAK_FACTOR_C = 1 - 1e-2 (PARTICLE_PEAK_FACTOR_C, include/Particle.h:55,
+// setPeakFactor src/Particle.cpp:1907-1910) -> resample(K, PAR_C): shuffle,
+// w u with the reset prior w = 1/K, systematic draw -> rand(cls): a uniform
+// entry of the resampled set (src/Particle.cpp:2109-2118).
+constexpr int KMAX_CLASS = 64;
+
+__global__ void __launch_bounds__(256) k_pf_class(int nImg, int K, const float* __restrict__ wC,
+                                                  uint64_t seed, uint32_t stream,
+                                                  int* __restrict__ cls)
+{
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= nImg) return;
+    const float* u = wC + (size_t)l * K;
+    float mx = 0.f;
+    for (int c = 0; c < K; c++) mx = fmaxf(mx, u[c]);
+    const double hh = (double)mx * (1.0 - 1e-2);
+    int pm[KMAX_CLASS];
+    for (int c = 0; c < K; c++) pm[c] = c;
+    Philox sh(seed, (uint32_t)l, stream, 0x5f1e);
+    for (int i = K - 1; i > 0; i--) {
+        const uint32_t x = sh.next().x;
+        const int j = (int)(((uint64_t)x * (uint64_t)(i + 1)) >> 32);
+        const int t = pm[i]; pm[i] = pm[j]; pm[j] = t;
+    }
+    double tot = 0.0;
+    for (int i = 0; i < K; i++) {
+        const double v = u[pm[i]];
+        tot += (v < hh ? 0.0 : v - hh) / K;
+    }
+    Philox rng(seed, (uint32_t)l, stream, 0x5e5a);
+    const double u0 = rng.uniform() / K;
+    const int j = (int)(((uint64_t)rng.next().x * (uint64_t)K) >> 32);   // rand(cls): U{0..K-1}
+    const double uj = (u0 + j * 1.0 / K) * tot;
+    double acc = 0.0;
+    int pick = pm[K - 1];
+    for (int i = 0; i < K; i++) {
+        const double v = u[pm[i]];
+        acc += (v < hh ? 0.0 : v - hh) / K;
+        if (!(uj > acc)) { pick = pm[i]; break; }
+    }
+    cls[l] = pick;
+}
+
+// The stopping rule of the phase loop with OPTIMISER_COMPRESS_CRITERIA
+// (src/Optimiser.cpp:1510-1615): from phase minPhase on, variR =
+// (k1 k2 k3)^(1/6) (Particle::variR, src/Particle.cpp:611-627) and variT =
+// sqrt of the eigenvalue product of [[s0^2, rho], [rho, s1^2]] = s0 s1 (rho =
+// 0: PARTICLE_RHO is off) of this phase's calVari are compared with the
+// smallest values so far.  All three bests start at DBL_MAX, so the first
+// check always finds "room" (variD = _s never changes without CTF search);
+// afterwards one phase without a 5 % decrease of either ends the image
+// (N_PHASE_WITH_NO_VARI_DECREASE = 1) and _nP = phase.  lastPhase: the loop's
+// end (MAX_N_PHASE_PER_ITER - 1).
+__global__ void k_pf_converge(int nImg, int phase, int minPhase, int lastPhase,
+                              const double* __restrict__ kv, const double* __restrict__ sv,
+                              double* __restrict__ bestR, double* __restrict__ bestT,
+                              int* __restrict__ done, int* __restrict__ nP)
+{
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= nImg || done[l]) return;
+    bool stop = phase >= lastPhase;
+    if (phase >= minPhase) {
+        const double vR = pow(kv[3 * l] * kv[3 * l + 1] * kv[3 * l + 2], 1.0 / 6);
+        const double vT = sv[2 * l] * sv[2 * l + 1];
+        const bool first = phase == minPhase;
+        const bool room = first || vR < bestR[l] * 0.95 || vT < bestT[l] * 0.95;
+        bestR[l] = first ? vR : fmin(bestR[l], vR);
+        bestT[l] = first ? vT : fmin(bestT[l], vT);
+        stop = stop || !room;
+    }
+    if (stop) {
+        done[l] = 1;
+        nP[l] = phase;
+    }
+}
+
+// Active-image list: act[0 .. *nAct) = the images with done == 0, in order
+// (one workgroup, ballot prefix per wave).
+__global__ void __launch_bounds__(1024) k_compact(int nImg, const int* __restrict__ done,
+                                                  int* __restrict__ act, int* __restrict__ nAct)
+{
+    __shared__ int sW[16];
+    __shared__ int sBase;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) sBase = 0;
+    __syncthreads();
+    for (int b = 0; b < nImg; b += 1024) {
+        const int i = b + tid;
+        const bool f = i < nImg && !(done && done[i]);
+        const unsigned long long m = __ballot(f);
+        const int pre = __popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) sW[wv] = __popcll(m);
+        __syncthreads();
+        int off = sBase;
+        for (int w = 0; w < wv; w++) off += sW[w];
+        if (f) act[off + pre] = i;
+        __syncthreads();
+        if (tid == 0)
+            for (int w = 0; w < 16; w++) sBase += sW[w];
+        __syncthreads();
+    }
+    if (tid == 0) *nAct = sBase;
+}
+
+// topQ[l] = the particle of largest prior pR (calRank1st on the caller's
+// state, for a local search that starts from it).
+__global__ void k_top_by_weight(int nImg, int mR, const double* __restrict__ quat,
+                                const double* __restrict__ pR, double* __restrict__ topQ)
+{
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= nImg) return;
+    int best = 0;
+    for (int i = 1; i < mR; i++)
+        if (pR[(size_t)l * mR + i] > pR[(size_t)l * mR + best]) best = i;
+    for (int k = 0; k < 4; k++) topQ[4 * l + k] = quat[((size_t)l * mR + best) * 4 + k];
+}
+
 struct Plan {
     // carve of the driver workspace
     float* rotP; double* gMat; float* traP;
@@ -621,6 +765,8 @@ struct Plan {
     double* kv; double* sv; double* peakR;   // calVari k1..k3, s0 s1; setPeakFactor(R)
     double* topQ;                            // calRank1st _topR
     float* wC; float* wR; float* wT; float* base; double* pC;
+    int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
+    double* bestR; double* bestT;                        // convergence: smallest variR / variT
     void* localWs; size_t localWsBytes;
     size_t bytes;
 };
@@ -629,17 +775,19 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
 {
     thx::Carver k(base, ~size_t(0));
     Plan p;
+    const int nK = c.nK > 0 ? c.nK : 1;
     int nMax = c.nR > c.nT ? c.nR : c.nT;           // every resampled support size
     if (c.mLR > nMax) nMax = c.mLR;
     if (c.mLT > nMax) nMax = c.mLT;
-    p.rotP = k.take<float>((size_t)2 * c.nR * nPxl);
-    p.gMat = k.take<double>((size_t)9 * c.nR);
-    p.traP = k.take<float>((size_t)2 * c.nT * nPxl);
-    p.gWC = k.take<float>(nImg);
-    p.gWR = k.take<float>((size_t)nImg * c.nR);
-    p.gWT = k.take<float>((size_t)nImg * c.nT);
+    const bool scan = c.searchType == 0;
+    p.rotP = k.take<float>(scan ? (size_t)2 * c.nR * nPxl : 0);
+    p.gMat = k.take<double>(scan ? (size_t)9 * c.nR : 0);
+    p.traP = k.take<float>(scan ? (size_t)2 * c.nT * nPxl : 0);
+    p.gWC = k.take<float>((size_t)nImg * nK);
+    p.gWR = k.take<float>(scan ? (size_t)nImg * nK * c.nR : 0);
+    p.gWT = k.take<float>(scan ? (size_t)nImg * nK * c.nT : 0);
     p.gBase = k.take<float>(nImg);
-    p.scanWsBytes = thx_global_scan_workspace(nImg, c.nR, c.nT, nPxl, c.algo);
+    p.scanWsBytes = scan ? thx_global_scan_workspace(nImg, c.nR, c.nT, nPxl, c.algo) : 0;
     p.scanWs = k.take<char>(p.scanWsBytes);
     p.anc = k.take<int>((size_t)nImg * (c.mLR > c.mLT ? c.mLR : c.mLT));
     p.cdf = k.take<double>((size_t)nImg * nMax);
@@ -657,6 +805,13 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     p.wT = k.take<float>((size_t)nImg * c.mLT);
     p.base = k.take<float>(nImg);
     p.pC = k.take<double>(nImg);
+    p.cls = k.take<int>(nImg);
+    p.nP = k.take<int>(nImg);
+    p.done = k.take<int>(nImg);
+    p.act = k.take<int>(nImg);
+    p.nAct = k.take<int>(1);
+    p.bestR = k.take<double>(nImg);
+    p.bestT = k.take<double>(nImg);
     p.localWsBytes = thx_local_phase_workspace(nImg, c.mLR, c.mLT, nVisit);
     p.localWs = k.take<char>(p.localWsBytes);
     p.bytes = k.off + 256;
@@ -665,15 +820,23 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
 
 // topQ[l] = src[l (or shared)][top[l]] -- Particle::_topR after calRank1st
 __global__ void k_top_copy(int nImg, const double* __restrict__ src, long lds,
-                           const int* __restrict__ top, double* __restrict__ topQ)
+                           const int* __restrict__ top, double* __restrict__ topQ,
+                           const int* __restrict__ done = nullptr)
 {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nImg * 4) return;
     const int l = q / 4, k = q % 4;
+    if (done && done[l]) return;
     topQ[q] = src[(size_t)l * lds + (size_t)top[l] * 4 + k];
 }
 
 __global__ void k_fill(double* p, long n, double v)
+{
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x)
+        p[q] = v;
+}
+
+__global__ void k_fill_int(int* p, long n, int v)
 {
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x)
         p[q] = v;
@@ -769,17 +932,28 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                                const int* iRow, const int* pxOrder, int nOrd, int nPxl, int nImg,
                                double* quat,
                                double* trans, double* pR, double* pT,
-                               float* score, void* workspace, size_t wsBytes,
-                               thx_stream_t stream)
+                               float* score, int* cls, int* nPhaseOut, void* workspace,
+                               size_t wsBytes, thx_stream_t stream)
 {
-    THX_CHECK_ARG(cfg && vol && gQuat && gTrans && gPR && gPT && dat && ctf && sigRcp &&
-                      iCol && iRow && quat && trans && pR && pT,
+    THX_CHECK_ARG(cfg && vol && dat && ctf && sigRcp && iCol && iRow && quat && trans && pR && pT,
                   "thx_expectation: null argument");
     const thx_expect_cfg& c = *cfg;
-    THX_CHECK_ARG(c.nR > 0 && c.nT > 0 && c.mLR > 0 && c.mLT > 0 && c.nPhase >= 0 &&
-                      c.vdim == c.pf * c.idim && nImg >= 0 && nImg <= 65535 && nPxl > 0,
+    const bool global = c.searchType == 0;
+    THX_CHECK_ARG(c.searchType == 0 || c.searchType == 1, "thx_expectation: searchType must be 0 or 1");
+    THX_CHECK_ARG(!global || (gQuat && gTrans && gPR && gPT),
+                  "thx_expectation: a global search needs the global sample set");
+    THX_CHECK_ARG(c.mLR > 0 && c.mLT > 0 && c.vdim == c.pf * c.idim && nImg >= 0 && nImg <= 65535 &&
+                      nPxl > 0 && (!global || (c.nR > 0 && c.nT > 0)),
                   "thx_expectation: bad configuration");
-    THX_CHECK_ARG(c.nR <= 65535, "thx_expectation: nR > 65535");
+    THX_CHECK_ARG(c.nK >= 1 && c.nK <= KMAX_CLASS, "thx_expectation: nK must be in [1, 64]");
+    THX_CHECK_ARG(global || c.nK == 1 || cls,
+                  "thx_expectation: a K-class local search needs the particles' classes (cls)");
+    THX_CHECK_ARG(c.converge ? (c.minPhase >= 0 && c.maxPhase > c.minPhase && c.maxPhase <= 1000)
+                             : (c.nPhase >= 0),
+                  "thx_expectation: bad phase counts");
+    THX_CHECK_ARG(c.perturbMean == 0 || c.perturbMean == 1, "thx_expectation: perturbMean must be 0 or 1");
+    THX_CHECK_ARG(c.perturbMean == 0 || c.acgIters > 0, "thx_expectation: acgIters must be > 0");
+    THX_CHECK_ARG(!global || c.nR <= 65535, "thx_expectation: nR > 65535");
     if (nImg == 0) return THX_OK;
     THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % 16 == 0),
                   "thx_expectation: nOrd must be a positive multiple of 16");
@@ -788,84 +962,155 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     hipStream_t s = thx::as_stream(stream);
     const unsigned gImg = thx::cdiv(nImg, 4);
     const unsigned gPf = thx::cdiv(nImg * GROUP, 256);
+    const unsigned gOne = thx::cdiv(nImg, 256);
+    const int nK = c.nK;
+    const size_t dimSize = (size_t)(c.vdim / 2 + 1) * c.vdim * c.vdim;
+    int* clsD = cls ? cls : p.cls;
+    int* nPD = nPhaseOut ? nPhaseOut : p.nP;
+    const int* clsSel = nK > 1 ? clsD : nullptr;    // rows / volumes picked per image
 
-    // ---- global scan (ExpectRotran + ExpectProject + ExpectGlobal3D)
-    THX_RET(thx_rotmat(gQuat, c.nR, p.gMat, stream));
-    THX_RET(thx_project3d(vol, c.vdim, c.pf, p.gMat, c.nR, iCol, iRow, nPxl, p.rotP, stream));
-    THX_RET(thx_trans_table(gTrans, c.nT, iCol, iRow, nPxl, c.idim, p.traP, stream));
-    THX_RET(thx_global_scan(p.rotP, c.nR, p.traP, c.nT, dat, ctf, sigRcp, nImg, nPxl, gPR,
-                            gPT, 0, 1, p.gWC, p.gWR, p.gWT, p.gBase, c.algo, p.scanWs,
-                            p.scanWsBytes, stream));
-
-    // ---- reseed from the scan marginals (src/Optimiser.cpp:1966-2079):
-    // setPeakFactor + keepHalfHeightPeak (R), resample R and T, calVari with
-    // the scan floors (OPTIMISER_SCAN_SET_MIN_STD_WITH_PERTURB)
-    hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.nR, p.gWR, c.nR, p.peakR, 1);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nR, c.mLR, gPR, 0,
-                       p.gWR, c.nR, c.seed, 1000u, p.anc, pR, p.topR, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, gQuat, 0L, c.nR,
-                       p.anc, quat);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg, gQuat,
-                       0L, p.topR, p.topQ);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nT, c.mLT, gPT, 0,
-                       p.gWT, c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, gTrans, 0L, c.nT,
-                       p.anc, trans);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT, trans,
-                       c.kMin, c.sMin, p.kv, p.sv);
-    THX_LAUNCH_CHECK();
+    if (global) {
+        // ---- global scan of every class (ExpectRotran + ExpectProject + ExpectGlobal3D
+        // with kIdx = class, src/Optimiser.cpp:1815-1847)
+        THX_RET(thx_rotmat(gQuat, c.nR, p.gMat, stream));
+        THX_RET(thx_trans_table(gTrans, c.nT, iCol, iRow, nPxl, c.idim, p.traP, stream));
+        for (int k = 0; k < nK; k++) {
+            THX_RET(thx_project3d(vol + 2 * dimSize * k, c.vdim, c.pf, p.gMat, c.nR, iCol, iRow,
+                                  nPxl, p.rotP, stream));
+            THX_RET(thx_global_scan(p.rotP, c.nR, p.traP, c.nT, dat, ctf, sigRcp, nImg, nPxl, gPR,
+                                    gPT, k, nK, p.gWC, p.gWR, p.gWT, p.gBase, c.algo, p.scanWs,
+                                    p.scanWsBytes, stream));
+        }
+        // ---- reseed (src/Optimiser.cpp:1930-2131): the class draw, then
+        // setPeakFactor + keepHalfHeightPeak (R), resample R and T of the drawn
+        // class, calVari with the scan floors (OPTIMISER_SCAN_SET_MIN_STD_WITH_PERTURB)
+        if (nK > 1) {
+            hipLaunchKernelGGL(k_pf_class, dim3(gOne), dim3(256), 0, s, nImg, nK, p.gWC, c.seed,
+                               999u, clsD);
+            THX_LAUNCH_CHECK();
+        } else {
+            THX_HIP(hipMemsetAsync(clsD, 0, sizeof(int) * nImg, s));
+        }
+        hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.nR, p.gWR, nK * c.nR,
+                           p.peakR, 1, clsSel, c.nR, nullptr);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nR, c.mLR, gPR, 0,
+                           p.gWR, nK * c.nR, c.seed, 1000u, p.anc, pR, p.topR, p.cdf,
+                           c.shuffle ? p.perm : nullptr, nullptr, nullptr, clsSel, c.nR, nullptr);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, gQuat, 0L, c.nR,
+                           p.anc, quat, nullptr);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg, gQuat,
+                           0L, p.topR, p.topQ, nullptr);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nT, c.mLT, gPT, 0,
+                           p.gWT, nK * c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf,
+                           c.shuffle ? p.perm : nullptr, nullptr, nullptr, clsSel, c.nT, nullptr);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, gTrans, 0L, c.nT,
+                           p.anc, trans, nullptr);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT, trans,
+                           c.kMin, c.sMin, p.kv, p.sv, nullptr);
+        THX_LAUNCH_CHECK();
+    } else {
+        // ---- local search from the caller's particle state: its spreads
+        // (calVari on the given cloud) and, for the top-particle mean, calRank1st
+        if (nK == 1 && !cls) THX_HIP(hipMemsetAsync(clsD, 0, sizeof(int) * nImg, s));
+        hipLaunchKernelGGL(k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT, trans,
+                           0.0, 0.0, p.kv, p.sv, nullptr);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_top_by_weight, dim3(gOne), dim3(256), 0, s, nImg, c.mLR, quat, pR, p.topQ);
+        THX_LAUNCH_CHECK();
+        // the rotation peak factor a fresh particle carries (resetPeakFactor,
+        // src/Particle.cpp:1957-1962: PEAK_FACTOR_MIN); a global search sets it
+        // in the reseed
+        hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, s, p.peakR, (long)nImg, 1e-3);
+        THX_LAUNCH_CHECK();
+    }
     hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, s, p.pC, (long)nImg, 1.0);
     THX_LAUNCH_CHECK();
 
-    // ---- particle-filter phases (src/Optimiser.cpp:1183-1500): perturb +
+    // ---- particle-filter phases (src/Optimiser.cpp:1183-1616): perturb +
     // balanceWeight, likelihood + marginals, keepHalfHeightPeak (R),
-    // calRank1st, calVari (pre-resample cloud), resample
-    for (int phase = 1; phase <= c.nPhase; phase++) {
-        hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
-                           trans, pR, pT, p.topQ, p.kv, p.sv, c.perturbFactor, c.transS, c.transM,
-                           c.seed, (uint32_t)(2000 + phase));
+    // calRank1st, calVari (pre-resample cloud), resample, stopping rule
+    const int phase0 = global ? 1 : 0;
+    const int nPh = c.converge ? c.maxPhase - phase0 : c.nPhase;
+    const int* done = nullptr;
+    thx_local_sel sel{nullptr, nullptr, clsSel, (long long)dimSize};
+    if (c.converge) {
+        THX_HIP(hipMemsetAsync(p.done, 0, sizeof(int) * nImg, s));
+        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
         THX_LAUNCH_CHECK();
-        THX_RET(thx_local_phase(vol, 0, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT, dat,
-                                ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, c.idim, nImg, p.wC, p.wR, p.wT,
-                                p.base, nullptr, p.localWs, p.localWsBytes, stream));
+        done = p.done;
+        sel.active = p.act;
+        sel.nActive = p.nAct;
+    }
+    for (int phase = phase0; phase < phase0 + nPh; phase++) {
+        const bool large = phase == phase0 && (!global || c.largeFirst);
+        hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
+                           trans, pR, pT, p.topQ, p.kv, p.sv,
+                           large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
+                           c.seed, (uint32_t)(2000 + phase), c.perturbMean, c.acgIters, done,
+                           nullptr);
+        THX_LAUNCH_CHECK();
+        THX_RET(thx_local_phase_sel(&sel, vol, 0, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC,
+                                    pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl,
+                                    c.idim, nImg, p.wC, p.wR, p.wT, p.base, nullptr, p.localWs,
+                                    p.localWsBytes, stream));
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
-                           p.peakR, 0);
+                           p.peakR, 0, nullptr, 0, done);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT,
-                           trans, 0.0, 0.0, p.kv, p.sv);
+                           trans, 0.0, 0.0, p.kv, p.sv, done);
         THX_LAUNCH_CHECK();
         // resample R and T by the phase marginals; ancestors gathered in place
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, c.mLR, pR,
                            c.mLR, p.wR, c.mLR, c.seed, (uint32_t)(3000 + phase), p.anc, pR,
-                           p.topR, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr);
+                           p.topR, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
+                           0, done);
         THX_LAUNCH_CHECK();
         THX_HIP(hipMemcpyAsync(p.tmpQ, quat, sizeof(double) * nImg * c.mLR * 4,
                                hipMemcpyDeviceToDevice, s));
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, p.tmpQ,
-                           (long)c.mLR * 4, c.mLR, p.anc, quat);
+                           (long)c.mLR * 4, c.mLR, p.anc, quat, done);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg,
-                           p.tmpQ, (long)c.mLR * 4, p.topR, p.topQ);
+                           p.tmpQ, (long)c.mLR * 4, p.topR, p.topQ, done);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLT, c.mLT, pT,
                            c.mLT, p.wT, c.mLT, c.seed, (uint32_t)(4000 + phase), p.anc, pT,
-                           p.topT, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr);
+                           p.topT, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
+                           0, done);
         THX_LAUNCH_CHECK();
         THX_HIP(hipMemcpyAsync(p.tmpT, trans, sizeof(double) * nImg * c.mLT * 2,
                                hipMemcpyDeviceToDevice, s));
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, p.tmpT,
-                           (long)c.mLT * 2, c.mLT, p.anc, trans);
+                           (long)c.mLT * 2, c.mLT, p.anc, trans, done);
+        THX_LAUNCH_CHECK();
+        if (c.converge) {
+            hipLaunchKernelGGL(k_pf_converge, dim3(gOne), dim3(256), 0, s, nImg, phase, c.minPhase,
+                               phase0 + nPh - 1, p.kv, p.sv, p.bestR, p.bestT, p.done, nPD);
+            THX_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
+            THX_LAUNCH_CHECK();
+            if (phase >= c.minPhase) {
+                int left = 0;
+                THX_HIP(hipMemcpyAsync(&left, p.nAct, sizeof(int), hipMemcpyDeviceToHost, s));
+                THX_HIP(hipStreamSynchronize(s));
+                if (left == 0) break;
+            }
+        }
+    }
+    if (!c.converge) {
+        hipLaunchKernelGGL(k_fill_int, dim3(64), dim3(256), 0, s, nPD, (long)nImg,
+                           phase0 + c.nPhase - 1);
         THX_LAUNCH_CHECK();
     }
     if (score) {
-        // per-image score: log of the last phase's class marginal + baseline
-        THX_HIP(hipMemcpyAsync(score, c.nPhase > 0 ? p.base : p.gBase, sizeof(float) * nImg,
+        // per-image score: the last phase's baseline (the scan's without phases)
+        THX_HIP(hipMemcpyAsync(score, nPh > 0 ? p.base : p.gBase, sizeof(float) * nImg,
                                hipMemcpyDeviceToDevice, s));
     }
     return THX_OK;

@@ -19,8 +19,11 @@ from ._lib import check, lib
 
 INCLUDE_OPTIMISER_H = {
     "MIN_N_PHASE_PER_ITER_GLOBAL": 10,   # include/Optimiser.h:56
+    "MIN_N_PHASE_PER_ITER_LOCAL": 3,     # include/Optimiser.h:57
+    "MAX_N_PHASE_PER_ITER": 100,         # include/Optimiser.h:58
     "MIN_STD_FACTOR": 1,                 # include/Optimiser.h:73
 }
+SEARCH = {"global": 0, "local": 1}      # SEARCH_TYPE_GLOBAL / SEARCH_TYPE_LOCAL
 
 
 class ExpectCfg(ctypes.Structure):
@@ -30,44 +33,78 @@ class ExpectCfg(ctypes.Structure):
                 ("perturbFactor", ctypes.c_double), ("kMin", ctypes.c_double),
                 ("sMin", ctypes.c_double), ("transS", ctypes.c_double),
                 ("transM", ctypes.c_double), ("seed", ctypes.c_ulonglong),
-                ("shuffle", ctypes.c_int)]
+                ("shuffle", ctypes.c_int),
+                # ABI 3
+                ("nK", ctypes.c_int), ("searchType", ctypes.c_int), ("converge", ctypes.c_int),
+                ("minPhase", ctypes.c_int), ("maxPhase", ctypes.c_int),
+                ("perturbMean", ctypes.c_int), ("acgIters", ctypes.c_int),
+                ("perturbFactorL", ctypes.c_double), ("largeFirst", ctypes.c_int)]
 
 
 class Expectation:
-    """One round of the global-search expectation on the current GPU.
+    """One round of expectation on the current GPU (Optimiser::expectationG).
 
-    vol: half-complex projectee [vdim, vdim, vdim/2+1] complex64 (device).
-    gset: (quat [nR,4], trans [nT,2], pR [nR], pT [nT]) numpy float64.
+    vol: half-complex projectee [vdim, vdim, vdim/2+1] complex64 (device), or
+         [nK, vdim, vdim, vdim/2+1] for K-class classification.
+    gset: (quat [nR,4], trans [nT,2], pR [nR], pT [nT]) numpy float64 (global
+          search; None for a local search).
+    search: "global" (scan + reseed + phases 1..) or "local" (phases 0.. from
+            the caller's particle state, passed to run()).
+    converge: per-image vari-decrease stopping rule between MIN_N_PHASE_PER_ITER
+              (10 global / 3 local) and MAX_N_PHASE_PER_ITER (100) phases;
+              False: exactly n_phase phases.
+    perturb_mean: "acg" = inferACG mean of the cloud (the reference's compiled
+                  PARTICLE_ROT_MEAN_USING_STAT_PERTURB), "top" = top particle.
+    large_first: OPTIMISER_GLOBAL_PERTURB_LARGE (off in the reference's
+                 include/Config.h): the first global phase perturbs by perturbFactorL.
     """
 
-    def __init__(self, vol, px, gset, mLR=125, mLT=9, n_phase=10, perturb=0.5,
-                 trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7, shuffle=True):
+    def __init__(self, vol, px, gset=None, mLR=125, mLT=9, n_phase=10, perturb=0.5,
+                 trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7, shuffle=True,
+                 search="global", converge=False, perturb_mean="acg", acg_iters=100,
+                 perturb_large=2.0, large_first=False, min_phase=None, max_phase=None):
         dev = vol.device
         self.vol, self.px, self.dev = vol, px, dev
-        q, t, pR, pT = gset
-        self.gQuat = torch.as_tensor(np.ascontiguousarray(q), dtype=torch.float64, device=dev)
-        self.gTrans = torch.as_tensor(np.ascontiguousarray(t), dtype=torch.float64, device=dev)
-        self.gPR = torch.as_tensor(np.ascontiguousarray(pR), dtype=torch.float64, device=dev)
-        self.gPT = torch.as_tensor(np.ascontiguousarray(pT), dtype=torch.float64, device=dev)
-        vdim = vol.shape[0]
-        nR, nT = len(q), len(t)
-        scan_min_std_r = nR ** (-1.0 / 3)                    # src/Optimiser.cpp:765-771
+        nK = vol.shape[0] if vol.dim() == 4 else 1
+        vdim = vol.shape[-3]
+        self.search = SEARCH[search]
+        if self.search == 0:
+            q, t, pR, pT = gset
+            self.gQuat = torch.as_tensor(np.ascontiguousarray(q), dtype=torch.float64, device=dev)
+            self.gTrans = torch.as_tensor(np.ascontiguousarray(t), dtype=torch.float64, device=dev)
+            self.gPR = torch.as_tensor(np.ascontiguousarray(pR), dtype=torch.float64, device=dev)
+            self.gPT = torch.as_tensor(np.ascontiguousarray(pT), dtype=torch.float64, device=dev)
+            nR, nT = len(q), len(t)
+        else:
+            self.gQuat = self.gTrans = self.gPR = self.gPT = None
+            nR, nT = 0, 0
+        scan_min_std_r = nR ** (-1.0 / 3) if nR else 0.0     # src/Optimiser.cpp:765-771
         scan_min_std_t = 1.0 / synth.CHI2_QINV_HALF_2DOF / math.sqrt(trans_search_factor * math.pi)
         trans_m = trans_s * (-2.0 * math.log(0.05))           # reCentre, TRANS_Q = 0.05
         # reseed floors with OPTIMISER_SCAN_SET_MIN_STD_WITH_PERTURB (include/Config.h:224,
         # src/Optimiser.cpp:1033-1079); MIN_STD_FACTOR = 1
         k_floor = (scan_min_std_r / perturb) ** 2
         s_floor = scan_min_std_t / perturb
+        if min_phase is None:
+            min_phase = INCLUDE_OPTIMISER_H["MIN_N_PHASE_PER_ITER_GLOBAL" if self.search == 0
+                                            else "MIN_N_PHASE_PER_ITER_LOCAL"]
+        if max_phase is None:
+            max_phase = INCLUDE_OPTIMISER_H["MAX_N_PHASE_PER_ITER"]
         self.cfg = ExpectCfg(px.idim, px.pf, vdim, nR, nT, mLR, mLT, n_phase, algo, perturb,
-                             k_floor, s_floor, trans_s, trans_m, seed, int(bool(shuffle)))
-        self.mLR, self.mLT = mLR, mLT
+                             k_floor, s_floor, trans_s, trans_m, seed, int(bool(shuffle)),
+                             nK, self.search, int(bool(converge)), min_phase, max_phase,
+                             {"top": 0, "acg": 1}[perturb_mean], acg_iters, perturb_large,
+                             int(bool(large_first)))
+        self.mLR, self.mLT, self.nK = mLR, mLT, nK
 
     def workspace_bytes(self, nImg):
         return lib().thx_expectation_workspace(ctypes.byref(self.cfg), nImg, self.px.n,
                                                len(self.px.order))
 
-    def run(self, dat, ctf, sig, out=None):
-        """Expectation of one image batch; returns (quat, trans, pR, pT, score) on device."""
+    def run(self, dat, ctf, sig, out=None, state=None):
+        """Expectation of one image batch; returns (quat, trans, pR, pT, score,
+        cls, nPhase) on device.  state: the starting particle state (quat,
+        trans, pR, pT[, cls]) of a local search (updated in place)."""
         nImg, nPxl = dat.shape
         if nPxl != self.px.n:
             raise ValueError("pixel set / image size mismatch")
@@ -75,21 +112,34 @@ class Expectation:
                             ("sigRcp", sig, torch.float32)):
             ops._req(t, dt, (nImg, nPxl), name)
         dev = self.dev
-        if out is None:
+        if self.search == 1:
+            if state is None:
+                raise ValueError("a local search starts from a particle state")
+            quat, trans, pR, pT = state[:4]
+            for name, t, shp in (("quat", quat, (nImg, self.mLR, 4)), ("trans", trans, (nImg, self.mLT, 2)),
+                                 ("pR", pR, (nImg, self.mLR)), ("pT", pT, (nImg, self.mLT))):
+                ops._req(t, torch.float64, shp, name)
+            cls = state[4] if len(state) > 4 else torch.zeros(nImg, dtype=torch.int32, device=dev)
+            ops._req(cls, torch.int32, (nImg,), "cls")
+            out = (quat, trans, pR, pT, torch.empty(nImg, dtype=torch.float32, device=dev), cls,
+                   torch.empty(nImg, dtype=torch.int32, device=dev))
+        elif out is None:
             out = (torch.empty(nImg, self.mLR, 4, dtype=torch.float64, device=dev),
                    torch.empty(nImg, self.mLT, 2, dtype=torch.float64, device=dev),
                    torch.empty(nImg, self.mLR, dtype=torch.float64, device=dev),
                    torch.empty(nImg, self.mLT, dtype=torch.float64, device=dev),
-                   torch.empty(nImg, dtype=torch.float32, device=dev))
-        quat, trans, pR, pT, score = out
+                   torch.empty(nImg, dtype=torch.float32, device=dev),
+                   torch.empty(nImg, dtype=torch.int32, device=dev),
+                   torch.empty(nImg, dtype=torch.int32, device=dev))
+        quat, trans, pR, pT, score, cls, nph = out
         ws = ops.workspace(self.workspace_bytes(nImg), dev)
         P = ops._ptr
         check(lib().thx_expectation(ctypes.byref(self.cfg), P(self.vol), P(self.gQuat),
                                     P(self.gTrans), P(self.gPR), P(self.gPT), P(dat), P(ctf),
                                     P(sig), P(self.px.d_iCol), P(self.px.d_iRow),
                                     P(self.px.d_order), len(self.px.order), nPxl, nImg,
-                                    P(quat), P(trans), P(pR), P(pT), P(score), P(ws), ws.numel(),
-                                    ops._stream(dev)), "thx_expectation")
+                                    P(quat), P(trans), P(pR), P(pT), P(score), P(cls), P(nph),
+                                    P(ws), ws.numel(), ops._stream(dev)), "thx_expectation")
         return out
 
 

@@ -60,7 +60,7 @@ def main():
     # likelihood of the true pose vs the scan's pick (direct dvp, translation = truth)
     for n_phase in (0, 1, 3, 10):
         e = ex.Expectation(vol, px, gset, n_phase=n_phase, algo=a.algo, seed=5)
-        quat, trans, pRo, pTo, score = e.run(dat, ctf, sig)
+        quat, trans, pRo, pTo, score = e.run(dat, ctf, sig)[:5]
         out[f"phase{n_phase}_mode_err"] = stats(angle_deg(ex.cloud_mode(quat), qtrue))
         out[f"phase{n_phase}_idx0_err"] = stats(angle_deg(quat[:, 0], qtrue))
         out[f"phase{n_phase}_trans_err_p50"] = float((trans[:, 0] - ttrue).norm(dim=-1).median())
