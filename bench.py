@@ -7,8 +7,17 @@ inputs resident in HBM: global scan over nR = 2000 rotations x nT = 151
 translations at the global-search radius (rU = 24, nPxl = 870), reseed, then
 10 particle-filter phases (mLR = 125, mLT = 9) -- SURVEY.md §8(d).  Weak
 scaling: every rank owns its own batch (gold-standard hemisphere = rank % 2),
-no collective on the expectation path.  Insert (mReco = 100) and the RCCL
-half-map all-reduce are timed separately and reported as extra fields.
+no collective on the expectation path.  Insert (mReco = 100), the RCCL
+half-map all-reduce (thx_halfmap_allreduce over each hemisphere's ranks) and
+the FSC are timed separately and reported as extra fields.
+
+`roofline` is the dominant kernel of the timed step, k_local_fused<false>
+(the particle-filter phase at global resolution), timed by HIP events the
+driver records around every one of its launches inside the timed region
+(thx_expect_cfg.phaseEvents) and priced at SURVEY §8(d)'s algorithmic FLOP
+(56 mLR nPxl + 15 mLR mLT nPxl per image-phase) against the FP32 peak.  The
+global scan and the full-resolution phase are reported beside it
+(roofline_scan, roofline_local).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -156,38 +165,63 @@ def local_roofline(vol, N, pf, device, n_img=512, reps=3):
     return sec, algo_bytes, px.n, sec_plain
 
 
-def cpu_baseline(vol_np, N, pf, gset, dat, ctf, sig, px_host, seconds):
-    """The C restatement (oracle/, OpenMP) on the host cores, same workload
-    shape, bounded sample of images (test infrastructure as CPU baseline)."""
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def cpu_baseline(vol_np, N, pf, gset, dat, ctf, sig, px, seconds, phases):
+    """The CPU path (oracle/cpu_fast.c: the reference's expectation loop
+    structure, OpenMP, -O3 -march=native, likelihood vectorised over images in
+    the scan and over pixels in the phases) on the host cores, same workload
+    shape per image, on a bounded sample of images."""
+    import ctypes
     from oracle import oracle as orc
-    threads = min(16, os.cpu_count() or 1)
-    q, t, pR, pT = gset
+    orc.build()
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "libcpufast.so"))
+    P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or (os.cpu_count() or 1))
+    q, t, pR, pT = (np.ascontiguousarray(x) for x in gset)
     vdim = pf * N
+    mR, mT = 125, 9
     rng = np.random.default_rng(0)
+    vol_np = np.ascontiguousarray(vol_np)
+    iCol, iRow = np.ascontiguousarray(px.iCol), np.ascontiguousarray(px.iRow)
 
     def run(n):
+        lq = np.ascontiguousarray(synth.clustered_quaternions(n * phases, mR, 3.0, rng))
+        lt = np.ascontiguousarray(rng.standard_normal((n * phases, mT, 2)))
+        d, c, s_ = (np.ascontiguousarray(x[:n]) for x in (dat, ctf, sig))
+        base = np.zeros(n, np.float32)
+        lb = np.zeros(n, np.float32)
         t0 = time.perf_counter()
-        d = orc.dvp_global(vol_np, vdim, pf, q, t, dat[:n], ctf[:n], sig[:n], px_host, N,
-                           threads=threads)
-        orc.weights_global(d, pR, pT)
-        # 10 local phases per image (125 x 9 samples), likelihood + marginals
-        for l in range(n):
-            for _ in range(10):
-                lq = synth.uniform_quaternions(125, rng)
-                lt = rng.standard_normal((9, 2))
-                orc.local_phase(vol_np, vdim, pf, lq, lt, 1.0, np.full(125, 1 / 125),
-                                np.full(9, 1 / 9), dat[l], ctf[l], sig[l], px_host, N)
+        L.cpu_step(P(vol_np), vdim, pf, P(q), len(q), P(t), len(t), P(pR), P(pT), P(d), P(c), P(s_),
+                   n, P(iCol), P(iRow), px.n, N, P(lq), mR, P(lt), mT, phases, P(base), P(lb))
         return time.perf_counter() - t0
 
-    n = 2
+    n = 16
     dt = run(n)
-    n2 = max(2, min(len(dat), int(n * seconds / max(dt, 1e-3))))
+    n2 = max(16, min(len(dat), int(n * seconds / max(dt, 1e-3))))
     if n2 > n:
         dt = run(n2)
         n = n2
+    model, ncpu = cpu_info()
     return {"value": n / dt, "unit": "particle-images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} images x (global scan nR={len(q)} nT={len(t)} nPxl={px_host.n} + "
-                      f"10 local phases 125x9), OpenMP {threads} threads, {dt:.1f} s"}
+            "cpu_model": model, "nproc": ncpu, "build": "gcc -O3 -march=native -fopenmp",
+            "sample": f"{n} images x (global scan nR={len(q)} nT={len(t)} nPxl={px.n} + "
+                      f"{phases} local phases {mR}x{mT}), oracle/cpu_fast.c, OpenMP {threads} "
+                      f"threads, {dt:.1f} s"}
+
+
+PEAK_FP32_TFLOPS = PEAK_FP32_MFMA_TFLOPS
 
 
 def main():
@@ -206,23 +240,32 @@ def main():
     lib()   # fail loudly if the HIP library is missing
 
     N, pf, rU, rL = a.box, 2, 24, 1
+    mR, mT = 125, 9
     log(rank, f"[bench] building synthetic volume N={N} pf={pf}")
     vol = synth.projectee(synth.blob_volume(N, seed=1, device=dev), pf)
     gset = synth.global_sample_set(a.nr, seed=2)
     px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, rL, a.images, dev, seed=5 + 101 * rank,
                                                  vol=vol)
-    e = ex.Expectation(vol, px, gset, n_phase=a.phases, algo=a.algo, seed=7 + rank,
-                       shuffle=bool(a.shuffle), perturb_mean=a.perturb_mean, acg_iters=a.acg_iters,
-                       large_first=bool(a.large_first))
+    mk = lambda algo: ex.Expectation(vol, px, gset, n_phase=a.phases, algo=algo, seed=7 + rank,
+                                     shuffle=bool(a.shuffle), perturb_mean=a.perturb_mean,
+                                     acg_iters=a.acg_iters, large_first=bool(a.large_first))
+    e = mk(a.algo)
     chunk = a.chunk or a.images
     chunks = [(l0, min(a.images, l0 + chunk)) for l0 in range(0, a.images, chunk)]
     outs = [None] * len(chunks)
+    # HIP events around every k_local_fused launch of the timed steps (one launch
+    # per phase when the batch runs as one expectation call)
+    timer = ex.PhaseTimer(e, a.phases * max(1, a.steps)) if len(chunks) == 1 and a.phases else None
 
-    def step():
+    def step(i=None):
+        if timer is not None and i is not None:
+            timer.select(i * a.phases)
         for c, (l0, l1) in enumerate(chunks):
             outs[c] = e.run(dat[l0:l1], ctf[l0:l1], sig[l0:l1], out=outs[c])
 
     log(rank, f"[bench] nPxl={px.n} nR={a.nr} nT={len(gset[1])} images/gpu={a.images}")
+    if timer is not None:
+        e.cfg.phaseEvents = None
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -230,8 +273,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    for i in range(a.steps):
+        step(i)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -243,6 +286,9 @@ def main():
         el = float(tt.item())
     ms_per_step = el / a.steps * 1e3
     value = a.gpus * a.images * a.steps / el
+    local_ms = timer.ms() if timer is not None else []
+    if timer is not None:
+        timer.close()
 
     # accuracy sanity of the timed path: top rotation vs true pose
     res = {}
@@ -269,26 +315,65 @@ def main():
         t = traffic.get(key) if ok else None
         return (t["traffic_bytes"], f"{traffic_src}: {key}") if t else (None, None)
 
+    # ---- dominant kernel of the timed step: k_local_fused<false>
+    if local_ms:
+        nL = chunks[0][1] - chunks[0][0]
+        per_img = 56.0 * mR * px.n + 15.0 * mR * mT * px.n        # SURVEY §8(d), per image-phase
+        flop = nL * per_img
+        t_launch = float(np.mean(local_ms)) / 1e3
+        achieved = flop / t_launch / 1e12
+        tr, tr_src = launch_traffic("local_bench", N == 256 and a.nr == 2000 and nL == 12500)
+        extras["roofline"] = {
+            "bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / PEAK_FP32_TFLOPS, "traffic": tr,
+            "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
+            "kernel": f"k_local_fused<false> (particle-filter phase, nPxl={px.n}, {mR}x{mT}, "
+                      f"{nL} images per launch)",
+            "launch_ms": t_launch * 1e3, "launches_timed": len(local_ms),
+            "share_of_step": float(np.sum(local_ms)) / (a.steps * ms_per_step),
+            "algorithmic_flop_per_launch": flop,
+            "tap_bytes_per_launch": 64.0 * mR * px.n * nL,
+            "tap_rate_TBps": 64.0 * mR * px.n * nL / t_launch / 1e12,
+            "note": "HIP events recorded by the driver on its launch stream around every "
+                    "k_local_fused launch of the timed steps; FP32 peak (the f32 MFMA rate equals "
+                    "the vector rate); algorithmic FLOP = 56 mLR nPxl (FP64 rotate, weights, 8-tap "
+                    "complex FMA) + 15 mLR mLT nPxl (direct likelihood) per image-phase, SURVEY 8(d); "
+                    "the 8 taps per rotation-pixel (64 B) come from LDS patch boxes, not HBM"}
+
     if not a.no_extras:
-        # dominant kernel: the global scan
+        # ---- secondary: the global scan (bf16x3 MFMA) and its FP32-MFMA twin
         nRoof = min(ROOF_IMAGES, a.images)
-        sec, issued, algorithmic, peak = scan_roofline(vol, px, gset, dat[:nRoof],
-                                                       ctf[:nRoof], sig[:nRoof], a.algo)
+        sec, issued, algorithmic, peak = scan_roofline(vol, px, gset, dat[:nRoof], ctf[:nRoof],
+                                                       sig[:nRoof], a.algo)
         kname = {1: "k_scan_mfma (fp32 32x32x2)", 2: "k_scan_split<BF16X3> (bf16 32x32x16, 3-product split)"}
         tr, tr_src = launch_traffic("scan_4096", a.algo == 2 and nRoof == 4096
                                     and a.nr == 2000 and N == 256)
-        extras["roofline"] = {"bound": "mfma", "achieved": issued / sec / 1e12,
-                              "peak": peak, "unit": "TFLOP/s",
-                              "frac": issued / sec / 1e12 / peak, "traffic": tr,
-                              "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
-                              "kernel": f"global scan {kname.get(a.algo, a.algo)} + prep + combine",
-                              "launch_ms": sec * 1e3, "images_per_launch": nRoof,
-                              "algorithmic_equiv_tflops": algorithmic / sec / 1e12,
-                              "note": "achieved = issued matrix-core flops after the expansion of "
-                                      "|d-cTP|^2 into a GEMM (4 fp32 flop, or 3x4 bf16 flop, per "
-                                      "image x rotation x translation x pixel); "
-                                      "algorithmic_equiv uses the direct 15-flop count of SURVEY "
-                                      "8(d) and can exceed the FP32 VALU peak"}
+        extras["roofline_scan"] = {
+            "bound": "mfma", "achieved": issued / sec / 1e12, "peak": peak, "unit": "TFLOP/s",
+            "frac": issued / sec / 1e12 / peak, "traffic": tr,
+            "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
+            "kernel": f"global scan {kname.get(a.algo, a.algo)} + prep + combine",
+            "launch_ms": sec * 1e3, "images_per_launch": nRoof,
+            "algorithmic_equiv_tflops": algorithmic / sec / 1e12,
+            "note": "achieved = issued matrix-core flops after the expansion of |d-cTP|^2 into a "
+                    "GEMM (4 fp32 flop, or 3x4 bf16 flop, per image x rotation x translation x "
+                    "pixel); algorithmic_equiv uses the direct 15-flop count of SURVEY 8(d)"}
+        sec1, issued1, _, _ = scan_roofline(vol, px, gset, dat[:nRoof], ctf[:nRoof], sig[:nRoof], 1)
+        extras["roofline_scan"]["fp32_mfma_launch_ms"] = sec1 * 1e3
+        extras["roofline_scan"]["fp32_mfma_frac"] = issued1 / sec1 / 1e12 / PEAK_FP32_MFMA_TFLOPS
+        if a.algo != 1:
+            # whole-step throughput with the FP32-MFMA scan (algo 1) beside the headline
+            e1 = mk(1)
+            o1 = e1.run(dat, ctf, sig)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(2):
+                e1.run(dat, ctf, sig, out=o1)
+            torch.cuda.synchronize()
+            extras["images_per_s_fp32_scan"] = a.gpus * a.images * 2 / (time.perf_counter() - t1)
+            del e1, o1
+
+        # ---- secondary: the north-star full-resolution phase against HBM
         lsec, lbytes, lnpx, lsec_plain = local_roofline(vol, N, pf, dev)
         tr, tr_src = launch_traffic("local_fullres_512", N == 256)
         extras["roofline_local"] = {"bound": "hbm", "achieved": lbytes / lsec / 1e9,
@@ -301,49 +386,76 @@ def main():
                                               "images, cell-expanded projectee)",
                                     "launch_ms": lsec * 1e3,
                                     "launch_ms_halfcomplex_layout": lsec_plain * 1e3}
-        # insert (mReco = 100) + half-map all-reduce over the hemisphere
-        rec = ex.Reconstructor(N, pf, dev)
+
+        # ---- insert (mReco = 100) into the two hemispheres' half-maps, the
+        # per-hemisphere RCCL all-reduce, FSC between the half-maps
         quat, trans = outs[0][0], outs[0][1]
         iq, it = ex.draw_insert_samples(quat, trans, 100)
         nI = iq.shape[0]
         offS = torch.zeros(nI, 2, dtype=torch.float64, device=dev)
         w = torch.full((nI,), 1.0 / 100, dtype=torch.float32, device=dev)
         st = torch.cuda.current_stream(dev)
-        isec = timed_events(lambda: rec.insert(dat[:nI], ctf[:nI], iq, it, offS, w, px), 2, st)
+        if world == 1:
+            # one GPU holds both hemispheres: odd / even images
+            recs = [ex.Reconstructor(N, pf, dev) for _ in range(2)]
+            halves = [torch.arange(h, nI, 2, device=dev) for h in (0, 1)]
+            parts = [(dat[hh].contiguous(), ctf[hh].contiguous(), iq[hh].contiguous(),
+                      it[hh].contiguous(), offS[hh].contiguous(), w[hh].contiguous()) for hh in halves]
+
+            def ins():
+                for r_, p_ in zip(recs, parts):
+                    r_.insert(*p_, px)
+        else:
+            recs = [ex.Reconstructor(N, pf, dev)]
+
+            def ins():
+                recs[0].insert(dat[:nI], ctf[:nI], iq, it, offS, w, px)
+        isec = timed_events(ins, 2, st)
         extras["insert_images_per_s"] = a.gpus * nI / isec
+        hm_bytes = recs[0].hm.F.numel() * 8 + recs[0].hm.T.numel() * 4
         if dist:
-            groups = [dist.new_group([r for r in range(world) if r % 2 == h]) for h in (0, 1)]
-            g = groups[rank % 2]
+            groups = ex.hemisphere_groups(world)
+            comm = ops.RcclComm.from_group(groups[rank % 2], dev)
             torch.cuda.synchronize()
             dist.barrier()
             t1 = time.perf_counter()
-            ex.halfmap_allreduce(rec.hm, group=g)
+            comm.allreduce(recs[0].hm)
             torch.cuda.synchronize()
             extras["allreduce_ms"] = (time.perf_counter() - t1) * 1e3
-            extras["allreduce_bytes"] = (rec.hm.F.numel() * 8 + rec.hm.T.numel() * 4)
+            extras["allreduce_bytes"] = hm_bytes
+            extras["allreduce_ranks_per_hemisphere"] = comm.nranks
+            comm.close()
         else:
             extras["allreduce_ms"] = 0.0
+            extras["allreduce_note"] = "1 GPU: both hemispheres on one device, no all-reduce"
+            fsc = ops.fsc(recs[0].hm.F, recs[1].hm.F, N)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            fsc = ops.fsc(recs[0].hm.F, recs[1].hm.F, N)
+            torch.cuda.synchronize()
+            extras["fsc_ms"] = (time.perf_counter() - t1) * 1e3
+            extras["halfmap_F_fsc_shells_2_8_16"] = [round(float(fsc[k]), 4) for k in (2, 8, 16)]
 
     if rank == 0 and not a.no_cpu_baseline:
         vol_np = vol.cpu().numpy()
-        n_cpu = 256
-        from oracle import oracle as orc
-        pxh = orc.pixel_set(N, pf, rU, rL)
+        n_cpu = 512
         extras["cpu_baseline"] = cpu_baseline(vol_np, N, pf, gset, dat[:n_cpu].cpu().numpy(),
                                               ctf[:n_cpu].cpu().numpy(), sig[:n_cpu].cpu().numpy(),
-                                              pxh, a.cpu_seconds)
+                                              px, a.cpu_seconds, a.phases)
 
     if rank == 0:
         line = {"metric": "particle-images/sec through expectation (box 256, 2000 rot samples)",
                 "value": value, "unit": "particle-images/s", "n_gpus": a.gpus, "steps": a.steps,
                 "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "scaling": "weak", "vs_baseline": None,
+                "dtype": "f32" if a.algo == 1 else "f32 (global scan: bf16x3 split, fp32 accumulate)",
                 "data": "synthetic (seeded Gaussian-blob volume, CTF-modulated noisy projections, SNR 0.05)",
                 "config": {"workload": f"C3: 3D refine box {N}, {a.nr} rotation x {len(gset[1])} "
                                        f"translation global scan at rU={rU} (nPxl={px.n}) + "
-                                       f"{a.phases} particle-filter phases (125 x 9)",
+                                       f"{a.phases} particle-filter phases ({mR} x {mT})",
                            "images_per_gpu": a.images, "global_batch": a.images * a.gpus,
                            "box": N, "pf": pf, "nR": a.nr, "nT": len(gset[1]), "nPxl": px.n,
+                           "scan_algo": a.algo, "perturb_mean": a.perturb_mean,
                            "parallelism": f"dp{a.gpus} (hemisphere = rank % 2)"},
                 **res, **extras}
         print(json.dumps(line), flush=True)

@@ -265,11 +265,16 @@ int thx_pf_peak(int nImg, int n, float* u, int ldu, double* peak, int setFactor,
  * O += -R_m (t - off, 0) and counter += 1 (insertDir, src/Reconstructor.cpp:
  * 407-422).  F: dimSize Complex, T: dimSize float, O: 3 double, counter: 1
  * int (all accumulated, not cleared).  quat: nImg x mReco x 4,
- * trans: nImg x mReco x 2, offS: nImg x 2, w: nImg. */
+ * trans: nImg x mReco x 2, offS: nImg x 2, w: nImg.  nC (device, nImg, may
+ * be NULL): image l inserts only its first nC[l] samples -- the K-class call
+ * of InsertFT (gpu/interface/Interface.h:267-292, cuthunder.cu:4115), where
+ * each class's reconstructor receives mReco = the largest per-image count of
+ * samples that drew it and nC[l] = image l's count (src/Optimiser.cpp:
+ * 6852-6950); O and counter see only the inserted samples. */
 int thx_insert3d(float* F, float* T, double* O, int* counter, int vdim,
                  int pf, const float* dat, const float* ctf,
                  const double* quat, const double* trans, const double* offS,
-                 const float* w, int nImg, int mReco, const int* iCol,
+                 const float* w, const int* nC, int nImg, int mReco, const int* iCol,
                  const int* iRow, int nPxl, int idim, thx_stream_t stream);
 
 /* Same insert, pixels visited in thx_pixel_tile_order patches (pxOrder:
@@ -283,10 +288,29 @@ size_t thx_insert3d_workspace(int nImg, int mReco, int nOrd);
 int thx_insert3d_tiled(float* F, float* T, double* O, int* counter, int vdim,
                        int pf, const float* dat, const float* ctf,
                        const double* quat, const double* trans,
-                       const double* offS, const float* w, int nImg, int mReco,
+                       const double* offS, const float* w, const int* nC, int nImg, int mReco,
                        const int* iCol, const int* iRow, const int* pxOrder,
                        int nOrd, int nPxl, int idim, void* workspace,
                        size_t wsBytes, thx_stream_t stream);
+
+/* ----------------------------------------------------------------- a13 ---
+ * The per-hemisphere half-map reduction of cuthunder::InsertFT
+ * (gpu/src/cuthunder.cu:5294-5324 communicator setup, :5903-5993 the
+ * all-reduces; CPU twin Reconstructor::allReduceF/T/O,
+ * src/Reconstructor.cpp:2350-2520) over RCCL.  One process per GPU: the
+ * communicator spans the ranks of one hemisphere.  The host moves the
+ * THX_RCCL_ID_BYTES unique id from the hemisphere's first rank to the others
+ * (MPI_Bcast over `hemi` in THUNDER, as the reference does).
+ * thx_halfmap_allreduce sums in place, as one RCCL group on `stream`:
+ * F (2 dimSize nK floats), T (dimSize nK floats), O (3 nK doubles, may be
+ * NULL) and counter (nK int32, may be NULL; the reference's ncclInt64 on an
+ * int, quirk q2, is not replicated). */
+#define THX_RCCL_ID_BYTES 128
+int thx_rccl_unique_id(void* id);
+int thx_rccl_comm_init(int nranks, const void* id, int rank, void** comm);
+int thx_rccl_comm_destroy(void* comm);
+int thx_halfmap_allreduce(void* comm, float* F, float* T, double* O, int* counter,
+                          long long dimSize, int nK, thx_stream_t stream);
 
 /* ----------------------------------------------------------------- a14 ---
  * Fourier shell correlation FSC(vec&, const Volume& A, const Volume& B)
@@ -359,6 +383,9 @@ typedef struct thx_expect_cfg {
     int largeFirst;           /* OPTIMISER_GLOBAL_PERTURB_LARGE (off in include/Config.h, so 0 is
                                  the reference): 1 perturbs the first global phase by
                                  perturbFactorL (src/Optimiser.cpp:1185-1186, 2424-2425) */
+    void* phaseEvents;        /* optional hipEvent_t[2 * phases]: events recorded on `stream`
+                                 around every phase's k_local_fused launch (begin, end), for
+                                 in-process kernel timing (bench.py); NULL: none */
 } thx_expect_cfg;
 
 /* nOrd: length of pxOrder (<= 0 when pxOrder is NULL). */
@@ -373,6 +400,12 @@ int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                     double* trans, double* pR, double* pT, float* score,
                     int* cls, int* nPhaseOut,
                     void* workspace, size_t wsBytes, thx_stream_t stream);
+
+/* HIP event pairs for thx_expect_cfg.phaseEvents: create n (begin, end)
+ * pairs, read back ms[i] per pair (-1: not recorded), destroy. */
+int thx_event_pairs_create(int n, void** events);
+int thx_event_pairs_elapsed(void* events, int n, float* ms);
+int thx_event_pairs_destroy(void* events, int n);
 
 /* ====================================================================== *
  * Reference-shaped host adapters (host pointers, stateless, synchronous).  *
@@ -412,6 +445,15 @@ int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
                  const float* w, const double* nR, const double* nT,
                  const int* iCol, const int* iRow, int opf, int npxl,
                  int mReco, int idim, int vdim, int imgNum);
+
+/* gpu/interface/Interface.h:267-292 InsertFT with nC (the K-class call, one
+ * per class reconstructor): as thx_InsertFT, image l inserting only its first
+ * nC[l] (host, imgNum ints) of the mReco samples. */
+int thx_InsertFTC(float* F3D, float* T3D, double* O3D, int* counter,
+                  const float* datP, const float* ctfP, const double* offS,
+                  const float* w, const double* nR, const double* nT, const int* nC,
+                  const int* iCol, const int* iRow, int opf, int npxl,
+                  int mReco, int idim, int vdim, int imgNum);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,124 @@
+"""K-class insert (InsertFT with nC, gpu/interface/Interface.h:267-292: each
+class's reconstructor inserts image l's first nC[l] samples,
+src/Optimiser.cpp:6852-6950) against the restatement, and the RCCL half-map
+reduction behind the C-ABI (thx_halfmap_allreduce, the ncclAllReduce of
+gpu/src/cuthunder.cu:5903-5993)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from stacks import small_stack
+from thunder_amd import ops, synth
+from thunder_amd._lib import lib
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def T(a):
+    return torch.as_tensor(np.ascontiguousarray(a), device=DEV)
+
+
+@pytest.fixture(scope="module")
+def stack(orc):
+    return small_stack(orc, N=32, nImg=6, nR=4, nT=3, seed=8)
+
+
+def _samples(nImg, mReco, seed):
+    rng = np.random.default_rng(seed)
+    quat = synth.clustered_quaternions(nImg, mReco, 3.0, rng)
+    trans = rng.standard_normal((nImg, mReco, 2)) * 2
+    off = rng.standard_normal((nImg, 2))
+    w = np.full(nImg, 1.0 / mReco, np.float32)
+    return quat, trans, off, w
+
+
+def _oracle_truncated(orc, s, quat, trans, off, w, nC):
+    """Sum over images of the restatement's insert of image l's first nC[l] samples."""
+    size = (s["vdim"] // 2 + 1) * s["vdim"] ** 2
+    F = np.zeros(2 * size, np.float32)
+    Tm = np.zeros(size, np.float32)
+    O = np.zeros(3)
+    cnt = 0
+    for l, n in enumerate(nC):
+        if n == 0:
+            continue
+        f, t, o, c = orc.insert_batch(s["vdim"], s["pf"], s["dat"][l:l + 1], s["ctf"][l:l + 1],
+                                      quat[l:l + 1, :n], trans[l:l + 1, :n], off[l:l + 1], w[l:l + 1],
+                                      s["px"], s["N"])
+        F += f.view(np.float32)
+        Tm += t
+        O += o
+        cnt += c
+    return F.view(np.complex64), Tm, O, cnt
+
+
+@pytest.mark.parametrize("tiled", [False, True])
+def test_insert_with_per_image_counts(orc, stack, tiled):
+    s = stack
+    nImg, mReco = 6, 140                   # two 128-sample tiles per image
+    nC = np.array([0, 5, 140, 129, 1, 77], np.int32)
+    quat, trans, off, w = _samples(nImg, mReco, 31)
+    px = ops.PixelSet(s["N"], s["pf"], s["rU"], s["rL"], device=DEV)
+    hm = ops.HalfMap(s["vdim"], DEV)
+    ops.insert3d(hm, T(s["dat"]), T(s["ctf"]), T(quat), T(trans), T(off), T(w), px, tiled=tiled,
+                 nC=T(nC))
+    F, Tm, O, cnt = _oracle_truncated(orc, s, quat, trans, off, w, nC)
+    gF = hm.F.cpu().numpy().reshape(-1)
+    gT = hm.T.cpu().numpy().reshape(-1)
+    assert np.max(np.abs(gF - F)) <= 1e-5 * np.max(np.abs(F))
+    assert np.max(np.abs(gT - Tm)) <= 1e-5 * np.max(np.abs(Tm))
+    assert np.allclose(hm.O.cpu().numpy(), O, rtol=1e-12, atol=1e-12)
+    assert int(hm.counter.item()) == cnt == int(nC.sum())
+
+
+def test_host_insert_ftc_matches_oracle(orc, stack):
+    """thx_InsertFTC: the Interface.h K-class InsertFT shape (host pointers,
+    padded pixel set, read-modify-write of the caller's F/T/O/counter)."""
+    s = stack
+    nImg, mReco = 6, 12
+    nC = np.array([3, 0, 12, 7, 1, 12], np.int32)
+    quat, trans, off, w = _samples(nImg, mReco, 32)
+    size = (s["vdim"] // 2 + 1) * s["vdim"] ** 2
+    F = np.zeros(2 * size, np.float32)
+    Tm = np.zeros(size, np.float32)
+    O = np.zeros(3)
+    cnt = np.zeros(1, np.int32)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    dat = np.ascontiguousarray(s["dat"]).view(np.float32)
+    ctf = np.ascontiguousarray(s["ctf"])
+    iq, it = np.ascontiguousarray(quat), np.ascontiguousarray(trans)
+    iColP = (s["px"].iCol * s["pf"]).astype(np.int32)
+    iRowP = (s["px"].iRow * s["pf"]).astype(np.int32)
+    st = lib().thx_InsertFTC(P(F), P(Tm), P(O), P(cnt), P(dat), P(ctf), P(off), P(w), P(iq), P(it),
+                             P(nC), P(iColP), P(iRowP), s["pf"], s["px"].n, mReco, s["N"], s["vdim"],
+                             nImg)
+    assert st == 0, lib().thx_last_error()
+    rF, rT, rO, rc = _oracle_truncated(orc, s, quat, trans, off, w, nC)
+    assert np.max(np.abs(F - rF.view(np.float32))) <= 1e-5 * np.max(np.abs(rF.view(np.float32)))
+    assert np.max(np.abs(Tm - rT)) <= 1e-5 * np.max(np.abs(rT))
+    assert np.allclose(O, rO, rtol=1e-12, atol=1e-12) and int(cnt[0]) == rc
+
+
+def test_rccl_halfmap_allreduce_single_rank():
+    """A one-rank hemisphere communicator: the in-place sum leaves F / T / O /
+    counter bit-identical (the multi-rank case is RCCL's own; bench.py runs it
+    across the hemisphere's GPUs at N > 1)."""
+    uid = ops.RcclComm.unique_id()
+    assert len(uid) == 128
+    comm = ops.RcclComm(1, uid, 0)
+    hm = ops.HalfMap(64, DEV)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    hm.F.copy_(torch.complex(torch.randn(hm.F.shape, generator=g, device=DEV),
+                             torch.randn(hm.F.shape, generator=g, device=DEV)))
+    hm.T.copy_(torch.rand(hm.T.shape, generator=g, device=DEV))
+    hm.O.copy_(torch.tensor([1.5, -2.0, 3.25], dtype=torch.float64))
+    hm.counter.fill_(17)
+    ref = [x.clone() for x in (hm.F, hm.T, hm.O, hm.counter)]
+    comm.allreduce(hm)
+    torch.cuda.synchronize()
+    for a, b in zip((hm.F, hm.T, hm.O, hm.counter), ref):
+        assert torch.equal(a, b)
+    comm.close()

@@ -38,11 +38,15 @@ SIGNATURES = {
     "thx_pf_calvari": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _c_double, _c_double, _p, _p, _p]),
     "thx_pf_balance_rot": (_c_int, [_c_int, _c_int, _p, _p, _p]),
     "thx_pf_peak": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _c_int, _p]),
-    "thx_insert3d": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_int,
+    "thx_insert3d": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _p, _c_int,
                               _c_int, _p, _p, _c_int, _c_int, _p]),
     "thx_insert3d_workspace": (_c_size, [_c_int, _c_int, _c_int]),
-    "thx_insert3d_tiled": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_int,
+    "thx_insert3d_tiled": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _p, _c_int,
                                     _c_int, _p, _p, _p, _c_int, _c_int, _c_int, _p, _c_size, _p]),
+    "thx_rccl_unique_id": (_c_int, [_p]),
+    "thx_rccl_comm_init": (_c_int, [_c_int, _p, _c_int, _p]),
+    "thx_rccl_comm_destroy": (_c_int, [_p]),
+    "thx_halfmap_allreduce": (_c_int, [_p, _p, _p, _p, _p, ctypes.c_longlong, _c_int, _p]),
     "thx_fsc_workspace": (_c_size, [_c_int]),
     "thx_fsc": (_c_int, [_p, _p, _c_int, _c_int, _p, _p, _c_size, _p]),
     "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int, _c_int]),
@@ -51,12 +55,17 @@ SIGNATURES = {
     "thx_local_phase_sel": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
                                      _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p,
                                      _p, _p, _p, _c_size, _p]),
+    "thx_event_pairs_create": (_c_int, [_c_int, _p]),
+    "thx_event_pairs_elapsed": (_c_int, [_p, _c_int, _p]),
+    "thx_event_pairs_destroy": (_c_int, [_p, _c_int]),
     "thx_ExpectRotran": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
     "thx_ExpectProject": (_c_int, [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int]),
     "thx_ExpectGlobal3D": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
                                     _c_int, _c_int, _c_int, _c_int]),
     "thx_InsertFT": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
                               _c_int, _c_int, _c_int, _c_int]),
+    "thx_InsertFTC": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
+                               _c_int, _c_int, _c_int, _c_int]),
 }
 
 _lib = None

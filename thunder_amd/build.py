@@ -57,7 +57,8 @@ def build(verbose=False, jobs=8):
         list(ex.map(_compile, todo))
     if todo or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
         tmp = LIB + ".tmp"
-        r = subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp],
+        r = subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs,
+                            "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrccl", "-o", tmp],
                            capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")

@@ -1,0 +1,75 @@
+// halfmap.hip -- a13: the per-hemisphere half-map reduction over RCCL.
+//
+// The reference sums every GPU's partial F3D / T3D / O3D / counter of one
+// gold-standard hemisphere inside cuthunder::InsertFT: ncclGetUniqueId on the
+// hemisphere's first rank, MPI_Bcast of the id over `hemi`, ncclCommInitRank
+// over (ranks x local GPUs) (gpu/src/cuthunder.cu:5294-5324), then in-place
+// ncclAllReduce of F (2 dimSize floats), T (dimSize floats), O (3 doubles)
+// and counter (gpu/src/cuthunder.cu:5903-5993).  Here the same exchange is a
+// C-ABI call on a caller-owned communicator -- one process per GPU, so the
+// communicator spans the hemisphere's ranks; the id travels over whatever the
+// host uses (MPI_Bcast in a C++/MPI THUNDER host, torch.distributed in
+// bench.py).  The counter is reduced as int32 (the reference passes a 4-byte
+// int as ncclInt64, quirk q2).  RCCL runs over xGMI between the GPUs of one
+// node; the four collectives are one ncclGroup so RCCL can schedule them
+// together.
+#include <rccl/rccl.h>
+
+#include <cstring>
+
+#include "common.h"
+
+#define THX_NCCL(call)                                                         \
+    do {                                                                       \
+        ncclResult_t r_ = (call);                                              \
+        if (r_ != ncclSuccess) {                                               \
+            ::thx::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call,        \
+                             ncclGetErrorString(r_));                          \
+            return THX_ERR_HIP;                                                \
+        }                                                                      \
+    } while (0)
+
+static_assert(NCCL_UNIQUE_ID_BYTES == THX_RCCL_ID_BYTES, "unique-id size");
+
+extern "C" int thx_rccl_unique_id(void* id)
+{
+    THX_CHECK_ARG(id, "thx_rccl_unique_id: null");
+    ncclUniqueId u;
+    THX_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof(u));
+    return THX_OK;
+}
+
+extern "C" int thx_rccl_comm_init(int nranks, const void* id, int rank, void** comm)
+{
+    THX_CHECK_ARG(id && comm && nranks > 0 && rank >= 0 && rank < nranks,
+                  "thx_rccl_comm_init: bad arguments");
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    ncclComm_t c = nullptr;
+    THX_NCCL(ncclCommInitRank(&c, nranks, u, rank));
+    *comm = c;
+    return THX_OK;
+}
+
+extern "C" int thx_rccl_comm_destroy(void* comm)
+{
+    if (comm) THX_NCCL(ncclCommDestroy(static_cast<ncclComm_t>(comm)));
+    return THX_OK;
+}
+
+extern "C" int thx_halfmap_allreduce(void* comm, float* F, float* T, double* O, int* counter,
+                                     long long dimSize, int nK, thx_stream_t stream)
+{
+    THX_CHECK_ARG(comm && F && T && dimSize > 0 && nK >= 1, "thx_halfmap_allreduce: bad arguments");
+    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    hipStream_t s = thx::as_stream(stream);
+    const size_t n = (size_t)dimSize * nK;
+    THX_NCCL(ncclGroupStart());
+    THX_NCCL(ncclAllReduce(F, F, 2 * n, ncclFloat32, ncclSum, c, s));
+    THX_NCCL(ncclAllReduce(T, T, n, ncclFloat32, ncclSum, c, s));
+    if (O) THX_NCCL(ncclAllReduce(O, O, 3 * (size_t)nK, ncclFloat64, ncclSum, c, s));
+    if (counter) THX_NCCL(ncclAllReduce(counter, counter, nK, ncclInt32, ncclSum, c, s));
+    THX_NCCL(ncclGroupEnd());
+    return THX_OK;
+}

@@ -53,12 +53,14 @@ __global__ void __launch_bounds__(256) k_insert3d(float2* __restrict__ F,
                                                   const double* __restrict__ trans,
                                                   const double* __restrict__ offS,
                                                   const float* __restrict__ w,
+                                                  const int* __restrict__ nC,
                                                   int mReco,
                                                   const int* __restrict__ iCol,
                                                   const int* __restrict__ iRow,
                                                   int nPxl, int idim)
 {
     const int m = blockIdx.y, l = blockIdx.z;
+    if (nC && m >= nC[l]) return;      // K-class call: image l drew this class nC[l] times
     const size_t sIdx = (size_t)l * mReco + m;
     __shared__ double sMat[9];
     if (threadIdx.x == 0) {
@@ -98,7 +100,7 @@ __global__ void __launch_bounds__(256) k_insert3d(float2* __restrict__ F,
 extern "C" int thx_insert3d(float* F, float* T, double* O, int* counter,
                             int vdim, int pf, const float* dat, const float* ctf,
                             const double* quat, const double* trans,
-                            const double* offS, const float* w, int nImg,
+                            const double* offS, const float* w, const int* nC, int nImg,
                             int mReco, const int* iCol, const int* iRow,
                             int nPxl, int idim, thx_stream_t stream)
 {
@@ -111,7 +113,7 @@ extern "C" int thx_insert3d(float* F, float* T, double* O, int* counter,
     hipLaunchKernelGGL(k_insert3d, dim3(gx, mReco, nImg), dim3(256), 0,
                        thx::as_stream(stream), reinterpret_cast<float2*>(F), T, O,
                        counter, vdim, pf, reinterpret_cast<const float2*>(dat),
-                       ctf, quat, trans, offS, w, mReco, iCol, iRow, nPxl, idim);
+                       ctf, quat, trans, offS, w, nC, mReco, iCol, iRow, nPxl, idim);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
@@ -149,6 +151,7 @@ __global__ void __launch_bounds__(INS_THREADS) k_insert_patches(float2* __restri
                                                                 const double* __restrict__ trans,
                                                                 const double* __restrict__ offS,
                                                                 const float* __restrict__ w,
+                                                                const int* __restrict__ nCnt,
                                                                 int mReco,
                                                                 const int* __restrict__ iCol,
                                                                 const int* __restrict__ iRow,
@@ -166,7 +169,10 @@ __global__ void __launch_bounds__(INS_THREADS) k_insert_patches(float2* __restri
     const int c = blockIdx.x, ry = blockIdx.y, l = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nC = (nVisit + KC - 1) / KC, nRT = (mReco + RT - 1) / RT;
-    const int m0 = ry * RT, nM = min(RT, mReco - m0);
+    const int m0 = ry * RT;
+    // samples of this tile (the K-class call inserts only the first nC[l])
+    const int nM = max(0, min(RT, (nCnt ? min(nCnt[l], mReco) : mReco) - m0));
+    if (nM == 0) return;
     const int* R = rec + (((size_t)l * nRT + ry) * nC + c) * REC;
     int rv[REC];
 #pragma unroll
@@ -319,7 +325,7 @@ extern "C" size_t thx_insert3d_workspace(int nImg, int mReco, int nOrd)
 extern "C" int thx_insert3d_tiled(float* F, float* T, double* O, int* counter, int vdim, int pf,
                                   const float* dat, const float* ctf, const double* quat,
                                   const double* trans, const double* offS, const float* w,
-                                  int nImg, int mReco, const int* iCol, const int* iRow,
+                                  const int* nC, int nImg, int mReco, const int* iCol, const int* iRow,
                                   const int* pxOrder, int nOrd, int nPxl, int idim,
                                   void* workspace, size_t wsBytes, thx_stream_t stream)
 {
@@ -339,8 +345,8 @@ extern "C" int thx_insert3d_tiled(float* F, float* T, double* O, int* counter, i
     if (st != THX_OK) return st;
     hipLaunchKernelGGL(k_insert_patches, dim3(nOrd / KC, thx::cdiv(mReco, RT), nImg),
                        dim3(INS_THREADS), 0, s, reinterpret_cast<float2*>(F), T, O, counter, vdim,
-                       pf, reinterpret_cast<const float2*>(dat), ctf, quat, trans, offS, w, mReco,
-                       iCol, iRow, pxOrder, nOrd, nPxl, idim, rec);
+                       pf, reinterpret_cast<const float2*>(dat), ctf, quat, trans, offS, w, nC,
+                       mReco, iCol, iRow, pxOrder, nOrd, nPxl, idim, rec);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }

@@ -147,19 +147,18 @@ extern "C" int thx_ExpectGlobal3D(const float* rotP, const float* traP,
     return THX_OK;
 }
 
-extern "C" int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
-                            const float* datP, const float* ctfP,
-                            const double* offS, const float* w, const double* nR,
-                            const double* nT, const int* iCol, const int* iRow,
-                            int opf, int npxl, int mReco, int idim, int vdim,
-                            int imgNum)
+static int insert_ft(float* F3D, float* T3D, double* O3D, int* counter, const float* datP,
+                     const float* ctfP, const double* offS, const float* w, const double* nR,
+                     const double* nT, const int* nC, const int* iCol, const int* iRow, int opf,
+                     int npxl, int mReco, int idim, int vdim, int imgNum)
 {
     THX_CHECK_ARG(F3D && T3D && O3D && counter && datP && ctfP && offS && w && nR &&
                       nT && iCol && iRow,
                   "thx_InsertFT: null");
+    THX_CHECK_ARG(imgNum >= 0 && mReco >= 0 && npxl >= 0 && opf > 0, "thx_InsertFT: bad sizes");
     const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
     const size_t nPx = (size_t)imgNum * npxl, nS = (size_t)imgNum * mReco;
-    DBuf dF, dT, dO, dC, dDat, dCtf, dOff, dW, dQ, dTr, dIc, dIr;
+    DBuf dF, dT, dO, dC, dDat, dCtf, dOff, dW, dQ, dTr, dIc, dIr, dN;
     THX_DALLOC(dF, sizeof(float) * 2 * dimSize);
     THX_DALLOC(dT, sizeof(float) * dimSize);
     THX_DALLOC(dO, sizeof(double) * 3);
@@ -172,6 +171,7 @@ extern "C" int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
     THX_DALLOC(dTr, sizeof(double) * 2 * nS);
     THX_DALLOC(dIc, sizeof(int) * npxl);
     THX_DALLOC(dIr, sizeof(int) * npxl);
+    THX_DALLOC(dN, sizeof(int) * imgNum);
     // the reference seeds GPU0 with the host F/T and accumulates on top
     // (gpu/src/cuthunder.cu:5422-5555)
     THX_HIP(hipMemcpy(dF.p, F3D, sizeof(float) * 2 * dimSize, hipMemcpyHostToDevice));
@@ -184,6 +184,7 @@ extern "C" int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
     THX_HIP(hipMemcpy(dW.p, w, sizeof(float) * imgNum, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dQ.p, nR, sizeof(double) * 4 * nS, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dTr.p, nT, sizeof(double) * 2 * nS, hipMemcpyHostToDevice));
+    if (nC) THX_HIP(hipMemcpy(dN.p, nC, sizeof(int) * imgNum, hipMemcpyHostToDevice));
     {
         // Reconstructor::insertI passes the padded pixel set (_iCol = iCol * pf,
         // src/Reconstructor.cpp:928-985); the kernels take the unpadded one + pf,
@@ -205,12 +206,35 @@ extern "C" int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
                              dCtf.as<float>() + (size_t)l0 * npxl,
                              dQ.as<double>() + 4 * (size_t)l0 * mReco,
                              dTr.as<double>() + 2 * (size_t)l0 * mReco,
-                             dOff.as<double>() + 2 * (size_t)l0, dW.as<float>() + l0, nb,
-                             mReco, dIc.as<int>(), dIr.as<int>(), npxl, idim, nullptr));
+                             dOff.as<double>() + 2 * (size_t)l0, dW.as<float>() + l0,
+                             nC ? dN.as<int>() + l0 : nullptr, nb, mReco, dIc.as<int>(),
+                             dIr.as<int>(), npxl, idim, nullptr));
     }
     THX_HIP(hipMemcpy(F3D, dF.p, sizeof(float) * 2 * dimSize, hipMemcpyDeviceToHost));
     THX_HIP(hipMemcpy(T3D, dT.p, sizeof(float) * dimSize, hipMemcpyDeviceToHost));
     THX_HIP(hipMemcpy(O3D, dO.p, sizeof(double) * 3, hipMemcpyDeviceToHost));
     THX_HIP(hipMemcpy(counter, dC.p, sizeof(int), hipMemcpyDeviceToHost));
     return THX_OK;
+}
+
+extern "C" int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
+                            const float* datP, const float* ctfP,
+                            const double* offS, const float* w, const double* nR,
+                            const double* nT, const int* iCol, const int* iRow,
+                            int opf, int npxl, int mReco, int idim, int vdim,
+                            int imgNum)
+{
+    return insert_ft(F3D, T3D, O3D, counter, datP, ctfP, offS, w, nR, nT, nullptr, iCol, iRow,
+                     opf, npxl, mReco, idim, vdim, imgNum);
+}
+
+extern "C" int thx_InsertFTC(float* F3D, float* T3D, double* O3D, int* counter,
+                             const float* datP, const float* ctfP, const double* offS,
+                             const float* w, const double* nR, const double* nT, const int* nC,
+                             const int* iCol, const int* iRow, int opf, int npxl, int mReco,
+                             int idim, int vdim, int imgNum)
+{
+    THX_CHECK_ARG(nC, "thx_InsertFTC: null nC");
+    return insert_ft(F3D, T3D, O3D, counter, datP, ctfP, offS, w, nR, nT, nC, iCol, iRow, opf,
+                     npxl, mReco, idim, vdim, imgNum);
 }

@@ -784,7 +784,8 @@ extern "C" size_t thx_local_phase_workspace(int nImg, int nR, int nT, int nVisit
     return dvp_bytes(nImg, nR, nT) + rec_bytes(nImg, nR, nVisit) + 512;
 }
 
-static int local_phase_impl(const thx_local_sel* sel, const float* vol, int volLayout, int vdim,
+static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
+                            const float* vol, int volLayout, int vdim,
                             int pf, const double* quat, int nR, const double* trans, int nT,
                             const double* pC, const double* pR, const double* pT, const float* dat,
                             const float* ctf, const float* sigRcp, const int* iCol, const int* iRow,
@@ -818,6 +819,7 @@ static int local_phase_impl(const thx_local_sel* sel, const float* vol, int volL
     THX_LAUNCH_CHECK();
     dim3 grid(nImg, thx::cdiv(nR, RT), thx::cdiv(nT, TT));
     const long vs = cls ? (long)sel->volStride : 0L;
+    if (evBeg) THX_HIP(hipEventRecord(evBeg, s));
     if (volLayout == 1)
         hipLaunchKernelGGL(k_local_fused<true>, grid, dim3(THREADS), 0, s,
                            reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
@@ -829,6 +831,7 @@ static int local_phase_impl(const thx_local_sel* sel, const float* vol, int volL
                            reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
                            nVisit, nPxl, idim, rec, d, act, nAct, cls, vs);
     THX_LAUNCH_CHECK();
+    if (evEnd) THX_HIP(hipEventRecord(evEnd, s));
     hipLaunchKernelGGL(k_local_weights, dim3(nImg), dim3(256), 0, s, d, nR, nT, pC, pR, pT, wC,
                        wR, wT, baseL, act, nAct);
     THX_LAUNCH_CHECK();
@@ -846,7 +849,8 @@ extern "C" int thx_local_phase(const float* vol, int volLayout, int vdim, int pf
                                void* workspace, size_t wsBytes,
                                thx_stream_t stream)
 {
-    return local_phase_impl(nullptr, vol, volLayout, vdim, pf, quat, nR, trans, nT, pC, pR, pT,
+    return local_phase_impl(nullptr, nullptr, nullptr, vol, volLayout, vdim, pf, quat, nR, trans,
+                            nT, pC, pR, pT,
                             dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg, wC, wR,
                             wT, baseL, dvp, workspace, wsBytes, stream);
 }
@@ -861,7 +865,23 @@ extern "C" int thx_local_phase_sel(const thx_local_sel* sel, const float* vol, i
                                    float* baseL, float* dvp, void* workspace, size_t wsBytes,
                                    thx_stream_t stream)
 {
-    return local_phase_impl(sel, vol, volLayout, vdim, pf, quat, nR, trans, nT, pC, pR, pT, dat,
-                            ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg, wC, wR, wT,
-                            baseL, dvp, workspace, wsBytes, stream);
+    return local_phase_impl(sel, nullptr, nullptr, vol, volLayout, vdim, pf, quat, nR, trans, nT,
+                            pC, pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim,
+                            nImg, wC, wR, wT, baseL, dvp, workspace, wsBytes, stream);
 }
+
+namespace thx {
+// the driver's phase launch, with optional events around k_local_fused
+int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
+                      const float* vol, int vdim, int pf, const double* quat, int nR,
+                      const double* trans, int nT, const double* pC, const double* pR,
+                      const double* pT, const float* dat, const float* ctf, const float* sigRcp,
+                      const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
+                      int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
+                      void* workspace, size_t wsBytes, thx_stream_t stream)
+{
+    return local_phase_impl(sel, evBeg, evEnd, vol, 0, vdim, pf, quat, nR, trans, nT, pC, pR, pT,
+                            dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg, wC, wR,
+                            wT, baseL, nullptr, workspace, wsBytes, stream);
+}
+}  // namespace thx

@@ -25,6 +25,16 @@
 // reference draws from an urandom-seeded GSL mt19937.
 #include "common.h"
 
+namespace thx {
+int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
+                      const float* vol, int vdim, int pf, const double* quat, int nR,
+                      const double* trans, int nT, const double* pC, const double* pR,
+                      const double* pT, const float* dat, const float* ctf, const float* sigRcp,
+                      const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
+                      int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
+                      void* workspace, size_t wsBytes, thx_stream_t stream);
+}
+
 namespace {
 
 // ------------------------------------------------------------- Philox RNG
@@ -1055,10 +1065,13 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                            c.seed, (uint32_t)(2000 + phase), c.perturbMean, c.acgIters, done,
                            nullptr);
         THX_LAUNCH_CHECK();
-        THX_RET(thx_local_phase_sel(&sel, vol, 0, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC,
-                                    pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl,
-                                    c.idim, nImg, p.wC, p.wR, p.wT, p.base, nullptr, p.localWs,
-                                    p.localWsBytes, stream));
+        hipEvent_t* ev = static_cast<hipEvent_t*>(c.phaseEvents);
+        const int pi = phase - phase0;
+        THX_RET(thx::local_phase_timed(&sel, ev ? ev[2 * pi] : nullptr, ev ? ev[2 * pi + 1] : nullptr,
+                                       vol, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT,
+                                       dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, c.idim,
+                                       nImg, p.wC, p.wR, p.wT, p.base, p.localWs, p.localWsBytes,
+                                       stream));
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
                            p.peakR, 0, nullptr, 0, done);
         THX_LAUNCH_CHECK();

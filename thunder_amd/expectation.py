@@ -38,7 +38,8 @@ class ExpectCfg(ctypes.Structure):
                 ("nK", ctypes.c_int), ("searchType", ctypes.c_int), ("converge", ctypes.c_int),
                 ("minPhase", ctypes.c_int), ("maxPhase", ctypes.c_int),
                 ("perturbMean", ctypes.c_int), ("acgIters", ctypes.c_int),
-                ("perturbFactorL", ctypes.c_double), ("largeFirst", ctypes.c_int)]
+                ("perturbFactorL", ctypes.c_double), ("largeFirst", ctypes.c_int),
+                ("phaseEvents", ctypes.c_void_p)]
 
 
 class Expectation:
@@ -94,7 +95,7 @@ class Expectation:
                              k_floor, s_floor, trans_s, trans_m, seed, int(bool(shuffle)),
                              nK, self.search, int(bool(converge)), min_phase, max_phase,
                              {"top": 0, "acg": 1}[perturb_mean], acg_iters, perturb_large,
-                             int(bool(large_first)))
+                             int(bool(large_first)), None)
         self.mLR, self.mLT, self.nK = mLR, mLT, nK
 
     def workspace_bytes(self, nImg):
@@ -141,6 +142,33 @@ class Expectation:
                                     P(quat), P(trans), P(pR), P(pT), P(score), P(cls), P(nph),
                                     P(ws), ws.numel(), ops._stream(dev)), "thx_expectation")
         return out
+
+
+class PhaseTimer:
+    """HIP event pairs the driver records around every phase's k_local_fused
+    launch (thx_expect_cfg.phaseEvents): attach to an Expectation, run, read
+    the per-phase kernel milliseconds."""
+
+    def __init__(self, expectation, n_pairs):
+        self.n = n_pairs
+        self.ev = ctypes.c_void_p()
+        check(lib().thx_event_pairs_create(n_pairs, ctypes.byref(self.ev)), "thx_event_pairs_create")
+        self.e = expectation
+        expectation.cfg.phaseEvents = self.ev
+
+    def select(self, first_pair):
+        """Record the next run's phases into pairs first_pair, first_pair + 1, ..."""
+        self.e.cfg.phaseEvents = ctypes.c_void_p(self.ev.value + 2 * first_pair *
+                                                 ctypes.sizeof(ctypes.c_void_p))
+
+    def ms(self):
+        out = (ctypes.c_float * self.n)()
+        check(lib().thx_event_pairs_elapsed(self.ev, self.n, out), "thx_event_pairs_elapsed")
+        return [v for v in out if v >= 0]
+
+    def close(self):
+        self.e.cfg.phaseEvents = None
+        lib().thx_event_pairs_destroy(self.ev, self.n)
 
 
 class Reconstructor:

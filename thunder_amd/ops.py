@@ -266,9 +266,10 @@ class HalfMap:
         self.counter = torch.zeros(1, dtype=torch.int32, device=device)
 
 
-def insert3d(hm, dat, ctf_, quat, trans, offS, w, px, tiled=True):
+def insert3d(hm, dat, ctf_, quat, trans, offS, w, px, tiled=True, nC=None):
     """tiled: LDS-accumulated patches (thx_insert3d_tiled) instead of one
-    memory-side atomic per tap (thx_insert3d)."""
+    memory-side atomic per tap (thx_insert3d).  nC: optional int32 [nImg],
+    image l inserts only its first nC[l] samples (the K-class InsertFT call)."""
     nImg, nPxl = dat.shape
     _req(dat, torch.complex64, (nImg, nPxl), "dat")
     _req(ctf_, torch.float32, (nImg, nPxl), "ctf")
@@ -277,6 +278,8 @@ def insert3d(hm, dat, ctf_, quat, trans, offS, w, px, tiled=True):
     _req(trans, torch.float64, (nImg, mReco, 2), "trans")
     _req(offS, torch.float64, (nImg, 2), "offS")
     _req(w, torch.float32, (nImg,), "w")
+    if nC is not None:
+        _req(nC, torch.int32, (nImg,), "nC")
     if nPxl != px.n:
         raise ValueError("pixel set / image size mismatch")
     if px.rU * px.pf >= hm.vdim // 2 - 1:
@@ -286,20 +289,69 @@ def insert3d(hm, dat, ctf_, quat, trans, offS, w, px, tiled=True):
         ws = workspace(lib().thx_insert3d_workspace(min(nImg, 65535), mReco, len(px.order)), dev)
     for l0 in range(0, nImg, 65535):
         nb = min(65535, nImg - l0)
+        nCp = _ptr(nC[l0:]) if nC is not None else None
         if tiled:
             check(lib().thx_insert3d_tiled(
                 _ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim, px.pf,
                 _ptr(dat[l0:]), _ptr(ctf_[l0:]), _ptr(quat[l0:]), _ptr(trans[l0:]), _ptr(offS[l0:]),
-                _ptr(w[l0:]), nb, mReco, _ptr(px.d_iCol), _ptr(px.d_iRow), _ptr(px.d_order),
+                _ptr(w[l0:]), nCp, nb, mReco, _ptr(px.d_iCol), _ptr(px.d_iRow), _ptr(px.d_order),
                 len(px.order), nPxl, px.idim, _ptr(ws), ws.numel(), _stream(dev)),
                 "thx_insert3d_tiled")
             continue
         check(lib().thx_insert3d(_ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim,
                                  px.pf, _ptr(dat[l0:]), _ptr(ctf_[l0:]), _ptr(quat[l0:]),
-                                 _ptr(trans[l0:]), _ptr(offS[l0:]), _ptr(w[l0:]), nb, mReco,
+                                 _ptr(trans[l0:]), _ptr(offS[l0:]), _ptr(w[l0:]), nCp, nb, mReco,
                                  _ptr(px.d_iCol), _ptr(px.d_iRow), nPxl, px.idim, _stream(dev)),
               "thx_insert3d")
     return hm
+
+
+# ------------------------------------------------------------------ a13
+class RcclComm:
+    """RCCL communicator of one hemisphere for thx_halfmap_allreduce, built
+    from a unique id the caller moves between its ranks (MPI_Bcast in THUNDER;
+    ``from_group`` uses torch.distributed)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, nranks, uid, rank):
+        self.comm = ctypes.c_void_p()
+        buf = (ctypes.c_char * self.ID_BYTES).from_buffer_copy(bytes(uid))
+        check(lib().thx_rccl_comm_init(nranks, buf, rank, ctypes.byref(self.comm)),
+              "thx_rccl_comm_init")
+        self.nranks, self.rank = nranks, rank
+
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_char * RcclComm.ID_BYTES)()
+        check(lib().thx_rccl_unique_id(buf), "thx_rccl_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def from_group(cls, group, device):
+        """Collective over ``group``: its first rank draws the id, a broadcast
+        hands it to the others (the MPI_Bcast of gpu/src/cuthunder.cu:5309-5322)."""
+        import torch.distributed as dist
+        ranks = dist.get_process_group_ranks(group)
+        me = dist.get_rank()
+        t = torch.zeros(cls.ID_BYTES, dtype=torch.uint8, device=device)
+        if me == ranks[0]:
+            t.copy_(torch.frombuffer(bytearray(cls.unique_id()), dtype=torch.uint8))
+        dist.broadcast(t, src=ranks[0], group=group)
+        return cls(len(ranks), t.cpu().numpy().tobytes(), ranks.index(me))
+
+    def allreduce(self, hm, nK=1):
+        """thx_halfmap_allreduce: in-place sum of F, T, O, counter."""
+        dim = hm.T.numel() // nK
+        check(lib().thx_halfmap_allreduce(self.comm, _ptr(hm.F), _ptr(hm.T), _ptr(hm.O),
+                                          _ptr(hm.counter), dim, nK, _stream(hm.F.device)),
+              "thx_halfmap_allreduce")
+        return hm
+
+    def close(self):
+        if self.comm:
+            check(lib().thx_rccl_comm_destroy(self.comm), "thx_rccl_comm_destroy")
+            self.comm = ctypes.c_void_p()
 
 
 # ------------------------------------------------------------------ a14

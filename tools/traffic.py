@@ -3,7 +3,8 @@
 passes of tools/gpu_round.sh (pmc1 = FETCH_SIZE, pmc2 = WRITE_SIZE, both run
 on `bench.py --steps 1 --warmup 0`).
 
-A "launch" is the whole launch sequence the bench times with HIP events:
+A "launch" is the whole launch sequence the bench times with HIP events
+(local_bench: the single k_local_fused<false> dispatch of a bench phase):
   scan  : k_prep_aconst .. k_scan_combine_bf of one thx_global_scan call whose
           k_scan_split grid is the 4096-image grid (bench.scan_roofline);
   local : k_patch_boxes .. k_local_weights of one thx_local_phase call that runs
@@ -57,6 +58,18 @@ def summarise(rd, wr, start, end, pick):
             "kernels": [n.split("(")[0] for n, _, _ in gr[-1]]}
 
 
+def single(rd, wr, name, grid):
+    """Average bytes per dispatch of one kernel at one grid size."""
+    r = [v for n, g, v in rd if name in n and g == grid]
+    w = [v for n, g, v in wr if name in n and g == grid]
+    if not r or not w:
+        return None
+    rb = sum(r) / len(r) * 1024 * 2
+    wb = sum(w) / len(w) * 1024
+    return {"read_bytes": rb, "write_bytes": wb, "traffic_bytes": rb + wb, "launches": len(r),
+            "kernels": [name]}
+
+
 def main():
     tag, out = sys.argv[1], sys.argv[2]
     rd = dispatches(os.path.join(tag, "pmc1", "run_counter_collection.csv"), "FETCH_SIZE")
@@ -70,6 +83,9 @@ def main():
                                              for n, gr, _ in g)),
         "local_fullres_512": summarise(rd, wr, "k_patch_boxes", "k_local_weights",
                                        lambda g: any("k_local_fused<true>" in n for n, _, _ in g)),
+        # the bench step's dominant kernel: one k_local_fused<false> launch per
+        # phase over the whole 12 500-image batch (grid 12500 x 1 x 1 of 512)
+        "local_bench": single(rd, wr, "k_local_fused<false>", 12500 * 512),
     }
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
