@@ -433,6 +433,51 @@ int thx_ExpectGlobal3D(const float* rotP, const float* traP, const float* datP,
                        const double* pT, float* baseL, int kIdx, int nK,
                        int nR, int nT, int npxl, int imgNum);
 
+/* ---- the per-image local-search surface, gpu/interface/Interface.h:16-164
+ * (called from the OpenMP image loop of Optimiser::expectationG,
+ * src/Optimiser.cpp:2160-2750).  Complex arrays are float[2]; the device
+ * pointers these return are owned by the caller and freed by the matching
+ * *Fin / *FreeIdx call.  The ManagedArrayTexture / ManagedCalPoint objects
+ * become opaque handles: thx_tex_create / thx_calpoint_create mirror their
+ * Init(mode, vdim, gpu) / Init(mode, searchType, gpu, mLR, mLT, mLD, nPxl).
+ * Only MODE_3D and no CTF search (searchType != 2, mLD <= 1). */
+int thx_getAviDevice(int* gpus, int cap, int* n);                               /* :16 */
+int thx_ExpectPreidx(int gpuIdx, int** deviCol, int** deviRow, const int* iCol,
+                     const int* iRow, int npxl);                                  /* :18 */
+int thx_ExpectPrefre(int gpuIdx, float** devfreQ, const float* freQ, int npxl); /* :26 */
+int thx_ExpectLocalIn(int gpuIdx, float** devdatP, float** devctfP, float** devdefO,
+                      float** devsigP, int nPxl, int cpyNumL, int searchType);   /* :31 */
+int thx_tex_create(int mode, int vdim, int gpuIdx, void** mgr);
+int thx_tex_destroy(void* mgr);
+int thx_ExpectLocalV3D(int gpuIdx, void* mgr, const float* volume, int vdim);   /* :44 */
+int thx_ExpectLocalP(int gpuIdx, float* devdatP, float* devctfP, float* devdefO,
+                     float* devsigP, const float* datP, const float* ctfP,
+                     const float* defO, const float* sigP, int threadId, int imgId,
+                     int npxl, int cSearch);                                      /* :49 */
+int thx_ExpectLocalHostA(int gpuIdx, float** wC, float** wR, float** wT, float** wD,
+                         double** oldR, double** oldT, double** oldD, double** trans,
+                         double** rot, double** dpara, int mR, int mT, int mD,
+                         int cSearch);                                            /* :63 */
+int thx_calpoint_create(int mode, int searchType, int gpuIdx, int mR, int mT, int mD,
+                        int npxl, void** mcp);
+int thx_calpoint_destroy(void* mcp);
+int thx_ExpectLocalRTD(int gpuIdx, void* mcp, const double* oldR, const double* oldT,
+                       const double* oldD, const double* trans, const double* rot,
+                       const double* dpara);                                      /* :79 */
+int thx_ExpectLocalPreI3D(int gpuIdx, int datShift, void* mgr, void* mcp,
+                          const float* devdefO, const float* devfreQ, const int* deviCol,
+                          const int* deviRow, float phaseShift, float conT, float k1,
+                          float k2, int pf, int idim, int vdim, int npxl, int interp); /* :106 */
+int thx_ExpectLocalM(int gpuIdx, int datShift, void* mcp, const float* devdatP,
+                     const float* devctfP, const float* devsigP, float* wC, float* wR,
+                     float* wT, float* wD, double oldC, int npxl);                /* :124 */
+int thx_ExpectLocalHostF(int gpuIdx, float** wC, float** wR, float** wT, float** wD,
+                         double** oldR, double** oldT, double** oldD, double** trans,
+                         double** rot, double** dpara, int cSearch);              /* :140 */
+int thx_ExpectLocalFin(int gpuIdx, float** devdatP, float** devctfP, float** devdefO,
+                       float** devfreQ, float** devsigP, int cSearch);            /* :153 */
+int thx_ExpectFreeIdx(int gpuIdx, int** deviCol, int** deviRow);                /* :161 */
+
 /* gpu/interface/Interface.h:294-318 InsertFT (K = 1, cSearch off): F3D
  * [dimSize*2], T3D[dimSize] (real), O3D[3], counter[1] are read-modify-write
  * host buffers; nR[imgNum*mReco*4], nT[imgNum*mReco*2], offS[imgNum*2],
@@ -454,6 +499,16 @@ int thx_InsertFTC(float* F3D, float* T3D, double* O3D, int* counter,
                   const float* w, const double* nR, const double* nT, const int* nC,
                   const int* iCol, const int* iRow, int opf, int npxl,
                   int mReco, int idim, int vdim, int imgNum);
+
+/* Either of the two with the reference call's hemisphere reduction inside
+ * (nC may be NULL): after the insert, thx_halfmap_allreduce of the device
+ * F / T / O / counter over `comm` (a communicator from thx_rccl_comm_init
+ * spanning the hemisphere's ranks; collective), then the copy back. */
+int thx_InsertFTComm(float* F3D, float* T3D, double* O3D, int* counter,
+                     const float* datP, const float* ctfP, const double* offS,
+                     const float* w, const double* nR, const double* nT, const int* nC,
+                     const int* iCol, const int* iRow, int opf, int npxl,
+                     int mReco, int idim, int vdim, int imgNum, void* comm);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,84 @@
+"""The per-image local-search plugin surface (gpu/interface/Interface.h:16-164)
+driven the way Optimiser::expectationG's image loop drives it
+(src/Optimiser.cpp:2190-2570): ExpectPreidx, handles, ExpectLocalIn /
+ExpectLocalP into image slots, HostA pinned buffers, per image ExpectLocalRTD
+-> ExpectLocalPreI3D -> ExpectLocalM, then the frees -- compared with the
+restatement's local phase (orc.local_phase) for every image and slot."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from stacks import small_stack
+from thunder_amd import synth
+from thunder_amd._lib import lib
+
+pytestmark = pytest.mark.gpu
+
+vp = ctypes.c_void_p
+
+
+def P(a):
+    return a.ctypes.data_as(vp)
+
+
+def test_local_path_through_interface_forwards(orc):
+    s = small_stack(orc, N=48, nImg=5, nR=4, nT=3, seed=12)
+    L = lib()
+    npxl = s["px"].n
+    mR, mT, cpy = 125, 9, 2
+    gpu = 0
+    n = ctypes.c_int()
+    assert L.thx_getAviDevice(None, 0, ctypes.byref(n)) == 0 and n.value >= 1
+    iCol, iRow = s["px"].iCol.copy(), s["px"].iRow.copy()
+    dCol, dRow = vp(), vp()
+    assert L.thx_ExpectPreidx(gpu, ctypes.byref(dCol), ctypes.byref(dRow), P(iCol), P(iRow), npxl) == 0
+    mgr = vp()
+    assert L.thx_tex_create(1, s["vdim"], gpu, ctypes.byref(mgr)) == 0
+    vol = np.ascontiguousarray(s["vol"])
+    assert L.thx_ExpectLocalV3D(gpu, mgr, P(vol), s["vdim"]) == 0
+    dat = np.ascontiguousarray(s["dat"]).view(np.float32)
+    ctf, sig = np.ascontiguousarray(s["ctf"]), np.ascontiguousarray(s["sig"])
+    dD, dC, dO, dS = vp(), vp(), vp(), vp()
+    assert L.thx_ExpectLocalIn(gpu, ctypes.byref(dD), ctypes.byref(dC), ctypes.byref(dO),
+                               ctypes.byref(dS), npxl, cpy, 1) == 0
+    host = [vp() for _ in range(10)]
+    assert L.thx_ExpectLocalHostA(gpu, *[ctypes.byref(h) for h in host], mR, mT, 1, 0) == 0
+    f32 = lambda h, k: np.ctypeslib.as_array(ctypes.cast(h, ctypes.POINTER(ctypes.c_float)), (k,))
+    f64 = lambda h, k: np.ctypeslib.as_array(ctypes.cast(h, ctypes.POINTER(ctypes.c_double)), (k,))
+    wC, wR, wT, wD = f32(host[0], 1), f32(host[1], mR), f32(host[2], mT), f32(host[3], 1)
+    oldR, oldT, trans, rot = f64(host[4], mR), f64(host[5], mT), f64(host[7], 2 * mT), f64(host[8], 4 * mR)
+    mcp = vp()
+    assert L.thx_calpoint_create(1, 1, gpu, mR, mT, 1, npxl, ctypes.byref(mcp)) == 0
+    rng = np.random.default_rng(5)
+    for img in range(5):
+        slot = img % cpy
+        assert L.thx_ExpectLocalP(gpu, dD, dC, dO, dS, P(dat), P(ctf), None, P(sig), slot, img,
+                                  npxl, 0) == 0
+        q = synth.clustered_quaternions(1, mR, 4.0, rng)[0]
+        t = rng.standard_normal((mT, 2))
+        pR = rng.uniform(0.5, 1.5, mR)
+        pR /= pR.sum()
+        pT = np.full(mT, 1.0 / mT)
+        oldR[:], oldT[:], rot[:], trans[:] = pR, pT, q.reshape(-1), t.reshape(-1)
+        oldC = 0.7
+        assert L.thx_ExpectLocalRTD(gpu, mcp, host[4], host[5], host[6], host[7], host[8], host[9]) == 0
+        assert L.thx_ExpectLocalPreI3D(gpu, slot, mgr, mcp, None, None, dCol, dRow, 0.0, 0.1, 0.0,
+                                       0.0, s["pf"], s["N"], s["vdim"], npxl, 1) == 0
+        assert L.thx_ExpectLocalM(gpu, slot, mcp, dD, dC, dS, host[0], host[1], host[2], host[3],
+                                  oldC, npxl) == 0, L.thx_last_error()
+        rC, rR, rT, rb, rd = orc.local_phase(s["vol"], s["vdim"], s["pf"], q, t, oldC, pR, pT,
+                                             s["dat"][img], s["ctf"][img], s["sig"][img], s["px"],
+                                             s["N"])
+        for got, want in ((wR, rR), (wT, rT)):
+            m = want >= 1e-4 * want.max()
+            assert np.max(np.abs(got - want)[m] / want[m]) < 1e-3
+        assert abs(wC[0] - rC) <= 1e-3 * abs(rC)
+        assert abs(wD[0] - oldC * wC[0]) <= 1e-6 * abs(wD[0])
+    assert L.thx_calpoint_destroy(mcp) == 0
+    assert L.thx_ExpectLocalHostF(gpu, *[ctypes.byref(h) for h in host], 0) == 0
+    assert L.thx_ExpectLocalFin(gpu, ctypes.byref(dD), ctypes.byref(dC), ctypes.byref(dO), None,
+                                ctypes.byref(dS), 0) == 0
+    assert L.thx_tex_destroy(mgr) == 0
+    assert L.thx_ExpectFreeIdx(gpu, ctypes.byref(dCol), ctypes.byref(dRow)) == 0
+    assert dCol.value is None and dD.value is None

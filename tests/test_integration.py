@@ -1,0 +1,60 @@
+"""The INTEGRATION.md forwards (gpu/interface/Interface.cpp bodies and the
+handle classes) compile against a restatement of the THUNDER types they touch
+(tests/integration/thunder_restated.h) and MPICH's mpi.h, and link against
+libthunder_amd.so with every symbol resolved: the drop-in boundary cannot
+drift from include/thunder_amd.h.  CPU only (nothing is called on a GPU)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+from thunder_amd import build
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MPI_INC = "/opt/conda/include"
+MPI_LIB = "/opt/conda/lib"
+
+
+def blocks():
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    out = []
+    for name in ("Interface.cpp", "handles"):
+        m = re.search(rf"// BEGIN {re.escape(name)}\n(.*?)// END {re.escape(name)}", txt, re.S)
+        assert m, f"INTEGRATION.md has no '{name}' block"
+        out.append(m.group(1))
+    return out
+
+
+def test_integration_blocks_present():
+    iface, handles = blocks()
+    # every hot-path Interface.h entry point of SURVEY §8(b) is forwarded
+    for fn in ("getAviDevice", "ExpectRotran", "ExpectProject", "ExpectGlobal3D", "ExpectPreidx",
+               "ExpectPrefre", "ExpectLocalIn", "ExpectLocalV3D", "ExpectLocalP",
+               "ExpectLocalHostA", "ExpectLocalRTD", "ExpectLocalPreI3D", "ExpectLocalM",
+               "ExpectLocalHostF", "ExpectLocalFin", "ExpectFreeIdx", "InsertFT"):
+        assert re.search(rf"\bvoid {fn}\(", iface), fn
+    assert "thx_tex_create" in handles and "thx_calpoint_create" in handles
+
+
+@pytest.mark.skipif(not (os.path.exists(os.path.join(MPI_INC, "mpi.h")) and shutil.which("g++")),
+                    reason="needs g++ and MPICH's mpi.h")
+def test_forwards_compile_and_link(tmp_path):
+    lib = build.build()
+    iface, handles = blocks()
+    src = tmp_path / "Interface_thx.cpp"
+    src.write_text('#include "thunder_restated.h"\n' + iface + "\n" + handles)
+    out = tmp_path / "libinterface_thx.so"
+    cmd = ["g++", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Werror", "-Wno-unused-parameter",
+           "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "tests", "integration"),
+           "-I", MPI_INC, str(src), "-o", str(out), "-Wl,--no-undefined",
+           "-L", os.path.dirname(lib), "-lthunder_amd", os.path.join(MPI_LIB, "libmpi.so"),
+           f"-Wl,-rpath,{os.path.dirname(lib)}"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    nm = subprocess.run(["nm", "-D", "--defined-only", "-C", str(out)], capture_output=True,
+                        text=True).stdout
+    for sig in ("ExpectLocalM(int, int, ManagedCalPoint*", "InsertFT(Volume&, Volume&, double*, int*",
+                "ManagedCalPoint::Init(int, int, int, int, int, int, int)", "getAviDevice("):
+        assert sig in nm, sig

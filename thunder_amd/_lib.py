@@ -58,6 +58,27 @@ SIGNATURES = {
     "thx_event_pairs_create": (_c_int, [_c_int, _p]),
     "thx_event_pairs_elapsed": (_c_int, [_p, _c_int, _p]),
     "thx_event_pairs_destroy": (_c_int, [_p, _c_int]),
+    "thx_getAviDevice": (_c_int, [_p, _c_int, _p]),
+    "thx_ExpectPreidx": (_c_int, [_c_int, _p, _p, _p, _p, _c_int]),
+    "thx_ExpectPrefre": (_c_int, [_c_int, _p, _p, _c_int]),
+    "thx_ExpectLocalIn": (_c_int, [_c_int, _p, _p, _p, _p, _c_int, _c_int, _c_int]),
+    "thx_tex_create": (_c_int, [_c_int, _c_int, _c_int, _p]),
+    "thx_tex_destroy": (_c_int, [_p]),
+    "thx_ExpectLocalV3D": (_c_int, [_c_int, _p, _p, _c_int]),
+    "thx_ExpectLocalP": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int,
+                                  _c_int]),
+    "thx_ExpectLocalHostA": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
+                                      _c_int, _c_int]),
+    "thx_calpoint_create": (_c_int, [_c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p]),
+    "thx_calpoint_destroy": (_c_int, [_p]),
+    "thx_ExpectLocalRTD": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _p]),
+    "thx_ExpectLocalPreI3D": (_c_int, [_c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_float, _c_float,
+                                       _c_float, _c_float, _c_int, _c_int, _c_int, _c_int, _c_int]),
+    "thx_ExpectLocalM": (_c_int, [_c_int, _c_int, _p, _p, _p, _p, _p, _p, _p, _p, _c_double,
+                                  _c_int]),
+    "thx_ExpectLocalHostF": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int]),
+    "thx_ExpectLocalFin": (_c_int, [_c_int, _p, _p, _p, _p, _p, _c_int]),
+    "thx_ExpectFreeIdx": (_c_int, [_c_int, _p, _p]),
     "thx_ExpectRotran": (_c_int, [_p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
     "thx_ExpectProject": (_c_int, [_p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _c_int]),
     "thx_ExpectGlobal3D": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
@@ -66,6 +87,8 @@ SIGNATURES = {
                               _c_int, _c_int, _c_int, _c_int]),
     "thx_InsertFTC": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int]),
+    "thx_InsertFTComm": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
+                                  _c_int, _c_int, _c_int, _c_int, _p]),
 }
 
 _lib = None

@@ -150,7 +150,7 @@ extern "C" int thx_ExpectGlobal3D(const float* rotP, const float* traP,
 static int insert_ft(float* F3D, float* T3D, double* O3D, int* counter, const float* datP,
                      const float* ctfP, const double* offS, const float* w, const double* nR,
                      const double* nT, const int* nC, const int* iCol, const int* iRow, int opf,
-                     int npxl, int mReco, int idim, int vdim, int imgNum)
+                     int npxl, int mReco, int idim, int vdim, int imgNum, void* comm)
 {
     THX_CHECK_ARG(F3D && T3D && O3D && counter && datP && ctfP && offS && w && nR &&
                       nT && iCol && iRow,
@@ -210,6 +210,12 @@ static int insert_ft(float* F3D, float* T3D, double* O3D, int* counter, const fl
                              nC ? dN.as<int>() + l0 : nullptr, nb, mReco, dIc.as<int>(),
                              dIr.as<int>(), npxl, idim, nullptr));
     }
+    // the hemisphere's all-reduce of the reference call (cuthunder.cu:5903-5993)
+    if (comm) {
+        THX_RET(thx_halfmap_allreduce(comm, dF.as<float>(), dT.as<float>(), dO.as<double>(),
+                                      dC.as<int>(), (long long)dimSize, 1, nullptr));
+        THX_HIP(hipDeviceSynchronize());
+    }
     THX_HIP(hipMemcpy(F3D, dF.p, sizeof(float) * 2 * dimSize, hipMemcpyDeviceToHost));
     THX_HIP(hipMemcpy(T3D, dT.p, sizeof(float) * dimSize, hipMemcpyDeviceToHost));
     THX_HIP(hipMemcpy(O3D, dO.p, sizeof(double) * 3, hipMemcpyDeviceToHost));
@@ -225,7 +231,7 @@ extern "C" int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
                             int imgNum)
 {
     return insert_ft(F3D, T3D, O3D, counter, datP, ctfP, offS, w, nR, nT, nullptr, iCol, iRow,
-                     opf, npxl, mReco, idim, vdim, imgNum);
+                     opf, npxl, mReco, idim, vdim, imgNum, nullptr);
 }
 
 extern "C" int thx_InsertFTC(float* F3D, float* T3D, double* O3D, int* counter,
@@ -236,5 +242,15 @@ extern "C" int thx_InsertFTC(float* F3D, float* T3D, double* O3D, int* counter,
 {
     THX_CHECK_ARG(nC, "thx_InsertFTC: null nC");
     return insert_ft(F3D, T3D, O3D, counter, datP, ctfP, offS, w, nR, nT, nC, iCol, iRow, opf,
-                     npxl, mReco, idim, vdim, imgNum);
+                     npxl, mReco, idim, vdim, imgNum, nullptr);
+}
+
+extern "C" int thx_InsertFTComm(float* F3D, float* T3D, double* O3D, int* counter,
+                                const float* datP, const float* ctfP, const double* offS,
+                                const float* w, const double* nR, const double* nT,
+                                const int* nC, const int* iCol, const int* iRow, int opf,
+                                int npxl, int mReco, int idim, int vdim, int imgNum, void* comm)
+{
+    return insert_ft(F3D, T3D, O3D, counter, datP, ctfP, offS, w, nR, nT, nC, iCol, iRow, opf,
+                     npxl, mReco, idim, vdim, imgNum, comm);
 }

@@ -1,0 +1,362 @@
+// local_iface.hip -- the reference's per-image local-search plugin surface
+// (gpu/interface/Interface.h:16-164: getAviDevice, ExpectPreidx, ExpectPrefre,
+// ExpectLocalIn, ExpectLocalV3D, ExpectLocalP, ExpectLocalHostA / HostF,
+// ExpectLocalRTD, ExpectLocalPreI3D, ExpectLocalM, ExpectLocalFin,
+// ExpectFreeIdx) over the device C-ABI, so the OpenMP image loop of
+// Optimiser::expectationG (src/Optimiser.cpp:2160-2750) can run unchanged on
+// MI355X with each Interface.cpp body a one-line forward.
+//
+// The reference's stateful handles become opaque thx handles:
+//   ManagedArrayTexture (gpu/include/ManagedArrayTexture.h) -> thx_tex: the
+//     half-complex projectee resident in device memory (no texture object:
+//     the fused kernel gathers from LDS patch boxes or plain global loads);
+//   ManagedCalPoint (gpu/include/ManagedCalPoint.h) -> thx_calpoint: one
+//     image's sample set, priors, marginals and the local-phase workspace on a
+//     HIP stream of its own.
+// ExpectLocalPreI3D (projection tables, cuthunder.cu:2834) only binds the
+// volume, pixel set and geometry to the calpoint; ExpectLocalM runs the fused
+// projection + likelihood + marginals (thx_local_phase for one image) and
+// copies wC / wR / wT / wD back, synchronising the calpoint's stream as the
+// reference does (cuthunder.cu:3140).  CTF search (mD > 1) is not supported.
+// This per-image path exists for drop-in compatibility; thx_expectation runs
+// the same phases for the whole batch on device.
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+struct Tex {
+    int vdim = 0, gpu = 0;
+    float* vol = nullptr;   // dimSize Complex
+};
+
+struct CalPoint {
+    int gpu = 0, mR = 0, mT = 0, npxl = 0;
+    hipStream_t stream = nullptr;
+    double *quat = nullptr, *trans = nullptr, *pR = nullptr, *pT = nullptr, *pC = nullptr;
+    float *wC = nullptr, *wR = nullptr, *wT = nullptr, *base = nullptr;
+    int* order = nullptr;     // tile order of the bound pixel set
+    int nOrd = 0;
+    const int* boundCol = nullptr;
+    void* ws = nullptr;
+    size_t wsBytes = 0;
+    // bound by PreI3D
+    const Tex* tex = nullptr;
+    const int *iCol = nullptr, *iRow = nullptr;
+    int pf = 0, idim = 0, vdim = 0;
+};
+
+#define THX_DEV_SET(g) THX_HIP(hipSetDevice(g))
+
+template <typename T>
+int dalloc(T** p, size_t n)
+{
+    THX_HIP(hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (n > 0 ? n : 1)));
+    return THX_OK;
+}
+
+#define THX_RET(call)                  \
+    do {                               \
+        int st_ = (call);              \
+        if (st_ != THX_OK) return st_; \
+    } while (0)
+
+}  // namespace
+
+extern "C" int thx_getAviDevice(int* gpus, int cap, int* n)
+{
+    THX_CHECK_ARG(n && (cap == 0 || gpus), "thx_getAviDevice: bad arguments");
+    int c = 0;
+    THX_HIP(hipGetDeviceCount(&c));
+    for (int i = 0; i < c && i < cap; i++) gpus[i] = i;
+    *n = c;
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectPreidx(int gpuIdx, int** deviCol, int** deviRow, const int* iCol,
+                                const int* iRow, int npxl)
+{
+    THX_CHECK_ARG(deviCol && deviRow && iCol && iRow && npxl > 0, "thx_ExpectPreidx: bad arguments");
+    THX_DEV_SET(gpuIdx);
+    THX_RET(dalloc(deviCol, npxl));
+    THX_RET(dalloc(deviRow, npxl));
+    THX_HIP(hipMemcpy(*deviCol, iCol, sizeof(int) * npxl, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(*deviRow, iRow, sizeof(int) * npxl, hipMemcpyHostToDevice));
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectPrefre(int gpuIdx, float** devfreQ, const float* freQ, int npxl)
+{
+    THX_CHECK_ARG(devfreQ && npxl > 0, "thx_ExpectPrefre: bad arguments");
+    THX_DEV_SET(gpuIdx);
+    THX_RET(dalloc(devfreQ, npxl));
+    if (freQ) THX_HIP(hipMemcpy(*devfreQ, freQ, sizeof(float) * npxl, hipMemcpyHostToDevice));
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectFreeIdx(int gpuIdx, int** deviCol, int** deviRow)
+{
+    THX_DEV_SET(gpuIdx);
+    if (deviCol && *deviCol) { THX_HIP(hipFree(*deviCol)); *deviCol = nullptr; }
+    if (deviRow && *deviRow) { THX_HIP(hipFree(*deviRow)); *deviRow = nullptr; }
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectLocalIn(int gpuIdx, float** devdatP, float** devctfP, float** devdefO,
+                                 float** devsigP, int nPxl, int cpyNumL, int searchType)
+{
+    THX_CHECK_ARG(devdatP && devctfP && devsigP && nPxl > 0 && cpyNumL > 0,
+                  "thx_ExpectLocalIn: bad arguments");
+    THX_CHECK_ARG(searchType != 2, "thx_ExpectLocalIn: CTF search is not supported");
+    THX_DEV_SET(gpuIdx);
+    const size_t n = (size_t)nPxl * cpyNumL;
+    THX_RET(dalloc(devdatP, 2 * n));
+    THX_RET(dalloc(devctfP, n));
+    THX_RET(dalloc(devsigP, n));
+    if (devdefO) *devdefO = nullptr;
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectLocalP(int gpuIdx, float* devdatP, float* devctfP, float* devdefO,
+                                float* devsigP, const float* datP, const float* ctfP,
+                                const float* defO, const float* sigP, int threadId, int imgId,
+                                int npxl, int cSearch)
+{
+    (void)devdefO; (void)defO;
+    THX_CHECK_ARG(devdatP && devctfP && devsigP && datP && ctfP && sigP && threadId >= 0 &&
+                      imgId >= 0 && npxl > 0,
+                  "thx_ExpectLocalP: bad arguments");
+    THX_CHECK_ARG(!cSearch, "thx_ExpectLocalP: CTF search is not supported");
+    THX_DEV_SET(gpuIdx);
+    const size_t d = (size_t)threadId * npxl, s = (size_t)imgId * npxl;
+    THX_HIP(hipMemcpy(devdatP + 2 * d, datP + 2 * s, sizeof(float) * 2 * npxl, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(devctfP + d, ctfP + s, sizeof(float) * npxl, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(devsigP + d, sigP + s, sizeof(float) * npxl, hipMemcpyHostToDevice));
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectLocalFin(int gpuIdx, float** devdatP, float** devctfP, float** devdefO,
+                                  float** devfreQ, float** devsigP, int cSearch)
+{
+    (void)cSearch;
+    THX_DEV_SET(gpuIdx);
+    float** all[5] = {devdatP, devctfP, devdefO, devfreQ, devsigP};
+    for (float** p : all)
+        if (p && *p) {
+            THX_HIP(hipFree(*p));
+            *p = nullptr;
+        }
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectLocalHostA(int gpuIdx, float** wC, float** wR, float** wT, float** wD,
+                                    double** oldR, double** oldT, double** oldD, double** trans,
+                                    double** rot, double** dpara, int mR, int mT, int mD,
+                                    int cSearch)
+{
+    THX_CHECK_ARG(wC && wR && wT && wD && oldR && oldT && oldD && trans && rot && dpara &&
+                      mR > 0 && mT > 0,
+                  "thx_ExpectLocalHostA: bad arguments");
+    THX_DEV_SET(gpuIdx);
+    const int nD = cSearch && mD > 0 ? mD : 1;
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(wC), sizeof(float)));
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(wR), sizeof(float) * mR));
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(wT), sizeof(float) * mT));
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(wD), sizeof(float) * nD));
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(oldR), sizeof(double) * mR));
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(oldT), sizeof(double) * mT));
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(oldD), sizeof(double) * nD));
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(trans), sizeof(double) * 2 * mT));
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(rot), sizeof(double) * 4 * mR));
+    THX_HIP(hipHostMalloc(reinterpret_cast<void**>(dpara), sizeof(double) * nD));
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectLocalHostF(int gpuIdx, float** wC, float** wR, float** wT, float** wD,
+                                    double** oldR, double** oldT, double** oldD, double** trans,
+                                    double** rot, double** dpara, int cSearch)
+{
+    (void)cSearch;
+    THX_DEV_SET(gpuIdx);
+    void** all[10] = {(void**)wC, (void**)wR, (void**)wT, (void**)wD, (void**)oldR,
+                      (void**)oldT, (void**)oldD, (void**)trans, (void**)rot, (void**)dpara};
+    for (void** p : all)
+        if (p && *p) {
+            THX_HIP(hipHostFree(*p));
+            *p = nullptr;
+        }
+    return THX_OK;
+}
+
+// ManagedArrayTexture::Init + ExpectLocalV3D
+extern "C" int thx_tex_create(int mode, int vdim, int gpuIdx, void** mgr)
+{
+    THX_CHECK_ARG(mgr && vdim > 0 && vdim % 2 == 0, "thx_tex_create: bad arguments");
+    THX_CHECK_ARG(mode == 1, "thx_tex_create: only MODE_3D (1) is supported");
+    THX_DEV_SET(gpuIdx);
+    Tex* t = new Tex;
+    t->vdim = vdim;
+    t->gpu = gpuIdx;
+    const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
+    if (hipMalloc(&t->vol, sizeof(float) * 2 * dimSize) != hipSuccess) {
+        delete t;
+        thx::set_error("thx_tex_create: device allocation failed");
+        return THX_ERR_NOMEM;
+    }
+    *mgr = t;
+    return THX_OK;
+}
+
+extern "C" int thx_tex_destroy(void* mgr)
+{
+    Tex* t = static_cast<Tex*>(mgr);
+    if (!t) return THX_OK;
+    THX_DEV_SET(t->gpu);
+    if (t->vol) THX_HIP(hipFree(t->vol));
+    delete t;
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectLocalV3D(int gpuIdx, void* mgr, const float* volume, int vdim)
+{
+    Tex* t = static_cast<Tex*>(mgr);
+    THX_CHECK_ARG(t && volume && vdim == t->vdim && gpuIdx == t->gpu,
+                  "thx_ExpectLocalV3D: volume handle / size / device mismatch");
+    THX_DEV_SET(gpuIdx);
+    const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
+    THX_HIP(hipMemcpy(t->vol, volume, sizeof(float) * 2 * dimSize, hipMemcpyHostToDevice));
+    return THX_OK;
+}
+
+// ManagedCalPoint::Init (mode, searchType, gpu, mLR, mLT, mLD, nPxl)
+extern "C" int thx_calpoint_create(int mode, int searchType, int gpuIdx, int mR, int mT, int mD,
+                                   int npxl, void** mcp)
+{
+    THX_CHECK_ARG(mcp && mR > 0 && mT > 0 && npxl > 0, "thx_calpoint_create: bad arguments");
+    THX_CHECK_ARG(mode == 1, "thx_calpoint_create: only MODE_3D (1) is supported");
+    THX_CHECK_ARG(searchType != 2 && mD <= 1, "thx_calpoint_create: CTF search is not supported");
+    THX_DEV_SET(gpuIdx);
+    CalPoint* c = new CalPoint;
+    c->gpu = gpuIdx;
+    c->mR = mR;
+    c->mT = mT;
+    c->npxl = npxl;
+    int st = THX_OK;
+    auto chk = [&](hipError_t e) {
+        if (e != hipSuccess && st == THX_OK) {
+            thx::set_error("thx_calpoint_create: %s", hipGetErrorString(e));
+            st = THX_ERR_NOMEM;
+        }
+    };
+    chk(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    chk(hipMalloc(&c->quat, sizeof(double) * 4 * mR));
+    chk(hipMalloc(&c->trans, sizeof(double) * 2 * mT));
+    chk(hipMalloc(&c->pR, sizeof(double) * mR));
+    chk(hipMalloc(&c->pT, sizeof(double) * mT));
+    chk(hipMalloc(&c->pC, sizeof(double)));
+    chk(hipMalloc(&c->wC, sizeof(float)));
+    chk(hipMalloc(&c->wR, sizeof(float) * mR));
+    chk(hipMalloc(&c->wT, sizeof(float) * mT));
+    chk(hipMalloc(&c->base, sizeof(float)));
+    // the tile order of a pixel set has at most ~1.25 npxl + 16 entries
+    const int ordCap = (npxl * 2 + 31) / 16 * 16;
+    chk(hipMalloc(&c->order, sizeof(int) * ordCap));
+    c->wsBytes = thx_local_phase_workspace(1, mR, mT, ordCap > npxl ? ordCap : npxl);
+    chk(hipMalloc(&c->ws, c->wsBytes));
+    *mcp = c;
+    return st;
+}
+
+extern "C" int thx_calpoint_destroy(void* mcp)
+{
+    CalPoint* c = static_cast<CalPoint*>(mcp);
+    if (!c) return THX_OK;
+    THX_DEV_SET(c->gpu);
+    void* all[] = {c->quat, c->trans, c->pR, c->pT, c->pC, c->wC, c->wR, c->wT, c->base, c->order, c->ws};
+    for (void* p : all)
+        if (p) (void)hipFree(p);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectLocalRTD(int gpuIdx, void* mcp, const double* oldR, const double* oldT,
+                                  const double* oldD, const double* trans, const double* rot,
+                                  const double* dpara)
+{
+    (void)oldD; (void)dpara;
+    CalPoint* c = static_cast<CalPoint*>(mcp);
+    THX_CHECK_ARG(c && oldR && oldT && trans && rot && gpuIdx == c->gpu,
+                  "thx_ExpectLocalRTD: bad arguments");
+    THX_DEV_SET(gpuIdx);
+    THX_HIP(hipMemcpyAsync(c->pR, oldR, sizeof(double) * c->mR, hipMemcpyHostToDevice, c->stream));
+    THX_HIP(hipMemcpyAsync(c->pT, oldT, sizeof(double) * c->mT, hipMemcpyHostToDevice, c->stream));
+    THX_HIP(hipMemcpyAsync(c->trans, trans, sizeof(double) * 2 * c->mT, hipMemcpyHostToDevice, c->stream));
+    THX_HIP(hipMemcpyAsync(c->quat, rot, sizeof(double) * 4 * c->mR, hipMemcpyHostToDevice, c->stream));
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectLocalPreI3D(int gpuIdx, int datShift, void* mgr, void* mcp,
+                                     const float* devdefO, const float* devfreQ,
+                                     const int* deviCol, const int* deviRow, float phaseShift,
+                                     float conT, float k1, float k2, int pf, int idim, int vdim,
+                                     int npxl, int interp)
+{
+    (void)datShift; (void)devdefO; (void)devfreQ; (void)phaseShift; (void)conT;
+    CalPoint* c = static_cast<CalPoint*>(mcp);
+    const Tex* t = static_cast<const Tex*>(mgr);
+    THX_CHECK_ARG(c && t && deviCol && deviRow && gpuIdx == c->gpu && npxl == c->npxl &&
+                      vdim == t->vdim && vdim == pf * idim,
+                  "thx_ExpectLocalPreI3D: bad arguments");
+    THX_CHECK_ARG(interp == 1, "thx_ExpectLocalPreI3D: only LINEAR_INTERP (1) is supported");
+    THX_CHECK_ARG(k1 == 0.f && k2 == 0.f, "thx_ExpectLocalPreI3D: CTF search is not supported");
+    THX_DEV_SET(gpuIdx);
+    if (c->boundCol != deviCol) {
+        // the pixel set's local-phase visiting order, once per calpoint and set
+        std::vector<int> hc(npxl), hr(npxl);
+        THX_HIP(hipMemcpy(hc.data(), deviCol, sizeof(int) * npxl, hipMemcpyDeviceToHost));
+        THX_HIP(hipMemcpy(hr.data(), deviRow, sizeof(int) * npxl, hipMemcpyDeviceToHost));
+        int nOrd = 0;
+        THX_RET(thx_pixel_tile_order(hc.data(), hr.data(), npxl, 0, nullptr, &nOrd));
+        const int ordCap = (npxl * 2 + 31) / 16 * 16;
+        THX_CHECK_ARG(nOrd <= ordCap, "thx_ExpectLocalPreI3D: tile order too long");
+        std::vector<int> ord(nOrd);
+        THX_RET(thx_pixel_tile_order(hc.data(), hr.data(), npxl, nOrd, ord.data(), &nOrd));
+        THX_HIP(hipMemcpy(c->order, ord.data(), sizeof(int) * nOrd, hipMemcpyHostToDevice));
+        c->nOrd = nOrd;
+        c->boundCol = deviCol;
+    }
+    c->tex = t;
+    c->iCol = deviCol;
+    c->iRow = deviRow;
+    c->pf = pf;
+    c->idim = idim;
+    c->vdim = vdim;
+    return THX_OK;
+}
+
+extern "C" int thx_ExpectLocalM(int gpuIdx, int datShift, void* mcp, const float* devdatP,
+                                const float* devctfP, const float* devsigP, float* wC, float* wR,
+                                float* wT, float* wD, double oldC, int npxl)
+{
+    CalPoint* c = static_cast<CalPoint*>(mcp);
+    THX_CHECK_ARG(c && c->tex && devdatP && devctfP && devsigP && wC && wR && wT &&
+                      gpuIdx == c->gpu && npxl == c->npxl && datShift >= 0,
+                  "thx_ExpectLocalM: bad arguments (ExpectLocalPreI3D must come first)");
+    THX_DEV_SET(gpuIdx);
+    const size_t off = (size_t)datShift * npxl;
+    THX_HIP(hipMemcpyAsync(c->pC, &oldC, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    THX_RET(thx_local_phase(c->tex->vol, 0, c->vdim, c->pf, c->quat, c->mR, c->trans, c->mT, c->pC,
+                            c->pR, c->pT, devdatP + 2 * off, devctfP + off, devsigP + off, c->iCol,
+                            c->iRow, c->order, c->nOrd, npxl, c->idim, 1, c->wC, c->wR, c->wT,
+                            c->base, nullptr, c->ws, c->wsBytes, c->stream));
+    THX_HIP(hipMemcpyAsync(wC, c->wC, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    THX_HIP(hipMemcpyAsync(wR, c->wR, sizeof(float) * c->mR, hipMemcpyDeviceToHost, c->stream));
+    THX_HIP(hipMemcpyAsync(wT, c->wT, sizeof(float) * c->mT, hipMemcpyDeviceToHost, c->stream));
+    THX_HIP(hipStreamSynchronize(c->stream));   // the reference's sync (cuthunder.cu:3140)
+    // nD = 1 (wD prior 1): wD(0) = sum s wC(0) wR(r) wT(t) = oldC * wC
+    // (src/Optimiser.cpp:1399-1402)
+    if (wD) wD[0] = (float)(oldC * (double)wC[0]);
+    return THX_OK;
+}
