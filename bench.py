@@ -330,6 +330,8 @@ def main():
             "kernel": f"k_local_fused<false> (particle-filter phase, nPxl={px.n}, {mR}x{mT}, "
                       f"{nL} images per launch)",
             "launch_ms": t_launch * 1e3, "launches_timed": len(local_ms),
+            "launch_ms_by_phase": [round(float(np.mean(local_ms[k::a.phases])), 3)
+                                   for k in range(a.phases)] if len(local_ms) == a.phases * a.steps else None,
             "share_of_step": float(np.sum(local_ms)) / (a.steps * ms_per_step),
             "algorithmic_flop_per_launch": flop,
             "tap_bytes_per_launch": 64.0 * mR * px.n * nL,
