@@ -436,7 +436,17 @@ def main():
             fsc = ops.fsc(recs[0].hm.F, recs[1].hm.F, N)
             torch.cuda.synchronize()
             extras["fsc_ms"] = (time.perf_counter() - t1) * 1e3
-            extras["halfmap_F_fsc_shells_2_8_16"] = [round(float(fsc[k]), 4) for k in (2, 8, 16)]
+            # f1: reconstruct both half-maps (grid-corrected solve, hipFFT at
+            # box pf N), FSC of the reconstructed maps
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            recs_out = [ops.reconstruct(r_.hm, N, pf) for r_ in recs]
+            torch.cuda.synchronize()
+            extras["reconstruct_ms_per_halfmap"] = (time.perf_counter() - t1) * 1e3 / 2
+            extras["reconstruct_balancing_iterations"] = [o[2] for o in recs_out]
+            fsc = ops.fsc(recs_out[0][1], recs_out[1][1], N // 2)
+            extras["reconstructed_fsc_shells_4_16_32_64"] = [round(float(fsc[k]), 4)
+                                                           for k in (4, 16, 32, 64)]
 
     if rank == 0 and not a.no_cpu_baseline:
         vol_np = vol.cpu().numpy()

@@ -312,6 +312,31 @@ int thx_rccl_comm_destroy(void* comm);
 int thx_halfmap_allreduce(void* comm, float* F, float* T, double* O, int* counter,
                           long long dimSize, int nK, thx_stream_t stream);
 
+/* ------------------------------------------------------------------ f1 ---
+ * The reconstruction solve of one half-map, Reconstructor::reconstruct
+ * (src/Reconstructor.cpp:1129-1831; GPU twin reconstructG :1835), 3D,
+ * trilinear kernel, on device with hipFFT: optional MAP Wiener factor from the
+ * half-map FSC (fsc[nFsc] per shell of the unpadded box, joinHalf), W = 1
+ * in the sphere |k| < maxRadius pf, T = max(T, 1e-25), gridCorr: W balanced
+ * against the MKB(a, alpha) real-space kernel until max||C| - 1| < 1e-2 (or
+ * the MIN / MAX / no-decrease rules), else W = 1 / max(|T|, 1e-6); then
+ * F W -> inverse FFT (1/size) -> the central N^3 box divided by
+ * j0(pi |r| / (pf N))^2.
+ *   F: dimSize Complex (read), T: dimSize float (modified in place),
+ *   dst: N^3 float real space, origin at [0][0][0], negatives wrapped
+ *   (Volume RL storage); dstFT (may be NULL): its forward transform,
+ *   (N/2+1) N N Complex, for thx_fsc; maxRadius <= 0: N/2 - ceil(a);
+ *   nIter / diffOut (may be NULL; diffOut >= 30 floats): balancing iterations
+ *   run and max||C| - 1| after each.
+ * Host-synchronous (one 4-byte read per balancing iteration); workspace >=
+ * thx_reconstruct_workspace(N, pf) device bytes (W, C, the real-space pad,
+ * the kernel table and hipFFT's work area). */
+size_t thx_reconstruct_workspace(int N, int pf);
+int thx_reconstruct(const float* F, float* T, int N, int pf, float a, float alpha,
+                    int gridCorr, int maxRadius, int map, const double* fsc, int nFsc,
+                    int joinHalf, float* dst, float* dstFT, int* nIter, float* diffOut,
+                    void* workspace, size_t wsBytes, thx_stream_t stream);
+
 /* ----------------------------------------------------------------- a14 ---
  * Fourier shell correlation FSC(vec&, const Volume& A, const Volume& B)
  * (src/Functions/Spectrum.cpp:302-337) of two half-complex volumes of real

@@ -1,0 +1,95 @@
+"""f1 on the GPU: thx_reconstruct (Reconstructor::reconstruct with hipFFT)
+against the float64 restatement (oracle/reconstruct.py), and the north-star
+parity chain end to end -- insert of two half-stacks (GPU vs the C
+restatement), reconstruction of both half-maps, FSC of the reconstructed maps
+(FSC, src/Functions/Spectrum.cpp:302-337) within 1e-4."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import reconstruct as orc_rc
+from stacks import small_stack
+from thunder_amd import ops, synth
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def T_(a):
+    return torch.as_tensor(np.ascontiguousarray(a), device=DEV)
+
+
+def _halfmap(F, T):
+    hm = ops.HalfMap(F.shape[0], DEV)
+    hm.F.copy_(T_(F.astype(np.complex64)))
+    hm.T.copy_(T_(T.astype(np.float32)))
+    return hm
+
+
+@pytest.mark.parametrize("grid_corr,map_", [(True, False), (False, False), (True, True)])
+def test_reconstruct_matches_restatement(grid_corr, map_):
+    N, pf = 32, 2
+    vdim = N * pf
+    rng = np.random.default_rng(11)
+    vol = synth.projectee(synth.blob_volume(N, n_blobs=6, seed=3), pf).numpy()
+    # T: a smooth positive sampling density like an insert's, F = T x the projectee
+    quad = orc_rc._ft_quad(vdim).astype(np.float64)
+    T = (50.0 / (1.0 + np.sqrt(quad))) * rng.uniform(0.8, 1.2, quad.shape)
+    F = vol.astype(np.complex128) * T
+    fsc = np.linspace(0.99, 0.2, N // 2 + 1) if map_ else None
+    hm = _halfmap(F, T)
+    got, gft, it, diffs = ops.reconstruct(hm, N, pf, grid_corr=grid_corr, fsc=fsc)
+    ref, rit, rdiffs = orc_rc.reconstruct(F.astype(np.complex64), T.astype(np.float32), N, pf,
+                                          grid_corr=grid_corr, fsc=fsc)
+    got = got.cpu().numpy()
+    assert it == rit
+    if grid_corr:
+        assert np.allclose(diffs, rdiffs, rtol=1e-3, atol=1e-5)
+    assert np.max(np.abs(got - ref)) <= 1e-4 * np.max(np.abs(ref))
+    # the map's transform for the FSC
+    assert np.allclose(gft.cpu().numpy(), np.fft.rfftn(got), atol=1e-3 * np.abs(np.fft.rfftn(got)).max())
+
+
+def test_halfmap_fsc_end_to_end(orc):
+    """Two half-stacks -> insert -> reconstruct -> FSC: GPU (tiled insert,
+    thx_reconstruct, thx_fsc) against the restatement (orc.insert_batch,
+    oracle/reconstruct.py, orc.fsc) -- the north-star 'reconstructed half-map
+    FSC within 1e-4' on a seeded synthetic stack."""
+    s = small_stack(orc, N=32, nImg=4, nR=4, nT=3, seed=21, snr=2.0)
+    N, pf, vdim = s["N"], s["pf"], s["vdim"]
+    # full-resolution pixel set for the insert (rU = N/2 - 2, Reconstructor's maxRadius)
+    pxh = orc.pixel_set(N, pf, N // 2 - 2, 0)
+    px = ops.PixelSet(N, pf, N // 2 - 2, 0, device=DEV)
+    rng = np.random.default_rng(22)
+    nImg, mReco = 600, 8     # 300 images per half: every shell well sampled
+    # images at random poses (recompute at the full-resolution pixel set)
+    qt = synth.uniform_quaternions(nImg, rng)
+    dat = np.stack([orc.project3d(s["vol"], vdim, pf, orc.rotate3d(q), pxh) for q in qt])
+    dat = (dat + 0.05 * (rng.standard_normal(dat.shape) + 1j * rng.standard_normal(dat.shape))
+           ).astype(np.complex64)
+    ctf = np.ones((nImg, pxh.n), np.float32)
+    quat = synth.clustered_quaternions(nImg, mReco, 1.0, rng)
+    quat[:, 0] = qt
+    trans = rng.standard_normal((nImg, mReco, 2)) * 0.3
+    off = np.zeros((nImg, 2))
+    w = np.full(nImg, 1.0 / mReco, np.float32)
+    maps_g, maps_r = [], []
+    for h in (0, 1):
+        sel = np.arange(h, nImg, 2)
+        hm = ops.HalfMap(vdim, DEV)
+        ops.insert3d(hm, T_(dat[sel]), T_(ctf[sel]), T_(quat[sel]), T_(trans[sel]), T_(off[sel]),
+                     T_(w[sel]), px)
+        F, Tm, O, cnt = orc.insert_batch(vdim, pf, dat[sel], ctf[sel], quat[sel], trans[sel],
+                                         off[sel], w[sel], pxh, N)
+        F = F.reshape(vdim, vdim, vdim // 2 + 1)
+        Tm = Tm.reshape(vdim, vdim, vdim // 2 + 1)
+        _, gft, it, _ = ops.reconstruct(hm, N, pf)
+        ref, rit, _ = orc_rc.reconstruct(F, Tm, N, pf)
+        maps_g.append(gft)
+        maps_r.append(np.fft.rfftn(ref).astype(np.complex64))
+    got = ops.fsc(maps_g[0], maps_g[1], N // 2).cpu().numpy()
+    ref = orc.fsc(maps_r[0], maps_r[1], N, N // 2)
+    assert np.all(np.isfinite(got)) and got[2] > 0.5
+    # relative to the FSC value, on the shells the half-maps cover
+    rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-3)
+    assert np.max(rel[1:]) < 1e-4, rel

@@ -47,6 +47,9 @@ SIGNATURES = {
     "thx_rccl_comm_init": (_c_int, [_c_int, _p, _c_int, _p]),
     "thx_rccl_comm_destroy": (_c_int, [_p]),
     "thx_halfmap_allreduce": (_c_int, [_p, _p, _p, _p, _p, ctypes.c_longlong, _c_int, _p]),
+    "thx_reconstruct_workspace": (_c_size, [_c_int, _c_int]),
+    "thx_reconstruct": (_c_int, [_p, _p, _c_int, _c_int, _c_float, _c_float, _c_int, _c_int, _c_int, _p,
+                                 _c_int, _c_int, _p, _p, _p, _p, _p, _c_size, _p]),
     "thx_fsc_workspace": (_c_size, [_c_int]),
     "thx_fsc": (_c_int, [_p, _p, _c_int, _c_int, _p, _p, _c_size, _p]),
     "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int, _c_int]),

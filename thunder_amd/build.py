@@ -58,7 +58,7 @@ def build(verbose=False, jobs=8):
     if todo or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
         tmp = LIB + ".tmp"
         r = subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs,
-                            "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrccl", "-o", tmp],
+                            "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib", "-lrccl", "-lhipfft", "-o", tmp],
                            capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")

@@ -1,0 +1,388 @@
+// reconstruct.hip -- f1: the reconstruction solve of one half-map,
+// Reconstructor::reconstruct (src/Reconstructor.cpp:1129-1831; GPU twin
+// reconstructG :1835, cuthunder PrepareTF / CalculateT / CalculateW /
+// CalculateF, gpu/src/cuthunder.cu:6176-8826), 3D, trilinear insert kernel,
+// on device with hipFFT:
+//
+//   MAP:      T /= FSC'(u) on shells 5 pf <= |k| < maxR pf, FSC' = the
+//             half-map FSC at shell u / pf clamped to [1e-3, 1 - 1e-3]
+//             (sqrt(2 FSC / (1 + FSC)) when joining halves)
+//             (RECONSTRUCTOR_WIENER_FILTER_FSC, :1150-1279);
+//   W = 1 inside the sphere |k| < maxR pf, 0 outside; T = max(T, 1e-25);
+//   grid correction (:1356-1552): repeat C = T W -> back-transform ->
+//             multiply by the MKB real-space kernel table / MKB_RL(0)
+//             (convoluteC, :2595-2675) -> forward transform ->
+//             W /= max(|C|, 1e-6) inside the sphere; stop when
+//             max | |C| - 1 | (RECONSTRUCTOR_CHECK_C_MAX, checkC :2522-2593)
+//             < 1e-2, or after >= MIN_N_ITER_BALANCE (10) iterations with two
+//             in a row not below 0.95 x the previous, or at 30
+//             (include/Reconstructor.h:61-69); without grid correction
+//             W = 1 / max(|T|, 1e-6) (:1553-1587);
+//   pad = F W inside the sphere -> back-transform (FFT::bw scales by 1/size,
+//             src/FFT.cpp:204-229) -> the central N^3 box (VOL_EXTRACT_RL)
+//             -> divided by TIK_RL(|r| / (pf N)) = j0(pi |r| / (pf N))^2
+//             (RECONSTRUCTOR_CORRECT_CONVOLUTION_KERNEL with the trilinear
+//             kernel, :1733-1818).
+// Layouts: F / T / W / C half-complex [k][j][i] of box vdim = pf N (the
+// Volume FT layout = hipFFT's R2C layout); real-space arrays [k][j][i] with
+// the origin at index 0 and negative coordinates wrapped (Volume RL).
+#include <hipfft/hipfft.h>
+
+#include <cmath>
+#include <vector>
+
+#include "common.h"
+
+#define THX_FFT(call)                                                          \
+    do {                                                                       \
+        hipfftResult r_ = (call);                                              \
+        if (r_ != HIPFFT_SUCCESS) {                                            \
+            ::thx::set_error("%s:%d %s: hipfft error %d", __FILE__, __LINE__, \
+                             #call, (int)r_);                                  \
+            return THX_ERR_HIP;                                                \
+        }                                                                      \
+    } while (0)
+
+namespace {
+
+constexpr int TAB_N = 100000;   // _kernelRL.init(MKB_RL_R2, 0, 1, 1e5) (src/Reconstructor.cpp:77-88)
+
+// k of a half-complex index: i in [0, vdim/2], j, k wrapped to [-vdim/2, vdim/2)
+THX_DEV void ft_coord(long q, int vdim, int& i, int& j, int& k)
+{
+    const int nc = vdim / 2 + 1;
+    i = (int)(q % nc);
+    const long r = q / nc;
+    j = (int)(r % vdim);
+    k = (int)(r / vdim);
+    if (j >= vdim / 2) j -= vdim;
+    if (k >= vdim / 2) k -= vdim;
+}
+
+#define GRID_STRIDE(q, n) \
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < (n); q += (long)gridDim.x * blockDim.x)
+
+__global__ void k_wiener(float* __restrict__ T, int vdim, int pf, int maxR,
+                         const double* __restrict__ fsc, int nFsc, int joinHalf)
+{
+    const long n = (long)(vdim / 2 + 1) * vdim * vdim;
+    const long lo = (long)5 * pf * 5 * pf, hi = (long)maxR * pf * maxR * pf;   // WIENER_FACTOR_MIN_R 5
+    GRID_STRIDE(q, n)
+    {
+        int i, j, k;
+        ft_coord(q, vdim, i, j, k);
+        const long quad = (long)i * i + (long)j * j + (long)k * k;
+        if (quad < lo || quad >= hi) continue;
+        const int u = (int)rintf(sqrtf((float)quad));            // AROUND(NORM_3)
+        float f = (u / pf >= nFsc) ? 0.f : (float)fsc[u / pf];
+        f = fmaxf(1e-3f, fminf(1.f - 1e-3f, f));                  // FSC_BASE_L / _H
+        if (joinHalf) f = sqrtf(2.f * f / (1.f + f));
+        T[q] = T[q] / f;
+    }
+}
+
+// W = 1 inside the sphere, 0 outside; T = max(T, 1e-25)
+__global__ void k_init_w(float* __restrict__ W, float* __restrict__ T, int vdim, long r2)
+{
+    const long n = (long)(vdim / 2 + 1) * vdim * vdim;
+    GRID_STRIDE(q, n)
+    {
+        int i, j, k;
+        ft_coord(q, vdim, i, j, k);
+        W[q] = ((long)i * i + (long)j * j + (long)k * k < r2) ? 1.f : 0.f;
+        T[q] = fmaxf(T[q], 1e-25f);
+    }
+}
+
+// no grid correction: W = 1 / max(|T|, 1e-6) inside the sphere
+__global__ void k_w_from_t(float* __restrict__ W, const float* __restrict__ T, int vdim, long r2)
+{
+    const long n = (long)(vdim / 2 + 1) * vdim * vdim;
+    GRID_STRIDE(q, n)
+    {
+        int i, j, k;
+        ft_coord(q, vdim, i, j, k);
+        if ((long)i * i + (long)j * j + (long)k * k < r2) W[q] = 1.f / fmaxf(fabsf(T[q]), 1e-6f);
+    }
+}
+
+// C = T W (T real, so C is real)
+__global__ void k_c_from_tw(float2* __restrict__ C, const float* __restrict__ T,
+                            const float* __restrict__ W, long n)
+{
+    GRID_STRIDE(q, n) C[q] = make_float2(T[q] * W[q], 0.f);
+}
+
+// convoluteC in real space: c(i,j,k) * kernelRL(QUAD_3 / (N pf)^2) / nf,
+// scaled by 1/size of FFT::bw
+__global__ void k_kernel_mul(float* __restrict__ c, int vdim, const float* __restrict__ tab,
+                             float nf, float scale)
+{
+    const long n = (long)vdim * vdim * vdim;
+    const float inv = 1.f / ((float)vdim * (float)vdim);
+    GRID_STRIDE(q, n)
+    {
+        int i = (int)(q % vdim);
+        const long r = q / vdim;
+        int j = (int)(r % vdim), k = (int)(r / vdim);
+        if (i >= vdim / 2) i -= vdim;
+        if (j >= vdim / 2) j -= vdim;
+        if (k >= vdim / 2) k -= vdim;
+        const float x = (float)(i * i + j * j + k * k) * inv;
+        const int t = min(TAB_N, (int)rintf(x / 1e-5f));          // TabFunction: _tab[AROUND((x - a) / s)]
+        c[q] = (c[q] * scale) * tab[t] / nf;
+    }
+}
+
+// W /= max(|C|, 1e-6) inside the sphere; max | |C| - 1 | over the sphere
+__global__ void __launch_bounds__(256) k_update_w(float* __restrict__ W, const float2* __restrict__ C,
+                                                  int vdim, long r2, unsigned* __restrict__ diffBits)
+{
+    const long n = (long)(vdim / 2 + 1) * vdim * vdim;
+    float dmax = 0.f;
+    GRID_STRIDE(q, n)
+    {
+        int i, j, k;
+        ft_coord(q, vdim, i, j, k);
+        if ((long)i * i + (long)j * j + (long)k * k >= r2) continue;
+        const float2 c = C[q];
+        const float a = sqrtf(c.x * c.x + c.y * c.y);
+        W[q] = W[q] / fmaxf(a, 1e-6f);
+        dmax = fmaxf(dmax, fabsf(a - 1.f));
+    }
+    dmax = wave_max(dmax);
+    __shared__ float s[4];
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = dmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float m = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
+        atomicMax(diffBits, __float_as_uint(m));   // non-negative floats order as their bits
+    }
+}
+
+// pad = F W inside the sphere, 0 outside
+__global__ void k_pad(float2* __restrict__ P, const float2* __restrict__ F, const float* __restrict__ W,
+                      int vdim, long r2)
+{
+    const long n = (long)(vdim / 2 + 1) * vdim * vdim;
+    GRID_STRIDE(q, n)
+    {
+        int i, j, k;
+        ft_coord(q, vdim, i, j, k);
+        const float2 f = F[q];
+        const float w = W[q];
+        P[q] = ((long)i * i + (long)j * j + (long)k * k < r2) ? make_float2(f.x * w, f.y * w)
+                                                              : make_float2(0.f, 0.f);
+    }
+}
+
+// the central N^3 box of the back-transformed pad (VOL_EXTRACT_RL) divided by
+// TIK_RL(|r| / (pf N)); both arrays origin-at-0 with wrapped negatives
+__global__ void k_extract(float* __restrict__ dst, const float* __restrict__ src, int N, int vdim,
+                          float scale)
+{
+    const long n = (long)N * N * N;
+    GRID_STRIDE(q, n)
+    {
+        int i = (int)(q % N);
+        const long r = q / N;
+        int j = (int)(r % N), k = (int)(r / N);
+        if (i >= N / 2) i -= N;
+        if (j >= N / 2) j -= N;
+        if (k >= N / 2) k -= N;
+        const long s = ((long)wrap_idx(k, vdim) * vdim + wrap_idx(j, vdim)) * vdim + wrap_idx(i, vdim);
+        const float rr = sqrtf((float)(i * i + j * j + k * k)) / (float)(vdim);
+        const float x = (float)M_PI * rr;
+        const float j0 = x == 0.f ? 1.f : sinf(x) / x;
+        dst[q] = src[s] * scale / (j0 * j0);
+    }
+}
+
+// ---------------------------------------------------------- MKB kernel table
+// MKB_RL_R2 (src/Functions/Functions.cpp, FUNCTIONS_MKB_ORDER_0):
+// (2 pi)^1.5 a^3 / I0(alpha) * I_{3/2}(v) / v^1.5 (u^2 <= alpha^2) or
+// J_{3/2}(v) / v^1.5, v = sqrt(|alpha^2 - u^2|), u^2 = (2 pi a)^2 r2.
+double bessel_i0(double x)
+{
+    double s = 1.0, t = 1.0;
+    for (int k = 1; k < 200; k++) {
+        t *= (x * x / 4.0) / ((double)k * k);
+        s += t;
+        if (t < 1e-17 * s) break;
+    }
+    return s;
+}
+
+// I_{3/2}(v) / v^1.5 (modified = true) or J_{3/2}(v) / v^1.5
+double nu15_over(double v, bool modified)
+{
+    if (v < 0.5) {   // series: sum (+-v^2/4)^k / (2^1.5 k! Gamma(k + 2.5))
+        const double g25 = 1.329340388179137;   // Gamma(2.5)
+        double term = 1.0 / (std::pow(2.0, 1.5) * g25), s = term;
+        for (int k = 1; k < 30; k++) {
+            term *= (modified ? 1.0 : -1.0) * (v * v / 4.0) / ((double)k * (k + 1.5));
+            s += term;
+        }
+        return s;
+    }
+    const double c = std::sqrt(2.0 / (M_PI * v)) / std::pow(v, 1.5);
+    return modified ? c * (std::cosh(v) - std::sinh(v) / v) : c * (std::sin(v) / v - std::cos(v));
+}
+
+double mkb_rl_r2(double r2, double a, double alpha)
+{
+    const double u2 = std::pow(2 * M_PI * a, 2) * r2;
+    const bool in = u2 <= alpha * alpha;
+    const double v = std::sqrt(in ? alpha * alpha - u2 : u2 - alpha * alpha);
+    return std::pow(2 * M_PI, 1.5) * a * a * a / bessel_i0(alpha) * nu15_over(v, in);
+}
+
+struct Plans {
+    hipfftHandle c2r = 0, r2c = 0, r2cN = 0;
+    ~Plans()
+    {
+        if (c2r) hipfftDestroy(c2r);
+        if (r2c) hipfftDestroy(r2c);
+        if (r2cN) hipfftDestroy(r2cN);
+    }
+};
+
+int make_plans(Plans& p, int vdim, int N, bool wantFT, size_t* work)
+{
+    size_t w1 = 0, w2 = 0, w3 = 0;
+    THX_FFT(hipfftCreate(&p.c2r));
+    THX_FFT(hipfftSetAutoAllocation(p.c2r, 0));
+    THX_FFT(hipfftMakePlan3d(p.c2r, vdim, vdim, vdim, HIPFFT_C2R, &w1));
+    THX_FFT(hipfftCreate(&p.r2c));
+    THX_FFT(hipfftSetAutoAllocation(p.r2c, 0));
+    THX_FFT(hipfftMakePlan3d(p.r2c, vdim, vdim, vdim, HIPFFT_R2C, &w2));
+    if (wantFT) {
+        THX_FFT(hipfftCreate(&p.r2cN));
+        THX_FFT(hipfftSetAutoAllocation(p.r2cN, 0));
+        THX_FFT(hipfftMakePlan3d(p.r2cN, N, N, N, HIPFFT_R2C, &w3));
+    }
+    *work = std::max(w1, std::max(w2, w3));
+    return THX_OK;
+}
+
+}  // namespace
+
+extern "C" size_t thx_reconstruct_workspace(int N, int pf)
+{
+    if (N <= 0 || pf <= 0) return 0;
+    const int vdim = N * pf;
+    Plans p;
+    size_t work = 0;
+    if (make_plans(p, vdim, N, true, &work) != THX_OK) return 0;
+    thx::Carver k(nullptr, ~size_t(0));
+    const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
+    k.take<float>(dimSize);                       // W
+    k.take<float2>(dimSize);                      // C / pad
+    k.take<float>((size_t)vdim * vdim * vdim);    // real space
+    k.take<float>(TAB_N + 1);                     // kernel table
+    k.take<unsigned>(64);                         // diff
+    k.take<char>(work);                           // hipFFT work area
+    return k.off + 256;
+}
+
+extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a, float alpha,
+                               int gridCorr, int maxRadius, int map, const double* fsc, int nFsc,
+                               int joinHalf, float* dst, float* dstFT, int* nIter, float* diffOut,
+                               void* workspace, size_t wsBytes, thx_stream_t stream)
+{
+    THX_CHECK_ARG(F && T && dst && N > 0 && N % 2 == 0 && pf > 0 && a > 0 && alpha > 0,
+                  "thx_reconstruct: bad arguments");
+    THX_CHECK_ARG(!map || (fsc && nFsc > 0), "thx_reconstruct: MAP needs the FSC");
+    const int vdim = N * pf;
+    const int maxR = maxRadius > 0 ? maxRadius : N / 2 - (int)std::ceil(a);   // Reconstructor::init
+    THX_CHECK_ARG(maxR > 0 && maxR <= N / 2, "thx_reconstruct: bad maxRadius");
+    const size_t need = thx_reconstruct_workspace(N, pf);
+    THX_CHECK_ARG(need > 0 && workspace && wsBytes >= need, "thx_reconstruct: workspace too small");
+    hipStream_t s = thx::as_stream(stream);
+    Plans pl;
+    size_t work = 0;
+    {
+        const int st = make_plans(pl, vdim, N, dstFT != nullptr, &work);
+        if (st != THX_OK) return st;
+    }
+    const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
+    thx::Carver k(workspace, wsBytes);
+    float* W = k.take<float>(dimSize);
+    float2* C = k.take<float2>(dimSize);
+    float* rl = k.take<float>((size_t)vdim * vdim * vdim);
+    float* tab = k.take<float>(TAB_N + 1);
+    unsigned* diff = k.take<unsigned>(64);
+    void* fftWork = k.take<char>(work);
+    THX_FFT(hipfftSetWorkArea(pl.c2r, fftWork));
+    THX_FFT(hipfftSetWorkArea(pl.r2c, fftWork));
+    THX_FFT(hipfftSetStream(pl.c2r, s));
+    THX_FFT(hipfftSetStream(pl.r2c, s));
+    if (dstFT) {
+        THX_FFT(hipfftSetWorkArea(pl.r2cN, fftWork));
+        THX_FFT(hipfftSetStream(pl.r2cN, s));
+    }
+    // the tabulated real-space kernel (float, as the reference's RFLOAT table)
+    std::vector<float> htab(TAB_N + 1);
+    for (int t = 0; t <= TAB_N; t++) htab[t] = (float)mkb_rl_r2(t * 1e-5, a, alpha);
+    const float nf = (float)mkb_rl_r2(0.0, a, alpha);   // MKB_RL(0, a, alpha)
+    THX_HIP(hipMemcpyAsync(tab, htab.data(), sizeof(float) * (TAB_N + 1), hipMemcpyHostToDevice, s));
+    THX_HIP(hipStreamSynchronize(s));   // htab leaves scope after this call
+
+    const long r2 = (long)maxR * pf * maxR * pf;
+    const long nFT = (long)dimSize;
+    const float scaleBw = 1.f / ((float)vdim * vdim * vdim);
+    const dim3 g(4096), b(256);
+    if (map) {
+        hipLaunchKernelGGL(k_wiener, g, b, 0, s, T, vdim, pf, maxR, fsc, nFsc, joinHalf);
+        THX_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k_init_w, g, b, 0, s, W, T, vdim, r2);
+    THX_LAUNCH_CHECK();
+    int m = 0;
+    float diffC = 0.f;
+    if (gridCorr) {
+        float diffPrev = 3.4e38f;
+        diffC = 3.4e38f;
+        int nNoDec = 0;
+        for (m = 0; m < 30; m++) {                                // MAX_N_ITER_BALANCE
+            hipLaunchKernelGGL(k_c_from_tw, g, b, 0, s, C, T, W, nFT);
+            THX_LAUNCH_CHECK();
+            THX_FFT(hipfftExecC2R(pl.c2r, reinterpret_cast<hipfftComplex*>(C), rl));
+            hipLaunchKernelGGL(k_kernel_mul, g, b, 0, s, rl, vdim, tab, nf, scaleBw);
+            THX_LAUNCH_CHECK();
+            THX_FFT(hipfftExecR2C(pl.r2c, rl, reinterpret_cast<hipfftComplex*>(C)));
+            THX_HIP(hipMemsetAsync(diff, 0, sizeof(unsigned), s));
+            hipLaunchKernelGGL(k_update_w, g, b, 0, s, W, C, vdim, r2, diff);
+            THX_LAUNCH_CHECK();
+            unsigned bits = 0;
+            THX_HIP(hipMemcpyAsync(&bits, diff, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+            THX_HIP(hipStreamSynchronize(s));
+            diffPrev = diffC;
+            diffC = __builtin_bit_cast(float, bits);
+            if (diffOut) diffOut[m] = diffC;
+            if (diffC > diffPrev * 0.95f) nNoDec += 1;            // DIFF_C_DECREASE_THRES
+            else nNoDec = 0;
+            if (diffC < 1e-2f || (m >= 10 && nNoDec == 2)) {       // DIFF_C_THRES, MIN_N_ITER, N_DIFF_C_NO_DECREASE
+                m++;
+                break;
+            }
+        }
+    } else {
+        hipLaunchKernelGGL(k_w_from_t, g, b, 0, s, W, T, vdim, r2);
+        THX_LAUNCH_CHECK();
+    }
+    if (nIter) *nIter = m;
+    // F W -> real space -> central box, kernel-corrected
+    hipLaunchKernelGGL(k_pad, g, b, 0, s, C, reinterpret_cast<const float2*>(F), W, vdim, r2);
+    THX_LAUNCH_CHECK();
+    THX_FFT(hipfftExecC2R(pl.c2r, reinterpret_cast<hipfftComplex*>(C), rl));
+    hipLaunchKernelGGL(k_extract, g, b, 0, s, dst, rl, N, vdim, scaleBw);
+    THX_LAUNCH_CHECK();
+    if (dstFT) {
+        // the map's transform for the FSC (fft.fw(ref), src/Optimiser.cpp:7379)
+        THX_FFT(hipfftExecR2C(pl.r2cN, dst, reinterpret_cast<hipfftComplex*>(dstFT)));
+    }
+    // plans (and their stream binding) are destroyed on return: finish first
+    THX_HIP(hipStreamSynchronize(s));
+    return THX_OK;
+}

@@ -354,6 +354,32 @@ class RcclComm:
             self.comm = ctypes.c_void_p()
 
 
+# ------------------------------------------------------------------- f1
+def reconstruct(hm, N, pf=2, a=1.9, alpha=15.0, grid_corr=True, max_radius=0, fsc=None,
+                join_half=False, want_ft=True):
+    """thx_reconstruct: the reconstruction solve of half-map hm (F, T at box
+    pf N; T is modified in place).  Returns (map [N, N, N] real space, origin
+    at [0, 0, 0], map_ft [N, N, N/2+1] complex or None, iterations, diffs)."""
+    vdim = pf * N
+    if hm.vdim != vdim:
+        raise ValueError("half-map box != pf N")
+    dev = hm.F.device
+    dst = torch.empty(N, N, N, dtype=torch.float32, device=dev)
+    dft = torch.empty(N, N, N // 2 + 1, dtype=torch.complex64, device=dev) if want_ft else None
+    n_it = ctypes.c_int(0)
+    diffs = (ctypes.c_float * 32)()
+    fs = None
+    if fsc is not None:
+        fs = torch.as_tensor(np.ascontiguousarray(fsc), dtype=torch.float64, device=dev)
+    ws = workspace(lib().thx_reconstruct_workspace(N, pf), dev)
+    check(lib().thx_reconstruct(_ptr(hm.F), _ptr(hm.T), N, pf, a, alpha, int(bool(grid_corr)),
+                                max_radius, int(fs is not None), _ptr(fs),
+                                0 if fs is None else fs.numel(), int(bool(join_half)), _ptr(dst),
+                                _ptr(dft), ctypes.byref(n_it), diffs, _ptr(ws), ws.numel(),
+                                _stream(dev)), "thx_reconstruct")
+    return dst, dft, n_it.value, [diffs[k] for k in range(n_it.value)]
+
+
 # ------------------------------------------------------------------ a14
 def fsc(A, B, n_shell):
     vdim = _vol_dim(A)

@@ -13,5 +13,5 @@ while [ $# -gt 1 ]; do
     objs+=($o)
   done
   wait
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 ${objs[@]} -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrccl -o $R/thunder_amd/ab/lib_$name.so
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 ${objs[@]} -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrccl -lhipfft -o $R/thunder_amd/ab/lib_$name.so
 done
