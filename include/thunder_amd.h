@@ -312,6 +312,39 @@ int thx_rccl_comm_destroy(void* comm);
 int thx_halfmap_allreduce(void* comm, float* F, float* T, double* O, int* counter,
                           long long dimSize, int nK, thx_stream_t stream);
 
+/* ------------------------------------------------------------------ f4 ---
+ * The 2D classification path (MODE_2D).  2D projectees / half-maps are
+ * half-complex images [vdim][vdim/2+1]; a 2D rotation is (cos, sin) (the
+ * particle's (_r(i,0), _r(i,1)) -> rotate2D, src/Geometry/Euler.cpp:125-131).
+ * thx_project2d -- Projector::project(Complex*, const dmat22&, ...)
+ *   (src/Projector.cpp:337-354; kernel_Project2D, gpu/src/Kernel.cu:786):
+ *   rotP[r][i] = bilinear(vol, R_r (iCol pf, iRow pf)).  rot: nR x 2.
+ * thx_local_phase2d -- one particle-filter phase of the 2D branch of
+ *   src/Optimiser.cpp:1183-1402 for a batch (per image mR rotations [nImg][mR][2],
+ *   mT translations, priors as thx_local_phase; cls (device, may be NULL):
+ *   image l projects class cls[l] of the nK images at vol); direct likelihood,
+ *   per-image marginals; dvp optional (else workspace >=
+ *   thx_local_phase2d_workspace).
+ * thx_insert2d -- the 2D insert (Reconstructor::insertP, src/Reconstructor.cpp:
+ *   708-781; kernel_InsertF2D / T2D / O2D, gpu/src/Kernel.cu:2276-2500): F, T
+ *   hold nK class half-maps back to back, O nK x 2, counter nK; rot / trans:
+ *   nImg x mReco x 2; nc (may be NULL = class 0): nImg x mReco class of each
+ *   sample. */
+int thx_project2d(const float* vol, int vdim, int pf, const double* rot, int nR,
+                  const int* iCol, const int* iRow, int nPxl, float* rotP,
+                  thx_stream_t stream);
+size_t thx_local_phase2d_workspace(int nImg, int nR, int nT);
+int thx_local_phase2d(const float* vol, int vdim, int pf, const int* cls, const double* rot,
+                      int nR, const double* trans, int nT, const double* pC, const double* pR,
+                      const double* pT, const float* dat, const float* ctf, const float* sigRcp,
+                      const int* iCol, const int* iRow, int nPxl, int idim, int nImg, float* wC,
+                      float* wR, float* wT, float* baseL, float* dvp, void* workspace,
+                      size_t wsBytes, thx_stream_t stream);
+int thx_insert2d(float* F, float* T, double* O, int* counter, int vdim, int pf,
+                 const float* dat, const float* ctf, const double* rot, const double* trans,
+                 const double* offS, const float* w, const int* nc, int nImg, int mReco,
+                 const int* iCol, const int* iRow, int nPxl, int idim, thx_stream_t stream);
+
 /* ------------------------------------------------------------------ f1 ---
  * The reconstruction solve of one half-map, Reconstructor::reconstruct
  * (src/Reconstructor.cpp:1129-1831; GPU twin reconstructG :1835), 3D,
@@ -502,6 +535,26 @@ int thx_ExpectLocalHostF(int gpuIdx, float** wC, float** wR, float** wT, float**
 int thx_ExpectLocalFin(int gpuIdx, float** devdatP, float** devctfP, float** devdefO,
                        float** devfreQ, float** devsigP, int cSearch);            /* :153 */
 int thx_ExpectFreeIdx(int gpuIdx, int** deviCol, int** deviRow);                /* :161 */
+
+/* gpu/interface/Interface.h:176-197 ExpectGlobal2D: the global scan of all
+ * nK 2D classes (vol: nK half-complex images) over the shared rotations
+ * rot[nR*2] (cos, sin) and translations trans[nT*2]; outputs as
+ * thx_ExpectGlobal3D with the running baseline across classes kept inside. */
+int thx_ExpectGlobal2D(const float* vol, const float* datP, const float* ctfP,
+                       const float* sigRcpP, const double* trans, float* wC, float* wR,
+                       float* wT, const double* pR, const double* pT, const double* rot,
+                       const int* iCol, const int* iRow, int nK, int nR, int nT, int pf,
+                       int interp, int idim, int vdim, int npxl, int imgNum);
+
+/* gpu/interface/Interface.h:239-265 InsertI2D (no CTF search): F2D[nk
+ * images], T2D, O2D[nk*2], counter[nk] read-modify-write; nC[imgNum*mReco]
+ * the sample classes, nR / nT[imgNum*mReco*2] (cos, sin) / translations;
+ * iCol / iRow the padded pixel set.  The hemisphere reduction is the
+ * caller's (thx_halfmap_allreduce). */
+int thx_InsertI2D(float* F2D, float* T2D, double* O2D, int* counter, const float* datP,
+                  const float* ctfP, const float* w, const double* offS, const int* nC,
+                  const double* nR, const double* nT, const int* iCol, const int* iRow,
+                  int nk, int opf, int npxl, int mReco, int idim, int vdim, int imgNum);
 
 /* gpu/interface/Interface.h:294-318 InsertFT (K = 1, cSearch off): F3D
  * [dimSize*2], T3D[dimSize] (real), O3D[3], counter[1] are read-modify-write

@@ -65,6 +65,12 @@ def lib():
     L.orc_insert_batch.argtypes = [_f32p, _f32p, _f64p, _i64p, _c_int, _c_int, _f32p, _f32p,
                                    _f64p, _f64p, _f64p, _f32p, _c_int, _c_int, _i32p, _i32p,
                                    _c_int, _c_int]
+    L.orc_project2d.restype = None
+    L.orc_project2d.argtypes = [_f32p, _f32p, _c_int, _c_int, _f64p, _i32p, _i32p, _c_int]
+    L.orc_insert2d_batch.restype = None
+    L.orc_insert2d_batch.argtypes = [_f32p, _f32p, _f64p, _i64p, _c_int, _c_int, _f32p, _f32p,
+                                     _f64p, _f64p, _f64p, _f32p, ctypes.c_void_p, _c_int, _c_int,
+                                     _i32p, _i32p, _c_int, _c_int]
     L.orc_fsc.restype = None
     L.orc_fsc.argtypes = [_f64p, _c_int, _f32p, _f32p, _c_int]
     _lib = L
@@ -192,6 +198,30 @@ def insert_batch(vdim, pf, dat, ctf_, quat, trans, offS, w, px, idim, F=None, T=
                            _c(offS, np.float64).reshape(-1), _c(w, np.float32), nImg, mReco,
                            px.iCol, px.iRow, px.n, idim)
     return F.view(np.complex64), T, O, int(cnt[0])
+
+
+def project2d(img, vdim, pf, cs, px):
+    out = np.zeros(2 * px.n, np.float32)
+    lib().orc_project2d(out, _cf(img).reshape(-1), vdim, pf, _c(cs, np.float64), px.iCol, px.iRow,
+                        px.n)
+    return out.view(np.complex64)
+
+
+def insert2d_batch(vdim, pf, dat, ctf_, rot, trans, offS, w, nc, px, idim, nK=1):
+    """rot / trans: [nImg, mReco, 2]; nc: [nImg, mReco] int32 or None."""
+    nImg, mReco = rot.shape[0], rot.shape[1]
+    size = (vdim // 2 + 1) * vdim
+    F = np.zeros(2 * size * nK, np.float32)
+    T = np.zeros(size * nK, np.float32)
+    O = np.zeros(2 * nK, np.float64)
+    cnt = np.zeros(nK, np.int64)
+    ncp = None if nc is None else np.ascontiguousarray(nc, np.int32)
+    lib().orc_insert2d_batch(F, T, O, cnt, vdim, pf, _cf(dat).reshape(-1),
+                             _c(ctf_, np.float32).reshape(-1), _c(rot, np.float64).reshape(-1),
+                             _c(trans, np.float64).reshape(-1), _c(offS, np.float64).reshape(-1),
+                             _c(w, np.float32), None if ncp is None else ncp.ctypes.data, nImg, mReco,
+                             px.iCol, px.iRow, px.n, idim)
+    return F.view(np.complex64), T, O, cnt
 
 
 def fsc(A, B, vdim, n_shell):

@@ -450,6 +450,96 @@ void orc_insert_batch(float* F, float* T, double* O, long* counter, int vdim,
     free(iRowPad);
 }
 
+/* ------------------------------------------------------------ f4 (2D) --- */
+void orc_project2d(float* dst, const float* img, int vdim, int pf, const double* cs,
+                   const int* iCol, const int* iRow, int nPxl)
+{
+    /* Projector::project(Complex*, const dmat22&, ...) (src/Projector.cpp:337-354),
+     * R = rotate2D(cs) (src/Geometry/Euler.cpp:125-131), then
+     * Image::getByInterpolationFT (src/Image/Image.cpp:345-367): conjHalf,
+     * WG_BI_INTERP_LINEAR (include/Functions/Interpolation.h:137-150), getFTHalf
+     * summing the 2 x 2 taps row by row */
+    const long nColFT = vdim / 2 + 1;
+    for (int i = 0; i < nPxl; i++) {
+        const double nx = (double)(iCol[i] * pf), ny = (double)(iRow[i] * pf);
+        float x = (float)(cs[0] * nx - cs[1] * ny);
+        float y = (float)(cs[1] * nx + cs[0] * ny);
+        int conj = 0;
+        if (!(x >= 0)) { x = -x; y = -y; conj = 1; }
+        const float fx = floorf(x), fy = floorf(y);
+        const int x0 = (int)fx, y0 = (int)fy;
+        const float dx = x - fx, dy = y - fy;
+        const float wx[2] = {1 - dx, dx}, wy[2] = {1 - dy, dy};
+        float re = 0, im = 0;
+        for (int j = 0; j < 2; j++) {
+            int yy = y0 + j;
+            if (yy < 0) yy += vdim;
+            for (int a = 0; a < 2; a++) {
+                const float w = wx[a] * wy[j];
+                const float* v = img + 2 * ((size_t)yy * nColFT + x0 + a);
+                re += v[0] * w;
+                im += v[1] * w;
+            }
+        }
+        dst[2 * i] = re;
+        dst[2 * i + 1] = conj ? -im : im;
+    }
+}
+
+void orc_insert2d_batch(float* F, float* T, double* O, long* counter, int vdim, int pf,
+                        const float* dat, const float* ctf, const double* rot,
+                        const double* trans, const double* offS, const float* w, const int* nc,
+                        int nImg, int mReco, const int* iCol, const int* iRow, int nPxl, int idim)
+{
+    /* the 2D insert of src/Optimiser.cpp:6752-6850 (samples (cls, rot, tran)
+     * from Particle::rand) -> Reconstructor::insertP(const Complex*, ...,
+     * const dmat22&, ...) (src/Reconstructor.cpp:708-781, trilinear-kernel
+     * branch = bilinear Image::addFT, src/Image/Image.cpp:369-409);
+     * insertDir(-R (t - off)) (:397-401) */
+    const long img = (long)(vdim / 2 + 1) * vdim;
+    const long nColFT = vdim / 2 + 1;
+    float* tr = (float*)malloc(sizeof(float) * 2 * nPxl);
+    for (int l = 0; l < nImg; l++)
+        for (int m = 0; m < mReco; m++) {
+            const size_t sIdx = (size_t)l * mReco + m;
+            const double* cs = rot + 2 * sIdx;
+            const int k = nc ? nc[sIdx] : 0;
+            float* Fk = F + 2 * img * k;
+            float* Tk = T + img * k;
+            const double dx = trans[2 * sIdx] - offS[2 * l], dy = trans[2 * sIdx + 1] - offS[2 * l + 1];
+            orc_translate_src(tr, dat + 2 * (size_t)l * nPxl, (float)(-dx), (float)(-dy), idim,
+                              idim, iCol, iRow, nPxl);
+            for (int i = 0; i < nPxl; i++) {
+                const double nx = (double)(iCol[i] * pf), ny = (double)(iRow[i] * pf);
+                float x = (float)(cs[0] * nx - cs[1] * ny);
+                float y = (float)(cs[1] * nx + cs[0] * ny);
+                const float c = ctf[(size_t)l * nPxl + i];
+                float vr = tr[2 * i] * c * w[l], vi = tr[2 * i + 1] * c * w[l];
+                const float tv = (float)((double)c * c) * w[l];
+                if (!(x >= 0)) { x = -x; y = -y; vi = -vi; }
+                const float fx = floorf(x), fy = floorf(y);
+                const int x0 = (int)fx, y0 = (int)fy;
+                const float ddx = x - fx, ddy = y - fy;
+                const float wx[2] = {1 - ddx, ddx}, wy[2] = {1 - ddy, ddy};
+                for (int j = 0; j < 2; j++) {
+                    int yy = y0 + j;
+                    if (yy < 0) yy += vdim;
+                    for (int a = 0; a < 2; a++) {
+                        const float ww = wx[a] * wy[j];
+                        const size_t q = (size_t)yy * nColFT + x0 + a;
+                        Fk[2 * q] += vr * ww;
+                        Fk[2 * q + 1] += vi * ww;
+                        Tk[q] += tv * ww;
+                    }
+                }
+            }
+            O[2 * k] += -(cs[0] * dx - cs[1] * dy);
+            O[2 * k + 1] += -(cs[1] * dx + cs[0] * dy);
+            counter[k] += 1;
+        }
+    free(tr);
+}
+
 /* --------------------------------------------------------------- a14 ---- */
 void orc_fsc(double* fsc, int nShell, const float* A, const float* B, int vdim)
 {

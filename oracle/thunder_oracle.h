@@ -131,4 +131,12 @@ void orc_fsc(double* fsc, int nShell, const float* A, const float* B,
 #ifdef __cplusplus
 }
 #endif
+/* f4 (2D): Projector::project (2D) and the 2D insert */
+void orc_project2d(float* dst, const float* img, int vdim, int pf, const double* cs,
+                   const int* iCol, const int* iRow, int nPxl);
+void orc_insert2d_batch(float* F, float* T, double* O, long* counter, int vdim, int pf,
+                        const float* dat, const float* ctf, const double* rot,
+                        const double* trans, const double* offS, const float* w, const int* nc,
+                        int nImg, int mReco, const int* iCol, const int* iRow, int nPxl, int idim);
+
 #endif

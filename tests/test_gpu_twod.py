@@ -1,0 +1,192 @@
+"""f4 on the GPU: the 2D classification path (MODE_2D) against the C
+restatement -- thx_project2d vs orc.project2d, the 2D global scan over nK
+classes (thx_ExpectGlobal2D, gpu/interface/Interface.h:176-197) vs
+orc.project2d + orc.logdatavs + orc.weights_global(kIdx, nK), one 2D
+particle-filter phase (thx_local_phase2d, the 2D branch of
+src/Optimiser.cpp:1183-1402) vs the restated direct likelihood, and the 2D
+insert with per-sample classes (thx_insert2d / thx_InsertI2D, Interface.h:
+239-265) vs orc.insert2d_batch."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from thunder_amd import ops
+from thunder_amd._lib import lib
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+vp = ctypes.c_void_p
+
+
+def T_(a):
+    return torch.as_tensor(np.ascontiguousarray(a), device=DEV)
+
+
+def P(a):
+    return a.ctypes.data_as(vp)
+
+
+def _classes(nK, N, pf, seed):
+    """nK half-complex class images [nK, vdim, vdim/2+1] (smooth blobs)."""
+    vdim = N * pf
+    rng = np.random.default_rng(seed)
+    out = np.empty((nK, vdim, vdim // 2 + 1), np.complex64)
+    yy, xx = np.mgrid[:vdim, :vdim] - vdim // 2
+    for k in range(nK):
+        img = np.zeros((vdim, vdim))
+        for _ in range(5):
+            cx, cy = rng.uniform(-N / 4, N / 4, 2)
+            img += rng.uniform(0.5, 1.5) * np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * rng.uniform(2, 5) ** 2))
+        out[k] = np.fft.rfft2(np.fft.ifftshift(img)) / vdim
+    return out
+
+
+def _rot(th):
+    return np.stack([np.cos(th), np.sin(th)], -1)
+
+
+def _stack(orc, N=32, pf=2, rU=12, nImg=6, nK=3, seed=0):
+    vdim = N * pf
+    px = orc.pixel_set(N, pf, rU, 1)
+    cl = _classes(nK, N, pf, seed)
+    rng = np.random.default_rng(seed + 1)
+    k = rng.integers(0, nK, nImg)
+    th = rng.uniform(0, 2 * np.pi, nImg)
+    t = rng.standard_normal((nImg, 2))
+    dat = np.stack([orc.project2d(cl[k[l]], vdim, pf, _rot(th[l]), px) * orc.translate(px, *t[l], N)
+                    for l in range(nImg)])
+    dat = (dat + 0.3 * (rng.standard_normal(dat.shape) + 1j * rng.standard_normal(dat.shape))
+           ).astype(np.complex64)
+    ctf = rng.uniform(0.3, 1.0, (nImg, px.n)).astype(np.float32)
+    sig = rng.uniform(0.5, 2.0, (nImg, px.n)).astype(np.float32)
+    return dict(N=N, pf=pf, vdim=vdim, px=px, cl=cl, dat=dat, ctf=ctf, sig=sig, k=k, th=th, t=t,
+                gpx=ops.PixelSet(N, pf, rU, 1, device=DEV), rng=rng)
+
+
+def test_project2d_matches_restatement(orc):
+    s = _stack(orc)
+    th = s["rng"].uniform(0, 2 * np.pi, 37)
+    got = ops.project2d(T_(s["cl"][1]), T_(_rot(th)), s["gpx"]).cpu().numpy()
+    ref = np.stack([orc.project2d(s["cl"][1], s["vdim"], s["pf"], _rot(a), s["px"]) for a in th])
+    assert np.max(np.abs(got - ref)) <= 1e-5 * np.abs(ref).max()
+
+
+def test_expect_global2d_matches_restatement(orc):
+    s = _stack(orc, nImg=4, nK=3)
+    N, pf, vdim, px = s["N"], s["pf"], s["vdim"], s["px"]
+    nK, nR, nT, nImg = 3, 24, 9, 4
+    rot = _rot(np.arange(nR) * 2 * np.pi / nR)
+    g = np.linspace(-1.5, 1.5, 3)
+    trans = np.stack(np.meshgrid(g, g, indexing="ij"), -1).reshape(-1, 2)
+    pR = np.full(nR, 1.0 / nR)
+    pT = np.full(nT, 1.0 / nT)
+    state = None
+    dvps = []
+    for k in range(nK):
+        dvp = np.empty((nImg, nR, nT), np.float32)
+        for r in range(nR):
+            pri = orc.project2d(s["cl"][k], vdim, pf, rot[r], px)
+            for t in range(nT):
+                pt = (orc.translate(px, *trans[t], N) * pri).astype(np.complex64)
+                for l in range(nImg):
+                    dvp[l, r, t] = orc.logdatavs(s["dat"][l], pt, s["ctf"][l], s["sig"][l])
+        dvps.append(dvp)
+        state = orc.weights_global(dvp, pR, pT, k, nK, state)
+    rC, rR, rT, rb = state
+    wC = np.zeros(nImg * nK, np.float32)
+    wR = np.zeros(nImg * nK * nR, np.float32)
+    wT = np.zeros(nImg * nK * nT, np.float32)
+    cl = np.ascontiguousarray(s["cl"]).view(np.float32)
+    dat = np.ascontiguousarray(s["dat"]).view(np.float32)
+    ctf, sig = np.ascontiguousarray(s["ctf"]), np.ascontiguousarray(s["sig"])
+    rc = lib().thx_ExpectGlobal2D(P(cl), P(dat), P(ctf), P(sig), P(trans), P(wC), P(wR), P(wT),
+                                  P(pR), P(pT), P(rot), P(px.iCol), P(px.iRow), nK, nR, nT, pf, 1,
+                                  N, vdim, px.n, nImg)
+    assert rc == 0, lib().thx_last_error()
+    # the GPU scan keeps its running baseline across classes exactly like the
+    # restatement; marginals agree to the FP32 likelihood's rounding
+    best = max(float(d.max()) for d in dvps)
+    assert np.all(np.abs(rb - best) < 1e-5 * abs(best) + 1e-3)
+    for got, want in ((wC, rC), (wR, rR), (wT, rT)):
+        m = want >= 1e-4 * want.max()
+        assert np.max(np.abs(got - want)[m] / want[m]) < 2e-3
+
+
+def test_local_phase2d_matches_restatement(orc):
+    s = _stack(orc, nImg=5, nK=2, seed=4)
+    N, pf, vdim, px = s["N"], s["pf"], s["vdim"], s["px"]
+    nImg, mR, mT = 5, 20, 6
+    rng = s["rng"]
+    th = s["th"][:, None] + rng.standard_normal((nImg, mR)) * 0.05
+    rot = _rot(th)
+    trans = s["t"][:, None, :] + rng.standard_normal((nImg, mT, 2)) * 0.5
+    pC = np.full(nImg, 0.8)
+    pR = rng.uniform(0.5, 1.5, (nImg, mR))
+    pR /= pR.sum(1, keepdims=True)
+    pT = np.full((nImg, mT), 1.0 / mT)
+    cls = s["k"].astype(np.int32)
+    wC, wR, wT, base, d = ops.local_phase2d(T_(s["cl"]), T_(rot), T_(trans), T_(pC), T_(pR), T_(pT),
+                                            T_(s["dat"]), T_(s["ctf"]), T_(s["sig"]), s["gpx"],
+                                            cls=T_(cls), want_dvp=True)
+    d = d.cpu().numpy()
+    wR, wT, wC = wR.cpu().numpy(), wT.cpu().numpy(), wC.cpu().numpy()
+    for l in range(nImg):
+        ref = np.empty((mR, mT), np.float32)
+        for r in range(mR):
+            pri = orc.project2d(s["cl"][cls[l]], vdim, pf, rot[l, r], px)
+            for t in range(mT):
+                pt = (orc.translate(px, *trans[l, t], N) * pri).astype(np.complex64)
+                ref[r, t] = orc.logdatavs(s["dat"][l], pt, s["ctf"][l], s["sig"][l])
+        assert np.max(np.abs(d[l] - ref)) <= 1e-5 * np.abs(ref).max()
+        # the restatement's marginals (src/Optimiser.cpp:1302-1340, nD = 1)
+        base_l = ref.max()
+        e = np.exp((ref - base_l).astype(np.float64))
+        rR = (e * pT[l][None, :]).sum(1) * pC[l]
+        rT = (e * pR[l][:, None]).sum(0) * pC[l]
+        rC = (e * pR[l][:, None] * pT[l][None, :]).sum()
+        tol = max(1e-3, 2.5 * float(np.max(np.abs(d[l] - ref))))
+        for got, want in ((wR[l], rR), (wT[l], rT)):
+            m = want >= 1e-4 * want.max()
+            assert np.max(np.abs(got - want)[m] / want[m]) < tol
+        assert abs(wC[l] - rC) <= tol * rC
+
+
+@pytest.mark.parametrize("nK", [1, 3])
+def test_insert2d_matches_restatement(orc, nK):
+    N, pf = 32, 2
+    vdim = N * pf
+    px = orc.pixel_set(N, pf, N // 2 - 2, 0)
+    gpx = ops.PixelSet(N, pf, N // 2 - 2, 0, device=DEV)
+    rng = np.random.default_rng(7 + nK)
+    nImg, mReco = 9, 5
+    dat = (rng.standard_normal((nImg, px.n)) + 1j * rng.standard_normal((nImg, px.n))).astype(np.complex64)
+    ctf = rng.uniform(-1, 1, (nImg, px.n)).astype(np.float32)
+    rot = _rot(rng.uniform(0, 2 * np.pi, (nImg, mReco)))
+    trans = rng.standard_normal((nImg, mReco, 2))
+    off = rng.standard_normal((nImg, 2)) * 0.2
+    w = rng.uniform(0.1, 0.3, nImg).astype(np.float32)
+    nc = rng.integers(0, nK, (nImg, mReco)).astype(np.int32) if nK > 1 else None
+    F, T, O, cnt = orc.insert2d_batch(vdim, pf, dat, ctf, rot, trans, off, w, nc, px, N, nK=nK)
+    hm = ops.HalfMap2D(vdim, nK, DEV)
+    ops.insert2d(hm, T_(dat), T_(ctf), T_(rot), T_(trans), T_(off), T_(w), gpx,
+                 nc=T_(nc) if nc is not None else None)
+    gF = hm.F.cpu().numpy().reshape(-1)
+    gT = hm.T.cpu().numpy().reshape(-1)
+    assert np.max(np.abs(gF - F)) <= 1e-5 * np.abs(F).max()
+    assert np.max(np.abs(gT - T)) <= 1e-5 * np.abs(T).max()
+    assert np.allclose(hm.O.cpu().numpy().reshape(-1), O, rtol=1e-12, atol=1e-12)
+    assert np.array_equal(hm.counter.cpu().numpy(), cnt.astype(np.int32))
+    # the host adapter (InsertI2D): read-modify-write of host buffers
+    hF = np.zeros(2 * F.size, np.float32)
+    hT = np.zeros(T.size, np.float32)
+    hO = np.zeros(2 * nK)
+    hc = np.zeros(nK, np.int32)
+    ncl = nc if nc is not None else np.zeros((nImg, mReco), np.int32)
+    rc = lib().thx_InsertI2D(P(hF), P(hT), P(hO), P(hc), P(dat.view(np.float32)), P(ctf), P(w),
+                             P(off), P(ncl), P(np.ascontiguousarray(rot)), P(trans),
+                             P(px.iColPad), P(px.iRowPad), nK, pf, px.n, mReco, N, vdim, nImg)
+    assert rc == 0, lib().thx_last_error()
+    assert np.max(np.abs(hF.view(np.complex64) - F)) <= 1e-5 * np.abs(F).max()
+    assert np.array_equal(hc, cnt.astype(np.int32))

@@ -254,3 +254,132 @@ extern "C" int thx_InsertFTComm(float* F3D, float* T3D, double* O3D, int* counte
     return insert_ft(F3D, T3D, O3D, counter, datP, ctfP, offS, w, nR, nT, nC, iCol, iRow, opf,
                      npxl, mReco, idim, vdim, imgNum, comm);
 }
+
+// ---- 2D (MODE_2D) host adapters
+extern "C" int thx_ExpectGlobal2D(const float* vol, const float* datP, const float* ctfP,
+                                  const float* sigRcpP, const double* trans, float* wC, float* wR,
+                                  float* wT, const double* pR, const double* pT, const double* rot,
+                                  const int* iCol, const int* iRow, int nK, int nR, int nT, int pf,
+                                  int interp, int idim, int vdim, int npxl, int imgNum)
+{
+    THX_CHECK_ARG(vol && datP && ctfP && sigRcpP && trans && wC && wR && wT && pR && pT && rot &&
+                      iCol && iRow,
+                  "thx_ExpectGlobal2D: null");
+    THX_CHECK_ARG(interp == 1, "thx_ExpectGlobal2D: only LINEAR_INTERP (1) is supported");
+    THX_CHECK_ARG(nK >= 1 && nR > 0 && nT > 0 && npxl > 0 && imgNum >= 0 && vdim == pf * idim,
+                  "thx_ExpectGlobal2D: bad sizes");
+    if (imgNum == 0) return THX_OK;
+    const size_t img = (size_t)(vdim / 2 + 1) * vdim, nPx = (size_t)imgNum * npxl;
+    const size_t ws = thx_global_scan_workspace(imgNum, nR, nT, npxl, 1);
+    DBuf dV, dRot, dTr, dTra, dDat, dCtf, dSig, dWC, dWR, dWT, dPR, dPT, dBase, dWs, dRP, dIc, dIr;
+    THX_DALLOC(dV, sizeof(float) * 2 * img * nK);
+    THX_DALLOC(dRot, sizeof(double) * 2 * nR);
+    THX_DALLOC(dTr, sizeof(double) * 2 * nT);
+    THX_DALLOC(dTra, sizeof(float) * 2 * (size_t)nT * npxl);
+    THX_DALLOC(dRP, sizeof(float) * 2 * (size_t)nR * npxl);
+    THX_DALLOC(dDat, sizeof(float) * 2 * nPx);
+    THX_DALLOC(dCtf, sizeof(float) * nPx);
+    THX_DALLOC(dSig, sizeof(float) * nPx);
+    THX_DALLOC(dWC, sizeof(float) * (size_t)imgNum * nK);
+    THX_DALLOC(dWR, sizeof(float) * (size_t)imgNum * nK * nR);
+    THX_DALLOC(dWT, sizeof(float) * (size_t)imgNum * nK * nT);
+    THX_DALLOC(dPR, sizeof(double) * nR);
+    THX_DALLOC(dPT, sizeof(double) * nT);
+    THX_DALLOC(dBase, sizeof(float) * imgNum);
+    THX_DALLOC(dWs, ws);
+    THX_DALLOC(dIc, sizeof(int) * npxl);
+    THX_DALLOC(dIr, sizeof(int) * npxl);
+    THX_HIP(hipMemcpy(dV.p, vol, sizeof(float) * 2 * img * nK, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dRot.p, rot, sizeof(double) * 2 * nR, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dTr.p, trans, sizeof(double) * 2 * nT, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dDat.p, datP, sizeof(float) * 2 * nPx, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dSig.p, sigRcpP, sizeof(float) * nPx, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dPR.p, pR, sizeof(double) * nR, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dPT.p, pT, sizeof(double) * nT, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dIc.p, iCol, sizeof(int) * npxl, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dIr.p, iRow, sizeof(int) * npxl, hipMemcpyHostToDevice));
+    THX_RET(thx_trans_table(dTr.as<double>(), nT, dIc.as<int>(), dIr.as<int>(), npxl, idim,
+                            dTra.as<float>(), nullptr));
+    for (int k = 0; k < nK; k++) {
+        // every class against the shared samples, one running baseline (expectGlobal2D)
+        THX_RET(thx_project2d(dV.as<float>() + 2 * img * k, vdim, pf, dRot.as<double>(), nR,
+                              dIc.as<int>(), dIr.as<int>(), npxl, dRP.as<float>(), nullptr));
+        THX_RET(thx_global_scan(dRP.as<float>(), nR, dTra.as<float>(), nT, dDat.as<float>(),
+                                dCtf.as<float>(), dSig.as<float>(), imgNum, npxl, dPR.as<double>(),
+                                dPT.as<double>(), k, nK, dWC.as<float>(), dWR.as<float>(),
+                                dWT.as<float>(), dBase.as<float>(), 1, dWs.p, ws, nullptr));
+    }
+    THX_HIP(hipMemcpy(wC, dWC.p, sizeof(float) * (size_t)imgNum * nK, hipMemcpyDeviceToHost));
+    THX_HIP(hipMemcpy(wR, dWR.p, sizeof(float) * (size_t)imgNum * nK * nR, hipMemcpyDeviceToHost));
+    THX_HIP(hipMemcpy(wT, dWT.p, sizeof(float) * (size_t)imgNum * nK * nT, hipMemcpyDeviceToHost));
+    return THX_OK;
+}
+
+extern "C" int thx_InsertI2D(float* F2D, float* T2D, double* O2D, int* counter, const float* datP,
+                             const float* ctfP, const float* w, const double* offS, const int* nC,
+                             const double* nR, const double* nT, const int* iCol, const int* iRow,
+                             int nk, int opf, int npxl, int mReco, int idim, int vdim, int imgNum)
+{
+    THX_CHECK_ARG(F2D && T2D && O2D && counter && datP && ctfP && w && offS && nC && nR && nT &&
+                      iCol && iRow,
+                  "thx_InsertI2D: null");
+    THX_CHECK_ARG(nk >= 1 && opf > 0 && npxl >= 0 && mReco >= 0 && imgNum >= 0,
+                  "thx_InsertI2D: bad sizes");
+    const size_t img = (size_t)(vdim / 2 + 1) * vdim, nPx = (size_t)imgNum * npxl;
+    const size_t nS = (size_t)imgNum * mReco;
+    for (size_t q = 0; q < nS; q++)
+        THX_CHECK_ARG(nC[q] >= 0 && nC[q] < nk, "thx_InsertI2D: class index out of range");
+    DBuf dF, dT, dO, dC, dDat, dCtf, dW, dOff, dN, dR, dTr, dIc, dIr;
+    THX_DALLOC(dF, sizeof(float) * 2 * img * nk);
+    THX_DALLOC(dT, sizeof(float) * img * nk);
+    THX_DALLOC(dO, sizeof(double) * 2 * nk);
+    THX_DALLOC(dC, sizeof(int) * nk);
+    THX_DALLOC(dDat, sizeof(float) * 2 * nPx);
+    THX_DALLOC(dCtf, sizeof(float) * nPx);
+    THX_DALLOC(dW, sizeof(float) * imgNum);
+    THX_DALLOC(dOff, sizeof(double) * 2 * imgNum);
+    THX_DALLOC(dN, sizeof(int) * nS);
+    THX_DALLOC(dR, sizeof(double) * 2 * nS);
+    THX_DALLOC(dTr, sizeof(double) * 2 * nS);
+    THX_DALLOC(dIc, sizeof(int) * npxl);
+    THX_DALLOC(dIr, sizeof(int) * npxl);
+    THX_HIP(hipMemcpy(dF.p, F2D, sizeof(float) * 2 * img * nk, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dT.p, T2D, sizeof(float) * img * nk, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dO.p, O2D, sizeof(double) * 2 * nk, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dC.p, counter, sizeof(int) * nk, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dDat.p, datP, sizeof(float) * 2 * nPx, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dW.p, w, sizeof(float) * imgNum, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dOff.p, offS, sizeof(double) * 2 * imgNum, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dN.p, nC, sizeof(int) * nS, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dR.p, nR, sizeof(double) * 2 * nS, hipMemcpyHostToDevice));
+    THX_HIP(hipMemcpy(dTr.p, nT, sizeof(double) * 2 * nS, hipMemcpyHostToDevice));
+    {
+        // the padded pixel set (_iColPad, src/Optimiser.cpp:6823) -> unpadded + opf
+        std::vector<int> uc(npxl), ur(npxl);
+        for (int i = 0; i < npxl; i++) {
+            THX_CHECK_ARG(iCol[i] % opf == 0 && iRow[i] % opf == 0,
+                          "thx_InsertI2D: iCol/iRow must be the padded (x opf) pixel set");
+            uc[i] = iCol[i] / opf;
+            ur[i] = iRow[i] / opf;
+        }
+        THX_HIP(hipMemcpy(dIc.p, uc.data(), sizeof(int) * npxl, hipMemcpyHostToDevice));
+        THX_HIP(hipMemcpy(dIr.p, ur.data(), sizeof(int) * npxl, hipMemcpyHostToDevice));
+    }
+    for (int l0 = 0; l0 < imgNum; l0 += 65535) {
+        const int nb = imgNum - l0 < 65535 ? imgNum - l0 : 65535;
+        THX_RET(thx_insert2d(dF.as<float>(), dT.as<float>(), dO.as<double>(), dC.as<int>(), vdim,
+                             opf, dDat.as<float>() + 2 * (size_t)l0 * npxl,
+                             dCtf.as<float>() + (size_t)l0 * npxl,
+                             dR.as<double>() + 2 * (size_t)l0 * mReco,
+                             dTr.as<double>() + 2 * (size_t)l0 * mReco, dOff.as<double>() + 2 * l0,
+                             dW.as<float>() + l0, dN.as<int>() + (size_t)l0 * mReco, nb, mReco,
+                             dIc.as<int>(), dIr.as<int>(), npxl, idim, nullptr));
+    }
+    THX_HIP(hipMemcpy(F2D, dF.p, sizeof(float) * 2 * img * nk, hipMemcpyDeviceToHost));
+    THX_HIP(hipMemcpy(T2D, dT.p, sizeof(float) * img * nk, hipMemcpyDeviceToHost));
+    THX_HIP(hipMemcpy(O2D, dO.p, sizeof(double) * 2 * nk, hipMemcpyDeviceToHost));
+    THX_HIP(hipMemcpy(counter, dC.p, sizeof(int) * nk, hipMemcpyDeviceToHost));
+    return THX_OK;
+}

@@ -756,6 +756,17 @@ namespace thx {
 
 size_t patch_rec_bytes(int nImg, int nR, int nVisit) { return rec_bytes(nImg, nR, nVisit); }
 
+// the per-image normalisation of a materialised dvp (also the 2D phase's)
+int launch_local_weights(const float* dvp, int nR, int nT, const double* pC, const double* pR,
+                         const double* pT, float* wC, float* wR, float* wT, float* baseL, int nImg,
+                         hipStream_t s)
+{
+    hipLaunchKernelGGL(k_local_weights, dim3(nImg), dim3(256), 0, s, dvp, nR, nT, pC, pR, pT, wC,
+                       wR, wT, baseL, nullptr, nullptr);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 int launch_patch_boxes(const double* quat, int nR, const int* iCol, const int* iRow,
                        const int* order, int nVisit, int pf, int vdim, int nImg, int* rec,
                        hipStream_t s)

@@ -354,6 +354,94 @@ class RcclComm:
             self.comm = ctypes.c_void_p()
 
 
+# ------------------------------------------------------------------- f4
+def _img2d_dim(vol):
+    if vol.dim() not in (2, 3) or vol.shape[-1] != vol.shape[-2] // 2 + 1:
+        raise ValueError(f"2D projectee: expected [(nK,) vdim, vdim/2+1], got {tuple(vol.shape)}")
+    _req(vol, torch.complex64, None, "vol")
+    return vol.shape[-2]
+
+
+def project2d(vol, rot, px):
+    """thx_project2d: vol [vdim, vdim/2+1] complex64, rot [nR, 2] (cos, sin)."""
+    vdim = _img2d_dim(vol)
+    if px.rU * px.pf >= vdim // 2 - 1:
+        raise ValueError("pixel radius * pf reaches the image edge")
+    nR = rot.shape[0]
+    _req(rot, torch.float64, (nR, 2), "rot")
+    out = torch.empty(nR, px.n, dtype=torch.complex64, device=vol.device)
+    check(lib().thx_project2d(_ptr(vol), vdim, px.pf, _ptr(rot), nR, _ptr(px.d_iCol),
+                              _ptr(px.d_iRow), px.n, _ptr(out), _stream(vol.device)), "thx_project2d")
+    return out
+
+
+def local_phase2d(vol, rot, trans, pC, pR, pT, dat, ctf_, sig, px, cls=None, want_dvp=False):
+    """thx_local_phase2d: vol [(nK,) vdim, vdim/2+1]; rot [nImg, mR, 2]; cls int32 [nImg]."""
+    vdim = _img2d_dim(vol)
+    nImg, nPxl = _images(dat, ctf_, sig)
+    nR, nT = rot.shape[1], trans.shape[1]
+    dev = dat.device
+    _req(rot, torch.float64, (nImg, nR, 2), "rot")
+    _req(trans, torch.float64, (nImg, nT, 2), "trans")
+    for name, t, shp in (("pC", pC, (nImg,)), ("pR", pR, (nImg, nR)), ("pT", pT, (nImg, nT))):
+        _req(t, torch.float64, shp, name)
+    if cls is not None:
+        _req(cls, torch.int32, (nImg,), "cls")
+        if vol.dim() != 3:
+            raise ValueError("cls needs [nK, vdim, vdim/2+1] projectees")
+    wC = torch.empty(nImg, dtype=torch.float32, device=dev)
+    wR = torch.empty(nImg, nR, dtype=torch.float32, device=dev)
+    wT = torch.empty(nImg, nT, dtype=torch.float32, device=dev)
+    base = torch.empty(nImg, dtype=torch.float32, device=dev)
+    d = torch.empty(nImg, nR, nT, dtype=torch.float32, device=dev) if want_dvp else None
+    ws = workspace(lib().thx_local_phase2d_workspace(nImg, nR, nT), dev)
+    check(lib().thx_local_phase2d(_ptr(vol), vdim, px.pf, _ptr(cls), _ptr(rot), nR, _ptr(trans), nT,
+                                  _ptr(pC), _ptr(pR), _ptr(pT), _ptr(dat), _ptr(ctf_), _ptr(sig),
+                                  _ptr(px.d_iCol), _ptr(px.d_iRow), nPxl, px.idim, nImg, _ptr(wC),
+                                  _ptr(wR), _ptr(wT), _ptr(base), _ptr(d), _ptr(ws), ws.numel(),
+                                  _stream(dev)), "thx_local_phase2d")
+    return wC, wR, wT, base, d
+
+
+class HalfMap2D:
+    """Device F / T / O / counter of nK 2D class reconstructors (padded box vdim)."""
+
+    def __init__(self, vdim, nK, device):
+        self.vdim, self.nK = vdim, nK
+        self.F = torch.zeros(nK, vdim, vdim // 2 + 1, dtype=torch.complex64, device=device)
+        self.T = torch.zeros(nK, vdim, vdim // 2 + 1, dtype=torch.float32, device=device)
+        self.O = torch.zeros(nK, 2, dtype=torch.float64, device=device)
+        self.counter = torch.zeros(nK, dtype=torch.int32, device=device)
+
+
+def insert2d(hm, dat, ctf_, rot, trans, offS, w, px, nc=None):
+    """thx_insert2d: rot / trans [nImg, mReco, 2], nc int32 [nImg, mReco] (classes)."""
+    nImg, nPxl = dat.shape
+    _req(dat, torch.complex64, (nImg, nPxl), "dat")
+    _req(ctf_, torch.float32, (nImg, nPxl), "ctf")
+    mReco = rot.shape[1]
+    _req(rot, torch.float64, (nImg, mReco, 2), "rot")
+    _req(trans, torch.float64, (nImg, mReco, 2), "trans")
+    _req(offS, torch.float64, (nImg, 2), "offS")
+    _req(w, torch.float32, (nImg,), "w")
+    if nc is not None:
+        _req(nc, torch.int32, (nImg, mReco), "nc")
+        if int(nc.min()) < 0 or int(nc.max()) >= hm.nK:
+            raise ValueError("class index out of range")
+    if px.rU * px.pf >= hm.vdim // 2 - 1:
+        raise ValueError("pixel radius * pf reaches the image edge")
+    dev = dat.device
+    for l0 in range(0, nImg, 65535):
+        nb = min(65535, nImg - l0)
+        check(lib().thx_insert2d(_ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim,
+                                 px.pf, _ptr(dat[l0:]), _ptr(ctf_[l0:]), _ptr(rot[l0:]),
+                                 _ptr(trans[l0:]), _ptr(offS[l0:]), _ptr(w[l0:]),
+                                 _ptr(nc[l0:]) if nc is not None else None, nb, mReco,
+                                 _ptr(px.d_iCol), _ptr(px.d_iRow), nPxl, px.idim, _stream(dev)),
+              "thx_insert2d")
+    return hm
+
+
 # ------------------------------------------------------------------- f1
 def reconstruct(hm, N, pf=2, a=1.9, alpha=15.0, grid_corr=True, max_radius=0, fsc=None,
                 join_half=False, want_ft=True):

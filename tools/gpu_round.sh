@@ -20,7 +20,11 @@ for s in $steps; do
     prof)
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
           -d $O/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline \
-          > $O/prof.json 2> $O/prof.err) ;;
+          --no-extras > $O/prof.json 2> $O/prof.err)
+      # the same command with the secondary kernels (scan / full-res / insert)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d $O/prof_extras -o run -- python3 $R/bench.py --steps 1 --warmup 0 \
+          --no-cpu-baseline > $O/prof_extras.json 2> $O/prof_extras.err) ;;
     pmc)
       # HBM bytes: FETCH_SIZE and WRITE_SIZE need separate passes (TCC slots)
       i=0
