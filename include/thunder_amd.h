@@ -293,6 +293,25 @@ int thx_insert3d_tiled(float* F, float* T, double* O, int* counter, int vdim,
                        int nOrd, int nPxl, int idim, void* workspace,
                        size_t wsBytes, thx_stream_t stream);
 
+/* Same insert as a binned deposition (the default of the host front end):
+ * samples of an image with bitwise-identical quaternions are merged (their
+ * taps coincide), every (group, pixel) entry is binned to a 16^3 tile of the
+ * half-map, and each tile is summed in LDS and flushed once per chunk of
+ * entries.  rMax: bound on the pixel radius sqrt(iCol^2 + iRow^2) (rU of the
+ * pixel set; pixels beyond it are still inserted, by direct atomics).
+ * Requires mReco <= 1024 and (pf rMax + 2) <= vdim/2 - 1; the tile grid
+ * (2 pf rMax / 16)^2 (pf rMax / 16) must stay within 16384 tiles.  Values and
+ * coordinates as thx_insert3d; the FP32 summation order differs.
+ * workspace: >= thx_insert3d_binned_workspace bytes (entries of at most
+ * 2^28 per image batch, 24 B each). */
+size_t thx_insert3d_binned_workspace(int nImg, int mReco, int nOrd, int pf, int rMax);
+int thx_insert3d_binned(float* F, float* T, double* O, int* counter, int vdim, int pf,
+                        const float* dat, const float* ctf, const double* quat,
+                        const double* trans, const double* offS, const float* w,
+                        const int* nC, int nImg, int mReco, const int* iCol, const int* iRow,
+                        const int* pxOrder, int nOrd, int nPxl, int idim, int rMax,
+                        void* workspace, size_t wsBytes, thx_stream_t stream);
+
 /* ----------------------------------------------------------------- a13 ---
  * The per-hemisphere half-map reduction of cuthunder::InsertFT
  * (gpu/src/cuthunder.cu:5294-5324 communicator setup, :5903-5993 the

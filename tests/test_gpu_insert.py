@@ -55,15 +55,15 @@ def _oracle_truncated(orc, s, quat, trans, off, w, nC):
     return F.view(np.complex64), Tm, O, cnt
 
 
-@pytest.mark.parametrize("tiled", [False, True])
-def test_insert_with_per_image_counts(orc, stack, tiled):
+@pytest.mark.parametrize("method", ["direct", "tiled", "binned"])
+def test_insert_with_per_image_counts(orc, stack, method):
     s = stack
     nImg, mReco = 6, 140                   # two 128-sample tiles per image
     nC = np.array([0, 5, 140, 129, 1, 77], np.int32)
     quat, trans, off, w = _samples(nImg, mReco, 31)
     px = ops.PixelSet(s["N"], s["pf"], s["rU"], s["rL"], device=DEV)
     hm = ops.HalfMap(s["vdim"], DEV)
-    ops.insert3d(hm, T(s["dat"]), T(s["ctf"]), T(quat), T(trans), T(off), T(w), px, tiled=tiled,
+    ops.insert3d(hm, T(s["dat"]), T(s["ctf"]), T(quat), T(trans), T(off), T(w), px, method=method,
                  nC=T(nC))
     F, Tm, O, cnt = _oracle_truncated(orc, s, quat, trans, off, w, nC)
     gF = hm.F.cpu().numpy().reshape(-1)

@@ -274,12 +274,16 @@ def test_resample_bit_exact(orc):
             assert imax[l] == ri
 
 
-@pytest.mark.parametrize("tiled,spread,mReco", [(False, 0.0, 6), (True, 0.0, 6), (True, 2.0, 100),
-                                                (True, 8.0, 150)])
-def test_insert3d(orc, stack, tiled, spread, mReco):
-    """spread 0: uniform samples (patch boxes overflow -> direct scatter);
-    spread 2 deg: a posterior cloud, every patch accumulated in LDS;
-    mReco 150 > 128: two sample tiles per image."""
+@pytest.mark.parametrize("method,spread,mReco,dup", [
+    ("direct", 0.0, 6, False), ("tiled", 0.0, 6, False), ("tiled", 2.0, 100, False),
+    ("tiled", 8.0, 150, False), ("binned", 0.0, 6, False), ("binned", 2.0, 100, False),
+    ("binned", 8.0, 150, False), ("binned", 2.0, 100, True), ("tiled", 2.0, 100, True)])
+def test_insert3d(orc, stack, method, spread, mReco, dup):
+    """spread 0: uniform samples (patch boxes overflow -> direct scatter;
+    binned: entries spread over every tile); spread 2 deg: a posterior cloud,
+    every patch accumulated in LDS; mReco 150 > 128: two sample tiles per
+    image; dup: resampled-like samples, copies of 12 ancestors with their own
+    translations (the binned insert merges each ancestor's copies)."""
     s = stack
     px = dev_pixels(s)
     nImg = 4
@@ -288,12 +292,15 @@ def test_insert3d(orc, stack, tiled, spread, mReco):
         quat = synth.clustered_quaternions(nImg, mReco, spread, rng)
     else:
         quat = synth.uniform_quaternions(nImg * mReco, rng).reshape(nImg, mReco, 4)
+    if dup:
+        anc = rng.integers(0, 12, (nImg, mReco))
+        quat = np.ascontiguousarray(np.take_along_axis(quat, anc[..., None], axis=1))
     trans = rng.standard_normal((nImg, mReco, 2)) * 3
     off = rng.standard_normal((nImg, 2))
     w = np.full(nImg, 1.0 / mReco, np.float32)
     hm = ops.HalfMap(s["vdim"], DEV)
     ops.insert3d(hm, T(s["dat"][:nImg]), T(s["ctf"][:nImg]), T(quat), T(trans), T(off), T(w), px,
-                 tiled=tiled)
+                 method=method)
     F, Tm, O, cnt = orc.insert_batch(s["vdim"], s["pf"], s["dat"][:nImg], s["ctf"][:nImg], quat,
                                      trans, off, w, s["px"], s["N"])
     gF = hm.F.cpu().numpy().reshape(-1)

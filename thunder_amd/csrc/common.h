@@ -168,3 +168,33 @@ THX_DEV void quat_to_mat(const double* q, double* m)
         }
 }
 
+// Trilinear scatter of Volume::addFT (src/Image/Volume.cpp:340-375):
+// Hermitian fold conjugates the complex value, 8 taps in box order, FP32
+// device-scope atomics (global_atomic_add_f32) on F (re, im) and T.
+THX_DEV void scatter_ft(float2* __restrict__ F, float* __restrict__ T, int vdim,
+                        float x, float y, float z, float vr, float vi, float tv)
+{
+    if (!(x >= 0.f)) { x = -x; y = -y; z = -z; vi = -vi; }
+    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+    const float dx = x - fx, dy = y - fy, dz = z - fz;
+    const float vx[2] = {1.f - dx, dx};
+    const float vy[2] = {1.f - dy, dy};
+    const float vz[2] = {1.f - dz, dz};
+    const int nColFT = vdim / 2 + 1;
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const size_t row = ((size_t)wrap_idx(z0 + k, vdim) * vdim +
+                                wrap_idx(y0 + j, vdim)) * nColFT + x0;
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const float w = vx[i] * vy[j] * vz[k];
+                float* f = reinterpret_cast<float*>(F + row + i);
+                atomicAdd(f, vr * w);
+                atomicAdd(f + 1, vi * w);
+                atomicAdd(T + row + i, tv * w);
+            }
+        }
+}

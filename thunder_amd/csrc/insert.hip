@@ -7,37 +7,6 @@
 #include "common.h"
 #include "patch.h"
 
-// Trilinear scatter of Volume::addFT (src/Image/Volume.cpp:340-375):
-// Hermitian fold conjugates the complex value, 8 taps in box order, FP32
-// device-scope atomics (global_atomic_add_f32) on F (re, im) and T.
-THX_DEV void scatter_ft(float2* __restrict__ F, float* __restrict__ T, int vdim,
-                        float x, float y, float z, float vr, float vi, float tv)
-{
-    if (!(x >= 0.f)) { x = -x; y = -y; z = -z; vi = -vi; }
-    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
-    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
-    const float dx = x - fx, dy = y - fy, dz = z - fz;
-    const float vx[2] = {1.f - dx, dx};
-    const float vy[2] = {1.f - dy, dy};
-    const float vz[2] = {1.f - dz, dz};
-    const int nColFT = vdim / 2 + 1;
-#pragma unroll
-    for (int k = 0; k < 2; k++)
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const size_t row = ((size_t)wrap_idx(z0 + k, vdim) * vdim +
-                                wrap_idx(y0 + j, vdim)) * nColFT + x0;
-#pragma unroll
-            for (int i = 0; i < 2; i++) {
-                const float w = vx[i] * vy[j] * vz[k];
-                float* f = reinterpret_cast<float*>(F + row + i);
-                atomicAdd(f, vr * w);
-                atomicAdd(f + 1, vi * w);
-                atomicAdd(T + row + i, tv * w);
-            }
-        }
-}
-
 // Workgroup = (pixel slice, sample m, image l).  The rotation comes from the
 // sample's quaternion (rotate3D), the image is re-centred by -(t - off)
 // (translate(dst, src, ...), src/Image/ImageFunctions.cpp:471-492), and the
@@ -283,6 +252,9 @@ __global__ void __launch_bounds__(INS_THREADS) k_insert_patches(float2* __restri
                     for (int ix = 0; ix < 2; ix++) {
                         const float wt = wx[ix] * wy[jy] * wz[kz];
                         const int v = a + kz * sp + jy * nx + ix;
+#ifdef THX_INS_NOACC      // diagnostic builds only (tools/diag_insert.py)
+                        if (wt != 12345.f) continue;
+#endif
                         atomicAdd(&sF[v].x, vr * wt);
                         atomicAdd(&sF[v].y, vi * wt);
                         atomicAdd(&sT[v], tv * wt);
@@ -291,6 +263,9 @@ __global__ void __launch_bounds__(INS_THREADS) k_insert_patches(float2* __restri
         }
         __syncthreads();
         // flush: one box row per wave pass, lanes over the row's floats
+#ifdef THX_INS_NOFLUSH    // diagnostic builds only (tools/diag_insert.py)
+        continue;
+#endif
         const int rowsSide = zn * ny;
         const int rows0 = nv0 > 0 ? rowsSide : 0, rows = rows0 + (nv1 > 0 ? rowsSide : 0);
         for (int row = wv; row < rows; row += INS_WAVES) {

@@ -6,6 +6,7 @@ Every function validates shapes / dtypes / devices on the host before a kernel
 is enqueued (a mis-shaped launch must never reach the GPU).
 """
 import ctypes
+import math
 
 import numpy as np
 import torch
@@ -266,10 +267,23 @@ class HalfMap:
         self.counter = torch.zeros(1, dtype=torch.int32, device=device)
 
 
-def insert3d(hm, dat, ctf_, quat, trans, offS, w, px, tiled=True, nC=None):
-    """tiled: LDS-accumulated patches (thx_insert3d_tiled) instead of one
-    memory-side atomic per tap (thx_insert3d).  nC: optional int32 [nImg],
-    image l inserts only its first nC[l] samples (the K-class InsertFT call)."""
+def insert_method(hm, mReco, px):
+    """The insert variant the front end uses: the binned deposition when its
+    limits hold (mReco <= 1024, tile grid <= 16384 tiles), else LDS patches."""
+    rMax = int(math.ceil(px.rU))
+    R = px.pf * rMax + 2
+    nt = ((R + 15) // 16) * ((2 * R + 15) // 16) ** 2
+    if mReco <= 1024 and nt <= 16384 and R <= hm.vdim // 2 - 1:
+        return "binned"
+    return "tiled"
+
+
+def insert3d(hm, dat, ctf_, quat, trans, offS, w, px, tiled=True, nC=None, method=None):
+    """method: "binned" (thx_insert3d_binned), "tiled" (LDS patches,
+    thx_insert3d_tiled) or "direct" (one memory-side atomic per tap,
+    thx_insert3d); default: binned where its limits hold, else tiled;
+    tiled=False selects direct.  nC: optional int32 [nImg], image l inserts
+    only its first nC[l] samples (the K-class InsertFT call)."""
     nImg, nPxl = dat.shape
     _req(dat, torch.complex64, (nImg, nPxl), "dat")
     _req(ctf_, torch.float32, (nImg, nPxl), "ctf")
@@ -284,13 +298,28 @@ def insert3d(hm, dat, ctf_, quat, trans, offS, w, px, tiled=True, nC=None):
         raise ValueError("pixel set / image size mismatch")
     if px.rU * px.pf >= hm.vdim // 2 - 1:
         raise ValueError("pixel radius * pf reaches the volume edge")
+    if method is None:
+        method = insert_method(hm, mReco, px) if tiled else "direct"
     dev = dat.device
-    if tiled:
+    if method == "binned":
+        rMax = int(math.ceil(px.rU))
+        ws = workspace(lib().thx_insert3d_binned_workspace(nImg, mReco, len(px.order), px.pf, rMax),
+                       dev)
+        check(lib().thx_insert3d_binned(
+            _ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim, px.pf, _ptr(dat),
+            _ptr(ctf_), _ptr(quat), _ptr(trans), _ptr(offS), _ptr(w),
+            _ptr(nC) if nC is not None else None, nImg, mReco, _ptr(px.d_iCol), _ptr(px.d_iRow),
+            _ptr(px.d_order), len(px.order), nPxl, px.idim, rMax, _ptr(ws), ws.numel(),
+            _stream(dev)), "thx_insert3d_binned")
+        return hm
+    if method == "tiled":
         ws = workspace(lib().thx_insert3d_workspace(min(nImg, 65535), mReco, len(px.order)), dev)
+    elif method != "direct":
+        raise ValueError(f"unknown insert method {method!r}")
     for l0 in range(0, nImg, 65535):
         nb = min(65535, nImg - l0)
         nCp = _ptr(nC[l0:]) if nC is not None else None
-        if tiled:
+        if method == "tiled":
             check(lib().thx_insert3d_tiled(
                 _ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim, px.pf,
                 _ptr(dat[l0:]), _ptr(ctf_[l0:]), _ptr(quat[l0:]), _ptr(trans[l0:]), _ptr(offS[l0:]),
