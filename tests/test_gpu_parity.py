@@ -311,6 +311,28 @@ def test_insert3d(orc, stack, method, spread, mReco, dup):
     assert int(hm.counter.item()) == cnt == nImg * mReco
 
 
+@pytest.mark.parametrize("scale", [1e-6, 1e6])
+def test_insert3d_binned_value_scale(orc, stack, scale):
+    """The binned deposit accumulates in 64-bit fixed point scaled by the
+    batch's largest |value|: data far from unit magnitude keep the 1e-5 bar."""
+    s = stack
+    px = dev_pixels(s)
+    nImg, mReco = 4, 50
+    rng = np.random.default_rng(5)
+    quat = synth.clustered_quaternions(nImg, mReco, 3.0, rng)
+    trans = rng.standard_normal((nImg, mReco, 2))
+    off = np.zeros((nImg, 2))
+    w = np.full(nImg, 1.0 / mReco, np.float32)
+    dat = (s["dat"][:nImg] * scale).astype(np.complex64)
+    hm = ops.HalfMap(s["vdim"], DEV)
+    ops.insert3d(hm, T(dat), T(s["ctf"][:nImg]), T(quat), T(trans), T(off), T(w), px, method="binned")
+    F, Tm, O, cnt = orc.insert_batch(s["vdim"], s["pf"], dat, s["ctf"][:nImg], quat, trans, off, w,
+                                     s["px"], s["N"])
+    gF = hm.F.cpu().numpy().reshape(-1)
+    assert np.max(np.abs(gF - F)) <= 1e-5 * np.max(np.abs(F))
+    assert np.max(np.abs(hm.T.cpu().numpy().reshape(-1) - Tm)) <= 1e-5 * np.max(np.abs(Tm))
+
+
 def test_fsc(orc):
     vdim = 48
     rng = np.random.default_rng(7)

@@ -23,8 +23,18 @@
 //      the entries (folded x, y, z; value sum over the group's members;
 //      ctf^2 w |group|) with wave-aggregated slots.
 //   5. k_bin_deposit  per chunk: the tile's 17^3 voxels (corners + the +1 tap
-//      halo) in LDS, 8 taps x 3 ds_add_f32 per entry, then one row-contiguous
-//      global float add per non-zero voxel component.
+//      halo) in LDS as 64-bit fixed point, 8 taps x 3 ds_add_u64 per entry,
+//      then one row-contiguous global float add per non-zero voxel component.
+// LDS float atomics are the wrong tool on gfx950: ds_add_f32 retires one
+// wave-instruction per ~193 CU cycles whatever the address pattern, while
+// ds_add_u64 takes 7-12 (tools/probes/lds_atomic.hip,
+// profiles/r02_lds_atomic.jsonl).  The fixed point is exact: k_bin_pass<true>
+// records the batch's largest |value|, and the deposit scales by 2^e with
+// |value * weight * 2^e| < 2^47, so <= 2^15 entries of a chunk sum without
+// overflow and the tap products (the float products of the float path) are
+// rounded once, at 2^-48 of the largest value; the tile sums are exact and
+// independent of order.  Non-finite values take a float-atomic path so NaN /
+// Inf propagate as in the reference.
 // Entries live in the caller's workspace; images are processed in batches
 // so the entry buffer stays bounded (thx_insert3d_binned_workspace).
 // The F / T values and coordinates are those of k_insert3d (same FP64
@@ -38,12 +48,13 @@ namespace {
 
 constexpr int BT = 16;                    // tile edge in cell corners
 constexpr int BH = BT + 1;                // + the taps' +1 halo
-constexpr int BVOX = BH * BH * BH;        // 4913 voxels, 59 KB of LDS (F + T)
+constexpr int BVOX = BH * BH * BH;        // 4913 voxels
 constexpr int BIN_E = 32768;              // entries per deposit chunk
 constexpr int BIN_MAXM = 1024;            // samples per image the grouping handles
 constexpr int BIN_MAX_TILES = 16384;      // LDS histogram (64 KB)
 constexpr long BIN_ENT_CAP = 1L << 28;    // entries per batch (6 GiB)
-constexpr int G_THREADS = 128, C_THREADS = 256, D_THREADS = 512;
+constexpr int G_THREADS = 128, C_THREADS = 256, D_THREADS = 1024;
+constexpr size_t DEP_LDS = 3 * BVOX * sizeof(unsigned long long);   // 118 KB: one workgroup per CU
 
 struct Entry {                            // 24 B: folded coordinate + values
     float x, y, z, vr, vi, tv;
@@ -205,6 +216,7 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
                                                         int* __restrict__ count,
                                                         int* __restrict__ cursor,
                                                         Entry* __restrict__ ent,
+                                                        unsigned* __restrict__ vmaxBits,
                                                         float2* __restrict__ F,
                                                         float* __restrict__ T)
 {
@@ -249,6 +261,7 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
     const float* C = ctf + (size_t)l * nPxl;
     const float2* ms = mShift + (size_t)b * mReco;
     const float wl = w[l];
+    float vmax = 0.f;
     for (long e0 = 0; e0 < nE; e0 += C_THREADS) {
         const long e = e0 + tid;
         int t = -1;
@@ -277,6 +290,8 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
                 en.vr = vr;
                 en.vi = cj ? -vi : vi;
                 en.tv = ((float)((double)c * c) * wl) * (float)(s1 - s0);
+                vmax = fmaxf(vmax, fmaxf(fabsf(en.vr), fmaxf(fabsf(en.vi), fabsf(en.tv))));
+                if (!(fabsf(en.vr) + fabsf(en.vi) + fabsf(en.tv) <= 3.4e38f)) vmax = INFINITY;
                 t = G.tile((int)floorf(en.x), (int)floorf(en.y), (int)floorf(en.z));
             }
         }
@@ -288,6 +303,9 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
             scatter_ft(F, T, vdim, en.x, en.y, en.z, en.vr, en.vi, en.tv);
         }
     }
+    // the batch's largest |value| (non-negative float bits order like uints)
+    vmax = wave_max(vmax);
+    if ((tid & 63) == 0 && vmax > 0.f) atomicMax(vmaxBits, __float_as_uint(vmax));
 }
 
 // 3. tile offsets, cursors and deposit chunks (one workgroup)
@@ -329,10 +347,10 @@ __global__ void __launch_bounds__(1024) k_bin_scan(const int* __restrict__ count
         if (tid == 1023) { carryE += sA[1023]; carryC += sB[1023]; }
         __syncthreads();
     }
-    if (tid == 0) { ctl[0] = min(carryC, maxChunks); ctl[1] = (int)carryE; }
+    if (tid == 0) { ctl[0] = min(carryC, maxChunks); ctl[1] = (int)carryE; ctl[2] = 0; }
 }
 
-// 5. one chunk of one tile: LDS accumulation, row-contiguous flush
+// 5. one chunk of one tile: 64-bit fixed-point LDS accumulation, row-contiguous flush
 __global__ void __launch_bounds__(D_THREADS) k_bin_deposit(TileGrid G, int vdim,
                                                            const int4* __restrict__ chunks,
                                                            const int* __restrict__ ctl,
@@ -340,15 +358,28 @@ __global__ void __launch_bounds__(D_THREADS) k_bin_deposit(TileGrid G, int vdim,
                                                            float* __restrict__ F,
                                                            float* __restrict__ T)
 {
-    __shared__ float sF[2 * BVOX];
-    __shared__ float sT[BVOX];
+    extern __shared__ unsigned long long sQ[];      // [voxel][re, im, T]
     const int c = blockIdx.x, tid = threadIdx.x;
     if (c >= ctl[0]) return;
     const int4 ch = chunks[c];
     const int t = ch.x;
     const int tx = t % G.ntx, ty = (t / G.ntx) % G.nty, tz = t / (G.ntx * G.nty);
     const int ox = tx * BT, oy = ty * BT - G.R, oz = tz * BT - G.R;
-    for (int v = tid; v < BVOX; v += D_THREADS) { sF[2 * v] = 0.f; sF[2 * v + 1] = 0.f; sT[v] = 0.f; }
+    const int nColFT = vdim / 2 + 1;
+    const float vmax = __uint_as_float((unsigned)ctl[2]);
+    if (!(vmax <= 3.4e38f)) {
+        // non-finite values: float atomics straight to HBM (NaN / Inf propagate)
+        for (int i = tid; i < ch.z; i += D_THREADS) {
+            const Entry e = ent[(size_t)ch.y + i];
+            scatter_ft(reinterpret_cast<float2*>(F), T, vdim, e.x, e.y, e.z, e.vr, e.vi, e.tv);
+        }
+        return;
+    }
+    // 2^e with vmax * 2^e < 2^47 (frexp: vmax = m 2^k, m in [0.5, 1))
+    int k = 0;
+    if (vmax > 0.f) frexpf(vmax, &k);
+    const int ex = 47 - k;
+    for (int v = tid; v < 3 * BVOX; v += D_THREADS) sQ[v] = 0ull;
     __syncthreads();
     for (int i = tid; i < ch.z; i += D_THREADS) {
         const Entry e = ent[(size_t)ch.y + i];
@@ -364,24 +395,25 @@ __global__ void __launch_bounds__(D_THREADS) k_bin_deposit(TileGrid G, int vdim,
 #pragma unroll
                 for (int ix = 0; ix < 2; ix++) {
                     const float wt = wx[ix] * wy[jy] * wz[kz];
-                    const int v = a + (kz * BH + jy) * BH + ix;
-                    atomicAdd(&sF[2 * v], e.vr * wt);
-                    atomicAdd(&sF[2 * v + 1], e.vi * wt);
-                    atomicAdd(&sT[v], e.tv * wt);
+                    const int v = 3 * (a + (kz * BH + jy) * BH + ix);
+                    // the float products of the float path, scaled exactly, rounded once
+                    atomicAdd(&sQ[v], (unsigned long long)__float2ll_rn(ldexpf(e.vr * wt, ex)));
+                    atomicAdd(&sQ[v + 1], (unsigned long long)__float2ll_rn(ldexpf(e.vi * wt, ex)));
+                    atomicAdd(&sQ[v + 2], (unsigned long long)__float2ll_rn(ldexpf(e.tv * wt, ex)));
                 }
     }
     __syncthreads();
     // flush: one (z, y) row per wave pass; lanes 0..33 the row's F floats,
     // lanes 34..50 its T floats
     const int lane = tid & 63, wv = tid >> 6;
-    const int nColFT = vdim / 2 + 1;
     for (int row = wv; row < BH * BH; row += D_THREADS / 64) {
         const int z = row / BH, y = row - z * BH;
-        float v = 0.f;
+        long long q = 0;
         int xi = -1;
-        if (lane < 2 * BH) { v = sF[2 * row * BH + lane]; xi = lane >> 1; }
-        else if (lane < 3 * BH) { v = sT[row * BH + lane - 2 * BH]; xi = lane - 2 * BH; }
-        if (xi < 0 || v == 0.f || ox + xi >= nColFT) continue;
+        if (lane < 2 * BH) { xi = lane >> 1; q = (long long)sQ[3 * (row * BH + xi) + (lane & 1)]; }
+        else if (lane < 3 * BH) { xi = lane - 2 * BH; q = (long long)sQ[3 * (row * BH + xi) + 2]; }
+        if (xi < 0 || q == 0 || ox + xi >= nColFT) continue;
+        const float v = (float)ldexp((double)q, -ex);
         const int gy = wrap_idx(oy + y, vdim), gz = wrap_idx(oz + z, vdim);
         const size_t g = ((size_t)gz * vdim + gy) * nColFT + ox + xi;
         if (lane < 2 * BH) atomicAdd(F + 2 * g + (lane & 1), v);
@@ -473,6 +505,16 @@ extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, 
     THX_CHECK_ARG(cv.ok() && wsBytes >= cv.off, "thx_insert3d_binned: workspace too small");
     hipStream_t s = thx::as_stream(stream);
     const size_t hist = (size_t)P.nt * sizeof(int);
+    static bool attr = false;
+    if (!attr) {
+        THX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_deposit),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)DEP_LDS));
+        THX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_pass<false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, BIN_MAX_TILES * 4));
+        THX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_pass<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, BIN_MAX_TILES * 4));
+        attr = true;
+    }
     for (int l0 = 0; l0 < nImg; l0 += P.nB) {
         const int nb = nImg - l0 < P.nB ? nImg - l0 : P.nB;
         THX_HIP(hipMemsetAsync(count, 0, hist, s));
@@ -482,7 +524,7 @@ extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, 
         hipLaunchKernelGGL(k_bin_pass<false>, dim3(nb), dim3(C_THREADS), hist, s, P.G, vdim, pf,
                            mReco, l0, nG, gStart, gMat, mShift, iCol, iRow, pxOrder, nOrd, nPxl,
                            reinterpret_cast<const float2*>(dat), ctf, w, count, cursor, ent,
-                           reinterpret_cast<float2*>(F), T);
+                           reinterpret_cast<unsigned*>(ctl + 2), reinterpret_cast<float2*>(F), T);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, count, P.nt, cursor, chunks,
                            P.maxChunks, ctl);
@@ -490,9 +532,9 @@ extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, 
         hipLaunchKernelGGL(k_bin_pass<true>, dim3(nb), dim3(C_THREADS), hist, s, P.G, vdim, pf,
                            mReco, l0, nG, gStart, gMat, mShift, iCol, iRow, pxOrder, nOrd, nPxl,
                            reinterpret_cast<const float2*>(dat), ctf, w, count, cursor, ent,
-                           reinterpret_cast<float2*>(F), T);
+                           reinterpret_cast<unsigned*>(ctl + 2), reinterpret_cast<float2*>(F), T);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_bin_deposit, dim3(P.maxChunks), dim3(D_THREADS), 0, s, P.G, vdim,
+        hipLaunchKernelGGL(k_bin_deposit, dim3(P.maxChunks), dim3(D_THREADS), DEP_LDS, s, P.G, vdim,
                            chunks, ctl, ent, F, T);
         THX_LAUNCH_CHECK();
     }
