@@ -198,3 +198,12 @@ THX_DEV void scatter_ft(float2* __restrict__ F, float* __restrict__ T, int vdim,
             }
         }
 }
+
+// 2^56 fixed point for LDS sums of a few values in [0, 8): ds_add_u64 retires
+// a wave-instruction in 7-12 CU cycles where ds_add_f32 takes ~193 on gfx950
+// (tools/probes/lds_atomic.hip); the integer sum is exact and order-free.
+THX_DEV unsigned long long fx56(float v)
+{
+    return (unsigned long long)__float2ll_rn(ldexpf(v, 56));
+}
+THX_DEV float unfx56(unsigned long long q) { return (float)ldexp((double)(long long)q, -56); }

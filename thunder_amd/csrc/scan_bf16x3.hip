@@ -305,7 +305,7 @@ struct Smem {
     static constexpr int A_F2 = IMG_TILE * APITCH;         // float2
     static constexpr int P_F2 = ROT_TILE * KC;             // float2
     static constexpr int STAGE_B = NPLANE * T_H * 2 + A_F2 * 8 + P_F2 * 8;
-    static constexpr int EPI_B = (ROT_TILE * 64 * 3 + 32 * NTP) * 4;
+    static constexpr int EPI_B = ROT_TILE * 64 * 3 * 4 + 32 * NTP * 8;
     static constexpr int TOTAL_B = STAGE_B > EPI_B ? STAGE_B : EPI_B;
     static constexpr int T16 = NTP * KC * 2 * 2 / 16;      // 16-B pieces per plane
 };
@@ -475,7 +475,8 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
     float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][64]  A_l + B[l][r]
     float* sInv = sBias + ROT_TILE * 64;               // [64]           2^-e_l
     float* sMax = sInv + ROT_TILE * 64;                // [8 waves][64 rows]
-    float* sWT = sMax + ROT_TILE * 64;                 // [32][NTP]
+    // [32][NTP] 2^56 fixed point (the 8 rotations' terms lie in [0, 1])
+    unsigned long long* sWT = reinterpret_cast<unsigned long long*>(sMax + ROT_TILE * 64);
     sBias[w * 64 + lane] = Aconst[l0 + lane] + (rValid ? bias[(size_t)(l0 + lane) * nRBias + r] : 0.f);
     if (w == 0) sInv[lane] = 1.f / scale[l0 + lane];
     __syncthreads();
@@ -520,7 +521,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
 
 #pragma unroll
     for (int a = 0; a < 2; a++) {          // merge the 8 rotations, 32 image rows at a time
-        for (int x = tid; x < 32 * NTP; x += THREADS) sWT[x] = 0.f;
+        for (int x = tid; x < 32 * NTP; x += THREADS) sWT[x] = 0ull;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < 16; j++) {
@@ -531,14 +532,14 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
             for (int k = 1; k < ROT_TILE; k++) M = fmaxf(M, sMax[k * 64 + row]);
             const float sc = rValid ? expf(sMax[w * 64 + row] - M) * pRr : 0.f;
 #pragma unroll
-            for (int f = 0; f < NF; f++) atomicAdd(&sWT[m * NTP + f * 32 + n], acc[a][f][j] * sc);
+            for (int f = 0; f < NF; f++) atomicAdd(&sWT[m * NTP + f * 32 + n], fx56(acc[a][f][j] * sc));
         }
         __syncthreads();
         for (int x = tid; x < 32 * NTP; x += THREADS) {
             const int m = x / NTP, t = x % NTP;
             const int row = a * 32 + m;
             const int l = l0 + row;
-            pWT[((size_t)rb * nImgPad + l) * NTP + t] = sWT[x];
+            pWT[((size_t)rb * nImgPad + l) * NTP + t] = unfx56(sWT[x]);
             if (t == 0) {
                 float M = sMax[row];
 #pragma unroll

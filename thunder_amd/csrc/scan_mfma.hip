@@ -159,7 +159,7 @@ struct Smem {
     static constexpr int B_F = KC * IMG_TILE;
     static constexpr int STAGE_F = T_F + P_F + A_F + B_F;
     // epilogue: bias[8][32] | rmax[2][4][32] | wT[32][NTP]
-    static constexpr int EPI_F = 8 * 32 + 2 * 4 * 32 + 32 * NTP;
+    static constexpr int EPI_F = 8 * 32 + 2 * 4 * 32 + 2 * 32 * NTP;   // sWT: u64
     static constexpr int TOTAL_F = STAGE_F > EPI_F ? STAGE_F : EPI_F;
     static constexpr int T4 = T_F / 4, A4 = A_F / 4, B4 = B_F / 4;
     static constexpr int G4 = T4 + A4 + B4;          // float4 loads per stage
@@ -270,7 +270,8 @@ __global__ void __launch_bounds__(THREADS) k_scan_mfma(const float* __restrict__
     // ------------------------------------------------------------ epilogue
     float* sBias = lds;                  // [8 waves][32]
     float* sMax = sBias + 8 * 32;        // [2][4][32]
-    float* sWT = sMax + 2 * 4 * 32;      // [32][NTP]
+    // [32][NTP] 2^56 fixed point (the 4 rotations' terms lie in [0, 1])
+    unsigned long long* sWT = reinterpret_cast<unsigned long long*>(sMax + 2 * 4 * 32);
     if (kk == 0) sBias[w * 32 + n] = bsum;
     __syncthreads();
 
@@ -314,7 +315,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_mfma(const float* __restrict__
 
     // merge the 4 rotations of this block, one image half at a time
     for (int hh = 0; hh < 2; hh++) {
-        for (int x = tid; x < 32 * NTP; x += THREADS) sWT[x] = 0.f;
+        for (int x = tid; x < 32 * NTP; x += THREADS) sWT[x] = 0ull;
         __syncthreads();
         if (h == hh) {
 #pragma unroll
@@ -325,14 +326,14 @@ __global__ void __launch_bounds__(THREADS) k_scan_mfma(const float* __restrict__
                 const float sc = rValid ? expf(rmax[j] - M) * pRr : 0.f;
 #pragma unroll
                 for (int f = 0; f < NF; f++)
-                    atomicAdd(&sWT[m * NTP + f * 32 + n], acc[f][j] * sc);
+                    atomicAdd(&sWT[m * NTP + f * 32 + n], fx56(acc[f][j] * sc));
             }
         }
         __syncthreads();
         for (int x = tid; x < 32 * NTP; x += THREADS) {
             const int m = x / NTP, t = x % NTP;
             const int l = l0 + hh * 32 + m;
-            pWT[((size_t)rb * nImgPad + l) * NTP + t] = sWT[x];
+            pWT[((size_t)rb * nImgPad + l) * NTP + t] = unfx56(sWT[x]);
             if (t == 0) {
                 const float M = fmaxf(fmaxf(sMax[(hh * 4 + 0) * 32 + m], sMax[(hh * 4 + 1) * 32 + m]),
                                       fmaxf(sMax[(hh * 4 + 2) * 32 + m], sMax[(hh * 4 + 3) * 32 + m]));
