@@ -141,28 +141,66 @@ def scan_roofline(vol, px, gset, dat, ctf, sig, algo, reps=3):
     return sec, issued, algorithmic, peak
 
 
-def local_roofline(vol, N, pf, device, n_img=512, reps=3):
+def local_roofline(vol, N, pf, device, n_img=512, reps=3, spread=1.5):
     """Full-resolution particle-filter phase (nPxl = 24746 at box 256,
-    mLR = 125, mLT = 9): HBM bytes 64 * mLR * nPxl + 16 * nPxl per image-phase."""
+    mLR = 125, mLT = 9): algorithmic bytes 64 * mLR * nPxl + 16 * nPxl per
+    image-phase.  Two clouds: a local-search cloud (`spread` degrees around
+    one pose per image, the narrow clouds of a C5-style local refinement) in
+    the half-complex layout the driver uses, where the patch boxes stage the
+    taps in LDS; and uniformly random rotations (every tap a gather), in both
+    the half-complex and the cell-expanded layout."""
     rU = N // 2 - 2
     px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, 1, n_img, device, seed=17, vol=vol)
     rng = np.random.default_rng(3)
     mR, mT = 125, 9
-    quat = torch.as_tensor(synth.uniform_quaternions(n_img * mR, rng).reshape(n_img, mR, 4),
-                           device=device)
+    st = torch.cuda.current_stream(device)
     trans = torch.as_tensor(rng.standard_normal((n_img, mT, 2)), device=device)
     pC = torch.ones(n_img, dtype=torch.float64, device=device)
     pR = torch.full((n_img, mR), 1.0 / mR, dtype=torch.float64, device=device)
     pT = torch.full((n_img, mT), 1.0 / mT, dtype=torch.float64, device=device)
-    st = torch.cuda.current_stream(device)
+    qc = torch.as_tensor(np.ascontiguousarray(synth.clustered_quaternions(n_img, mR, spread, rng)),
+                         device=device)
+    qu = torch.as_tensor(synth.uniform_quaternions(n_img * mR, rng).reshape(n_img, mR, 4),
+                         device=device)
+    out = {}
+    out["clustered_ms"] = timed_events(lambda: ops.local_phase(vol, qc, trans, pC, pR, pT, dat, ctf,
+                                                               sig, px), reps, st) * 1e3
+    out["uniform_ms"] = timed_events(lambda: ops.local_phase(vol, qu, trans, pC, pR, pT, dat, ctf,
+                                                             sig, px), reps, st) * 1e3
     cells = ops.volume_cells(vol)
-    sec = timed_events(lambda: ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px,
-                                               cells=cells), reps, st)
-    sec_plain = timed_events(lambda: ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig,
-                                                     px), reps, st)
+    out["uniform_cells_ms"] = timed_events(lambda: ops.local_phase(vol, qu, trans, pC, pR, pT, dat,
+                                                                   ctf, sig, px, cells=cells),
+                                           reps, st) * 1e3
     del cells
-    algo_bytes = n_img * (64.0 * mR * px.n + 16.0 * px.n)
-    return sec, algo_bytes, px.n, sec_plain
+    out["algo_bytes"] = n_img * (64.0 * mR * px.n + 16.0 * px.n)
+    out["nPxl"] = px.n
+    out["spread_deg"] = spread
+    out["n_img"] = n_img
+    return out
+
+
+def insert_fullres(vol, N, pf, device, n_img=256, m_reco=100, spread=1.5):
+    """Full-resolution insert (nPxl = 24746 at box 256) of mReco samples per
+    image drawn from 125-particle clouds (Particle::rand: uniform draws, so
+    copies of one particle repeat); algorithmic bytes 192 mReco nPxl per image
+    (8 taps x 3 floats x 8 B read-modify-write)."""
+    rU = N // 2 - 2
+    px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, 1, n_img, device, seed=19, vol=vol)
+    rng = np.random.default_rng(4)
+    q = torch.as_tensor(np.ascontiguousarray(synth.clustered_quaternions(n_img, 125, spread, rng)),
+                        device=device)
+    t = torch.as_tensor(rng.standard_normal((n_img, 9, 2)), device=device)
+    iq, it = ex.draw_insert_samples(q, t, m_reco)
+    off = torch.zeros(n_img, 2, dtype=torch.float64, device=device)
+    w = torch.full((n_img,), 1.0 / m_reco, dtype=torch.float32, device=device)
+    hm = ops.HalfMap(N * pf, device)
+    st = torch.cuda.current_stream(device)
+    sec = timed_events(lambda: ops.insert3d(hm, dat, ctf, iq, it, off, w, px), 2, st)
+    algo = 192.0 * m_reco * px.n * n_img
+    return {"images": n_img, "mReco": m_reco, "nPxl": px.n, "ms": sec * 1e3,
+            "images_per_s": n_img / sec, "algorithmic_bytes": algo,
+            "algorithmic_TBps": algo / sec / 1e12, "method": ops.insert_method(hm, m_reco, px),
+            "note": "clouds of 125 particles at %.1f deg, mReco uniform draws" % spread}
 
 
 def cpu_info():
@@ -376,18 +414,25 @@ def main():
             del e1, o1
 
         # ---- secondary: the north-star full-resolution phase against HBM
-        lsec, lbytes, lnpx, lsec_plain = local_roofline(vol, N, pf, dev)
+        lr = local_roofline(vol, N, pf, dev)
         tr, tr_src = launch_traffic("local_fullres_512", N == 256)
-        extras["roofline_local"] = {"bound": "hbm", "achieved": lbytes / lsec / 1e9,
-                                    "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                    "frac": lbytes / lsec / 1e9 / PEAK_HBM_GBS, "traffic": tr,
-                                    "traffic_unit": "bytes per launch (HBM, PMC)",
-                                    "traffic_source": tr_src,
-                                    "algorithmic_bytes": lbytes,
-                                    "kernel": f"local phase full-res (nPxl={lnpx}, 125x9, 512 "
-                                              "images, cell-expanded projectee)",
-                                    "launch_ms": lsec * 1e3,
-                                    "launch_ms_halfcomplex_layout": lsec_plain * 1e3}
+        lbytes = lr["algo_bytes"]
+        lsec = lr["clustered_ms"] / 1e3
+        extras["roofline_local"] = {
+            "bound": "hbm", "achieved": lbytes / lsec / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": lbytes / lsec / 1e9 / PEAK_HBM_GBS, "traffic": tr,
+            "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
+            "algorithmic_bytes": lbytes,
+            "kernel": f"local phase full-res (nPxl={lr['nPxl']}, 125x9, {lr['n_img']} images), "
+                      f"{lr['spread_deg']} deg local-search clouds, half-complex projectee "
+                      f"(the driver's layout), taps staged in LDS patch boxes",
+            "launch_ms": lr["clustered_ms"],
+            "uniform_rotations": {
+                "launch_ms_halfcomplex": lr["uniform_ms"],
+                "frac_halfcomplex": lbytes / (lr["uniform_ms"] / 1e3) / 1e9 / PEAK_HBM_GBS,
+                "launch_ms_cells": lr["uniform_cells_ms"],
+                "frac_cells": lbytes / (lr["uniform_cells_ms"] / 1e3) / 1e9 / PEAK_HBM_GBS}}
+        extras["insert_fullres"] = insert_fullres(vol, N, pf, dev)
 
         # ---- insert (mReco = 100) into the two hemispheres' half-maps, the
         # per-hemisphere RCCL all-reduce, FSC between the half-maps

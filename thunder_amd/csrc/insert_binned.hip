@@ -15,13 +15,13 @@
 //      at the bench's median) form one group -- the taps depend only on the
 //      rotation, so a group deposits sum_m src_m once.  Also insertDir /
 //      counter (src/Reconstructor.cpp:407-422).
-//   2. k_bin_count    per image: folded cell corner of every (group, pixel)
-//      -> tile of 16^3 corners, per-workgroup LDS histogram, one global add
-//      per (workgroup, tile).
+//   2. k_bin_pass<false>  per (image, 2048 visiting slots): folded cell
+//      corner of every (group, pixel) -> tile of 16^3 corners, per-workgroup
+//      LDS histogram, one global add per (workgroup, tile).
 //   3. k_bin_scan     tile offsets and deposit chunks (<= BIN_E entries each).
-//   4. k_bin_fill     per image: reserve each tile's range once, then write
-//      the entries (folded x, y, z; value sum over the group's members;
-//      ctf^2 w |group|) with wave-aggregated slots.
+//   4. k_bin_pass<true>   the same workgroups: reserve each tile's range
+//      once, then write the entries (folded x, y, z; value sum over the
+//      group's members; ctf^2 w |group|) with wave-aggregated slots.
 //   5. k_bin_deposit  per chunk: the tile's 17^3 voxels (corners + the +1 tap
 //      halo) in LDS as 64-bit fixed point, 8 taps x 3 ds_add_u64 per entry,
 //      then one row-contiguous global float add per non-zero voxel component.
@@ -51,6 +51,7 @@ constexpr int BH = BT + 1;                // + the taps' +1 halo
 constexpr int BVOX = BH * BH * BH;        // 4913 voxels
 constexpr int BIN_E = 32768;              // entries per deposit chunk
 constexpr int BIN_MAXM = 1024;            // samples per image the grouping handles
+constexpr int BIN_KCH = 2048;             // visiting slots per binning workgroup
 constexpr int BIN_MAX_TILES = 16384;      // LDS histogram (64 KB)
 constexpr long BIN_ENT_CAP = 1L << 28;    // entries per batch (6 GiB)
 constexpr int G_THREADS = 128, C_THREADS = 256, D_THREADS = 1024;
@@ -228,13 +229,15 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
     const double* gm = gMat + (size_t)b * mReco * 6;
     for (int t = tid; t < nt; t += C_THREADS) sHist[t] = 0;
     __syncthreads();
-    const long nE = (long)ng * nOrd;
+    // this workgroup's visiting slots [k0, k0 + nK) of every group
+    const int k0 = blockIdx.y * BIN_KCH, nK = min(BIN_KCH, nOrd - k0);
+    const long nE = (long)ng * nK;
     // the histogram of this image's entries over the tiles
     for (long e0 = 0; e0 < nE; e0 += C_THREADS) {      // uniform trip count (wave ballots)
         const long e = e0 + tid;
         int t = -1;
         if (e < nE) {
-            const int g = (int)(e / nOrd), k = (int)(e - (long)g * nOrd);
+            const int g = (int)(e / nK), k = k0 + (int)(e - (long)g * nK);
             const int p = order[k];
             if (p >= 0) {
                 double m[6];
@@ -268,7 +271,7 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
         Entry en;
         bool live = false;
         if (e < nE) {
-            const int g = (int)(e / nOrd), k = (int)(e - (long)g * nOrd);
+            const int g = (int)(e / nK), k = k0 + (int)(e - (long)g * nK);
             const int p = order[k];
             if (p >= 0) {
                 live = true;
@@ -521,7 +524,8 @@ extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, 
         hipLaunchKernelGGL(k_bin_groups, dim3(nb), dim3(G_THREADS), 0, s, quat, trans, offS, nC,
                            mReco, l0, idim, nG, gStart, gMat, mShift, O, counter);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_bin_pass<false>, dim3(nb), dim3(C_THREADS), hist, s, P.G, vdim, pf,
+        const dim3 pg(nb, (nOrd + BIN_KCH - 1) / BIN_KCH);
+        hipLaunchKernelGGL(k_bin_pass<false>, pg, dim3(C_THREADS), hist, s, P.G, vdim, pf,
                            mReco, l0, nG, gStart, gMat, mShift, iCol, iRow, pxOrder, nOrd, nPxl,
                            reinterpret_cast<const float2*>(dat), ctf, w, count, cursor, ent,
                            reinterpret_cast<unsigned*>(ctl + 2), reinterpret_cast<float2*>(F), T);
@@ -529,7 +533,7 @@ extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, 
         hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, count, P.nt, cursor, chunks,
                            P.maxChunks, ctl);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_bin_pass<true>, dim3(nb), dim3(C_THREADS), hist, s, P.G, vdim, pf,
+        hipLaunchKernelGGL(k_bin_pass<true>, pg, dim3(C_THREADS), hist, s, P.G, vdim, pf,
                            mReco, l0, nG, gStart, gMat, mShift, iCol, iRow, pxOrder, nOrd, nPxl,
                            reinterpret_cast<const float2*>(dat), ctf, w, count, cursor, ent,
                            reinterpret_cast<unsigned*>(ctl + 2), reinterpret_cast<float2*>(F), T);

@@ -7,8 +7,11 @@ A "launch" is the whole launch sequence the bench times with HIP events
 (local_bench: the single k_local_fused<false> dispatch of a bench phase):
   scan  : k_prep_aconst .. k_scan_combine_bf of one thx_global_scan call whose
           k_scan_split grid is the 4096-image grid (bench.scan_roofline);
-  local : k_patch_boxes .. k_local_weights of one thx_local_phase call that runs
-          k_local_fused<true> (bench.local_roofline, full resolution, 512 images).
+  local : k_patch_boxes .. k_local_weights of one thx_local_phase call of
+          bench.local_roofline (full resolution, 512 images): the clustered
+          cloud in the half-complex layout (first four 512-image
+          k_local_fused<false> sequences), and the uniform cloud in the cell
+          layout (k_local_fused<true>).
 Bytes: FETCH_SIZE x 1024 x 2 (FETCH_SIZE is in KiB and reads half of a wide
 read on gfx950) + WRITE_SIZE x 1024 -- MI355X_MICROARCH.md, HBM section.
 
@@ -47,9 +50,9 @@ def groups(disp, start, end):
     return out
 
 
-def summarise(rd, wr, start, end, pick):
-    gr = [g for g in groups(rd, start, end) if pick(g)]
-    gw = [g for g in groups(wr, start, end) if pick(g)]
+def summarise(rd, wr, start, end, pick, first=None):
+    gr = [g for g in groups(rd, start, end) if pick(g)][:first]
+    gw = [g for g in groups(wr, start, end) if pick(g)][:first]
     if not gr or not gw:
         return None
     r = sum(sum(v for _, _, v in g) for g in gr) / len(gr) * 1024 * 2
@@ -81,8 +84,14 @@ def main():
         "scan_4096": summarise(rd, wr, "k_prep_aconst", "k_scan_combine_bf",
                                lambda g: any("k_scan_split" in n and gr == scan_grid
                                              for n, gr, _ in g)),
+        # bench.local_roofline: 4 clustered-cloud launches (half-complex), then
+        # 4 uniform ones, then 4 uniform in the cell-expanded layout
         "local_fullres_512": summarise(rd, wr, "k_patch_boxes", "k_local_weights",
-                                       lambda g: any("k_local_fused<true>" in n for n, _, _ in g)),
+                                       lambda g: any("k_local_fused<false>" in n and gr == 512 * 512
+                                                     for n, gr, _ in g), first=4),
+        "local_fullres_512_uniform_cells": summarise(rd, wr, "k_patch_boxes", "k_local_weights",
+                                                     lambda g: any("k_local_fused<true>" in n
+                                                                   for n, _, _ in g)),
         # the bench step's dominant kernel: one k_local_fused<false> launch per
         # phase over the whole 12 500-image batch (grid 12500 x 1 x 1 of 512)
         "local_bench": single(rd, wr, "k_local_fused<false>", 12500 * 512),
