@@ -483,6 +483,9 @@ def main():
             extras["fsc_ms"] = (time.perf_counter() - t1) * 1e3
             # f1: reconstruct both half-maps (grid-corrected solve, hipFFT at
             # box pf N), FSC of the reconstructed maps
+            # (a first call makes the hipFFT plans -- kernels compiled at run
+            # time on a fresh box -- which stay cached for later iterations)
+            ops.reconstruct(recs[0].hm, N, pf)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             recs_out = [ops.reconstruct(r_.hm, N, pf) for r_ in recs]

@@ -1,7 +1,7 @@
 // optimiser.hip -- device-resident expectation driver (host orchestration in
 // C++ over the device kernels), the MI355X counterpart of
-// Optimiser::expectationG (src/Optimiser.cpp:1684-3403) for K = 1, 3D,
-// no CTF search:
+// Optimiser::expectationG (src/Optimiser.cpp:1684-3403) for 3D, K >= 1
+// classes, global or local search, no CTF search:
 //
 //   global scan (a4-a8) -> reseed every particle from the scan marginals
 //   (keepHalfHeightPeak, resample nR -> mLR, nT -> mLT, calVari with the scan

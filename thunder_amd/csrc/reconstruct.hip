@@ -31,6 +31,10 @@
 #include <cmath>
 #include <vector>
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "common.h"
 
 #define THX_FFT(call)                                                          \
@@ -239,15 +243,10 @@ double mkb_rl_r2(double r2, double a, double alpha)
 
 struct Plans {
     hipfftHandle c2r = 0, r2c = 0, r2cN = 0;
-    ~Plans()
-    {
-        if (c2r) hipfftDestroy(c2r);
-        if (r2c) hipfftDestroy(r2c);
-        if (r2cN) hipfftDestroy(r2cN);
-    }
+    size_t work = 0;
 };
 
-int make_plans(Plans& p, int vdim, int N, bool wantFT, size_t* work)
+int make_plans(Plans& p, int vdim, int N)
 {
     size_t w1 = 0, w2 = 0, w3 = 0;
     THX_FFT(hipfftCreate(&p.c2r));
@@ -256,12 +255,41 @@ int make_plans(Plans& p, int vdim, int N, bool wantFT, size_t* work)
     THX_FFT(hipfftCreate(&p.r2c));
     THX_FFT(hipfftSetAutoAllocation(p.r2c, 0));
     THX_FFT(hipfftMakePlan3d(p.r2c, vdim, vdim, vdim, HIPFFT_R2C, &w2));
-    if (wantFT) {
-        THX_FFT(hipfftCreate(&p.r2cN));
-        THX_FFT(hipfftSetAutoAllocation(p.r2cN, 0));
-        THX_FFT(hipfftMakePlan3d(p.r2cN, N, N, N, HIPFFT_R2C, &w3));
+    THX_FFT(hipfftCreate(&p.r2cN));
+    THX_FFT(hipfftSetAutoAllocation(p.r2cN, 0));
+    THX_FFT(hipfftMakePlan3d(p.r2cN, N, N, N, HIPFFT_R2C, &w3));
+    p.work = std::max(w1, std::max(w2, w3));
+    return THX_OK;
+}
+
+// Plans per (device, vdim, N), made once: creating a 512^3 hipFFT plan costs
+// hundreds of ms, the transforms themselves ~0.6 ms.  Calls using the same
+// plans are serialised (the work area and stream are bound per call).
+struct PlanCache {
+    std::mutex mu;
+    std::map<std::tuple<int, int, int>, Plans> plans;
+};
+
+PlanCache& plan_cache()
+{
+    static PlanCache* c = new PlanCache;    // never destroyed: no teardown ordering at exit
+    return *c;
+}
+
+int cached_plans(int vdim, int N, Plans** out)
+{
+    int dev = 0;
+    THX_HIP(hipGetDevice(&dev));
+    PlanCache& c = plan_cache();
+    const auto key = std::make_tuple(dev, vdim, N);
+    auto it = c.plans.find(key);
+    if (it == c.plans.end()) {
+        Plans p;
+        const int st = make_plans(p, vdim, N);
+        if (st != THX_OK) return st;
+        it = c.plans.emplace(key, p).first;
     }
-    *work = std::max(w1, std::max(w2, w3));
+    *out = &it->second;
     return THX_OK;
 }
 
@@ -271,9 +299,13 @@ extern "C" size_t thx_reconstruct_workspace(int N, int pf)
 {
     if (N <= 0 || pf <= 0) return 0;
     const int vdim = N * pf;
-    Plans p;
     size_t work = 0;
-    if (make_plans(p, vdim, N, true, &work) != THX_OK) return 0;
+    {
+        std::lock_guard<std::mutex> lk(plan_cache().mu);
+        Plans* p = nullptr;
+        if (cached_plans(vdim, N, &p) != THX_OK) return 0;
+        work = p->work;
+    }
     thx::Carver k(nullptr, ~size_t(0));
     const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
     k.take<float>(dimSize);                       // W
@@ -299,12 +331,14 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
     const size_t need = thx_reconstruct_workspace(N, pf);
     THX_CHECK_ARG(need > 0 && workspace && wsBytes >= need, "thx_reconstruct: workspace too small");
     hipStream_t s = thx::as_stream(stream);
-    Plans pl;
-    size_t work = 0;
+    std::lock_guard<std::mutex> lk(plan_cache().mu);
+    Plans* pp = nullptr;
     {
-        const int st = make_plans(pl, vdim, N, dstFT != nullptr, &work);
+        const int st = cached_plans(vdim, N, &pp);
         if (st != THX_OK) return st;
     }
+    Plans& pl = *pp;
+    const size_t work = pl.work;
     const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
     thx::Carver k(workspace, wsBytes);
     float* W = k.take<float>(dimSize);
@@ -322,11 +356,15 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
         THX_FFT(hipfftSetStream(pl.r2cN, s));
     }
     // the tabulated real-space kernel (float, as the reference's RFLOAT table)
-    std::vector<float> htab(TAB_N + 1);
-    for (int t = 0; t <= TAB_N; t++) htab[t] = (float)mkb_rl_r2(t * 1e-5, a, alpha);
+    // (computed once per (a, alpha) and kept: 1e5 Bessel evaluations)
+    static std::map<std::pair<float, float>, std::vector<float>> tabs;
+    std::vector<float>& htab = tabs[std::make_pair(a, alpha)];
+    if (htab.empty()) {
+        htab.resize(TAB_N + 1);
+        for (int t = 0; t <= TAB_N; t++) htab[t] = (float)mkb_rl_r2(t * 1e-5, a, alpha);
+    }
     const float nf = (float)mkb_rl_r2(0.0, a, alpha);   // MKB_RL(0, a, alpha)
     THX_HIP(hipMemcpyAsync(tab, htab.data(), sizeof(float) * (TAB_N + 1), hipMemcpyHostToDevice, s));
-    THX_HIP(hipStreamSynchronize(s));   // htab leaves scope after this call
 
     const long r2 = (long)maxR * pf * maxR * pf;
     const long nFT = (long)dimSize;
@@ -382,7 +420,7 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
         // the map's transform for the FSC (fft.fw(ref), src/Optimiser.cpp:7379)
         THX_FFT(hipfftExecR2C(pl.r2cN, dst, reinterpret_cast<hipfftComplex*>(dstFT)));
     }
-    // plans (and their stream binding) are destroyed on return: finish first
+    // the plans are shared: finish before another call rebinds their stream
     THX_HIP(hipStreamSynchronize(s));
     return THX_OK;
 }
