@@ -269,12 +269,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    # (local % device count: lets a one-GPU box rehearse the multi-rank path
+    # with THX_BENCH_BACKEND=gloo; on a node local < device count)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
+    backend = os.environ.get("THX_BENCH_BACKEND", "nccl")
+    cdev = dev if backend == "nccl" else torch.device("cpu")   # collectives' tensors
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     lib()   # fail loudly if the HIP library is missing
 
     N, pf, rU, rL = a.box, 2, 24, 1
@@ -319,7 +327,7 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        tt = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     ms_per_step = el / a.steps * 1e3
@@ -462,7 +470,7 @@ def main():
         hm_bytes = recs[0].hm.F.numel() * 8 + recs[0].hm.T.numel() * 4
         if dist:
             groups = ex.hemisphere_groups(world)
-            comm = ops.RcclComm.from_group(groups[rank % 2], dev)
+            comm = ops.RcclComm.from_group(groups[rank % 2], cdev)
             torch.cuda.synchronize()
             dist.barrier()
             t1 = time.perf_counter()
