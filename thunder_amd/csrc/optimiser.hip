@@ -143,9 +143,27 @@ THX_DEV double quad4(const double* q, const double* M)
 // point B = 4/nf sum q q^T / (q^T A^-1 q) from B = I while sum|A - B| > 1e-3
 // (a NaN criterion ends the loop, as in the reference's `while`); returns the
 // last A.  Particle q_i is read as pre q_i (pre = conj(mean) de-means).
-THX_DEV int infer_acg(const double* Q, int m, const double* pre, int lane, double* A,
-                      int maxIt = 256)
+// Clouds of up to GROUP * QREG particles keep this lane's (de-meaned)
+// particles in registers across the iterations -- the loop is a serial
+// chain, and re-reading them from L2 every iteration was its latency; the
+// arithmetic and its order are the same either way.
+constexpr int QREG = 8;
+
+template <bool REG>
+THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, double* A,
+                           int maxIt)
 {
+    double qr[REG ? QREG : 1][4];
+    if (REG) {
+#pragma unroll
+        for (int p = 0; p < QREG; p++) {
+            const int i = lane + p * GROUP;
+            if (i < m) {
+                if (pre) qmul(pre, Q + 4 * i, qr[p]);
+                else for (int k = 0; k < 4; k++) qr[p][k] = Q[4 * i + k];
+            }
+        }
+    }
     double B[16];
     for (int k = 0; k < 16; k++) B[k] = (k % 5 == 0) ? 1.0 : 0.0;
     for (int it = 0; it < maxIt; it++) {
@@ -153,15 +171,24 @@ THX_DEV int infer_acg(const double* Q, int m, const double* pre, int lane, doubl
         double Ai[16];
         inv4(A, Ai);
         double b[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nf = 0.0;
-        for (int i = lane; i < m; i += GROUP) {
-            double q[4];
-            if (pre) qmul(pre, Q + 4 * i, q);
-            else for (int k = 0; k < 4; k++) q[k] = Q[4 * i + k];
+        auto term = [&](const double* q) {
             const double r = 1.0 / quad4(q, Ai);
             int t = 0;
             for (int j = 0; j < 4; j++)
                 for (int k = j; k < 4; k++) b[t++] += q[j] * q[k] * r;
             nf += r;
+        };
+        if (REG) {
+#pragma unroll
+            for (int p = 0; p < QREG; p++)
+                if (lane + p * GROUP < m) term(qr[p]);
+        } else {
+            for (int i = lane; i < m; i += GROUP) {
+                double q[4];
+                if (pre) qmul(pre, Q + 4 * i, q);
+                else for (int k = 0; k < 4; k++) q[k] = Q[4 * i + k];
+                term(q);
+            }
         }
         for (int t = 0; t < 10; t++) b[t] = group_sum(b[t]);
         nf = group_sum(nf);
@@ -173,6 +200,13 @@ THX_DEV int infer_acg(const double* Q, int m, const double* pre, int lane, doubl
         if (!(crit > 1e-3)) return it + 1;
     }
     return maxIt;
+}
+
+THX_DEV int infer_acg(const double* Q, int m, const double* pre, int lane, double* A,
+                      int maxIt = 256)
+{
+    return m <= GROUP * QREG ? infer_acg_impl<true>(Q, m, pre, lane, A, maxIt)
+                             : infer_acg_impl<false>(Q, m, pre, lane, A, maxIt);
 }
 
 // Unit eigenvector of the largest eigenvalue of a symmetric 4x4 (cyclic
@@ -580,7 +614,8 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
     double mean[4], cm[4];
     if (meanMode == 1) {
         double A[16];
-        const int it = infer_acg(Q, mR, nullptr, lane, A, acgIters);
+        // (the register-cached variant pushes this kernel past 256 VGPRs)
+        const int it = infer_acg_impl<false>(Q, mR, nullptr, lane, A, acgIters);
         principal_axis(A, mean);
         if (itOut && lane == 0) itOut[l] = it;
     } else {
