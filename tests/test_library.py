@@ -101,3 +101,60 @@ def test_workspace_queries_are_host_only(L):
     assert L.thx_fsc_workspace(64) >= 3 * 64 * 8
     # dvp + one 64-B neighbourhood record per (image, rotation tile, patch)
     assert L.thx_local_phase_workspace(10, 125, 9, 944) >= 10 * 125 * 9 * 4 + 10 * 59 * 64
+
+
+def test_round2_entry_points_validate_without_gpu(L):
+    """Argument checks of the round-2 entry points run before any device work,
+    and empty batches return THX_OK without touching a device."""
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    ok, bad = 0, 1
+    # binned insert: rMax * pf reaching the volume edge, mReco above the grouping
+    # limit, a missing pixel order; an empty batch is a no-op
+    args = lambda vdim, mReco, rMax, order, nImg: (
+        None, None, None, None, vdim, 2, None, None, None, None, None, None, None, nImg, mReco,
+        None, None, order, 944, 870, 32, rMax, None, 0, None)
+    dummy = ctypes.c_void_p(1)
+    assert L.thx_insert3d_binned(*args(64, 100, 15, dummy, 4)) == bad
+    assert L.thx_insert3d_binned(*args(512, 2000, 24, dummy, 4)) == bad
+    assert b"mReco" in L.thx_last_error()
+    assert L.thx_insert3d_binned(*args(512, 100, 24, None, 4)) == bad
+    assert L.thx_insert3d_binned(*args(512, 100, 24, dummy, 0)) == ok
+    # its workspace: entries of at most 2^28 per image batch (24 B each)
+    ws_small = L.thx_insert3d_binned_workspace(10, 100, 944, 2, 24)
+    ws_big = L.thx_insert3d_binned_workspace(100000, 100, 944, 2, 24)
+    assert ws_small >= 10 * 100 * 944 * 24
+    assert ws_big <= (1 << 28) * 24 + (64 << 20)
+    # 2D: bad sizes, then empty batches
+    assert L.thx_project2d(None, 63, 2, None, 4, None, None, 10, None, None) == bad
+    assert L.thx_project2d(None, 64, 2, None, 0, None, None, 10, None, None) == ok
+    assert L.thx_insert2d(None, None, None, None, 64, 2, None, None, None, None, None, None, None, 0,
+                          5, None, None, 10, 32, None) == ok
+    assert L.thx_local_phase2d(None, 64, 2, None, None, 4, None, 9, None, None, None, None, None,
+                               None, None, None, 10, 32, 0, None, None, None, None, None, None, 0,
+                               None) == ok
+    # the host 2D insert rejects a sample class outside [0, nk) before allocating
+    nImg, mReco, npxl, nk = 2, 3, 4, 2
+    F = np.zeros(2 * 33 * 64 * nk, np.float32)
+    T = np.zeros(33 * 64 * nk, np.float32)
+    O = np.zeros(2 * nk)
+    cnt = np.zeros(nk, np.int32)
+    dat = np.zeros(2 * nImg * npxl, np.float32)
+    ctf = np.ones(nImg * npxl, np.float32)
+    w = np.ones(nImg, np.float32)
+    off = np.zeros(2 * nImg)
+    nc = np.array([0, 1, 2, 0, 1, 0], np.int32)          # 2 >= nk
+    rot = np.zeros(2 * nImg * mReco)
+    tr = np.zeros(2 * nImg * mReco)
+    ic = np.array([2, 4, 6, 8], np.int32)
+    ir = np.zeros(4, np.int32)
+    assert L.thx_InsertI2D(P(F), P(T), P(O), P(cnt), P(dat), P(ctf), P(w), P(off), P(nc), P(rot),
+                           P(tr), P(ic), P(ir), nk, 2, npxl, mReco, 32, 64, nImg) == bad
+    assert b"class index" in L.thx_last_error()
+    # ExpectGlobal2D supports the reference's linear interpolation only
+    assert L.thx_ExpectGlobal2D(P(F), P(dat), P(ctf), P(ctf), P(tr), P(w), P(w), P(w), P(off),
+                                P(off), P(rot), P(ic), P(ir), 1, 3, 3, 2, 0, 32, 64, npxl,
+                                nImg) == bad
+    # reconstruction and the half-map reduction reject null inputs
+    assert L.thx_reconstruct(None, None, 32, 2, 1.9, 15.0, 1, 0, 0, None, 0, 0, None, None, None,
+                             None, None, 0, None) == bad
+    assert L.thx_halfmap_allreduce(None, None, None, None, None, 10, 1, None) == bad
