@@ -589,6 +589,8 @@ __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
 //   T: t_i += pf N(0, s) (:1232-1262), reCentre beyond transM (:2473-2495),
 //      pT = 1/pdf normalised (balanceWeight(PAR_T), :2342-2375).
 // itOut (optional): inferACG iterations of the mean per image.
+constexpr int PERT_LDS_Q = 4 * 128;     // doubles per image: clouds up to 128 particles
+
 __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
                                                     double* __restrict__ quat,
                                                     double* __restrict__ trans,
@@ -603,6 +605,10 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
                                                     const int* __restrict__ done,
                                                     int* __restrict__ itOut)
 {
+    // the mean's fixed point reads this image's cloud from LDS (a serial
+    // chain of up to acgIters passes; registers would push the kernel past
+    // 256 VGPRs)
+    __shared__ double sQ[256 / GROUP][PERT_LDS_Q];
     const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
     const int lane = threadIdx.x % GROUP;
     if (l >= nImg || (done && done[l])) return;
@@ -614,8 +620,16 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
     double mean[4], cm[4];
     if (meanMode == 1) {
         double A[16];
-        // (the register-cached variant pushes this kernel past 256 VGPRs)
-        const int it = infer_acg_impl<false>(Q, mR, nullptr, lane, A, acgIters);
+        const double* src = Q;
+        if (4 * mR <= PERT_LDS_Q) {
+            double* dst = sQ[threadIdx.x / GROUP];
+            for (int k = lane; k < 4 * mR; k += GROUP) dst[k] = Q[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            src = dst;
+        }
+        const int it = infer_acg_impl<false>(src, mR, nullptr, lane, A, acgIters);
         principal_axis(A, mean);
         if (itOut && lane == 0) itOut[l] = it;
     } else {
