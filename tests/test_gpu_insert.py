@@ -122,3 +122,32 @@ def test_rccl_halfmap_allreduce_single_rank():
     for a, b in zip((hm.F, hm.T, hm.O, hm.counter), ref):
         assert torch.equal(a, b)
     comm.close()
+
+
+@pytest.mark.parametrize("rmax_div,mReco,nImg", [(2, 7, 3), (1, 1, 1)])
+def test_binned_insert_outside_tile_grid_and_single_sample(orc, stack, rmax_div, mReco, nImg):
+    """thx_insert3d_binned with an rMax below the pixel set's radius: the
+    entries past the tile grid go straight to HBM by direct atomics and the
+    result still matches the restatement; mReco = 1, one image."""
+    from thunder_amd.ops import _ptr, _stream, workspace
+    s = stack
+    quat, trans, off, w = _samples(nImg, mReco, 41)
+    px = ops.PixelSet(s["N"], s["pf"], s["rU"], s["rL"], device=DEV)
+    hm = ops.HalfMap(s["vdim"], DEV)
+    rMax = max(1, int(np.ceil(s["rU"])) // rmax_div)
+    L = lib()
+    ws = workspace(L.thx_insert3d_binned_workspace(nImg, mReco, len(px.order), s["pf"], rMax), DEV)
+    d, c = T(s["dat"][:nImg]), T(s["ctf"][:nImg])
+    q, t, o, ww = T(quat), T(trans), T(off), T(w)
+    assert L.thx_insert3d_binned(_ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim,
+                                 s["pf"], _ptr(d), _ptr(c), _ptr(q), _ptr(t), _ptr(o), _ptr(ww), None,
+                                 nImg, mReco, _ptr(px.d_iCol), _ptr(px.d_iRow), _ptr(px.d_order),
+                                 len(px.order), px.n, px.idim, rMax, _ptr(ws), ws.numel(),
+                                 _stream(DEV)) == 0, L.thx_last_error()
+    F, Tm, O, cnt = orc.insert_batch(s["vdim"], s["pf"], s["dat"][:nImg], s["ctf"][:nImg], quat,
+                                     trans, off, w, s["px"], s["N"])
+    gF = hm.F.cpu().numpy().reshape(-1)
+    gT = hm.T.cpu().numpy().reshape(-1)
+    assert np.max(np.abs(gF - F)) <= 1e-5 * np.max(np.abs(F))
+    assert np.max(np.abs(gT - Tm)) <= 1e-5 * np.max(np.abs(Tm))
+    assert int(hm.counter.item()) == cnt == nImg * mReco
