@@ -8,6 +8,8 @@
 // current HIP device: the MI355X layout is one process per GPU.
 #include <vector>
 
+#include <cmath>
+
 #include "common.h"
 
 namespace {
@@ -199,16 +201,48 @@ static int insert_ft(float* F3D, float* T3D, double* O3D, int* counter, const fl
         THX_HIP(hipMemcpy(dIc.p, uc.data(), sizeof(int) * npxl, hipMemcpyHostToDevice));
         THX_HIP(hipMemcpy(dIr.p, ur.data(), sizeof(int) * npxl, hipMemcpyHostToDevice));
     }
-    for (int l0 = 0; l0 < imgNum; l0 += 65535) {
-        const int nb = imgNum - l0 < 65535 ? imgNum - l0 : 65535;
-        THX_RET(thx_insert3d(dF.as<float>(), dT.as<float>(), dO.as<double>(), dC.as<int>(),
-                             vdim, opf, dDat.as<float>() + 2 * (size_t)l0 * npxl,
-                             dCtf.as<float>() + (size_t)l0 * npxl,
-                             dQ.as<double>() + 4 * (size_t)l0 * mReco,
-                             dTr.as<double>() + 2 * (size_t)l0 * mReco,
-                             dOff.as<double>() + 2 * (size_t)l0, dW.as<float>() + l0,
-                             nC ? dN.as<int>() + l0 : nullptr, nb, mReco, dIc.as<int>(),
-                             dIr.as<int>(), npxl, idim, nullptr));
+    // the binned deposition where its limits hold (the pixel set's radius
+    // and 4x4-patch visiting order from the host copy), else direct atomics
+    int rMax = 1;
+    std::vector<int> order(16 * (size_t)npxl + 16);
+    int nOrd = 0;
+    {
+        std::vector<int> uc(npxl), ur(npxl);
+        for (int i = 0; i < npxl; i++) {
+            uc[i] = iCol[i] / opf;
+            ur[i] = iRow[i] / opf;
+            const int r = (int)std::ceil(std::sqrt((double)uc[i] * uc[i] + (double)ur[i] * ur[i]));
+            rMax = r > rMax ? r : rMax;
+        }
+        THX_RET(thx_pixel_tile_order(uc.data(), ur.data(), npxl, (int)order.size(), order.data(),
+                                     &nOrd));
+    }
+    const size_t binWs = thx_insert3d_binned_workspace(imgNum, mReco, nOrd, opf, rMax);
+    const int R = opf * rMax + 2;
+    const long nTiles = (long)((R + 15) / 16) * ((2 * R + 15) / 16) * ((2 * R + 15) / 16);
+    if (mReco <= 1024 && R <= vdim / 2 - 1 && nTiles <= 16384 && imgNum > 0) {
+        DBuf dOrd, dWs;
+        THX_DALLOC(dOrd, sizeof(int) * nOrd);
+        THX_DALLOC(dWs, binWs);
+        THX_HIP(hipMemcpy(dOrd.p, order.data(), sizeof(int) * nOrd, hipMemcpyHostToDevice));
+        THX_RET(thx_insert3d_binned(dF.as<float>(), dT.as<float>(), dO.as<double>(), dC.as<int>(),
+                                    vdim, opf, dDat.as<float>(), dCtf.as<float>(), dQ.as<double>(),
+                                    dTr.as<double>(), dOff.as<double>(), dW.as<float>(),
+                                    nC ? dN.as<int>() : nullptr, imgNum, mReco, dIc.as<int>(),
+                                    dIr.as<int>(), dOrd.as<int>(), nOrd, npxl, idim, rMax, dWs.p,
+                                    binWs, nullptr));
+    } else {
+        for (int l0 = 0; l0 < imgNum; l0 += 65535) {
+            const int nb = imgNum - l0 < 65535 ? imgNum - l0 : 65535;
+            THX_RET(thx_insert3d(dF.as<float>(), dT.as<float>(), dO.as<double>(), dC.as<int>(),
+                                 vdim, opf, dDat.as<float>() + 2 * (size_t)l0 * npxl,
+                                 dCtf.as<float>() + (size_t)l0 * npxl,
+                                 dQ.as<double>() + 4 * (size_t)l0 * mReco,
+                                 dTr.as<double>() + 2 * (size_t)l0 * mReco,
+                                 dOff.as<double>() + 2 * (size_t)l0, dW.as<float>() + l0,
+                                 nC ? dN.as<int>() + l0 : nullptr, nb, mReco, dIc.as<int>(),
+                                 dIr.as<int>(), npxl, idim, nullptr));
+        }
     }
     // the hemisphere's all-reduce of the reference call (cuthunder.cu:5903-5993)
     if (comm) {
