@@ -77,15 +77,16 @@ Dims dims(int nImg, int nR, int nT, int nPxl)
 }
 
 struct WS {
-    float2* Ac;     // [nCk][nImgPad][KC]   a = -2 s c d (x 2^e_l for F16X2)
+    float2* Ac;     // [nCk][nImgPad][APITCH]  a = -2 s c d (x 2^e_l for F16X2), LDS image
     float* Bc;      // [nCk][nImgPad][KC]   b = s c^2
     float* Aconst;  // [nImgPad]
     float* amax;    // [nImgPad]   max_i |a.re| + |a.im|
     float* scale;   // [nImgPad]   2^e_l
     float* pmaxB;   // [PMAX_BLOCKS]
     float* bias;    // [nImgPad][nRBias]  B[l][r]
-    uint16_t* Thi;  // [nCk][nTPad][KC*2]   T split, (re, im) interleaved
+    uint16_t* Thi;  // [nCk][nTPad][TROW]   T split, (re, im) interleaved, LDS image
     uint16_t* Tlo;
+    float2* Pc;     // [nCk][nRB * ROT_TILE][KC]  projections, chunk-major
     float2* wRp;    // [nImg][nR]
     float* pM;      // [nRB][nImgPad]
     float* pWT;     // [nRB][nImgPad][nTPad]
@@ -97,15 +98,16 @@ WS carve(void* base, const Dims& d)
 {
     thx::Carver c(base, ~size_t(0));
     WS w;
-    w.Ac = c.take<float2>((size_t)d.nPxlPad * d.nImgPad);
+    w.Ac = c.take<float2>((size_t)d.nCk * d.nImgPad * APITCH);
     w.Bc = c.take<float>((size_t)d.nPxlPad * d.nImgPad);
     w.Aconst = c.take<float>(d.nImgPad);
     w.amax = c.take<float>(d.nImgPad);
     w.scale = c.take<float>(d.nImgPad);
     w.pmaxB = c.take<float>(PMAX_BLOCKS);
     w.bias = c.take<float>((size_t)d.nImgPad * d.nRBias);
-    w.Thi = c.take<uint16_t>((size_t)d.nPxlPad * d.nTPad * 2);
-    w.Tlo = c.take<uint16_t>((size_t)d.nPxlPad * d.nTPad * 2);
+    w.Thi = c.take<uint16_t>((size_t)d.nCk * d.nTPad * TROW);
+    w.Tlo = c.take<uint16_t>((size_t)d.nCk * d.nTPad * TROW);
+    w.Pc = c.take<float2>((size_t)d.nCk * d.nRB * ROT_TILE * KC);
     w.wRp = c.take<float2>((size_t)d.nImg * d.nR);
     w.pM = c.take<float>((size_t)d.nRB * d.nImgPad);
     w.pWT = c.take<float>((size_t)d.nRB * d.nImgPad * d.nTPad);
@@ -216,9 +218,23 @@ __global__ void __launch_bounds__(256) k_prep_img(const float2* __restrict__ dat
             a = make_float2((k * d.x) * sc, (k * d.y) * sc);
             b = sg * c * c;
         }
-        const size_t o = ((size_t)(i / KC) * nImgPad + l) * KC + (i % KC);
-        Ac[o] = a;
-        Bc[o] = b;
+        Ac[((size_t)(i / KC) * nImgPad + l) * APITCH + (i % KC)] = a;
+        Bc[((size_t)(i / KC) * nImgPad + l) * KC + (i % KC)] = b;
+    }
+}
+
+// P rows regrouped chunk-major so one rotation block's chunk is contiguous
+// (KC / 16 KiB; zero past nR / nPxl)
+__global__ void __launch_bounds__(256) k_prep_pchunk(const float2* __restrict__ rotP, int nR,
+                                                     int nPxl, int nRRows, int nPxlPad,
+                                                     float2* __restrict__ Pc)
+{
+    const long n = (long)nRRows * nPxlPad;
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
+         q += (long)gridDim.x * blockDim.x) {
+        const int i = (int)(q % nPxlPad), r = (int)(q / nPxlPad);
+        Pc[((size_t)(i / KC) * nRRows + r) * KC + (i % KC)] =
+            (r < nR && i < nPxl) ? rotP[(size_t)r * nPxl + i] : make_float2(0.f, 0.f);
     }
 }
 
@@ -236,7 +252,7 @@ __global__ void __launch_bounds__(256) k_prep_tsplit(const float2* __restrict__ 
          q += (long)gridDim.x * blockDim.x) {
         const int i = (int)(q % nPxlPad), t = (int)(q / nPxlPad);
         const float2 v = (t < nT && i < nPxl) ? traP[(size_t)t * nPxl + i] : make_float2(0.f, 0.f);
-        const size_t o = (((size_t)(i / KC) * nTPad + t) * KC + (i % KC)) * 2;
+        const size_t o = ((size_t)(i / KC) * nTPad + t) * TROW + (i % KC) * 2;
         H h, lo;
         split16(v.x, h, lo);
         Thi[o] = __builtin_bit_cast(uint16_t, h);
@@ -304,11 +320,32 @@ struct Smem {
     static constexpr int T_H = NTP * TROW;                 // 16-bit elements per plane
     static constexpr int A_F2 = IMG_TILE * APITCH;         // float2
     static constexpr int P_F2 = ROT_TILE * KC;             // float2
-    static constexpr int STAGE_B = NPLANE * T_H * 2 + A_F2 * 8 + P_F2 * 8;
+    // one stage = [T planes | a tile] (the global LDS images, copied by LDS-DMA
+    // in 16-B pieces, each part rounded up to whole 1-KiB wave instructions so
+    // every instruction reads one part) + the P rows; two stages
+    static constexpr int T_PC = T_H * 2 / 16;              // 16-B pieces per plane
+    static constexpr int A_PC = A_F2 * 8 / 16;
+    static constexpr int TQ = (T_PC + 63) / 64;            // wave instructions per plane
+    static constexpr int AQ = (A_PC + 63) / 64;
+    static constexpr int PQ = P_F2 * 8 / 1024;             // KC / 16 (ROT_TILE = 8)
+    static_assert(PQ * 1024 == P_F2 * 8, "P rows = whole wave instructions");
+    static constexpr int NQ = NPLANE * TQ + AQ + PQ;
+    static constexpr int TL_OFF = TQ * 1024;               // bytes: lo plane, a tile, P rows
+    static constexpr int A_OFF = NPLANE * TQ * 1024;
+    static constexpr int P_OFF = (NPLANE * TQ + AQ) * 1024;
+    static constexpr int STAGE_B = NQ * 1024;
     static constexpr int EPI_B = ROT_TILE * 64 * 3 * 4 + 32 * NTP * 8;
-    static constexpr int TOTAL_B = STAGE_B > EPI_B ? STAGE_B : EPI_B;
-    static constexpr int T16 = NTP * KC * 2 * 2 / 16;      // 16-B pieces per plane
+    static constexpr int TOTAL_B = 2 * STAGE_B > EPI_B ? 2 * STAGE_B : EPI_B;
 };
+
+// 16 bytes global -> LDS without registers: lane L's piece lands at
+// ldsBase + 16 L (ldsBase wave-uniform)
+THX_DEV void dma16(const void* g, void* ldsBase)
+{
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)g,
+        (__attribute__((address_space(3))) void*)ldsBase, 16, 0, 0);
+}
 
 template <int MODE, int NF>
 __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict__ Ac,
@@ -317,7 +354,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
                                                         const float* __restrict__ bias,
                                                         const uint16_t* __restrict__ Thi,
                                                         const uint16_t* __restrict__ Tlo,
-                                                        const float2* __restrict__ rotP,
+                                                        const float2* __restrict__ Pc,
                                                         const float* __restrict__ pTf,
                                                         const double* __restrict__ pR,
                                                         int nImg, int nR, int nT, int nPxl,
@@ -331,11 +368,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
     typedef typename Elt<MODE>::V HV;
     using S = Smem<MODE, NF>;
     constexpr int NTP = S::NTP;
-    __shared__ __attribute__((aligned(16))) char lds[S::TOTAL_B];
-    uint16_t* sTh = reinterpret_cast<uint16_t*>(lds);               // [NTP][TROW]
-    uint16_t* sTl = sTh + S::T_H;                                   // BF16X3 only
-    float2* sA = reinterpret_cast<float2*>(sTh + S::NPLANE * S::T_H);   // [64][APITCH]
-    float2* sP = sA + S::A_F2;                                      // [8][KC]
+    extern __shared__ __attribute__((aligned(16))) char lds[];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n = lane & 31, h = lane >> 5;
@@ -361,57 +394,41 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
 #pragma unroll
             for (int j = 0; j < 16; j++) acc[a][f][j] = 0.f;
 
-    // register-staged prefetch of one pixel chunk (global -> regs during the
-    // previous chunk's MFMAs, regs -> LDS after the barrier)
-    constexpr int TPER = (S::T16 + THREADS - 1) / THREADS;
-    constexpr int APER = KC / 16;            // float4 of the a tile per thread
-    float4 gTh[TPER], gTl[TPER], gA[APER];
-    float2 gP = make_float2(0.f, 0.f);
-    auto load_chunk = [&](int ck) {
-        const float4* gh = reinterpret_cast<const float4*>(Thi + (size_t)ck * nTPad * KC * 2);
-        const float4* gl = reinterpret_cast<const float4*>(Tlo + (size_t)ck * nTPad * KC * 2);
+    // Two stages.  Chunk ck+1's T planes and a tile are copied by LDS-DMA into
+    // the other stage while chunk ck is multiplied, and its P rows ride in one
+    // register; the barrier closing chunk ck retires both.
+    auto issue_chunk = [&](int ck, char* stage) {
+        const char* gTh = reinterpret_cast<const char*>(Thi + (size_t)ck * nTPad * TROW);
+        const char* gTl = reinterpret_cast<const char*>(Tlo + (size_t)ck * nTPad * TROW);
+        const char* gA = reinterpret_cast<const char*>(Ac + ((size_t)ck * nImgPad + l0) * APITCH);
+        const char* gP = reinterpret_cast<const char*>(Pc + ((size_t)ck * nRBk + rb) * ROT_TILE * KC);
 #pragma unroll
-        for (int u = 0; u < TPER; u++) {
-            const int x = tid + u * THREADS;
-            if (x < S::T16) {
-                gTh[u] = gh[x];
-                if (MODE == BF16X3) gTl[u] = gl[x];
+        for (int u = 0; u < (S::NQ + 7) / 8; u++) {
+            const int q = u * 8 + w;                         // wave-uniform instruction
+            if (q < S::NQ) {
+                const char* g;
+                int pc, lim;
+                if (q < S::TQ) { g = gTh; pc = q * 64; lim = S::T_PC; }
+                else if (MODE == BF16X3 && q < 2 * S::TQ) { g = gTl; pc = (q - S::TQ) * 64; lim = S::T_PC; }
+                else if (q < S::NQ - S::PQ) { g = gA; pc = (q - S::NPLANE * S::TQ) * 64; lim = S::A_PC; }
+                else { g = gP; pc = (q - (S::NQ - S::PQ)) * 64; lim = S::PQ * 64; }
+                if (pc + lane < lim) dma16(g + (size_t)(pc + lane) * 16, stage + q * 1024);
             }
         }
-#pragma unroll
-        for (int v = 0; v < APER; v++)
-            gA[v] = reinterpret_cast<const float4*>(Ac + ((size_t)ck * nImgPad + l0) * KC)[tid + v * THREADS];
-        if (tid < ROT_TILE * KC) {
-            const int qq = tid / KC, kc = tid % KC;
-            const int rr = rb * ROT_TILE + qq, i = ck * KC + kc;
-            gP = (rr < nR && i < nPxl) ? rotP[(size_t)rr * nPxl + i] : make_float2(0.f, 0.f);
-        }
     };
-    auto store_chunk = [&]() {
-#pragma unroll
-        for (int u = 0; u < TPER; u++) {
-            const int x = tid + u * THREADS;
-            if (x < S::T16) {                      // KC/4 pieces of 16 B per row
-                const int row = x / (KC / 4), qd = x % (KC / 4);
-                *reinterpret_cast<float4*>(sTh + row * TROW + qd * 8) = gTh[u];
-                if (MODE == BF16X3) *reinterpret_cast<float4*>(sTl + row * TROW + qd * 8) = gTl[u];
-            }
-        }
-#pragma unroll
-        for (int v = 0; v < APER; v++) {           // 2 float2 of image row x / (KC/2)
-            const int x = tid + v * THREADS;
-            const int row = x / (KC / 2), c2 = (x % (KC / 2)) * 2;
-            *reinterpret_cast<float4*>(sA + row * APITCH + c2) = gA[v];
-        }
-        if (tid < ROT_TILE * KC) sP[tid] = gP;
-    };
-
-    load_chunk(0);
-    for (int ck = 0; ck * KC < nPxlPad; ck++) {
-        __syncthreads();                   // previous chunk consumed
-        store_chunk();
-        __syncthreads();
-        if ((ck + 1) * KC < nPxlPad) load_chunk(ck + 1);
+    auto stage_at = [&](int ck) { return lds + (ck & 1) * S::STAGE_B; };
+    const int nCk = nPxlPad / KC;
+    issue_chunk(0, stage_at(0));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int ck = 0; ck < nCk; ck++) {
+        const bool more = ck + 1 < nCk;
+        if (more) issue_chunk(ck + 1, stage_at(ck + 1));
+        const char* stage = stage_at(ck);
+        const uint16_t* sTh = reinterpret_cast<const uint16_t*>(stage);
+        const uint16_t* sTl = reinterpret_cast<const uint16_t*>(stage + S::TL_OFF);
+        const float2* sA = reinterpret_cast<const float2*>(stage + S::A_OFF);
+        const float2* sP = reinterpret_cast<const float2*>(stage + S::P_OFF);
 #pragma unroll
         for (int s = 0; s < KC / 8; s++) {
             // A fragments: w = a conj(P_r) for images a*32 + n, pixels 8s+4h+{0..3}
@@ -468,8 +485,9 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
                 }
             }
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
     }
-    __syncthreads();
 
     // ------------------------------------------------------------ epilogue
     float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][64]  A_l + B[l][r]
@@ -506,7 +524,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
             float sR = 0.f;
 #pragma unroll
             for (int f = 0; f < NF; f++) {
-                const float e = (f * 32 + n < nT && rValid) ? expf(acc[a][f][j] - mx) : 0.f;
+                const float e = (f * 32 + n < nT && rValid) ? __expf(acc[a][f][j] - mx) : 0.f;
                 acc[a][f][j] = e;
                 sR += e * pTv[f];
             }
@@ -530,7 +548,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
             float M = sMax[row];
 #pragma unroll
             for (int k = 1; k < ROT_TILE; k++) M = fmaxf(M, sMax[k * 64 + row]);
-            const float sc = rValid ? expf(sMax[w * 64 + row] - M) * pRr : 0.f;
+            const float sc = rValid ? __expf(sMax[w * 64 + row] - M) * pRr : 0.f;
 #pragma unroll
             for (int f = 0; f < NF; f++) atomicAdd(&sWT[m * NTP + f * 32 + n], fx56(acc[a][f][j] * sc));
         }
@@ -602,8 +620,16 @@ int launch_main(const WS& ws, const Dims& d, const float* rotP, const double* pR
 {
     const int nIT = d.nImgPad / IMG_TILE;
     dim3 grid((unsigned)(8 * thx::cdiv(nIT * d.nRB, 8)));
-    hipLaunchKernelGGL((k_scan_split<MODE, NF>), grid, dim3(THREADS), 0, s, ws.Ac, ws.Aconst,
-                       ws.scale, ws.bias, ws.Thi, ws.Tlo, reinterpret_cast<const float2*>(rotP),
+    constexpr int lds = Smem<MODE, NF>::TOTAL_B;
+    static_assert(lds <= 160 * 1024, "scan stages exceed the LDS");
+    static bool attr = false;                 // idempotent: a race only repeats the call
+    if (!attr) {
+        THX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan_split<MODE, NF>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_scan_split<MODE, NF>), grid, dim3(THREADS), lds, s, ws.Ac, ws.Aconst,
+                       ws.scale, ws.bias, ws.Thi, ws.Tlo, ws.Pc,
                        ws.pTf, pR, d.nImg, d.nR, d.nT, d.nPxl, d.nImgPad, d.nPxlPad, d.nTPad,
                        d.nRBias, nIT, ws.wRp, ws.pM, ws.pWT);
     THX_LAUNCH_CHECK();
@@ -633,6 +659,9 @@ int scan_split(const float* rotP, int nR, const float* traP, int nT, const float
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_prep_img, dim3(2048), dim3(256), 0, s, dat2, ctf, sigRcp, ws.scale, nImg,
                        nPxl, d.nImgPad, d.nPxlPad, ws.Ac, ws.Bc);
+    THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_prep_pchunk, dim3(2048), dim3(256), 0, s, rot2, nR, nPxl,
+                       d.nRB * ROT_TILE, d.nPxlPad, ws.Pc);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_prep_tsplit<MODE>, dim3(512), dim3(256), 0, s,
                        reinterpret_cast<const float2*>(traP), pT, nT, nPxl, d.nTPad, d.nPxlPad,

@@ -300,7 +300,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_mfma(const float* __restrict__
         float sR = 0.f;
 #pragma unroll
         for (int f = 0; f < NF; f++) {
-            const float e = (f * 32 + n < nT && rValid) ? expf(acc[f][j] - mx) : 0.f;
+            const float e = (f * 32 + n < nT && rValid) ? __expf(acc[f][j] - mx) : 0.f;
             acc[f][j] = e;
             sR += e * pTv[f];
         }
@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(THREADS) k_scan_mfma(const float* __restrict__
                 const int m = (j & 3) + 8 * (j >> 2) + 4 * kk;
                 const float M = fmaxf(fmaxf(sMax[(h * 4 + 0) * 32 + m], sMax[(h * 4 + 1) * 32 + m]),
                                       fmaxf(sMax[(h * 4 + 2) * 32 + m], sMax[(h * 4 + 3) * 32 + m]));
-                const float sc = rValid ? expf(rmax[j] - M) * pRr : 0.f;
+                const float sc = rValid ? __expf(rmax[j] - M) * pRr : 0.f;
 #pragma unroll
                 for (int f = 0; f < NF; f++)
                     atomicAdd(&sWT[m * NTP + f * 32 + n], fx56(acc[f][j] * sc));
