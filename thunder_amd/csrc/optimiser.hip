@@ -93,50 +93,69 @@ THX_DEV void qmul(const double* a, const double* b, double* o)
 // one wave per image: lanes stride over the particles, every lane holds the
 // 4x4 matrices (FP64) and repeats the tiny dense algebra.
 
-// Inverse of a 4x4 matrix by cofactors; det == 0 or a non-finite input gives
-// NaNs (the reference's Eigen inverse of a singular A does too).
+// Inverse of a symmetric 4x4 matrix (every A of the ACG estimates is built
+// symmetric): the adjugate from the six 2x2 minors of the top and bottom row
+// pairs (Laplace expansion), upper triangle only, mirrored; det == 0 or a
+// non-finite input gives NaNs (the reference's Eigen inverse of a singular A
+// does too).  ~90 FP64 operations instead of the ~300 of 16 full cofactors.
 THX_DEV double inv4(const double* m, double* o)
 {
-    o[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
-    o[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
-    o[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
-    o[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
-    o[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
-    o[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
-    o[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
-    o[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
-    o[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
-    o[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
-    o[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
-    o[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
-    o[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
-    o[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
-    o[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
-    o[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
-    const double det = m[0] * o[0] + m[1] * o[4] + m[2] * o[8] + m[3] * o[12];
+    const double s0 = m[0] * m[5] - m[4] * m[1], s1 = m[0] * m[6] - m[4] * m[2];
+    const double s2 = m[0] * m[7] - m[4] * m[3], s3 = m[1] * m[6] - m[5] * m[2];
+    const double s4 = m[1] * m[7] - m[5] * m[3], s5 = m[2] * m[7] - m[6] * m[3];
+    const double c5 = m[10] * m[15] - m[14] * m[11], c4 = m[9] * m[15] - m[13] * m[11];
+    const double c3 = m[9] * m[14] - m[13] * m[10], c2 = m[8] * m[15] - m[12] * m[11];
+    const double c1 = m[8] * m[14] - m[12] * m[10], c0 = m[8] * m[13] - m[12] * m[9];
+    const double det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
     const double r = det != 0.0 ? 1.0 / det : __builtin_nan("");
-    for (int k = 0; k < 16; k++) o[k] *= r;
+    o[0] = (m[5] * c5 - m[6] * c4 + m[7] * c3) * r;
+    o[1] = (-m[1] * c5 + m[2] * c4 - m[3] * c3) * r;
+    o[2] = (m[13] * s5 - m[14] * s4 + m[15] * s3) * r;
+    o[3] = (-m[9] * s5 + m[10] * s4 - m[11] * s3) * r;
+    o[5] = (m[0] * c5 - m[2] * c2 + m[3] * c1) * r;
+    o[6] = (-m[12] * s5 + m[14] * s2 - m[15] * s1) * r;
+    o[7] = (m[8] * s5 - m[10] * s2 + m[11] * s1) * r;
+    o[10] = (m[12] * s4 - m[13] * s2 + m[15] * s0) * r;
+    o[11] = (-m[8] * s4 + m[9] * s2 - m[11] * s0) * r;
+    o[15] = (m[8] * s3 - m[9] * s1 + m[10] * s0) * r;
+    o[4] = o[1]; o[8] = o[2]; o[12] = o[3];
+    o[9] = o[6]; o[13] = o[7]; o[14] = o[11];
     return det;
+}
+
+// A symmetric matrix packed as its upper triangle with the off-diagonal
+// entries doubled, so q^T M q = sum_j q_j sum_{k >= j} Mp_jk q_k (14 FMAs).
+THX_DEV void pack10(const double* M, double* Mp)
+{
+    int t = 0;
+    for (int j = 0; j < 4; j++)
+        for (int k = j; k < 4; k++) Mp[t++] = (j == k ? 1.0 : 2.0) * M[4 * j + k];
+}
+THX_DEV double quad10(const double* Mp, const double* q)
+{
+    double s = 0.0;
+    int t = 0;
+    for (int j = 0; j < 4; j++) {
+        double a = 0.0;
+        for (int k = j; k < 4; k++) a += Mp[t++] * q[k];
+        s += q[j] * a;
+    }
+    return s;
 }
 
 // Particle statistics run one image per GROUP lanes (4 images per wave): the
 // 4x4 algebra is repeated by every lane anyway, so narrower groups mean 4x
 // fewer waves for the same latency-bound FP64 chains.
-constexpr int GROUP = 16;
+#ifndef THX_PF_GROUP
+#define THX_PF_GROUP 16
+#endif
+constexpr int GROUP = THX_PF_GROUP;
 
 THX_DEV double group_sum(double v)
 {
 #pragma unroll
     for (int o = GROUP / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
-}
-
-THX_DEV double quad4(const double* q, const double* M)
-{
-    double s = 0.0;
-    for (int j = 0; j < 4; j++)
-        for (int k = 0; k < 4; k++) s += q[j] * M[4 * j + k] * q[k];
-    return s;
 }
 
 // inferACG(dmat44&, const dmat4&), DirectionalStat.cpp:93-145: Tyler's fixed
@@ -147,7 +166,7 @@ THX_DEV double quad4(const double* q, const double* M)
 // particles in registers across the iterations -- the loop is a serial
 // chain, and re-reading them from L2 every iteration was its latency; the
 // arithmetic and its order are the same either way.
-constexpr int QREG = 8;
+constexpr int QREG = 128 / GROUP;
 
 template <bool REG>
 THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, double* A,
@@ -168,14 +187,17 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
     for (int k = 0; k < 16; k++) B[k] = (k % 5 == 0) ? 1.0 : 0.0;
     for (int it = 0; it < maxIt; it++) {
         for (int k = 0; k < 16; k++) A[k] = B[k];
-        double Ai[16];
+        double Ai[16], Mp[10];
         inv4(A, Ai);
+        pack10(Ai, Mp);
         double b[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nf = 0.0;
         auto term = [&](const double* q) {
-            const double r = 1.0 / quad4(q, Ai);
+            const double r = 1.0 / quad10(Mp, q);
             int t = 0;
-            for (int j = 0; j < 4; j++)
-                for (int k = j; k < 4; k++) b[t++] += q[j] * q[k] * r;
+            for (int j = 0; j < 4; j++) {
+                const double qj = q[j] * r;
+                for (int k = j; k < 4; k++) b[t++] += qj * q[k];
+            }
             nf += r;
         };
         if (REG) {
@@ -297,13 +319,14 @@ __global__ void __launch_bounds__(256) k_pf_calvari(int nImg, int mR, const doub
 // resample's w u / sum).
 THX_DEV void balance_rot(const double* Q, int m, int lane, double* w)
 {
-    double A[16], Ai[16];
+    double A[16], Ai[16], Mp[10];
     infer_acg(Q, m, nullptr, lane, A);
     const double det = inv4(A, Ai);
+    pack10(Ai, Mp);
     const double sd = sqrt(det);
     double tot = 0.0;
     for (int i = lane; i < m; i += GROUP) {
-        const double u = quad4(Q + 4 * i, Ai);
+        const double u = quad10(Mp, Q + 4 * i);
         const double x = sd * u * u;
         w[i] = x;
         tot += x;
