@@ -454,6 +454,11 @@ THX_DEV void rotation_slots(const double* __restrict__ q4, int nRl, int tid,
     __syncthreads();
 }
 
+#ifdef THX_LOCAL_STAMPS
+// diagnostic: per-iteration phase cycles of staged patches, waves 0 and 7
+__device__ unsigned long long g_local_stamps[12];
+#endif
+
 template <bool CELLS>
 // two workgroups per CU (LDS-bound): 4 waves per SIMD, 128 VGPRs
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4)))
@@ -545,6 +550,12 @@ k_local_fused(const float2* __restrict__ vol,
     fetch_box<CELLS>(pre, dst, rc, vol, vdim, tid);
 
     __syncthreads();
+#ifdef THX_LOCAL_STAMPS
+    unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tp = __builtin_amdgcn_s_memtime(), tq;
+#define STAMP(k) do { tq = __builtin_amdgcn_s_memtime(); if (rc.staged()) st[k] += tq - tp; tp = tq; } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
     for (int c = 0; c < nC; c++) {
         // ---- stage patch c: box voxels, image tile B[px][U, V][t], b, (iCol, iRow) pf
         if (rc.staged()) {
@@ -579,7 +590,9 @@ k_local_fused(const float2* __restrict__ vol,
                 sXY[bpx] = make_double2((double)(ic * pf), (double)(ir * pf));
             }
         }
+        STAMP(0);
         __syncthreads();
+        STAMP(1);
         // ---- prefetch patch c + 1 (in flight during the gathers below)
         Rec r2 = rn;
         if (c + 1 < nC) {
@@ -590,6 +603,7 @@ k_local_fused(const float2* __restrict__ vol,
             fetch_box<CELLS>(pre, dst, rn, vol, vdim, tid);
             if (c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
         }
+        STAMP(2);
         // ---- projection samples: this lane's rotation x pixels 4s + g
         // one step: the sample's bias term, then (re, im) of pixels 4s, 4s+2 and
         // 4s+1, 4s+3 regrouped into two MFMA A operands against [U, V]
@@ -633,10 +647,23 @@ k_local_fused(const float2* __restrict__ vol,
                                      : interp_ft(vol, vdim, x, y, z));
             }
         }
+        STAMP(3);
+#ifdef THX_LOCAL_STAMPS
+        const bool stg = rc.staged();
+#endif
         rc = rn;
         rn = r2;
         __syncthreads();
+#ifdef THX_LOCAL_STAMPS
+        tq = __builtin_amdgcn_s_memtime();
+        if (stg) { st[4] += tq - tp; st[5] += 1; }
+        tp = tq;
+#endif
     }
+#ifdef THX_LOCAL_STAMPS
+    if (lane == 0 && (wv == 0 || wv == 7))
+        for (int k = 0; k < 6; k++) atomicAdd(&g_local_stamps[(wv == 7) * 6 + k], st[k]);
+#endif
     // A_l = sum_i s |d|^2 (staging threads with bt == 0 accumulated it)
     aConst = wave_sum(aConst);
     if (lane == 0) sRed[wv] = aConst;
@@ -789,6 +816,18 @@ extern "C" int thx_volume_cells(const float* vol, int vdim, float* cells,
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
+
+#ifdef THX_LOCAL_STAMPS
+extern "C" int thx_debug_local_stamps(unsigned long long* out, int reset)
+{
+    THX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_local_stamps), sizeof(unsigned long long) * 12));
+    if (reset) {
+        const unsigned long long z[12] = {0};
+        THX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_local_stamps), z, sizeof(z)));
+    }
+    return THX_OK;
+}
+#endif
 
 extern "C" size_t thx_local_phase_workspace(int nImg, int nR, int nT, int nVisit)
 {
