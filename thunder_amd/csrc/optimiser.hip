@@ -387,6 +387,17 @@ __global__ void __launch_bounds__(256) k_pf_balance_rot(int nImg, int mR,
 }
 
 // --------------------------------------------------------------- resample
+constexpr int RESAMPLE_KMAX = 2048;
+
+// Dynamic LDS of a k_pf_resample launch (keys of the bitonic shuffle).
+size_t resample_lds(int nIn, bool shuffle)
+{
+    if (!shuffle || nIn > RESAMPLE_KMAX) return 0;
+    int n = 1;
+    while (n < nIn) n <<= 1;
+    return (size_t)4 * n * sizeof(uint64_t);
+}
+
 // One wave per image: systematic resampling (src/Particle.cpp:1343-1383) of
 // (w, u) -> ancestors and 1/u priors; w may be shared by all images (ldw = 0).
 // u0 ~ U(0, 1/nOut) is drawn from the counter RNG.  w and wOut may alias (the
@@ -427,14 +438,17 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
     // (a one-lane Fisher-Yates took 1.4 ms per 12 500-image call at 2000
     // entries, a rank count 7 ms).  Larger supports fall back to Fisher-Yates
     // by lane 0 in global memory.
-    constexpr int KMAX = 2048;
-    __shared__ __attribute__((aligned(16))) uint64_t sKey[4][KMAX];
+    // The keys live in dynamic LDS sized by the launch (resample_lds): 4 waves
+    // x the next power of two >= nIn keys, so small supports (the phases'
+    // mLR, mLT) do not pin 64 KiB per workgroup.
+    constexpr int KMAX = RESAMPLE_KMAX;
+    extern __shared__ __attribute__((aligned(16))) uint64_t sKeyDyn[];
     int* pm = permWs ? permWs + (size_t)l * nIn : nullptr;
     if (pm && nIn <= KMAX) {
-        uint64_t* kk = sKey[threadIdx.x >> 6];
         int ib = 0;
         while ((1 << ib) < nIn) ib++;
         const int N = 1 << ib;
+        uint64_t* kk = sKeyDyn + (size_t)(threadIdx.x >> 6) * N;
         Philox sh(seed, (uint32_t)l, stream, 0x5f1e0000u | (uint32_t)lane);
         uint4 v = make_uint4(0, 0, 0, 0);
         for (int i = lane, k = 0; i < N; i += 64, k = (k + 1) & 3) {
@@ -986,7 +1000,8 @@ extern "C" int thx_pf_resample(int nImg, int nIn, int nOut, const double* w, int
     thx::Carver k(workspace, wsBytes);
     double* cdf = k.take<double>((size_t)nImg * nIn);
     int* pw = k.take<int>((size_t)nImg * nIn);
-    hipLaunchKernelGGL(k_pf_resample, dim3(thx::cdiv(nImg, 4)), dim3(256), 0, thx::as_stream(stream),
+    hipLaunchKernelGGL(k_pf_resample, dim3(thx::cdiv(nImg, 4)), dim3(256), resample_lds(nIn, shuffle),
+                       thx::as_stream(stream),
                        nImg, nIn, nOut, w, ldw, u, ldu, (uint64_t)seed, (uint32_t)stream_id, anc,
                        wOut, iMax, cdf, shuffle ? pw : nullptr, perm, u0);
     THX_LAUNCH_CHECK();
@@ -1076,7 +1091,8 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.nR, p.gWR, nK * c.nR,
                            p.peakR, 1, clsSel, c.nR, nullptr);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nR, c.mLR, gPR, 0,
+        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.nR, c.shuffle), s,
+                           nImg, c.nR, c.mLR, gPR, 0,
                            p.gWR, nK * c.nR, c.seed, 1000u, p.anc, pR, p.topR, p.cdf,
                            c.shuffle ? p.perm : nullptr, nullptr, nullptr, clsSel, c.nR, nullptr);
         THX_LAUNCH_CHECK();
@@ -1086,7 +1102,8 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg, gQuat,
                            0L, p.topR, p.topQ, nullptr);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.nT, c.mLT, gPT, 0,
+        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.nT, c.shuffle), s,
+                           nImg, c.nT, c.mLT, gPT, 0,
                            p.gWT, nK * c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf,
                            c.shuffle ? p.perm : nullptr, nullptr, nullptr, clsSel, c.nT, nullptr);
         THX_LAUNCH_CHECK();
@@ -1151,7 +1168,8 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                            trans, 0.0, 0.0, p.kv, p.sv, done);
         THX_LAUNCH_CHECK();
         // resample R and T by the phase marginals; ancestors gathered in place
-        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, c.mLR, pR,
+        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.mLR, c.shuffle), s,
+                           nImg, c.mLR, c.mLR, pR,
                            c.mLR, p.wR, c.mLR, c.seed, (uint32_t)(3000 + phase), p.anc, pR,
                            p.topR, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
                            0, done);
@@ -1164,7 +1182,8 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg,
                            p.tmpQ, (long)c.mLR * 4, p.topR, p.topQ, done);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), 0, s, nImg, c.mLT, c.mLT, pT,
+        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.mLT, c.shuffle), s,
+                           nImg, c.mLT, c.mLT, pT,
                            c.mLT, p.wT, c.mLT, c.seed, (uint32_t)(4000 + phase), p.anc, pT,
                            p.topT, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
                            0, done);
