@@ -724,10 +724,28 @@ __global__ void __launch_bounds__(256) k_local_weights(const float* __restrict__
         wR[(size_t)l * nR + r] = (float)(a * c);
         cacc += a * pRl[r];
     }
-    for (int t = threadIdx.x; t < nT; t += blockDim.x) {
+    __shared__ double sT[256];
+    if (nT <= 64) {
+        // wT: groups of nT threads stride over the rotations (a handful of
+        // translations would leave 247 of 256 threads idle on a 125-long
+        // serial chain), partial sums in a fixed order through LDS
+        const int G = 256 / nT, t = threadIdx.x % nT, gq = threadIdx.x / nT;
         double a = 0.0;
-        for (int r = 0; r < nR; r++) a += (double)expf(Dl[r * nT + t] - base) * pRl[r];
-        wT[(size_t)l * nT + t] = (float)(a * c);
+        if (gq < G)
+            for (int r = gq; r < nR; r += G) a += (double)expf(Dl[r * nT + t] - base) * pRl[r];
+        sT[threadIdx.x] = a;
+        __syncthreads();
+        if (threadIdx.x < nT) {
+            double w = 0.0;
+            for (int k = 0; k < G; k++) w += sT[k * nT + threadIdx.x];
+            wT[(size_t)l * nT + threadIdx.x] = (float)(w * c);
+        }
+    } else {
+        for (int t = threadIdx.x; t < nT; t += blockDim.x) {
+            double a = 0.0;
+            for (int r = 0; r < nR; r++) a += (double)expf(Dl[r * nT + t] - base) * pRl[r];
+            wT[(size_t)l * nT + t] = (float)(a * c);
+        }
     }
     cacc = wave_sum(cacc);
     if (lane == 0) sd[wv] = cacc;
