@@ -237,6 +237,16 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
         if (cLo <= cHi) {
             const float X0 = (float)(cLo * pf), X1 = (float)(cHi * pf);
             const float Y0 = (float)(rLo * pf), Y1 = (float)(rHi * pf);
+            // every rotated patch point lies in the corner hull; the bounds
+            // are FP32 (|error| < 1e-4 voxel against the FP64-then-rounded
+            // sample coordinates), widened by EPS before the floor; a cell
+            // spans floor(c) .. floor(c) + 1.  The extremes are tracked in
+            // FP32 and floored once: floor and the clamp at 0 are monotone,
+            // so this equals flooring every rotation's bound.
+            constexpr float EPS = 1e-3f;
+            float f[12];
+#pragma unroll
+            for (int k = 0; k < 12; k++) f[k] = (k % 6) < 3 ? INFINITY : -INFINITY;
             for (int r = rBeg; r < rEnd; r++) {
                 const float* m = sM[r];
                 float mn[3], mx[3];
@@ -246,27 +256,34 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
                     mn[a] = u * (u >= 0 ? X0 : X1) + v * (v >= 0 ? Y0 : Y1);
                     mx[a] = u * (u >= 0 ? X1 : X0) + v * (v >= 0 ? Y1 : Y0);
                 }
-                // every rotated patch point lies in the corner hull; the bounds
-                // are FP32 (|error| < 1e-4 voxel against the FP64-then-rounded
-                // sample coordinates), widened by EPS before the floor; a cell
-                // spans floor(c) .. floor(c) + 1
-                constexpr float EPS = 1e-3f;
-                if (mx[0] >= -EPS) {
-                    e[0] = min(e[0], (int)floorf(fmaxf(mn[0] - EPS, 0.f)));
-                    e[1] = min(e[1], (int)floorf(mn[1] - EPS));
-                    e[2] = min(e[2], (int)floorf(mn[2] - EPS));
-                    e[3] = max(e[3], (int)floorf(mx[0] + EPS) + 1);
-                    e[4] = max(e[4], (int)floorf(mx[1] + EPS) + 1);
-                    e[5] = max(e[5], (int)floorf(mx[2] + EPS) + 1);
-                }
-                if (mn[0] < EPS) {
-                    e[6] = min(e[6], (int)floorf(fmaxf(-mx[0] - EPS, 0.f)));
-                    e[7] = min(e[7], (int)floorf(-mx[1] - EPS));
-                    e[8] = min(e[8], (int)floorf(-mx[2] - EPS));
-                    e[9] = max(e[9], (int)floorf(-mn[0] + EPS) + 1);
-                    e[10] = max(e[10], (int)floorf(-mn[1] + EPS) + 1);
-                    e[11] = max(e[11], (int)floorf(-mn[2] + EPS) + 1);
-                }
+                if (mx[0] >= -EPS)
+#pragma unroll
+                    for (int a = 0; a < 3; a++) {
+                        f[a] = fminf(f[a], mn[a]);
+                        f[3 + a] = fmaxf(f[3 + a], mx[a]);
+                    }
+                if (mn[0] < EPS)
+#pragma unroll
+                    for (int a = 0; a < 3; a++) {
+                        f[6 + a] = fminf(f[6 + a], -mx[a]);
+                        f[9 + a] = fmaxf(f[9 + a], -mn[a]);
+                    }
+            }
+            if (f[0] != INFINITY) {
+                e[0] = (int)floorf(fmaxf(f[0] - EPS, 0.f));
+                e[1] = (int)floorf(f[1] - EPS);
+                e[2] = (int)floorf(f[2] - EPS);
+                e[3] = (int)floorf(f[3] + EPS) + 1;
+                e[4] = (int)floorf(f[4] + EPS) + 1;
+                e[5] = (int)floorf(f[5] + EPS) + 1;
+            }
+            if (f[6] != INFINITY) {
+                e[6] = (int)floorf(fmaxf(f[6] - EPS, 0.f));
+                e[7] = (int)floorf(f[7] - EPS);
+                e[8] = (int)floorf(f[8] - EPS);
+                e[9] = (int)floorf(f[9] + EPS) + 1;
+                e[10] = (int)floorf(f[10] + EPS) + 1;
+                e[11] = (int)floorf(f[11] + EPS) + 1;
             }
         }
 #pragma unroll
