@@ -611,6 +611,30 @@ __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
     }
 }
 
+// The perturbation mean of PARTICLE_ROT_MEAN_USING_STAT_PERTURB
+// (include/Config.h:79): inferACG(mean, _r) of the current (resampled) cloud
+// -- Tyler's fixed point from B = I until sum|A - B| <= 1e-3
+// (DirectionalStat.cpp:93-145), capped at acgIters iterations -- then its
+// principal axis (:224-251).  Its own launch so the fixed point can keep the
+// cloud in registers (in k_pf_perturb they would push past 256 VGPRs).
+// itOut (optional): fixed-point iterations per image.
+__global__ void __launch_bounds__(256) k_pf_mean(int nImg, int mR, const double* __restrict__ quat,
+                                                 int acgIters, const int* __restrict__ done,
+                                                 double* __restrict__ meanQ,
+                                                 int* __restrict__ itOut)
+{
+    const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
+    const int lane = threadIdx.x % GROUP;
+    if (l >= nImg || (done && done[l])) return;
+    double A[16], mean[4];
+    const int it = infer_acg(quat + (size_t)l * mR * 4, mR, nullptr, lane, A, acgIters);
+    principal_axis(A, mean);
+    if (lane == 0) {
+        for (int k = 0; k < 4; k++) meanQ[4 * l + k] = mean[k];
+        if (itOut) itOut[l] = it;
+    }
+}
+
 // Particle::perturb + balanceWeight for one image per GROUP lanes
 // (src/Particle.cpp:1149-1289, 2309-2375), with k / s from k_pf_calvari:
 //   R: mean = inferACG(mean, _r) of the current (resampled) cloud -- the
@@ -618,15 +642,14 @@ __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
 //      (include/Config.h:79): Tyler's fixed point from B = I until
 //      sum|A - B| <= 1e-3 (DirectionalStat.cpp:93-145), here capped at
 //      acgIters iterations, then the principal axis (:224-251) -- when
-//      meanMode == 1; the top particle (calRank1st's _topR, the branch without
+//      meanMode == 1 (k_pf_mean); the top particle (calRank1st's _topR, the branch without
 //      the switch) when meanMode == 0.  r_i <- mean d_i mean^-1 r_i with
 //      d ~ ACG(diag(1, pf^2 min(1,k1), pf^2 min(1,k2), pf^2 min(1,k3)))
 //      (sampleACG: normalised N(0, diag)), then pR = 1 / pdfACG on the
 //      perturbed cloud (balanceWeight(PAR_R)).
 //   T: t_i += pf N(0, s) (:1232-1262), reCentre beyond transM (:2473-2495),
 //      pT = 1/pdf normalised (balanceWeight(PAR_T), :2342-2375).
-// itOut (optional): inferACG iterations of the mean per image.
-constexpr int PERT_LDS_Q = 4 * 128;     // doubles per image: clouds up to 128 particles
+// meanMode 1 reads the mean k_pf_mean left in meanQ.
 
 __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
                                                     double* __restrict__ quat,
@@ -638,14 +661,10 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
                                                     const double* __restrict__ sIn,
                                                     double pf, double transS, double transM,
                                                     uint64_t seed, uint32_t stream,
-                                                    int meanMode, int acgIters,
-                                                    const int* __restrict__ done,
-                                                    int* __restrict__ itOut)
+                                                    int meanMode,
+                                                    const double* __restrict__ meanQ,
+                                                    const int* __restrict__ done)
 {
-    // the mean's fixed point reads this image's cloud from LDS (a serial
-    // chain of up to acgIters passes; registers would push the kernel past
-    // 256 VGPRs)
-    __shared__ double sQ[256 / GROUP][PERT_LDS_Q];
     const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
     const int lane = threadIdx.x % GROUP;
     if (l >= nImg || (done && done[l])) return;
@@ -655,23 +674,8 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
 
     // ---- rotation
     double mean[4], cm[4];
-    if (meanMode == 1) {
-        double A[16];
-        const double* src = Q;
-        if (4 * mR <= PERT_LDS_Q) {
-            double* dst = sQ[threadIdx.x / GROUP];
-            for (int k = lane; k < 4 * mR; k += GROUP) dst[k] = Q[k];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            src = dst;
-        }
-        const int it = infer_acg_impl<false>(src, mR, nullptr, lane, A, acgIters);
-        principal_axis(A, mean);
-        if (itOut && lane == 0) itOut[l] = it;
-    } else {
-        for (int k = 0; k < 4; k++) mean[k] = topQ[4 * l + k];
-    }
+    const double* mq = meanMode == 1 ? meanQ : topQ;
+    for (int k = 0; k < 4; k++) mean[k] = mq[4 * l + k];
     cm[0] = mean[0]; cm[1] = -mean[1]; cm[2] = -mean[2]; cm[3] = -mean[3];
     const double sd1 = pf * sqrt(fmin(1.0, kIn[3 * l]));       // PERTURB_K_MAX = 1
     const double sd2 = pf * sqrt(fmin(1.0, kIn[3 * l + 1]));
@@ -860,6 +864,7 @@ struct Plan {
     double* tmpQ; double* tmpT;
     double* kv; double* sv; double* peakR;   // calVari k1..k3, s0 s1; setPeakFactor(R)
     double* topQ;                            // calRank1st _topR
+    double* meanQ;                           // k_pf_mean's perturbation mean
     float* wC; float* wR; float* wT; float* base; double* pC;
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
     double* bestR; double* bestT;                        // convergence: smallest variR / variT
@@ -896,6 +901,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     p.sv = k.take<double>((size_t)nImg * 2);
     p.peakR = k.take<double>(nImg);
     p.topQ = k.take<double>((size_t)nImg * 4);
+    p.meanQ = k.take<double>((size_t)nImg * 4);
     p.wC = k.take<float>(nImg);
     p.wR = k.take<float>((size_t)nImg * c.mLR);
     p.wT = k.take<float>((size_t)nImg * c.mLT);
@@ -1148,11 +1154,15 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     }
     for (int phase = phase0; phase < phase0 + nPh; phase++) {
         const bool large = phase == phase0 && (!global || c.largeFirst);
+        if (c.perturbMean == 1) {
+            hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat,
+                               c.acgIters, done, p.meanQ, nullptr);
+            THX_LAUNCH_CHECK();
+        }
         hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
                            trans, pR, pT, p.topQ, p.kv, p.sv,
                            large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
-                           c.seed, (uint32_t)(2000 + phase), c.perturbMean, c.acgIters, done,
-                           nullptr);
+                           c.seed, (uint32_t)(2000 + phase), c.perturbMean, p.meanQ, done);
         THX_LAUNCH_CHECK();
         hipEvent_t* ev = static_cast<hipEvent_t*>(c.phaseEvents);
         const int pi = phase - phase0;
