@@ -50,8 +50,12 @@ template <> struct Elt<F16X2> { typedef _Float16 T; typedef f16x8 V; };
 constexpr int KC = SCAN_KC;       // pixels per LDS stage (KC / 8 MFMA k-steps)
 static_assert(KC % 16 == 0, "whole float4 rows per thread in the stagers");
 constexpr int IMG_TILE = 64;
-constexpr int ROT_TILE = 8;
-constexpr int THREADS = 512;
+#ifndef SCAN_RT
+#define SCAN_RT 8
+#endif
+constexpr int ROT_TILE = SCAN_RT;     // rotations per workgroup, one per wave
+constexpr int THREADS = 64 * ROT_TILE;
+constexpr int NWAVE = ROT_TILE;
 constexpr int TROW = KC * 2 + 8;  // 16-bit elements per translation row of the T tile (80 B)
 constexpr int APITCH = KC + 2;    // float2 per image row of the a tile (144 B: aligned, conflict-free b128)
 constexpr int PMAX_BLOCKS = 256;
@@ -327,8 +331,8 @@ struct Smem {
     static constexpr int A_PC = A_F2 * 8 / 16;
     static constexpr int TQ = (T_PC + 63) / 64;            // wave instructions per plane
     static constexpr int AQ = (A_PC + 63) / 64;
-    static constexpr int PQ = P_F2 * 8 / 1024;             // KC / 16 (ROT_TILE = 8)
-    static_assert(PQ * 1024 == P_F2 * 8, "P rows = whole wave instructions");
+    static constexpr int P_PC = P_F2 * 8 / 16;             // 16-B pieces of the P rows
+    static constexpr int PQ = (P_PC + 63) / 64;
     static constexpr int NQ = NPLANE * TQ + AQ + PQ;
     static constexpr int TL_OFF = TQ * 1024;               // bytes: lo plane, a tile, P rows
     static constexpr int A_OFF = NPLANE * TQ * 1024;
@@ -348,7 +352,7 @@ THX_DEV void dma16(const void* g, void* ldsBase)
 }
 
 template <int MODE, int NF>
-__global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict__ Ac,
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) k_scan_split(const float2* __restrict__ Ac,
                                                         const float* __restrict__ Aconst,
                                                         const float* __restrict__ scale,
                                                         const float* __restrict__ bias,
@@ -403,15 +407,15 @@ __global__ void __launch_bounds__(THREADS) k_scan_split(const float2* __restrict
         const char* gA = reinterpret_cast<const char*>(Ac + ((size_t)ck * nImgPad + l0) * APITCH);
         const char* gP = reinterpret_cast<const char*>(Pc + ((size_t)ck * nRBk + rb) * ROT_TILE * KC);
 #pragma unroll
-        for (int u = 0; u < (S::NQ + 7) / 8; u++) {
-            const int q = u * 8 + w;                         // wave-uniform instruction
+        for (int u = 0; u < (S::NQ + NWAVE - 1) / NWAVE; u++) {
+            const int q = u * NWAVE + w;                     // wave-uniform instruction
             if (q < S::NQ) {
                 const char* g;
                 int pc, lim;
                 if (q < S::TQ) { g = gTh; pc = q * 64; lim = S::T_PC; }
                 else if (MODE == BF16X3 && q < 2 * S::TQ) { g = gTl; pc = (q - S::TQ) * 64; lim = S::T_PC; }
                 else if (q < S::NQ - S::PQ) { g = gA; pc = (q - S::NPLANE * S::TQ) * 64; lim = S::A_PC; }
-                else { g = gP; pc = (q - (S::NQ - S::PQ)) * 64; lim = S::PQ * 64; }
+                else { g = gP; pc = (q - (S::NQ - S::PQ)) * 64; lim = S::P_PC; }
                 if (pc + lane < lim) dma16(g + (size_t)(pc + lane) * 16, stage + q * 1024);
             }
         }
