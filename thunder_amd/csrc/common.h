@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
@@ -37,6 +38,20 @@ void set_error(const char* fmt, ...);
     } while (0)
 
 #define THX_LAUNCH_CHECK() THX_HIP(hipGetLastError())
+
+// Raise a kernel's dynamic-LDS limit once per device (the attribute is per
+// device; a host may drive several GPUs from one process).  `done` is the
+// kernel's own device bit mask.
+inline int set_max_lds(const void* fn, int bytes, std::atomic<unsigned>& done)
+{
+    int dev = 0;
+    THX_HIP(hipGetDevice(&dev));
+    const unsigned bit = dev < 32 ? 1u << dev : 0u;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return THX_OK;
+    THX_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done.fetch_or(bit, std::memory_order_release);
+    return THX_OK;
+}
 
 inline hipStream_t as_stream(thx_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -508,16 +508,15 @@ extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, 
     THX_CHECK_ARG(cv.ok() && wsBytes >= cv.off, "thx_insert3d_binned: workspace too small");
     hipStream_t s = thx::as_stream(stream);
     const size_t hist = (size_t)P.nt * sizeof(int);
-    static bool attr = false;
-    if (!attr) {
-        THX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_deposit),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)DEP_LDS));
-        THX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_pass<false>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, BIN_MAX_TILES * 4));
-        THX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_bin_pass<true>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, BIN_MAX_TILES * 4));
-        attr = true;
-    }
+    static std::atomic<unsigned> ldsSet[3];
+    int st = thx::set_max_lds(reinterpret_cast<const void*>(k_bin_deposit), (int)DEP_LDS, ldsSet[0]);
+    if (st == THX_OK)
+        st = thx::set_max_lds(reinterpret_cast<const void*>(k_bin_pass<false>), BIN_MAX_TILES * 4,
+                              ldsSet[1]);
+    if (st == THX_OK)
+        st = thx::set_max_lds(reinterpret_cast<const void*>(k_bin_pass<true>), BIN_MAX_TILES * 4,
+                              ldsSet[2]);
+    if (st != THX_OK) return st;
     for (int l0 = 0; l0 < nImg; l0 += P.nB) {
         const int nb = nImg - l0 < P.nB ? nImg - l0 : P.nB;
         THX_HIP(hipMemsetAsync(count, 0, hist, s));

@@ -639,12 +639,9 @@ int launch_main(const WS& ws, const Dims& d, const float* rotP, const double* pR
     dim3 grid((unsigned)(8 * thx::cdiv(nIT * d.nRB, 8)));
     constexpr int lds = Smem<MODE, NF>::TOTAL_B;
     static_assert(lds <= 160 * 1024, "scan stages exceed the LDS");
-    static bool attr = false;                 // idempotent: a race only repeats the call
-    if (!attr) {
-        THX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k_scan_split<MODE, NF>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        attr = true;
-    }
+    static std::atomic<unsigned> ldsSet{0};
+    const int st = thx::set_max_lds(reinterpret_cast<const void*>(k_scan_split<MODE, NF>), lds, ldsSet);
+    if (st != THX_OK) return st;
     hipLaunchKernelGGL((k_scan_split<MODE, NF>), grid, dim3(THREADS), lds, s, ws.Ac, ws.Aconst,
                        ws.scale, ws.bias, ws.Thi, ws.Tlo, ws.Pc,
                        ws.pTf, pR, d.nImg, d.nR, d.nT, d.nPxl, d.nImgPad, d.nPxlPad, d.nTPad,
