@@ -506,7 +506,7 @@ def main():
 
     if rank == 0 and not a.no_cpu_baseline:
         vol_np = vol.cpu().numpy()
-        n_cpu = 512
+        n_cpu = min(4096, dat.shape[0])   # room for the --cpu-seconds target (~12 s)
         extras["cpu_baseline"] = cpu_baseline(vol_np, N, pf, gset, dat[:n_cpu].cpu().numpy(),
                                               ctf[:n_cpu].cpu().numpy(), sig[:n_cpu].cpu().numpy(),
                                               px, a.cpu_seconds, a.phases)
