@@ -197,6 +197,36 @@ int thx_local_phase_sel(const thx_local_sel* sel, const float* vol, int volLayou
                         float* baseL, float* dvp, void* workspace, size_t wsBytes,
                         thx_stream_t stream);
 
+/* ---------------------------------------------------- CTF search (a2/a9) ---
+ * SEARCH_TYPE_CTF: the local phase over nD defocus samples per image.
+ * thx_defocus_pre -- allocPreCal's cSearch branch (src/Optimiser.cpp:
+ *   8124-8170) on device: freq[nPxl] (may be NULL), defocusP[nImg][nPxl],
+ *   K1[nImg], K2[nImg] from attr (nImg x 8, as thx_ctf).
+ * thx_ctf_search -- kernel_CalCTFL (gpu/src/Kernel.cu:481-515; CPU
+ *   src/Optimiser.cpp:1252-1271): ctfD[nImg][nD][nPxl] for the defocus
+ *   factors dD[nImg][nD]; phase shift and amplitude contrast from attr.
+ * thx_local_phase_d -- thx_local_phase_sel over (r, t, d) triples
+ *   (kernel_logDataVSLC + kernel_UpdateWLC, gpu/src/Kernel.cu:889-939,
+ *   1459-1554; CPU src/Optimiser.cpp:1225-1427): ctfD as above, pD[nImg][nD]
+ *   the defocus priors, wD[nImg][nD] their marginals; dvp (optional)
+ *   [nImg][nR][nT][nD]; nT * nD <= 1024; workspace
+ *   thx_local_phase_workspace(nImg, nR, nT * nD, nVisit); sel may be NULL. */
+int thx_defocus_pre(const float* attr, int nImg, const int* iCol, const int* iRow,
+                    int nPxl, int idim, float* freq, float* defocusP, float* K1,
+                    float* K2, thx_stream_t stream);
+int thx_ctf_search(const float* defocusP, const float* freq, const double* dD,
+                   int nD, const float* K1, const float* K2, const float* attr,
+                   int nImg, int nPxl, float* ctfD, thx_stream_t stream);
+int thx_local_phase_d(const thx_local_sel* sel, const float* vol, int volLayout,
+                      int vdim, int pf, const double* quat, int nR,
+                      const double* trans, int nT, int nD, const double* pC,
+                      const double* pR, const double* pT, const double* pD,
+                      const float* dat, const float* ctfD, const float* sigRcp,
+                      const int* iCol, const int* iRow, const int* pxOrder, int nOrd,
+                      int nPxl, int idim, int nImg, float* wC, float* wR, float* wT,
+                      float* wD, float* baseL, float* dvp, void* workspace,
+                      size_t wsBytes, thx_stream_t stream);
+
 /* Cell-expanded copy of a half-complex volume: cells[(k*vdim + j)*(vdim/2+1)
  * + i] holds the 8 Complex taps v(i+dx, j+dy, k+dz), (dz, dy, dx) in the box
  * order of getFTHalf (src/Image/Volume.cpp:491-563), rows / slices wrapped,

@@ -73,6 +73,21 @@ def lib():
                                      _i32p, _i32p, _c_int, _c_int]
     L.orc_fsc.restype = None
     L.orc_fsc.argtypes = [_f64p, _c_int, _f32p, _f32p, _c_int]
+    L.orc_defocus_pre.restype = None
+    L.orc_defocus_pre.argtypes = [_f32p, _i32p, _i32p, _c_int, _c_int, _f32p, _f32p,
+                                  ctypes.POINTER(_c_float), ctypes.POINTER(_c_float)]
+    L.orc_ctf_search.restype = None
+    L.orc_ctf_search.argtypes = [_f32p, _f32p, _f32p, _f64p, _c_int, _c_float, _c_float, _c_float,
+                                 _c_float, _c_int]
+    L.orc_local_phase_d.restype = None
+    L.orc_local_phase_d.argtypes = [_f32p, _c_int, _c_int, _f64p, _c_int, _f64p, _c_int, _c_int,
+                                    _c_double, _f64p, _f64p, _f64p, _f32p, _f32p, _f32p, _i32p,
+                                    _i32p, _c_int, _c_int, _f32p, _f32p, _f32p, _f32p, _f32p,
+                                    ctypes.c_void_p]
+    L.orc_insert_batch_d.restype = None
+    L.orc_insert_batch_d.argtypes = [_f32p, _f32p, _f64p, _i64p, _c_int, _c_int, _f32p, _f32p,
+                                     _f64p, _f64p, _f64p, _f64p, _f32p, _c_int, _c_int, _i32p,
+                                     _i32p, _c_int, _c_int]
     _lib = L
     return L
 
@@ -172,6 +187,57 @@ def local_phase(vol, vdim, pf, quat, trans, pC, pR, pT, dat, ctf_, sig, px, idim
                           _c(pT, np.float64), _cf(dat), _c(ctf_, np.float32), _c(sig, np.float32),
                           px.iCol, px.iRow, px.n, idim, wC, wR, wT, base, dvp.ctypes.data)
     return wC[0], wR, wT, base[0], dvp.reshape(nR, nT)
+
+
+def defocus_pre(px, attr, N):
+    """CTF-search precalculation of one image: (freq, defocusP, K1, K2)."""
+    freq = np.zeros(px.n, np.float32)
+    dfo = np.zeros(px.n, np.float32)
+    k1, k2 = _c_float(), _c_float()
+    lib().orc_defocus_pre(_c(attr, np.float32), px.iCol, px.iRow, px.n, N, freq, dfo,
+                          ctypes.byref(k1), ctypes.byref(k2))
+    return freq, dfo, k1.value, k2.value
+
+
+def ctf_search(dfo, freq, d, K1, K2, phase_shift, con_t):
+    """ctfD[nD][nPxl] of one image for the defocus factors d."""
+    d = _c(d, np.float64)
+    out = np.zeros(len(d) * len(freq), np.float32)
+    lib().orc_ctf_search(out, _c(dfo, np.float32), _c(freq, np.float32), d, len(d), K1, K2,
+                         phase_shift, con_t, len(freq))
+    return out.reshape(len(d), len(freq))
+
+
+def local_phase_d(vol, vdim, pf, quat, trans, pC, pR, pT, pD, dat, ctfD, sig, px, idim):
+    nR, nT, nD = len(quat), len(trans), len(pD)
+    wC = np.zeros(1, np.float32)
+    wR = np.zeros(nR, np.float32)
+    wT = np.zeros(nT, np.float32)
+    wD = np.zeros(nD, np.float32)
+    base = np.zeros(1, np.float32)
+    dvp = np.zeros(nR * nT * nD, np.float32)
+    lib().orc_local_phase_d(_cf(vol).reshape(-1), vdim, pf, _c(quat, np.float64).reshape(-1), nR,
+                            _c(trans, np.float64).reshape(-1), nT, nD, float(pC),
+                            _c(pR, np.float64), _c(pT, np.float64), _c(pD, np.float64), _cf(dat),
+                            _c(ctfD, np.float32).reshape(-1), _c(sig, np.float32), px.iCol,
+                            px.iRow, px.n, idim, wC, wR, wT, wD, base, dvp.ctypes.data)
+    return wC[0], wR, wT, wD, base[0], dvp.reshape(nR, nT, nD)
+
+
+def insert_batch_d(vdim, pf, dat, attr, nD, quat, trans, offS, w, px, idim):
+    """CTF-search insert: attr [nImg, 8], nD [nImg, mReco]."""
+    nImg, mReco = quat.shape[0], quat.shape[1]
+    size = (vdim // 2 + 1) * vdim * vdim
+    F = np.zeros(2 * size, np.float32)
+    T = np.zeros(size, np.float32)
+    O = np.zeros(3, np.float64)
+    cnt = np.zeros(1, np.int64)
+    lib().orc_insert_batch_d(F, T, O, cnt, vdim, pf, _cf(dat).reshape(-1),
+                             _c(attr, np.float32).reshape(-1), _c(nD, np.float64).reshape(-1),
+                             _c(quat, np.float64).reshape(-1), _c(trans, np.float64).reshape(-1),
+                             _c(offS, np.float64).reshape(-1), _c(w, np.float32), nImg, mReco,
+                             px.iCol, px.iRow, px.n, idim)
+    return F.view(np.complex64), T, O, int(cnt[0])
 
 
 def resample(w, u, n_out, u0):

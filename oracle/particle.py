@@ -66,6 +66,27 @@ def cal_vari_trans(T):
     return float(np.std(T[:, 0], ddof=1)), float(np.std(T[:, 1], ddof=1))
 
 
+def cal_vari_defocus(d):
+    """Particle::calVari(PAR_D) (src/Particle.cpp:1120-1141, ZERO_MEAN off):
+    gsl_stats_sd, 0 for a single sample."""
+    d = np.asarray(d, np.float64)
+    return 0.0 if d.size == 1 else float(np.std(d, ddof=1))
+
+
+def balance_defocus(d):
+    """Particle::balanceWeight(PAR_D) (src/Particle.cpp:2374-2409): w_i =
+    1 / N(d_i - m; 0, s) with the sample mean m and gsl_stats_sd_m s, 1 when
+    s == 0; returned normalised (normW)."""
+    d = np.asarray(d, np.float64)
+    m = d.mean()
+    s = 0.0 if d.size == 1 else np.sqrt(np.sum((d - m) ** 2) / (d.size - 1))
+    if s == 0:
+        w = np.ones_like(d)
+    else:
+        w = 1.0 / (np.exp(-0.5 * ((d - m) / s) ** 2) / (s * np.sqrt(2 * np.pi)))
+    return w / w.sum()
+
+
 def pdf_acg(x, A):
     """pdfACG (DirectionalStat.cpp:19-24): det(A)^-1/2 (x^T A^-1 x)^-2."""
     Ai = np.linalg.inv(A)

@@ -79,6 +79,42 @@ void orc_ctf(float* dst, float pixelSize, float voltage, float defocusU,
     }
 }
 
+/* a2, CTF search: allocPreCal's cSearch branch (src/Optimiser.cpp:8124-8170)
+ * for one image: frequency, per-pixel defocus, K1, K2 (its wavelength
+ * constant 12.2643274, quirk q5). */
+void orc_defocus_pre(const float* attr, const int* iCol, const int* iRow, int nPxl,
+                     int idim, float* freq, float* defocusP, float* K1, float* K2)
+{
+    const float pixelSize = attr[0], voltage = attr[1], dU = attr[2], dV = attr[3];
+    const float theta = attr[4], Cs = attr[5];
+    for (int i = 0; i < nPxl; i++) {
+        /* NORM(iCol, iRow) / size / pixelSize (:8138-8142) */
+        freq[i] = (float)(sqrt((double)iCol[i] * iCol[i] + (double)iRow[i] * iRow[i]) / idim /
+                          pixelSize);
+        float angle = (float)(atan2((double)iRow[i], (double)iCol[i]) - theta); /* :8149-8151 */
+        defocusP[i] = -(dU + dV + (dU - dV) * cosf(2 * angle)) / 2;             /* :8153-8157 */
+    }
+    float lambda = (float)(12.2643274 / sqrt((double)voltage * (1 + (double)voltage * 0.978466e-6)));
+    *K1 = (float)(M_PI * lambda);                                              /* :8167 */
+    *K2 = (float)(M_PI_2 * Cs * ((double)lambda * lambda * lambda));           /* :8168 */
+}
+
+/* a2, CTF search: the per-defocus-sample CTF of a local phase,
+ * src/Optimiser.cpp:1252-1271 (GPU twin kernel_CalCTFL, gpu/src/Kernel.cu:
+ * 481-515): ctfD[iD][i] for the image's defocus factors d[nD]. */
+void orc_ctf_search(float* ctfD, const float* defocusP, const float* freq, const double* d,
+                    int nD, float K1, float K2, float phaseShift, float conT, int nPxl)
+{
+    const float w1 = sqrtf(1 - (float)((double)conT * conT));
+    for (int iD = 0; iD < nD; iD++)
+        for (int i = 0; i < nPxl; i++) {
+            const double f2 = (double)freq[i] * freq[i];
+            const float ki = (float)((double)(K1 * defocusP[i]) * d[iD] * f2 + K2 * (f2 * f2) -
+                                     phaseShift);
+            ctfD[(size_t)iD * nPxl + i] = -w1 * sinf(ki) + conT * cosf(ki);
+        }
+}
+
 /* ---------------------------------------------------------------- a4 ---- */
 void orc_translate(float* dst, float nTransCol, float nTransRow, int nCol,
                    int nRow, const int* iCol, const int* iRow, int nPxl)
@@ -328,6 +364,60 @@ void orc_local_phase(const float* vol, int vdim, int pf, const double* quat,
     free(priAllP);
 }
 
+/* a9, CTF search: the same phase over (r, t, d) with one CTF per defocus
+ * sample (ctfD[nD][nPxl], orc_ctf_search) and the defocus priors pD --
+ * src/Optimiser.cpp:1225-1427 with nC = 1; dvp[r][t][d] (the layout of
+ * kernel_logDataVSLC, gpu/src/Kernel.cu:889-939). */
+void orc_local_phase_d(const float* vol, int vdim, int pf, const double* quat, int nR,
+                       const double* trans, int nT, int nD, double pC, const double* pR,
+                       const double* pT, const double* pD, const float* dat,
+                       const float* ctfD, const float* sigRcp, const int* iCol,
+                       const int* iRow, int nPxl, int idim, float* wC, float* wR, float* wT,
+                       float* wD, float* baseL, float* dvp)
+{
+    float* traP = (float*)malloc(sizeof(float) * 2 * (size_t)nT * nPxl);
+    float* priRotP = (float*)malloc(sizeof(float) * 2 * nPxl);
+    float* priAllP = (float*)malloc(sizeof(float) * 2 * nPxl);
+    for (int t = 0; t < nT; t++)
+        orc_translate(traP + 2 * (size_t)t * nPxl, (float)trans[2 * t],
+                      (float)trans[2 * t + 1], idim, idim, iCol, iRow, nPxl);
+    float baseLine = NAN;
+    wC[0] = 0;
+    for (int r = 0; r < nR; r++) wR[r] = 0;
+    for (int t = 0; t < nT; t++) wT[t] = 0;
+    for (int d = 0; d < nD; d++) wD[d] = 0;
+    for (int r = 0; r < nR; r++) {
+        double mat[9];
+        orc_rotate3d(mat, quat + 4 * r);
+        orc_project3d(priRotP, vol, vdim, pf, mat, iCol, iRow, nPxl);
+        for (int t = 0; t < nT; t++) {
+            cmul(priAllP, traP + 2 * (size_t)t * nPxl, priRotP, nPxl);
+            for (int d = 0; d < nD; d++) {
+                float w = orc_logdatavs(dat, priAllP, ctfD + (size_t)d * nPxl, sigRcp, nPxl);
+                if (dvp) dvp[((size_t)r * nT + t) * nD + d] = w;
+                baseLine = isnan(baseLine) ? w : baseLine;
+                if (w > baseLine) {
+                    float nf = expf(baseLine - w);
+                    wC[0] *= nf;
+                    for (int q = 0; q < nR; q++) wR[q] *= nf;
+                    for (int q = 0; q < nT; q++) wT[q] *= nf;
+                    for (int q = 0; q < nD; q++) wD[q] *= nf;
+                    baseLine = w;
+                }
+                float s = expf(w - baseLine);
+                wC[0] = (float)(wC[0] + s * (pR[r] * pT[t] * pD[d]));
+                wR[r] = (float)(wR[r] + s * (pC * pT[t] * pD[d]));
+                wT[t] = (float)(wT[t] + s * (pC * pR[r] * pD[d]));
+                wD[d] = (float)(wD[d] + s * (pC * pR[r] * pT[t]));
+            }
+        }
+    }
+    *baseL = baseLine;
+    free(traP);
+    free(priRotP);
+    free(priAllP);
+}
+
 /* --------------------------------------------------------------- a10 ---- */
 int orc_resample(int nIn, const double* w, const double* u, int nOut,
                  double u0, int* ancestor, double* wOut)
@@ -446,6 +536,50 @@ void orc_insert_batch(float* F, float* T, double* O, long* counter, int vdim,
             *counter += 1;
         }
     free(tr);
+    free(iColPad);
+    free(iRowPad);
+}
+
+/* a12 with CTF search: every sample (l, m) inserts with its own CTF,
+ * CTF(defocusU * d, defocusV * d) of the image's attributes (src/Optimiser.cpp:
+ * 7101-7120; GPU kernel_CalculateCTF, gpu/src/Kernel.cu:2206-2270); attr:
+ * nImg x 8 as thx_ctf, nD: nImg x mReco defocus factors. */
+void orc_insert_batch_d(float* F, float* T, double* O, long* counter, int vdim, int pf,
+                        const float* dat, const float* attr, const double* nD,
+                        const double* quat, const double* trans, const double* offS,
+                        const float* w, int nImg, int mReco, const int* iCol, const int* iRow,
+                        int nPxl, int idim)
+{
+    float* tr = (float*)malloc(sizeof(float) * 2 * nPxl);
+    float* ctf = (float*)malloc(sizeof(float) * nPxl);
+    int* iColPad = (int*)malloc(sizeof(int) * nPxl);
+    int* iRowPad = (int*)malloc(sizeof(int) * nPxl);
+    for (int i = 0; i < nPxl; i++) {
+        iColPad[i] = iCol[i] * pf;
+        iRowPad[i] = iRow[i] * pf;
+    }
+    for (int l = 0; l < nImg; l++)
+        for (int m = 0; m < mReco; m++) {
+            const size_t s = (size_t)l * mReco + m;
+            const double* q = quat + 4 * s;
+            const double* t = trans + 2 * s;
+            const float* a = attr + 8 * (size_t)l;
+            const double d = nD[s];
+            double dx = t[0] - offS[2 * l], dy = t[1] - offS[2 * l + 1];
+            double mat[9];
+            orc_rotate3d(mat, q);
+            orc_translate_src(tr, dat + 2 * (size_t)l * nPxl, (float)(-dx), (float)(-dy), idim,
+                              idim, iCol, iRow, nPxl);
+            orc_ctf(ctf, a[0], a[1], (float)(a[2] * d), (float)(a[3] * d), a[4], a[5], a[6], a[7],
+                    idim, idim, iCol, iRow, nPxl);
+            orc_insert3d(F, T, vdim, tr, ctf, mat, w[l], iColPad, iRowPad, nPxl);
+            O[0] += -(mat[0] * dx + mat[3] * dy);
+            O[1] += -(mat[1] * dx + mat[4] * dy);
+            O[2] += -(mat[2] * dx + mat[5] * dy);
+            *counter += 1;
+        }
+    free(tr);
+    free(ctf);
     free(iColPad);
     free(iRowPad);
 }

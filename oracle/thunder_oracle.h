@@ -42,6 +42,31 @@ void orc_ctf(float* dst, float pixelSize, float voltage, float defocusU,
              float phaseShift, int nCol, int nRow, const int* iCol,
              const int* iRow, int nPxl);
 
+/* a2, CTF search: allocPreCal's cSearch branch (src/Optimiser.cpp:8124-8170)
+ * for one image (attr as thx_ctf), and the per-defocus-sample CTF of a local
+ * phase (src/Optimiser.cpp:1252-1271, kernel_CalCTFL gpu/src/Kernel.cu:481). */
+void orc_defocus_pre(const float* attr, const int* iCol, const int* iRow, int nPxl,
+                     int idim, float* freq, float* defocusP, float* K1, float* K2);
+void orc_ctf_search(float* ctfD, const float* defocusP, const float* freq, const double* d,
+                    int nD, float K1, float K2, float phaseShift, float conT, int nPxl);
+
+/* a9, CTF search: local phase over (r, t, d), dvp[r][t][d]
+ * (src/Optimiser.cpp:1225-1427, nC = 1). */
+void orc_local_phase_d(const float* vol, int vdim, int pf, const double* quat, int nR,
+                       const double* trans, int nT, int nD, double pC, const double* pR,
+                       const double* pT, const double* pD, const float* dat,
+                       const float* ctfD, const float* sigRcp, const int* iCol,
+                       const int* iRow, int nPxl, int idim, float* wC, float* wR, float* wT,
+                       float* wD, float* baseL, float* dvp);
+
+/* a12, CTF search: insert with a per-sample CTF(defocus x d)
+ * (src/Optimiser.cpp:7101-7120). */
+void orc_insert_batch_d(float* F, float* T, double* O, long* counter, int vdim, int pf,
+                        const float* dat, const float* attr, const double* nD,
+                        const double* quat, const double* trans, const double* offS,
+                        const float* w, int nImg, int mReco, const int* iCol, const int* iRow,
+                        int nPxl, int idim);
+
 /* a4: translate(Complex* dst, tx, ty, ...) (src/Image/ImageFunctions.cpp:233-252). */
 void orc_translate(float* dst, float nTransCol, float nTransRow, int nCol,
                    int nRow, const int* iCol, const int* iRow, int nPxl);

@@ -31,6 +31,11 @@ SIGNATURES = {
     "thx_local_phase": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _p, _p,
                                  _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p, _p,
                                  _c_size, _p]),
+    "thx_defocus_pre": (_c_int, [_p, _c_int, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p]),
+    "thx_ctf_search": (_c_int, [_p, _p, _p, _c_int, _p, _p, _p, _c_int, _c_int, _p, _p]),
+    "thx_local_phase_d": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _c_int,
+                                   _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int,
+                                   _c_int, _p, _p, _p, _p, _p, _p, _p, _c_size, _p]),
     "thx_resample": (_c_int, [_c_int, _c_int, _p, _p, _c_int, _p, _p, _p, _p, _p]),
     "thx_pf_resample_workspace": (_c_size, [_c_int, _c_int]),
     "thx_pf_resample": (_c_int, [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, ctypes.c_ulonglong,

@@ -167,6 +167,31 @@ THX_DEV float2 phase_shift(int ic, int ir, float rCol, float rRow)
     return make_float2(__builtin_amdgcn_cosf(f), __builtin_amdgcn_sinf(f));
 }
 
+// CTF(RFLOAT*, ...) (src/CTF.cpp:113-151) at pixel (ic, ir) of an idim box
+// for attr a = {pixelSize, voltage, dU, dV, theta, Cs, ampContrast,
+// phaseShift} with the defocus pair (dU, dV) given separately (the CTF
+// search inserts with (dU d, dV d), src/Optimiser.cpp:7105-7119); the
+// per-image constants are formed as there (FP64 wavelength, then RFLOAT).
+THX_DEV float ctf_at(const float* a, float dU, float dV, int ic, int ir, int idim)
+{
+    const float pixelSize = a[0], voltage = a[1], theta = a[4], Cs = a[5];
+    const float ampC = a[6], phaseShift = a[7];
+    const float lambda =
+        (float)(12.2643247 / sqrt((double)voltage * (1 + (double)voltage * 0.978466e-6)));
+    const float w1 = sqrtf(1.f - (float)((double)ampC * ampC));
+    const float K1 = (float)(M_PI * lambda);
+    const float K2 = (float)(M_PI_2 * Cs * (float)((double)lambda * lambda * lambda));
+    const float fa = ic / (pixelSize * idim);
+    const float fb = ir / (pixelSize * idim);
+    const float u = (float)hypot((double)fa, (double)fb);
+    const float angle = (float)(atan2((double)ir, (double)ic) - theta);
+    const float defocus = -(dU + dV + (dU - dV) * cosf(2.f * angle)) / 2.f;
+    const float u2 = (float)((double)u * u);
+    const float u4 = (float)((double)u * u * u * u);
+    const float ki = K1 * defocus * u2 + K2 * u4 - phaseShift;
+    return -w1 * sinf(ki) + ampC * cosf(ki);
+}
+
 // rotate3D, src/Geometry/Euler.cpp:181-189: R = I + 2 q0 A + 2 A A with
 // A = [[0,-q3,q2],[q3,0,-q1],[-q2,q1,0]], stored column-major.
 THX_DEV void quat_to_mat(const double* q, double* m)

@@ -114,8 +114,7 @@ extern "C" int thx_pixel_tile_order(const int* iCol, const int* iRow, int nPxl, 
 
 // ---------------------------------------------------------------------- a2
 // One workgroup column per image, pixels across threads.  CTF(RFLOAT*, ...),
-// src/CTF.cpp:113-151; per-image constants are formed exactly as there (FP64
-// wavelength, then RFLOAT).
+// src/CTF.cpp:113-151 (ctf_at, common.h).
 __global__ void __launch_bounds__(256) k_ctf(const float* __restrict__ attr,
                                              const int* __restrict__ iCol,
                                              const int* __restrict__ iRow,
@@ -124,27 +123,9 @@ __global__ void __launch_bounds__(256) k_ctf(const float* __restrict__ attr,
 {
     const int l = blockIdx.y;
     const float* a = attr + 8 * l;
-    const float pixelSize = a[0], voltage = a[1], dU = a[2], dV = a[3];
-    const float theta = a[4], Cs = a[5], ampC = a[6], phaseShift = a[7];
-    const float lambda =
-        (float)(12.2643247 / sqrt((double)voltage * (1 + (double)voltage * 0.978466e-6)));
-    const float w1 = sqrtf(1.f - (float)((double)ampC * ampC));
-    const float w2 = ampC;
-    const float K1 = (float)(M_PI * lambda);
-    const float K2 = (float)(M_PI_2 * Cs * (float)((double)lambda * lambda * lambda));
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nPxl;
-         i += gridDim.x * blockDim.x) {
-        const int ic = iCol[i], ir = iRow[i];
-        const float fa = ic / (pixelSize * idim);
-        const float fb = ir / (pixelSize * idim);
-        const float u = (float)hypot((double)fa, (double)fb);
-        const float angle = (float)(atan2((double)ir, (double)ic) - theta);
-        const float defocus = -(dU + dV + (dU - dV) * cosf(2.f * angle)) / 2.f;
-        const float u2 = (float)((double)u * u);
-        const float u4 = (float)((double)u * u * u * u);
-        const float ki = K1 * defocus * u2 + K2 * u4 - phaseShift;
-        ctfP[(size_t)l * nPxl + i] = -w1 * sinf(ki) + w2 * cosf(ki);
-    }
+         i += gridDim.x * blockDim.x)
+        ctfP[(size_t)l * nPxl + i] = ctf_at(a, a[2], a[3], iCol[i], iRow[i], idim);
 }
 
 extern "C" int thx_ctf(const float* attr, int nImg, const int* iCol,
@@ -157,6 +138,91 @@ extern "C" int thx_ctf(const float* attr, int nImg, const int* iCol,
     dim3 grid(thx::cdiv(nPxl, 256) > 64 ? 64 : thx::cdiv(nPxl, 256), nImg);
     hipLaunchKernelGGL(k_ctf, grid, dim3(256), 0, thx::as_stream(stream), attr,
                        iCol, iRow, nPxl, idim, ctfP);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+// CTF search precalculation, the cSearch branch of allocPreCal
+// (src/Optimiser.cpp:8124-8170): frequency (shared), per-pixel defocus, K1,
+// K2 per image (the wavelength constant 12.2643274 of that branch, quirk q5).
+__global__ void __launch_bounds__(256) k_defocus_pre(const float* __restrict__ attr,
+                                                     const int* __restrict__ iCol,
+                                                     const int* __restrict__ iRow, int nPxl,
+                                                     int idim, float* __restrict__ freq,
+                                                     float* __restrict__ defocusP,
+                                                     float* __restrict__ K1,
+                                                     float* __restrict__ K2)
+{
+    const int l = blockIdx.y;
+    const float* a = attr + 8 * l;
+    const float pixelSize = a[0], voltage = a[1], dU = a[2], dV = a[3], theta = a[4];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nPxl; i += gridDim.x * blockDim.x) {
+        const int ic = iCol[i], ir = iRow[i];
+        if (l == 0 && freq)
+            freq[i] = (float)(sqrt((double)ic * ic + (double)ir * ir) / idim / pixelSize);
+        const float angle = (float)(atan2((double)ir, (double)ic) - theta);
+        defocusP[(size_t)l * nPxl + i] = -(dU + dV + (dU - dV) * cosf(2.f * angle)) / 2.f;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const float lambda =
+            (float)(12.2643274 / sqrt((double)voltage * (1 + (double)voltage * 0.978466e-6)));
+        K1[l] = (float)(M_PI * lambda);
+        K2[l] = (float)(M_PI_2 * a[5] * ((double)lambda * lambda * lambda));
+    }
+}
+
+// kernel_CalCTFL (gpu/src/Kernel.cu:481-515) / src/Optimiser.cpp:1252-1271:
+// ctfD[l][d][i] for the image's defocus factors dD[l][d]; one workgroup
+// column per (image, defocus sample).
+__global__ void __launch_bounds__(256) k_ctf_search(const float* __restrict__ defocusP,
+                                                    const float* __restrict__ freq,
+                                                    const double* __restrict__ dD, int nD,
+                                                    const float* __restrict__ K1,
+                                                    const float* __restrict__ K2,
+                                                    const float* __restrict__ attr, int nPxl,
+                                                    float* __restrict__ ctfD)
+{
+    const int l = blockIdx.y / nD, iD = blockIdx.y % nD;
+    const float conT = attr[8 * l + 6], ps = attr[8 * l + 7];
+    const float w1 = sqrtf(1.f - (float)((double)conT * conT));
+    const float k1 = K1[l], k2 = K2[l];
+    const double d = dD[(size_t)l * nD + iD];
+    const float* dfo = defocusP + (size_t)l * nPxl;
+    float* out = ctfD + ((size_t)l * nD + iD) * nPxl;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nPxl; i += gridDim.x * blockDim.x) {
+        const double f2 = (double)freq[i] * freq[i];
+        const float ki = (float)((double)(k1 * dfo[i]) * d * f2 + k2 * (f2 * f2) - ps);
+        out[i] = -w1 * sinf(ki) + conT * cosf(ki);
+    }
+}
+
+extern "C" int thx_defocus_pre(const float* attr, int nImg, const int* iCol, const int* iRow,
+                               int nPxl, int idim, float* freq, float* defocusP, float* K1,
+                               float* K2, thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && nPxl >= 0 && idim > 0, "thx_defocus_pre: bad sizes");
+    if (nImg == 0 || nPxl == 0) return THX_OK;
+    THX_CHECK_ARG(nImg <= 65535 * 64, "thx_defocus_pre: nImg too large");
+    THX_CHECK_ARG(attr && iCol && iRow && defocusP && K1 && K2, "thx_defocus_pre: null pointer");
+    dim3 grid(thx::cdiv(nPxl, 256) > 64 ? 64 : thx::cdiv(nPxl, 256), nImg);
+    hipLaunchKernelGGL(k_defocus_pre, grid, dim3(256), 0, thx::as_stream(stream), attr, iCol,
+                       iRow, nPxl, idim, freq, defocusP, K1, K2);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" int thx_ctf_search(const float* defocusP, const float* freq, const double* dD,
+                              int nD, const float* K1, const float* K2, const float* attr,
+                              int nImg, int nPxl, float* ctfD, thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && nPxl >= 0 && nD > 0, "thx_ctf_search: bad sizes");
+    if (nImg == 0 || nPxl == 0) return THX_OK;
+    THX_CHECK_ARG((long)nImg * nD <= 65535L * 64, "thx_ctf_search: nImg * nD too large");
+    THX_CHECK_ARG(defocusP && freq && dD && K1 && K2 && attr && ctfD,
+                  "thx_ctf_search: null pointer");
+    dim3 grid(thx::cdiv(nPxl, 256) > 16 ? 16 : thx::cdiv(nPxl, 256), nImg * nD);
+    hipLaunchKernelGGL(k_ctf_search, grid, dim3(256), 0, thx::as_stream(stream), defocusP, freq,
+                       dD, nD, K1, K2, attr, nPxl, ctfD);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }

@@ -476,7 +476,12 @@ THX_DEV void rotation_slots(const double* __restrict__ q4, int nRl, int tid,
 __device__ unsigned long long g_local_stamps[12];
 #endif
 
-template <bool CELLS>
+// CS (CTF search, SEARCH_TYPE_CTF): the columns are the nT x nD (t, d) pairs
+// of kernel_logDataVSLC (gpu/src/Kernel.cu:889-939), column j = t nD + d; the
+// image tile takes its CTF from ctfD[l][d] (thx_ctf_search) per column, and
+// the bias sum_i s c_d^2 |P|^2 now depends on the column, so it runs on the
+// MFMA as well: A = (re^2, im^2) regrouped like (re, im), B = (b_j, b_j).
+template <bool CELLS, bool CS = false>
 // two workgroups per CU (LDS-bound): 4 waves per SIMD, 128 VGPRs
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 k_local_fused(const float2* __restrict__ vol,
@@ -497,7 +502,7 @@ k_local_fused(const float2* __restrict__ vol,
                                                             const int* __restrict__ act,
                                                             const int* __restrict__ nAct,
                                                             const int* __restrict__ cls,
-                                                            long volStride)
+                                                            long volStride, int nD = 1)
 {
     int l = blockIdx.x;
     if (act) {
@@ -512,7 +517,7 @@ k_local_fused(const float2* __restrict__ vol,
     __shared__ __attribute__((aligned(16))) float2 sBox[BOX_CAP];
     __shared__ __attribute__((aligned(16))) float sB[KC * 2 * TT];   // [px][U, V][t]
     __shared__ __attribute__((aligned(16))) double2 sXY[KC];        // (iCol pf, iRow pf)
-    __shared__ float sBq[KC];                                        // b = s c^2
+    __shared__ float sBq[CS ? KC * TT : KC];                         // b = s c^2 ([px][col] for CS)
     __shared__ int sValid[KC];                                       // 0: padding entry
     __shared__ float sTr[TT][2];
     __shared__ float sRed[NWAVE];
@@ -533,10 +538,11 @@ k_local_fused(const float2* __restrict__ vol,
         quat_to_mat(q, mm);
         for (int k = 0; k < 6; k++) m[k] = mm[k];
     }
+    // columns: translations, or (t, d) pairs for CS (nT counts the columns)
     if (tid < TT) {
-        const int t = t0 + tid;
+        const int t = CS ? (t0 + tid) / nD : t0 + tid;
         float tx = 0.f, ty = 0.f;
-        if (t < nT) {
+        if (t0 + tid < nT) {
             tx = (float)trans[((size_t)l * nT + t) * 2];
             ty = (float)trans[((size_t)l * nT + t) * 2 + 1];
         }
@@ -545,7 +551,9 @@ k_local_fused(const float2* __restrict__ vol,
     }
 
     const float2* D = dat + (size_t)l * nPxl;
-    const float* C = ctf + (size_t)l * nPxl;
+    const int bpx = tid / TT, bt = tid % TT;
+    // CS: a staging thread's column has one defocus sample, so its CTF row is fixed
+    const float* C = ctf + ((size_t)l * nD + (CS ? (t0 + bt) % nD : 0)) * nPxl;
     const float* S = sig + (size_t)l * nPxl;
     const int nC = (nVisit + KC - 1) / KC;
     const int* R = rec + ((size_t)l * gridDim.y + blockIdx.y) * nC * REC;
@@ -553,7 +561,6 @@ k_local_fused(const float2* __restrict__ vol,
     float bias = 0.f, aConst = 0.f;
     // image-tile element staged by threads tid < KC * TT
     const bool stager = tid < KC * TT;
-    const int bpx = tid / TT, bt = tid % TT;
     const int g = lane >> 4;       // pixel slot of this lane in a step
     const int kk = lane >> 4, tc = lane & 15;   // B-operand row / column
 
@@ -598,9 +605,10 @@ k_local_fused(const float2* __restrict__ vol,
             }
             sB[(bpx * 2) * TT + bt] = U;
             sB[(bpx * 2 + 1) * TT + bt] = V;
+            if (CS) sBq[bpx * TT + bt] = ok && t0 + bt < nT ? px.s * px.c * px.c : 0.f;
             if (bt == 0) {
                 if (ok) aConst += px.s * (px.d.x * px.d.x + px.d.y * px.d.y);
-                sBq[bpx] = ok ? px.s * px.c * px.c : 0.f;
+                if (!CS) sBq[bpx] = ok ? px.s * px.c * px.c : 0.f;
                 sValid[bpx] = ok;
                 // padding entries sample the patch's first pixel (inside the box)
                 const int ic = ok ? px.ic : rc.v[17], ir = ok ? px.ir : rc.v[18];
@@ -625,7 +633,7 @@ k_local_fused(const float2* __restrict__ vol,
         // one step: the sample's bias term, then (re, im) of pixels 4s, 4s+2 and
         // 4s+1, 4s+3 regrouped into two MFMA A operands against [U, V]
         auto reduce_step = [&](int s, float2 P) {
-            bias += sBq[4 * s + g] * (P.x * P.x + P.y * P.y);
+            if (!CS) bias += sBq[4 * s + g] * (P.x * P.x + P.y * P.y);
             const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(P.x),
                                                              __float_as_uint(P.y), false, false);
             const int q0 = 4 * s + (kk < 2 ? 0 : 2), q1 = q0 + 1;
@@ -633,6 +641,14 @@ k_local_fused(const float2* __restrict__ vol,
             const float b1 = sB[(q1 * 2 + (kk & 1)) * TT + tc];
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[0]), b0, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[1]), b1, acc, 0, 0, 0);
+            if (CS) {
+                const auto sq = __builtin_amdgcn_permlane16_swap(
+                    __float_as_uint(P.x * P.x), __float_as_uint(P.y * P.y), false, false);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sq[0]),
+                                                           sBq[q0 * TT + tc], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sq[1]),
+                                                           sBq[q1 * TT + tc], acc, 0, 0, 0);
+            }
         };
         // a step whose four pixels are all padding adds exactly zero (U = V = b
         // = 0): skipped, wave-uniformly
@@ -687,7 +703,7 @@ k_local_fused(const float2* __restrict__ vol,
     // B_r: the four pixel slots of a rotation are lanes l, l + 16, l + 32, l + 48
     bias += __shfl_xor(bias, 16, 64);
     bias += __shfl_xor(bias, 32, 64);
-    if (lane < 16) sBias[rl] = bias;
+    if (lane < 16) sBias[rl] = CS ? 0.f : bias;
     __syncthreads();
     float Al = 0.f;
     for (int k = 0; k < NWAVE; k++) Al += sRed[k];
@@ -769,6 +785,76 @@ __global__ void __launch_bounds__(256) k_local_weights(const float* __restrict__
     __syncthreads();
     if (threadIdx.x == 0) {
         wC[l] = (float)(sd[0] + sd[1] + sd[2] + sd[3]);
+        baseL[l] = base;
+    }
+}
+
+// CTF search: the normalisation of src/Optimiser.cpp:1383-1402 with the
+// defocus axis (nC = 1): over dvp[r][t][d], s = exp(dvp - max),
+// wC = sum s pR pT pD, wR[r] = pC sum_{t,d} s pT pD, wT[t] = pC sum_{r,d} s pR pD,
+// wD[d] = pC sum_{r,t} s pR pT.  a[t][d] = sum_r s pR goes through LDS.
+constexpr int LOCAL_D_MAXCOL = 1024;
+__global__ void __launch_bounds__(256) k_local_weights_d(const float* __restrict__ dvp, int nR,
+                                                         int nT, int nD,
+                                                         const double* __restrict__ pC,
+                                                         const double* __restrict__ pR,
+                                                         const double* __restrict__ pT,
+                                                         const double* __restrict__ pD,
+                                                         float* __restrict__ wC,
+                                                         float* __restrict__ wR,
+                                                         float* __restrict__ wT,
+                                                         float* __restrict__ wD,
+                                                         float* __restrict__ baseL,
+                                                         const int* __restrict__ act,
+                                                         const int* __restrict__ nAct)
+{
+    int l = blockIdx.x;
+    if (act) {
+        if (l >= *nAct) return;
+        l = act[l];
+    }
+    const int nCol = nT * nD;
+    const float* Dl = dvp + (size_t)l * nR * nCol;
+    const double* pRl = pR + (size_t)l * nR;
+    const double* pTl = pT + (size_t)l * nT;
+    const double* pDl = pD + (size_t)l * nD;
+    const double c = pC[l];
+    __shared__ float sm[4];
+    __shared__ double sA[LOCAL_D_MAXCOL];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float m = -INFINITY;
+    for (int q = threadIdx.x; q < nR * nCol; q += blockDim.x) m = fmaxf(m, Dl[q]);
+    m = wave_max(m);
+    if (lane == 0) sm[wv] = m;
+    __syncthreads();
+    const float base = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+    for (int r = threadIdx.x; r < nR; r += blockDim.x) {
+        double a = 0.0;
+        for (int t = 0; t < nT; t++)
+            for (int d = 0; d < nD; d++)
+                a += (double)expf(Dl[(size_t)r * nCol + t * nD + d] - base) * (pTl[t] * pDl[d]);
+        wR[(size_t)l * nR + r] = (float)(a * c);
+    }
+    for (int q = threadIdx.x; q < nCol; q += blockDim.x) {
+        double a = 0.0;
+        for (int r = 0; r < nR; r++) a += (double)expf(Dl[(size_t)r * nCol + q] - base) * pRl[r];
+        sA[q] = a;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < nT; t += blockDim.x) {
+        double a = 0.0;
+        for (int d = 0; d < nD; d++) a += sA[t * nD + d] * pDl[d];
+        wT[(size_t)l * nT + t] = (float)(a * c);
+    }
+    for (int d = threadIdx.x; d < nD; d += blockDim.x) {
+        double a = 0.0;
+        for (int t = 0; t < nT; t++) a += sA[t * nD + d] * pTl[t];
+        wD[(size_t)l * nD + d] = (float)(a * c);
+    }
+    if (threadIdx.x == 0) {
+        double a = 0.0;
+        for (int q = 0; q < nCol; q++) a += sA[q] * (pTl[q / nD] * pDl[q % nD]);
+        wC[l] = (float)a;
         baseL[l] = base;
     }
 }
@@ -869,6 +955,8 @@ extern "C" size_t thx_local_phase_workspace(int nImg, int nR, int nT, int nVisit
     return dvp_bytes(nImg, nR, nT) + rec_bytes(nImg, nR, nVisit) + 512;
 }
 
+// nD = 0: the phase without CTF search; nD >= 1: CTF search over nD defocus
+// samples (ctf = ctfD[nImg][nD][nPxl], priors pD[nImg][nD], marginal wD).
 static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
                             const float* vol, int volLayout, int vdim,
                             int pf, const double* quat, int nR, const double* trans, int nT,
@@ -876,13 +964,17 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
                             const float* ctf, const float* sigRcp, const int* iCol, const int* iRow,
                             const int* pxOrder, int nOrd, int nPxl, int idim, int nImg, float* wC,
                             float* wR, float* wT, float* baseL, float* dvp, void* workspace,
-                            size_t wsBytes, thx_stream_t stream)
+                            size_t wsBytes, thx_stream_t stream, int nD = 0,
+                            const double* pD = nullptr, float* wD = nullptr)
 {
-    THX_CHECK_ARG(nR > 0 && nT > 0 && nPxl > 0 && nImg >= 0 && vdim > 0 && pf > 0,
+    THX_CHECK_ARG(nR > 0 && nT > 0 && nPxl > 0 && nImg >= 0 && vdim > 0 && pf > 0 && nD >= 0,
                   "thx_local_phase: bad sizes");
+    THX_CHECK_ARG(!nD || (pD && wD && (long)nT * nD <= LOCAL_D_MAXCOL),
+                  "thx_local_phase_d: needs pD, wD and nT * nD <= 1024");
+    const int nCol = nD ? nT * nD : nT;
     THX_CHECK_ARG(volLayout == 0 || volLayout == 1, "thx_local_phase: volLayout must be 0 or 1");
     THX_CHECK_ARG((long)nImg * ((nR + RT - 1) / RT) <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 &&
-                      (nT + TT - 1) / TT <= 65535,
+                      (nCol + TT - 1) / TT <= 65535,
                   "thx_local_phase: grid too large");
     THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % KC == 0),
                   "thx_local_phase: nOrd must be a positive multiple of 16 (thx_pixel_tile_order)");
@@ -893,18 +985,31 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     THX_CHECK_ARG(!cls || (sel->volStride > 0), "thx_local_phase_sel: cls needs a volStride");
     if (nImg == 0) return THX_OK;
     const int nVisit = pxOrder ? nOrd : nPxl;
-    THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase_workspace(nImg, nR, nT, nVisit),
+    THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase_workspace(nImg, nR, nCol, nVisit),
                   "thx_local_phase: workspace too small");
     thx::Carver ws(workspace, wsBytes);
-    float* d = dvp ? dvp : ws.take<float>((size_t)nImg * nR * nT);
+    float* d = dvp ? dvp : ws.take<float>((size_t)nImg * nR * nCol);
     int* rec = ws.take<int>(rec_bytes(nImg, nR, nVisit) / sizeof(int));
     hipStream_t s = thx::as_stream(stream);
     hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * thx::cdiv(nR, RT)), dim3(64 * PB_WAVES),
                        0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct);
     THX_LAUNCH_CHECK();
-    dim3 grid(nImg, thx::cdiv(nR, RT), thx::cdiv(nT, TT));
+    dim3 grid(nImg, thx::cdiv(nR, RT), thx::cdiv(nCol, TT));
     const long vs = cls ? (long)sel->volStride : 0L;
     if (evBeg) THX_HIP(hipEventRecord(evBeg, s));
+    if (nD) {
+        auto kern = volLayout == 1 ? k_local_fused<true, true> : k_local_fused<false, true>;
+        hipLaunchKernelGGL(kern, grid, dim3(THREADS), 0, s, reinterpret_cast<const float2*>(vol),
+                           vdim, pf, quat, nR, trans, nCol, reinterpret_cast<const float2*>(dat),
+                           ctf, sigRcp, iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, d, act, nAct,
+                           cls, vs, nD);
+        THX_LAUNCH_CHECK();
+        if (evEnd) THX_HIP(hipEventRecord(evEnd, s));
+        hipLaunchKernelGGL(k_local_weights_d, dim3(nImg), dim3(256), 0, s, d, nR, nT, nD, pC, pR,
+                           pT, pD, wC, wR, wT, wD, baseL, act, nAct);
+        THX_LAUNCH_CHECK();
+        return THX_OK;
+    }
     if (volLayout == 1)
         hipLaunchKernelGGL(k_local_fused<true>, grid, dim3(THREADS), 0, s,
                            reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
@@ -953,6 +1058,22 @@ extern "C" int thx_local_phase_sel(const thx_local_sel* sel, const float* vol, i
     return local_phase_impl(sel, nullptr, nullptr, vol, volLayout, vdim, pf, quat, nR, trans, nT,
                             pC, pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim,
                             nImg, wC, wR, wT, baseL, dvp, workspace, wsBytes, stream);
+}
+
+extern "C" int thx_local_phase_d(const thx_local_sel* sel, const float* vol, int volLayout,
+                                 int vdim, int pf, const double* quat, int nR,
+                                 const double* trans, int nT, int nD, const double* pC,
+                                 const double* pR, const double* pT, const double* pD,
+                                 const float* dat, const float* ctfD, const float* sigRcp,
+                                 const int* iCol, const int* iRow, const int* pxOrder, int nOrd,
+                                 int nPxl, int idim, int nImg, float* wC, float* wR, float* wT,
+                                 float* wD, float* baseL, float* dvp, void* workspace,
+                                 size_t wsBytes, thx_stream_t stream)
+{
+    THX_CHECK_ARG(nD > 0, "thx_local_phase_d: nD must be positive");
+    return local_phase_impl(sel, nullptr, nullptr, vol, volLayout, vdim, pf, quat, nR, trans, nT,
+                            pC, pR, pT, dat, ctfD, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim,
+                            nImg, wC, wR, wT, baseL, dvp, workspace, wsBytes, stream, nD, pD, wD);
 }
 
 namespace thx {

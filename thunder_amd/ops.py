@@ -96,6 +96,38 @@ def ctf(attr, px):
     return out
 
 
+def defocus_pre(attr, px):
+    """CTF-search precalculation (allocPreCal's cSearch branch): freq [nPxl],
+    defocusP [nImg, nPxl], K1, K2 [nImg]."""
+    nImg = attr.shape[0]
+    _req(attr, torch.float32, (nImg, 8), "attr")
+    dev = attr.device
+    freq = torch.empty(px.n, dtype=torch.float32, device=dev)
+    dfo = torch.empty(nImg, px.n, dtype=torch.float32, device=dev)
+    k1 = torch.empty(nImg, dtype=torch.float32, device=dev)
+    k2 = torch.empty(nImg, dtype=torch.float32, device=dev)
+    check(lib().thx_defocus_pre(_ptr(attr), nImg, _ptr(px.d_iCol), _ptr(px.d_iRow), px.n, px.idim,
+                                _ptr(freq), _ptr(dfo), _ptr(k1), _ptr(k2), _stream(dev)),
+          "thx_defocus_pre")
+    return freq, dfo, k1, k2
+
+
+def ctf_search(dfo, freq, dD, k1, k2, attr):
+    """kernel_CalCTFL: ctfD [nImg, nD, nPxl] for the defocus factors dD [nImg, nD]."""
+    nImg, nPxl = dfo.shape
+    nD = dD.shape[1]
+    _req(dfo, torch.float32, (nImg, nPxl), "defocusP")
+    _req(freq, torch.float32, (nPxl,), "freq")
+    _req(dD, torch.float64, (nImg, nD), "dD")
+    _req(k1, torch.float32, (nImg,), "K1")
+    _req(k2, torch.float32, (nImg,), "K2")
+    _req(attr, torch.float32, (nImg, 8), "attr")
+    out = torch.empty(nImg, nD, nPxl, dtype=torch.float32, device=dfo.device)
+    check(lib().thx_ctf_search(_ptr(dfo), _ptr(freq), _ptr(dD), nD, _ptr(k1), _ptr(k2), _ptr(attr),
+                               nImg, nPxl, _ptr(out), _stream(dfo.device)), "thx_ctf_search")
+    return out
+
+
 # ------------------------------------------------------------------- a4
 def trans_table(trans, px):
     nT = trans.shape[0]
@@ -238,6 +270,50 @@ def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False
                                     _ptr(d[l0:]) if d is not None else None, _ptr(ws),
                                     ws.numel(), _stream(dev)), "thx_local_phase")
     return wC, wR, wT, base, d
+
+
+def local_phase_d(vol, quat, trans, pC, pR, pT, pD, dat, ctfD, sig, px, want_dvp=False,
+                  cells=None, tiled=True):
+    """CTF-search phase (thx_local_phase_d): ctfD [nImg, nD, nPxl], pD [nImg, nD];
+    returns wC, wR, wT, wD, baseL, dvp [nImg, nR, nT, nD] (or None)."""
+    vdim = _vol_dim(vol)
+    layout = 0
+    if cells is not None:
+        _req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
+        layout = 1
+    nImg, nPxl = dat.shape
+    nR, nT, nD = quat.shape[1], trans.shape[1], pD.shape[1]
+    dev = dat.device
+    _req(dat, torch.complex64, (nImg, nPxl), "dat")
+    _req(ctfD, torch.float32, (nImg, nD, nPxl), "ctfD")
+    _req(sig, torch.float32, (nImg, nPxl), "sig")
+    if nPxl != px.n:
+        raise ValueError("pixel set / image size mismatch")
+    _req(quat, torch.float64, (nImg, nR, 4), "quat")
+    _req(trans, torch.float64, (nImg, nT, 2), "trans")
+    _req(pC, torch.float64, (nImg,), "pC")
+    _req(pR, torch.float64, (nImg, nR), "pR")
+    _req(pT, torch.float64, (nImg, nT), "pT")
+    _req(pD, torch.float64, (nImg, nD), "pD")
+    if nImg > 65535:
+        raise ValueError("local_phase_d: at most 65535 images per call")
+    wC = torch.empty(nImg, dtype=torch.float32, device=dev)
+    wR = torch.empty(nImg, nR, dtype=torch.float32, device=dev)
+    wT = torch.empty(nImg, nT, dtype=torch.float32, device=dev)
+    wD = torch.empty(nImg, nD, dtype=torch.float32, device=dev)
+    base = torch.empty(nImg, dtype=torch.float32, device=dev)
+    d = torch.empty(nImg, nR, nT, nD, dtype=torch.float32, device=dev) if want_dvp else None
+    ws = workspace(lib().thx_local_phase_workspace(nImg, nR, nT * nD,
+                                                   len(px.order) if tiled else nPxl), dev)
+    check(lib().thx_local_phase_d(None, _ptr(cells if layout else vol), layout, vdim, px.pf,
+                                  _ptr(quat), nR, _ptr(trans), nT, nD, _ptr(pC), _ptr(pR),
+                                  _ptr(pT), _ptr(pD), _ptr(dat), _ptr(ctfD), _ptr(sig),
+                                  _ptr(px.d_iCol), _ptr(px.d_iRow),
+                                  _ptr(px.d_order) if tiled else None, len(px.order), nPxl,
+                                  px.idim, nImg, _ptr(wC), _ptr(wR), _ptr(wT), _ptr(wD),
+                                  _ptr(base), _ptr(d), _ptr(ws), ws.numel(), _stream(dev)),
+          "thx_local_phase_d")
+    return wC, wR, wT, wD, base, d
 
 
 # ------------------------------------------------------------------ a10
