@@ -280,6 +280,14 @@ int thx_pf_resample(int nImg, int nIn, int nOut, const double* w, int ldw,
 int thx_pf_calvari(int nImg, int mR, const double* quat, int mT, const double* trans,
                    double kFloor, double sFloor, double* k, double* sd, thx_stream_t stream);
 int thx_pf_balance_rot(int nImg, int mR, const double* quat, double* pR, thx_stream_t stream);
+/* Defocus particles of a CTF search (nImg x mD, one image per 16 lanes):
+ * op 0 initD (src/Particle.cpp:281-310): d = 1 + N(0, arg), pD =
+ * balanceWeight(PAR_D) (:2374-2409); op 1 perturb(arg, PAR_D) (:1278-1288):
+ * d += N(0, sd[l]) arg, pD as op 0; op 2 calVari(PAR_D) (:1120-1141): sd[l]
+ * = sample standard deviation (0 for mD = 1).  Counter RNG (seed, stream_id). */
+int thx_pf_defocus(int nImg, int mD, int op, double arg, unsigned long long seed,
+                   unsigned stream_id, double* d, double* pD, double* sd,
+                   thx_stream_t stream);
 int thx_pf_peak(int nImg, int n, float* u, int ldu, double* peak, int setFactor,
                 thx_stream_t stream);
 
@@ -507,6 +515,34 @@ int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                     double* trans, double* pR, double* pT, float* score,
                     int* cls, int* nPhaseOut,
                     void* workspace, size_t wsBytes, thx_stream_t stream);
+
+/* SEARCH_TYPE_CTF (cfg->searchType == 2): a local search from the caller's
+ * particle state whose phases also sample mLD defocus factors per image --
+ * initD at phase 0, perturb(perturbFactorSCTF, PAR_D) after, the CTF per
+ * defocus sample from the images' CTF attributes (allocPreCal's cSearch
+ * branch + kernel_CalCTFL), the (r, t, d) likelihood, calVari / resample of
+ * the defocus set and variD in the stopping rule (src/Optimiser.cpp:
+ * 1159-1616, the SEARCH_TYPE_CTF branches; src/Particle.cpp:281-310,
+ * 1120-1141, 1278-1288, 2374-2409).  d / pD (device, nImg x mLD) receive
+ * the final defocus particles and their priors. */
+typedef struct thx_ctf_search_cfg {
+    int mLD;                   /* defocus samples per particle ("Number of Sampling Points of
+                                  Defocus in Local Search", 9 in script/demo.json) */
+    double ctfRefineS;         /* initD spread ("CTF Refine Standard Deviation", 0.01) */
+    double perturbFactorSCTF;  /* "Perturbation Factor (Small, CTF)" (0.5) */
+    const float* attr;         /* device, nImg x 8 CTF attributes (as thx_ctf) */
+    double* d;                 /* device, nImg x mLD: out */
+    double* pD;                /* device, nImg x mLD: out */
+} thx_ctf_search_cfg;
+size_t thx_expectation_ctf_workspace(const thx_expect_cfg* cfg,
+                                     const thx_ctf_search_cfg* cs, int nImg,
+                                     int nPxl, int nOrd);
+int thx_expectation_ctf(const thx_expect_cfg* cfg, const thx_ctf_search_cfg* cs,
+                        const float* vol, const float* dat, const float* sigRcp,
+                        const int* iCol, const int* iRow, const int* pxOrder, int nOrd,
+                        int nPxl, int nImg, double* quat, double* trans, double* pR,
+                        double* pT, float* score, int* cls, int* nPhaseOut,
+                        void* workspace, size_t wsBytes, thx_stream_t stream);
 
 /* HIP event pairs for thx_expect_cfg.phaseEvents: create n (begin, end)
  * pairs, read back ms[i] per pair (-1: not recorded), destroy. */

@@ -116,3 +116,77 @@ def test_local_phase_d_one_sample_matches_plain_phase(orc, stack):
         m = a >= 1e-4 * a.max(axis=1, keepdims=True)
         assert np.all(np.abs(a - b)[m] <= 1e-3 * a[m])
     assert torch.allclose(r2[3][:, 0], r1[0] * T(pC, torch.float32), rtol=1e-4)
+
+
+@pytest.mark.parametrize("mD", [1, 9, 40])
+def test_pf_defocus_ops(mD):
+    from oracle import particle
+    nImg = 64
+    d = torch.zeros(nImg, mD, dtype=torch.float64, device=DEV)
+    pD = torch.zeros_like(d)
+    sd = torch.zeros(nImg, dtype=torch.float64, device=DEV)
+    ops.pf_defocus("init", d, pD, arg=0.01, seed=3)
+    dn, pn = d.cpu().numpy(), pD.cpu().numpy()
+    assert np.all(np.abs(dn - 1) < 0.08)
+    if mD == 40:
+        assert abs(np.std(dn - 1) - 0.01) < 0.001
+    for l in range(nImg):
+        assert np.allclose(pn[l], particle.balance_defocus(dn[l]), rtol=1e-12, atol=0)
+    ops.pf_defocus("vari", d, sd=sd)
+    sn = sd.cpu().numpy()
+    for l in range(nImg):
+        assert np.isclose(sn[l], particle.cal_vari_defocus(dn[l]), rtol=1e-12, atol=0)
+    d0 = dn.copy()
+    ops.pf_defocus("perturb", d, pD, sd, arg=0.5, seed=3, stream_id=1)
+    dn, pn = d.cpu().numpy(), pD.cpu().numpy()
+    if mD > 1:
+        step = (dn - d0) / (sn[:, None] * 0.5)
+        assert abs(np.std(step) - 1) < 0.2 and abs(np.mean(step)) < 0.2
+    else:
+        assert np.array_equal(dn, d0)       # s = 0 for a single sample
+    for l in range(nImg):
+        assert np.allclose(pn[l], particle.balance_defocus(dn[l]), rtol=1e-12, atol=0)
+
+
+def test_ctf_search_driver_refines_defocus():
+    """SEARCH_TYPE_CTF from a particle state near the true pose: the defocus
+    particles move toward each image's true defocus factor, the pose stays
+    refined, the priors are normalised and the stopping rule runs."""
+    from thunder_amd import expectation as ex
+    N, rU, n = 64, 16, 128
+    vol = synth.projectee(synth.blob_volume(N, seed=31, device=DEV), 2)
+    px = ops.PixelSet(N, 2, rU, 1, device=DEV)
+    rng = np.random.default_rng(32)
+    qtrue = synth.uniform_quaternions(n, rng)
+    ttrue = rng.standard_normal((n, 2))
+    attrs = synth.ctf_attrs(n, seed=33)
+    dtrue = 1 + rng.uniform(-0.03, 0.03, n)
+    a_true = attrs.copy()
+    a_true[:, 2:4] *= dtrue[:, None]
+    ctf = ops.ctf(T(a_true), px)
+    sigl = ctf * ops.project3d(vol, ops.rotmat(T(qtrue)), px) * ops.trans_table(T(ttrue), px)
+    dat, sig = synth.noisy_images(sigl, px.iSig, N // 2 + 1, snr=5.0, seed=34)
+    mR, mT = 125, 9
+    e0 = rng.standard_normal((n, mR, 4)) * np.radians(1.0) / 2
+    e0[..., 0] = 1.0
+    e0 /= np.linalg.norm(e0, axis=-1, keepdims=True)
+    w0, x0, y0, z0 = [qtrue[:, None, k] for k in range(4)]
+    w1, x1, y1, z1 = [e0[..., k] for k in range(4)]
+    quat = np.stack([w0 * w1 - x0 * x1 - y0 * y1 - z0 * z1, w0 * x1 + x0 * w1 + y0 * z1 - z0 * y1,
+                     w0 * y1 - x0 * z1 + y0 * w1 + z0 * x1, w0 * z1 + x0 * y1 - y0 * x1 + z0 * w1], -1)
+    trans = ttrue[:, None, :] + rng.uniform(-0.5, 0.5, (n, mT, 2))
+    state = (T(quat), T(trans), T(np.full((n, mR), 1.0 / mR)), T(np.full((n, mT), 1.0 / mT)))
+    e = ex.Expectation(vol, px, None, search="ctf", converge=True, seed=5, mLD=9)
+    q, t, pR, pT, score, cls, nph, d, pD = e.run_ctf(dat, T(attrs), sig, state)
+    dm = d.mean(1).cpu().numpy()
+    err0 = np.median(np.abs(1 - dtrue))
+    err = np.median(np.abs(dm - dtrue))
+    assert err < 0.6 * err0, (err, err0)
+    assert torch.allclose(pD.sum(1), torch.ones(n, dtype=torch.float64, device=DEV), rtol=1e-9)
+    assert torch.allclose(pR.sum(1), torch.ones(n, dtype=torch.float64, device=DEV), rtol=1e-9)
+    assert torch.isfinite(score).all() and torch.isfinite(d).all()
+    nph = nph.cpu().numpy()
+    assert nph.min() >= 4 and nph.max() <= 99
+    qm = ex.cloud_mode(q).cpu().numpy()
+    ang = np.degrees(2 * np.arccos(np.clip(np.abs(np.sum(qm * qtrue, 1)), 0, 1)))
+    assert np.median(ang) < 2.0

@@ -36,6 +36,11 @@ SIGNATURES = {
     "thx_local_phase_d": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _c_int,
                                    _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int,
                                    _c_int, _p, _p, _p, _p, _p, _p, _p, _c_size, _p]),
+    "thx_pf_defocus": (_c_int, [_c_int, _c_int, _c_int, _c_double, ctypes.c_ulonglong, ctypes.c_uint,
+                                _p, _p, _p, _p]),
+    "thx_expectation_ctf_workspace": (_c_size, [_p, _p, _c_int, _c_int, _c_int]),
+    "thx_expectation_ctf": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _p, _p,
+                                     _p, _p, _p, _p, _p, _p, _c_size, _p]),
     "thx_resample": (_c_int, [_c_int, _c_int, _p, _p, _c_int, _p, _p, _p, _p, _p]),
     "thx_pf_resample_workspace": (_c_size, [_c_int, _c_int]),
     "thx_pf_resample": (_c_int, [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, ctypes.c_ulonglong,

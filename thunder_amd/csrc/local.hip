@@ -543,8 +543,9 @@ k_local_fused(const float2* __restrict__ vol,
         const int t = CS ? (t0 + tid) / nD : t0 + tid;
         float tx = 0.f, ty = 0.f;
         if (t0 + tid < nT) {
-            tx = (float)trans[((size_t)l * nT + t) * 2];
-            ty = (float)trans[((size_t)l * nT + t) * 2 + 1];
+            const size_t ti = (size_t)l * (CS ? nT / nD : nT) + t;   // translation rows
+            tx = (float)trans[ti * 2];
+            ty = (float)trans[ti * 2 + 1];
         }
         sTr[tid][0] = tx / idim;   // rCol of translate(), ImageFunctions.cpp:243
         sTr[tid][1] = ty / idim;
@@ -1084,10 +1085,11 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       const double* pT, const float* dat, const float* ctf, const float* sigRcp,
                       const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
                       int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
-                      void* workspace, size_t wsBytes, thx_stream_t stream)
+                      void* workspace, size_t wsBytes, thx_stream_t stream, int nD,
+                      const double* pD, float* wD)
 {
     return local_phase_impl(sel, evBeg, evEnd, vol, 0, vdim, pf, quat, nR, trans, nT, pC, pR, pT,
                             dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg, wC, wR,
-                            wT, baseL, nullptr, workspace, wsBytes, stream);
+                            wT, baseL, nullptr, workspace, wsBytes, stream, nD, pD, wD);
 }
 }  // namespace thx

@@ -32,7 +32,8 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       const double* pT, const float* dat, const float* ctf, const float* sigRcp,
                       const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
                       int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
-                      void* workspace, size_t wsBytes, thx_stream_t stream);
+                      void* workspace, size_t wsBytes, thx_stream_t stream, int nD = 0,
+                      const double* pD = nullptr, float* wD = nullptr);
 }
 
 namespace {
@@ -791,10 +792,14 @@ __global__ void __launch_bounds__(256) k_pf_class(int nImg, int K, const float* 
 // afterwards one phase without a 5 % decrease of either ends the image
 // (N_PHASE_WITH_NO_VARI_DECREASE = 1) and _nP = phase.  lastPhase: the loop's
 // end (MAX_N_PHASE_PER_ITER - 1).
+// sdD / bestD (CTF search, else NULL): variD = _s (src/Particle.cpp:642-645)
+// joins the criterion (src/Optimiser.cpp:1557-1559, 1591).
 __global__ void k_pf_converge(int nImg, int phase, int minPhase, int lastPhase,
                               const double* __restrict__ kv, const double* __restrict__ sv,
                               double* __restrict__ bestR, double* __restrict__ bestT,
-                              int* __restrict__ done, int* __restrict__ nP)
+                              int* __restrict__ done, int* __restrict__ nP,
+                              const double* __restrict__ sdD = nullptr,
+                              double* __restrict__ bestD = nullptr)
 {
     const int l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= nImg || done[l]) return;
@@ -803,9 +808,14 @@ __global__ void k_pf_converge(int nImg, int phase, int minPhase, int lastPhase,
         const double vR = pow(kv[3 * l] * kv[3 * l + 1] * kv[3 * l + 2], 1.0 / 6);
         const double vT = sv[2 * l] * sv[2 * l + 1];
         const bool first = phase == minPhase;
-        const bool room = first || vR < bestR[l] * 0.95 || vT < bestT[l] * 0.95;
+        bool room = first || vR < bestR[l] * 0.95 || vT < bestT[l] * 0.95;
         bestR[l] = first ? vR : fmin(bestR[l], vR);
         bestT[l] = first ? vT : fmin(bestT[l], vT);
+        if (sdD) {
+            const double vD = sdD[l];
+            room = room || vD < bestD[l] * 0.95;
+            bestD[l] = first ? vD : fmin(bestD[l], vD);
+        }
         stop = stop || !room;
     }
     if (stop) {
@@ -855,6 +865,67 @@ __global__ void k_top_by_weight(int nImg, int mR, const double* __restrict__ qua
     for (int k = 0; k < 4; k++) topQ[4 * l + k] = quat[((size_t)l * mR + best) * 4 + k];
 }
 
+// ---- defocus particles (PAR_D) of a CTF search, one image per GROUP lanes.
+// balanceWeight(PAR_D) (src/Particle.cpp:2374-2409): w_i = 1 / N(d_i - m; s)
+// with the sample mean m and s = gsl_stats_sd_m (n - 1), 1 when s == 0
+// (one sample, or all equal); normW.
+THX_DEV void balance_d(const double* D, int mD, int lane, double* pD)
+{
+    double m = 0.0;
+    for (int i = lane; i < mD; i += GROUP) m += D[i];
+    m = group_sum(m) / mD;
+    double v = 0.0;
+    for (int i = lane; i < mD; i += GROUP) v += (D[i] - m) * (D[i] - m);
+    v = group_sum(v);
+    const double sd = mD > 1 ? sqrt(v / (mD - 1)) : 0.0;
+    double tot = 0.0;
+    for (int i = lane; i < mD; i += GROUP) {
+        const double u = (D[i] - m) / sd;
+        const double x = sd == 0.0 ? 1.0 : 1.0 / (exp(-0.5 * u * u) / (sd * sqrt(2 * M_PI)));
+        pD[i] = x;
+        tot += x;
+    }
+    tot = group_sum(tot);
+    for (int i = lane; i < mD; i += GROUP) pD[i] /= tot;
+}
+
+// op 0: initD (src/Particle.cpp:281-310, PARTICLE_DEFOCUS_INIT_GAUSSIAN):
+//       d_i = 1 + N(0, arg), balanceWeight;
+// op 1: perturb(arg, PAR_D) (:1278-1288): d_i += N(0, sd[l]) arg, balanceWeight;
+// op 2: calVari(PAR_D) (:1120-1141): sd[l] = gsl_stats_sd(d), 0 for one sample.
+__global__ void __launch_bounds__(256) k_pf_defocus(int nImg, int mD, int op, double arg,
+                                                    uint64_t seed, uint32_t stream,
+                                                    double* __restrict__ d,
+                                                    double* __restrict__ pD,
+                                                    double* __restrict__ sd,
+                                                    const int* __restrict__ done)
+{
+    const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
+    const int lane = threadIdx.x % GROUP;
+    if (l >= nImg || (done && done[l])) return;
+    double* D = d + (size_t)l * mD;
+    if (op == 2) {
+        double m = 0.0;
+        for (int i = lane; i < mD; i += GROUP) m += D[i];
+        m = group_sum(m) / mD;
+        double v = 0.0;
+        for (int i = lane; i < mD; i += GROUP) v += (D[i] - m) * (D[i] - m);
+        v = group_sum(v);
+        if (lane == 0) sd[l] = mD > 1 ? sqrt(v / (mD - 1)) : 0.0;
+        return;
+    }
+    Philox rng(seed, (uint32_t)l, stream, 0xde00u | (uint32_t)lane);
+    const double scale = op == 0 ? arg : sd[l] * arg;
+    for (int i = lane; i < mD; i += GROUP) {
+        const double g = rng.gauss2().x;
+        D[i] = (op == 0 ? 1.0 : D[i]) + g * scale;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    balance_d(D, mD, lane, pD + (size_t)l * mD);
+}
+
 struct Plan {
     // carve of the driver workspace
     float* rotP; double* gMat; float* traP;
@@ -869,10 +940,14 @@ struct Plan {
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
     double* bestR; double* bestT;                        // convergence: smallest variR / variT
     void* localWs; size_t localWsBytes;
+    // CTF search: defocus precalculation, per-phase CTF table, D statistics
+    float* freq; float* dfo; float* K1; float* K2; float* ctfD; float* wD;
+    double* sdD; double* bestD; double* tmpD; int* topD;
     size_t bytes;
 };
 
-Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
+// mLD > 0: the workspace of a CTF search over mLD defocus samples
+Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, int mLD = 0)
 {
     thx::Carver k(base, ~size_t(0));
     Plan p;
@@ -880,6 +955,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     int nMax = c.nR > c.nT ? c.nR : c.nT;           // every resampled support size
     if (c.mLR > nMax) nMax = c.mLR;
     if (c.mLT > nMax) nMax = c.mLT;
+    if (mLD > nMax) nMax = mLD;
     const bool scan = c.searchType == 0;
     p.rotP = k.take<float>(scan ? (size_t)2 * c.nR * nPxl : 0);
     p.gMat = k.take<double>(scan ? (size_t)9 * c.nR : 0);
@@ -890,7 +966,8 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     p.gBase = k.take<float>(nImg);
     p.scanWsBytes = scan ? thx_global_scan_workspace(nImg, c.nR, c.nT, nPxl, c.algo) : 0;
     p.scanWs = k.take<char>(p.scanWsBytes);
-    p.anc = k.take<int>((size_t)nImg * (c.mLR > c.mLT ? c.mLR : c.mLT));
+    p.anc = k.take<int>((size_t)nImg * (c.mLR > c.mLT ? (c.mLR > mLD ? c.mLR : mLD)
+                                                      : (c.mLT > mLD ? c.mLT : mLD)));
     p.cdf = k.take<double>((size_t)nImg * nMax);
     p.perm = k.take<int>((size_t)nImg * nMax);
     p.topR = k.take<int>(nImg);
@@ -914,8 +991,19 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit)
     p.nAct = k.take<int>(1);
     p.bestR = k.take<double>(nImg);
     p.bestT = k.take<double>(nImg);
-    p.localWsBytes = thx_local_phase_workspace(nImg, c.mLR, c.mLT, nVisit);
+    p.localWsBytes = thx_local_phase_workspace(nImg, c.mLR, c.mLT * (mLD > 0 ? mLD : 1), nVisit);
     p.localWs = k.take<char>(p.localWsBytes);
+    const size_t nd = mLD > 0 ? (size_t)mLD : 0, on = mLD > 0 ? 1 : 0;
+    p.freq = k.take<float>(on * nPxl);
+    p.dfo = k.take<float>(on * nImg * nPxl);
+    p.K1 = k.take<float>(on * nImg);
+    p.K2 = k.take<float>(on * nImg);
+    p.ctfD = k.take<float>(nd * nImg * nPxl);
+    p.wD = k.take<float>(nd * nImg);
+    p.sdD = k.take<double>(on * nImg);
+    p.bestD = k.take<double>(on * nImg);
+    p.tmpD = k.take<double>(nd * nImg);
+    p.topD = k.take<int>(on * nImg);
     p.bytes = k.off + 256;
     return p;
 }
@@ -971,6 +1059,21 @@ extern "C" int thx_pf_balance_rot(int nImg, int mR, const double* quat, double* 
     return THX_OK;
 }
 
+extern "C" int thx_pf_defocus(int nImg, int mD, int op, double arg, unsigned long long seed,
+                              unsigned stream_id, double* d, double* pD, double* sd,
+                              thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && mD > 0 && op >= 0 && op <= 2, "thx_pf_defocus: bad arguments");
+    THX_CHECK_ARG(nImg == 0 || (d && (op == 2 || pD) && (op == 0 || sd)),
+                  "thx_pf_defocus: null argument");
+    if (nImg == 0) return THX_OK;
+    hipLaunchKernelGGL(k_pf_defocus, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0,
+                       thx::as_stream(stream), nImg, mD, op, arg, (uint64_t)seed,
+                       (uint32_t)stream_id, d, pD, sd, nullptr);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 extern "C" int thx_pf_peak(int nImg, int n, float* u, int ldu, double* peak, int setFactor,
                            thx_stream_t stream)
 {
@@ -1021,28 +1124,47 @@ extern "C" size_t thx_expectation_workspace(const thx_expect_cfg* cfg, int nImg,
     return plan(nullptr, *cfg, nImg, nPxl, nOrd > 0 ? nOrd : nPxl).bytes;
 }
 
+extern "C" size_t thx_expectation_ctf_workspace(const thx_expect_cfg* cfg,
+                                                const thx_ctf_search_cfg* cs, int nImg,
+                                                int nPxl, int nOrd)
+{
+    if (!cfg || !cs || cs->mLD <= 0) return 0;
+    return plan(nullptr, *cfg, nImg, nPxl, nOrd > 0 ? nOrd : nPxl, cs->mLD).bytes;
+}
+
 #define THX_RET(call)                  \
     do {                               \
         int st_ = (call);              \
         if (st_ != THX_OK) return st_; \
     } while (0)
 
-extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
-                               const double* gQuat, const double* gTrans,
-                               const double* gPR, const double* gPT,
-                               const float* dat, const float* ctf,
-                               const float* sigRcp, const int* iCol,
-                               const int* iRow, const int* pxOrder, int nOrd, int nPxl, int nImg,
-                               double* quat,
-                               double* trans, double* pR, double* pT,
-                               float* score, int* cls, int* nPhaseOut, void* workspace,
-                               size_t wsBytes, thx_stream_t stream)
+// cs != NULL: SEARCH_TYPE_CTF (searchType 2) -- a local search whose phases
+// also sample nD = cs->mLD defocus factors per image (src/Optimiser.cpp:
+// 1183-1616 with the _searchType == SEARCH_TYPE_CTF branches).
+static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg* cs,
+                            const float* vol, const double* gQuat, const double* gTrans,
+                            const double* gPR, const double* gPT, const float* dat,
+                            const float* ctf, const float* sigRcp, const int* iCol,
+                            const int* iRow, const int* pxOrder, int nOrd, int nPxl, int nImg,
+                            double* quat, double* trans, double* pR, double* pT, float* score,
+                            int* cls, int* nPhaseOut, void* workspace, size_t wsBytes,
+                            thx_stream_t stream)
 {
-    THX_CHECK_ARG(cfg && vol && dat && ctf && sigRcp && iCol && iRow && quat && trans && pR && pT,
+    THX_CHECK_ARG(cfg && vol && dat && (ctf || cs) && sigRcp && iCol && iRow && quat && trans &&
+                      pR && pT,
                   "thx_expectation: null argument");
     const thx_expect_cfg& c = *cfg;
     const bool global = c.searchType == 0;
-    THX_CHECK_ARG(c.searchType == 0 || c.searchType == 1, "thx_expectation: searchType must be 0 or 1");
+    if (cs) {
+        THX_CHECK_ARG(c.searchType == 2, "thx_expectation_ctf: searchType must be 2 (SEARCH_TYPE_CTF)");
+        THX_CHECK_ARG(cs->mLD > 0 && cs->attr && cs->d && cs->pD && cs->ctfRefineS >= 0.0 &&
+                          (long)c.mLT * cs->mLD <= 1024,
+                      "thx_expectation_ctf: bad CTF-search configuration");
+    } else {
+        THX_CHECK_ARG(c.searchType == 0 || c.searchType == 1,
+                      "thx_expectation: searchType must be 0 or 1");
+    }
+    const int mLD = cs ? cs->mLD : 0;
     THX_CHECK_ARG(!global || (gQuat && gTrans && gPR && gPT),
                   "thx_expectation: a global search needs the global sample set");
     THX_CHECK_ARG(c.mLR > 0 && c.mLT > 0 && c.vdim == c.pf * c.idim && nImg >= 0 && nImg <= 65535 &&
@@ -1060,7 +1182,7 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     if (nImg == 0) return THX_OK;
     THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % 16 == 0),
                   "thx_expectation: nOrd must be a positive multiple of 16");
-    const Plan p = plan(workspace, c, nImg, nPxl, pxOrder ? nOrd : nPxl);
+    const Plan p = plan(workspace, c, nImg, nPxl, pxOrder ? nOrd : nPxl, mLD);
     THX_CHECK_ARG(workspace && p.bytes <= wsBytes, "thx_expectation: workspace too small");
     hipStream_t s = thx::as_stream(stream);
     const unsigned gImg = thx::cdiv(nImg, 4);
@@ -1134,6 +1256,11 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, s, p.peakR, (long)nImg, 1e-3);
         THX_LAUNCH_CHECK();
     }
+    if (cs) {
+        // allocPreCal's cSearch branch (src/Optimiser.cpp:8124-8170), once per call
+        THX_RET(thx_defocus_pre(cs->attr, nImg, iCol, iRow, nPxl, c.idim, p.freq, p.dfo, p.K1,
+                                p.K2, stream));
+    }
     hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, s, p.pC, (long)nImg, 1.0);
     THX_LAUNCH_CHECK();
 
@@ -1164,13 +1291,25 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                            large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
                            c.seed, (uint32_t)(2000 + phase), c.perturbMean, p.meanQ, done);
         THX_LAUNCH_CHECK();
+        if (cs) {
+            // phase 0: initD(mLD, ctfRefineS); later: perturb(perturbFactorSCTF,
+            // PAR_D) (src/Optimiser.cpp:1194-1195, 1208-1209); then the phase's
+            // CTF per defocus sample (:1248-1273)
+            hipLaunchKernelGGL(k_pf_defocus, dim3(gPf), dim3(256), 0, s, nImg, mLD,
+                               phase == phase0 ? 0 : 1,
+                               phase == phase0 ? cs->ctfRefineS : cs->perturbFactorSCTF, c.seed,
+                               (uint32_t)(6000 + phase), cs->d, cs->pD, p.sdD, done);
+            THX_LAUNCH_CHECK();
+            THX_RET(thx_ctf_search(p.dfo, p.freq, cs->d, mLD, p.K1, p.K2, cs->attr, nImg, nPxl,
+                                   p.ctfD, stream));
+        }
         hipEvent_t* ev = static_cast<hipEvent_t*>(c.phaseEvents);
         const int pi = phase - phase0;
         THX_RET(thx::local_phase_timed(&sel, ev ? ev[2 * pi] : nullptr, ev ? ev[2 * pi + 1] : nullptr,
                                        vol, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT,
-                                       dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, c.idim,
-                                       nImg, p.wC, p.wR, p.wT, p.base, p.localWs, p.localWsBytes,
-                                       stream));
+                                       dat, cs ? p.ctfD : ctf, sigRcp, iCol, iRow, pxOrder, nOrd,
+                                       nPxl, c.idim, nImg, p.wC, p.wR, p.wT, p.base, p.localWs,
+                                       p.localWsBytes, stream, mLD, cs ? cs->pD : nullptr, p.wD));
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
                            p.peakR, 0, nullptr, 0, done);
         THX_LAUNCH_CHECK();
@@ -1203,9 +1342,27 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, p.tmpT,
                            (long)c.mLT * 2, c.mLT, p.anc, trans, done);
         THX_LAUNCH_CHECK();
+        if (cs) {
+            // calRank1st, calVari, resample (mLD, PAR_D) (src/Optimiser.cpp:1483-1488);
+            // no peak factor (OPTIMISER_PEAK_FACTOR_D is off, include/Config.h:220)
+            hipLaunchKernelGGL(k_pf_defocus, dim3(gPf), dim3(256), 0, s, nImg, mLD, 2, 0.0, c.seed,
+                               0u, cs->d, cs->pD, p.sdD, done);
+            THX_LAUNCH_CHECK();
+            hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(mLD, c.shuffle),
+                               s, nImg, mLD, mLD, cs->pD, mLD, p.wD, mLD, c.seed,
+                               (uint32_t)(5000 + phase), p.anc, cs->pD, p.topD, p.cdf,
+                               c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr, 0, done);
+            THX_LAUNCH_CHECK();
+            THX_HIP(hipMemcpyAsync(p.tmpD, cs->d, sizeof(double) * nImg * mLD,
+                                   hipMemcpyDeviceToDevice, s));
+            hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, mLD, 1, p.tmpD,
+                               (long)mLD, mLD, p.anc, cs->d, done);
+            THX_LAUNCH_CHECK();
+        }
         if (c.converge) {
             hipLaunchKernelGGL(k_pf_converge, dim3(gOne), dim3(256), 0, s, nImg, phase, c.minPhase,
-                               phase0 + nPh - 1, p.kv, p.sv, p.bestR, p.bestT, p.done, nPD);
+                               phase0 + nPh - 1, p.kv, p.sv, p.bestR, p.bestT, p.done, nPD,
+                               cs ? p.sdD : nullptr, cs ? p.bestD : nullptr);
             THX_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
             THX_LAUNCH_CHECK();
@@ -1228,4 +1385,33 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
                                hipMemcpyDeviceToDevice, s));
     }
     return THX_OK;
+}
+
+extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
+                               const double* gQuat, const double* gTrans,
+                               const double* gPR, const double* gPT,
+                               const float* dat, const float* ctf,
+                               const float* sigRcp, const int* iCol,
+                               const int* iRow, const int* pxOrder, int nOrd, int nPxl, int nImg,
+                               double* quat,
+                               double* trans, double* pR, double* pT,
+                               float* score, int* cls, int* nPhaseOut, void* workspace,
+                               size_t wsBytes, thx_stream_t stream)
+{
+    return expectation_impl(cfg, nullptr, vol, gQuat, gTrans, gPR, gPT, dat, ctf, sigRcp, iCol,
+                            iRow, pxOrder, nOrd, nPxl, nImg, quat, trans, pR, pT, score, cls,
+                            nPhaseOut, workspace, wsBytes, stream);
+}
+
+extern "C" int thx_expectation_ctf(const thx_expect_cfg* cfg, const thx_ctf_search_cfg* cs,
+                                   const float* vol, const float* dat, const float* sigRcp,
+                                   const int* iCol, const int* iRow, const int* pxOrder, int nOrd,
+                                   int nPxl, int nImg, double* quat, double* trans, double* pR,
+                                   double* pT, float* score, int* cls, int* nPhaseOut,
+                                   void* workspace, size_t wsBytes, thx_stream_t stream)
+{
+    THX_CHECK_ARG(cs, "thx_expectation_ctf: null CTF-search configuration");
+    return expectation_impl(cfg, cs, vol, nullptr, nullptr, nullptr, nullptr, dat, nullptr,
+                            sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, nImg, quat, trans, pR, pT,
+                            score, cls, nPhaseOut, workspace, wsBytes, stream);
 }

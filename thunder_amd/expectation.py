@@ -23,7 +23,7 @@ INCLUDE_OPTIMISER_H = {
     "MAX_N_PHASE_PER_ITER": 100,         # include/Optimiser.h:58
     "MIN_STD_FACTOR": 1,                 # include/Optimiser.h:73
 }
-SEARCH = {"global": 0, "local": 1}      # SEARCH_TYPE_GLOBAL / SEARCH_TYPE_LOCAL
+SEARCH = {"global": 0, "local": 1, "ctf": 2}   # SEARCH_TYPE_GLOBAL / _LOCAL / _CTF
 
 
 class ExpectCfg(ctypes.Structure):
@@ -42,6 +42,12 @@ class ExpectCfg(ctypes.Structure):
                 ("phaseEvents", ctypes.c_void_p)]
 
 
+class CtfSearchCfg(ctypes.Structure):
+    _fields_ = [("mLD", ctypes.c_int), ("ctfRefineS", ctypes.c_double),
+                ("perturbFactorSCTF", ctypes.c_double), ("attr", ctypes.c_void_p),
+                ("d", ctypes.c_void_p), ("pD", ctypes.c_void_p)]
+
+
 class Expectation:
     """One round of expectation on the current GPU (Optimiser::expectationG).
 
@@ -49,8 +55,10 @@ class Expectation:
          [nK, vdim, vdim, vdim/2+1] for K-class classification.
     gset: (quat [nR,4], trans [nT,2], pR [nR], pT [nT]) numpy float64 (global
           search; None for a local search).
-    search: "global" (scan + reseed + phases 1..) or "local" (phases 0.. from
-            the caller's particle state, passed to run()).
+    search: "global" (scan + reseed + phases 1..), "local" (phases 0.. from
+            the caller's particle state, passed to run()) or "ctf"
+            (SEARCH_TYPE_CTF: a local search that also samples mLD defocus
+            factors per image; run() takes the CTF attributes).
     converge: per-image vari-decrease stopping rule between MIN_N_PHASE_PER_ITER
               (10 global / 3 local) and MAX_N_PHASE_PER_ITER (100) phases;
               False: exactly n_phase phases.
@@ -63,7 +71,8 @@ class Expectation:
     def __init__(self, vol, px, gset=None, mLR=125, mLT=9, n_phase=10, perturb=0.5,
                  trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7, shuffle=True,
                  search="global", converge=False, perturb_mean="acg", acg_iters=100,
-                 perturb_large=2.0, large_first=False, min_phase=None, max_phase=None):
+                 perturb_large=2.0, large_first=False, min_phase=None, max_phase=None,
+                 mLD=9, ctf_refine_s=0.01, perturb_ctf=0.5):
         dev = vol.device
         self.vol, self.px, self.dev = vol, px, dev
         nK = vol.shape[0] if vol.dim() == 4 else 1
@@ -97,10 +106,47 @@ class Expectation:
                              {"top": 0, "acg": 1}[perturb_mean], acg_iters, perturb_large,
                              int(bool(large_first)), None)
         self.mLR, self.mLT, self.nK = mLR, mLT, nK
+        self.cs = CtfSearchCfg(mLD, ctf_refine_s, perturb_ctf, None, None, None)
 
     def workspace_bytes(self, nImg):
+        if self.search == 2:
+            return lib().thx_expectation_ctf_workspace(ctypes.byref(self.cfg), ctypes.byref(self.cs),
+                                                       nImg, self.px.n, len(self.px.order))
         return lib().thx_expectation_workspace(ctypes.byref(self.cfg), nImg, self.px.n,
                                                len(self.px.order))
+
+    def run_ctf(self, dat, attr, sig, state):
+        """SEARCH_TYPE_CTF: attr [nImg, 8] CTF attributes (device float32), state
+        (quat, trans, pR, pT[, cls]) updated in place; returns (quat, trans, pR,
+        pT, score, cls, nPhase, d [nImg, mLD], pD [nImg, mLD])."""
+        if self.search != 2:
+            raise ValueError("run_ctf needs search='ctf'")
+        nImg, nPxl = dat.shape
+        if nPxl != self.px.n:
+            raise ValueError("pixel set / image size mismatch")
+        ops._req(dat, torch.complex64, (nImg, nPxl), "dat")
+        ops._req(sig, torch.float32, (nImg, nPxl), "sigRcp")
+        ops._req(attr, torch.float32, (nImg, 8), "attr")
+        dev = self.dev
+        quat, trans, pR, pT = state[:4]
+        for name, t, shp in (("quat", quat, (nImg, self.mLR, 4)), ("trans", trans, (nImg, self.mLT, 2)),
+                             ("pR", pR, (nImg, self.mLR)), ("pT", pT, (nImg, self.mLT))):
+            ops._req(t, torch.float64, shp, name)
+        cls = state[4] if len(state) > 4 else torch.zeros(nImg, dtype=torch.int32, device=dev)
+        mLD = self.cs.mLD
+        d = torch.empty(nImg, mLD, dtype=torch.float64, device=dev)
+        pD = torch.empty(nImg, mLD, dtype=torch.float64, device=dev)
+        score = torch.empty(nImg, dtype=torch.float32, device=dev)
+        nph = torch.empty(nImg, dtype=torch.int32, device=dev)
+        self.cs.attr, self.cs.d, self.cs.pD = attr.data_ptr(), d.data_ptr(), pD.data_ptr()
+        ws = ops.workspace(self.workspace_bytes(nImg), dev)
+        P = ops._ptr
+        check(lib().thx_expectation_ctf(ctypes.byref(self.cfg), ctypes.byref(self.cs), P(self.vol),
+                                        P(dat), P(sig), P(self.px.d_iCol), P(self.px.d_iRow),
+                                        P(self.px.d_order), len(self.px.order), nPxl, nImg,
+                                        P(quat), P(trans), P(pR), P(pT), P(score), P(cls), P(nph),
+                                        P(ws), ws.numel(), ops._stream(dev)), "thx_expectation_ctf")
+        return quat, trans, pR, pT, score, cls, nph, d, pD
 
     def run(self, dat, ctf, sig, out=None, state=None):
         """Expectation of one image batch; returns (quat, trans, pR, pT, score,
@@ -113,6 +159,8 @@ class Expectation:
                             ("sigRcp", sig, torch.float32)):
             ops._req(t, dt, (nImg, nPxl), name)
         dev = self.dev
+        if self.search == 2:
+            raise ValueError("a CTF search runs through run_ctf (it needs the CTF attributes)")
         if self.search == 1:
             if state is None:
                 raise ValueError("a local search starts from a particle state")

@@ -630,6 +630,20 @@ def pf_balance_rot(quat):
     return pR
 
 
+def pf_defocus(op, d, pD=None, sd=None, arg=0.0, seed=1, stream_id=0):
+    """thx_pf_defocus: op "init" (d <- 1 + N(0, arg)), "perturb" (d += N(0, sd) arg),
+    both rebalancing pD; "vari" (sd <- std of d)."""
+    nImg, mD = d.shape
+    _req(d, torch.float64, (nImg, mD), "d")
+    k = {"init": 0, "perturb": 1, "vari": 2}[op]
+    if k != 2:
+        _req(pD, torch.float64, (nImg, mD), "pD")
+    if k != 0:
+        _req(sd, torch.float64, (nImg,), "sd")
+    check(lib().thx_pf_defocus(nImg, mD, k, float(arg), seed, stream_id, _ptr(d), _ptr(pD),
+                               _ptr(sd), _stream(d.device)), "thx_pf_defocus")
+
+
 def pf_peak(u, peak=None):
     """thx_pf_peak: keepHalfHeightPeak on marginals u [nImg, n] float32 (in
     place); sets the 3D peak factor first when ``peak`` is None.  Returns
