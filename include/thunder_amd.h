@@ -349,6 +349,17 @@ int thx_insert3d_binned(float* F, float* T, double* O, int* counter, int vdim, i
                         const int* nC, int nImg, int mReco, const int* iCol, const int* iRow,
                         const int* pxOrder, int nOrd, int nPxl, int idim, int rMax,
                         void* workspace, size_t wsBytes, thx_stream_t stream);
+/* The same with CTF search (InsertFT's cSearch, src/Optimiser.cpp:7101-7120;
+ * kernel_CalculateCTF gpu/src/Kernel.cu:2206-2270): sample (l, m) inserts with
+ * CTF(defocusU nD[l][m], defocusV nD[l][m]) of image l's attributes attr
+ * (nImg x 8, as thx_ctf) instead of a per-image ctf row. */
+int thx_insert3d_binned_d(float* F, float* T, double* O, int* counter, int vdim,
+                          int pf, const float* dat, const float* attr,
+                          const double* nD, const double* quat, const double* trans,
+                          const double* offS, const float* w, const int* nC, int nImg,
+                          int mReco, const int* iCol, const int* iRow,
+                          const int* pxOrder, int nOrd, int nPxl, int idim, int rMax,
+                          void* workspace, size_t wsBytes, thx_stream_t stream);
 
 /* ----------------------------------------------------------------- a13 ---
  * The per-hemisphere half-map reduction of cuthunder::InsertFT
@@ -439,7 +450,7 @@ int thx_fsc(const float* A, const float* B, int vdim, int nShell, double* fsc,
 
 /* ------------------------------------------------- a3..a11 expectation ---
  * Device-resident Optimiser::expectationG (src/Optimiser.cpp:1684-3403) for
- * one image batch, 3D, no CTF search.
+ * one image batch, 3D (CTF search: thx_expectation_ctf below).
  *
  * searchType 0 (SEARCH_TYPE_GLOBAL): global scan of every class k < nK over
  * the shared sample set (gQuat[nR*4], gTrans[nT*2], priors gPR[nR], gPT[nT];
@@ -583,7 +594,12 @@ int thx_ExpectGlobal3D(const float* rotP, const float* traP, const float* datP,
  * *Fin / *FreeIdx call.  The ManagedArrayTexture / ManagedCalPoint objects
  * become opaque handles: thx_tex_create / thx_calpoint_create mirror their
  * Init(mode, vdim, gpu) / Init(mode, searchType, gpu, mLR, mLT, mLD, nPxl).
- * Only MODE_3D and no CTF search (searchType != 2, mLD <= 1). */
+ * MODE_3D only.  CTF search (searchType 2 / cSearch): ExpectLocalIn also
+ * allocates devdefO, ExpectLocalP copies defO (the image's per-pixel defocus,
+ * thx_defocus_pre), ExpectLocalRTD takes dpara (mLD defocus factors) and oldD
+ * (their priors), ExpectLocalPreI3D builds the CTF per defocus sample from
+ * devdefO + datShift * npxl, devfreQ, phaseShift, conT, k1, k2, and
+ * ExpectLocalM returns wD[mLD]. */
 int thx_getAviDevice(int* gpus, int cap, int* n);                               /* :16 */
 int thx_ExpectPreidx(int gpuIdx, int** deviCol, int** deviRow, const int* iCol,
                      const int* iRow, int npxl);                                  /* :18 */
@@ -662,6 +678,20 @@ int thx_InsertFTC(float* F3D, float* T3D, double* O3D, int* counter,
                   const float* w, const double* nR, const double* nT, const int* nC,
                   const int* iCol, const int* iRow, int opf, int npxl,
                   int mReco, int idim, int vdim, int imgNum);
+
+/* gpu/interface/Interface.h:267-318 InsertFT with cSearch = true: sample
+ * (l, m) inserts with the CTF of image l at defocus factor nD[l*mReco + m]
+ * (kernel_CalculateCTF, gpu/src/Kernel.cu:2206-2270; CPU src/Optimiser.cpp:
+ * 7101-7120); ctfaData: CTFAttr[imgNum] as 7 floats each {voltage, defocusU,
+ * defocusV, defocusTheta, Cs, amplitudeContrast, phaseShift}
+ * (include/Database.h:302-327); nC and comm may be NULL (then as
+ * thx_InsertFT / thx_InsertFTC / thx_InsertFTComm). */
+int thx_InsertFTCS(float* F3D, float* T3D, double* O3D, int* counter,
+                   const float* datP, const float* ctfaData, const double* offS,
+                   const float* w, const double* nR, const double* nT,
+                   const double* nD, const int* nC, const int* iCol, const int* iRow,
+                   float pixelSize, int opf, int npxl, int mReco, int idim, int vdim,
+                   int imgNum, void* comm);
 
 /* Either of the two with the reference call's hemisphere reduction inside
  * (nC may be NULL): after the insert, thx_halfmap_allreduce of the device

@@ -190,3 +190,35 @@ def test_ctf_search_driver_refines_defocus():
     qm = ex.cloud_mode(q).cpu().numpy()
     ang = np.degrees(2 * np.arccos(np.clip(np.abs(np.sum(qm * qtrue, 1)), 0, 1)))
     assert np.median(ang) < 2.0
+
+
+@pytest.mark.parametrize("spread,mReco,dup", [(0.0, 6, False), (2.0, 100, True), (8.0, 150, True)])
+def test_insert_ctf_search(orc, stack, spread, mReco, dup):
+    """Every sample at its own defocus factor; dup: copies of 12 ancestors
+    (one rotation group holds members of different defocus)."""
+    s = stack
+    px = dev_pixels(s)
+    nImg = 4
+    rng = np.random.default_rng(22)
+    if spread > 0:
+        quat = synth.clustered_quaternions(nImg, mReco, spread, rng)
+    else:
+        quat = synth.uniform_quaternions(nImg * mReco, rng).reshape(nImg, mReco, 4)
+    if dup:
+        anc = rng.integers(0, 12, (nImg, mReco))
+        quat = np.ascontiguousarray(np.take_along_axis(quat, anc[..., None], axis=1))
+    trans = rng.standard_normal((nImg, mReco, 2)) * 3
+    off = rng.standard_normal((nImg, 2))
+    w = np.full(nImg, 1.0 / mReco, np.float32)
+    attrs = synth.ctf_attrs(nImg, seed=12)
+    nD = 1 + rng.standard_normal((nImg, mReco)) * 0.02
+    hm = ops.HalfMap(s["vdim"], DEV)
+    ops.insert3d_ctf(hm, T(s["dat"][:nImg]), T(attrs), T(nD), T(quat), T(trans), T(off), T(w), px)
+    F, Tm, O, cnt = orc.insert_batch_d(s["vdim"], s["pf"], s["dat"][:nImg], attrs, nD, quat, trans,
+                                       off, w, s["px"], s["N"])
+    gF = hm.F.cpu().numpy().reshape(-1)
+    gT = hm.T.cpu().numpy().reshape(-1)
+    assert np.max(np.abs(gF - F)) <= 1e-5 * np.max(np.abs(F))
+    assert np.max(np.abs(gT - Tm)) <= 1e-5 * np.max(np.abs(Tm))
+    assert np.allclose(hm.O.cpu().numpy(), O, rtol=1e-12, atol=1e-12)
+    assert int(hm.counter.item()) == cnt == nImg * mReco

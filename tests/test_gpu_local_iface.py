@@ -82,3 +82,112 @@ def test_local_path_through_interface_forwards(orc):
     assert L.thx_tex_destroy(mgr) == 0
     assert L.thx_ExpectFreeIdx(gpu, ctypes.byref(dCol), ctypes.byref(dRow)) == 0
     assert dCol.value is None and dD.value is None
+
+
+def test_ctf_search_through_interface_forwards(orc):
+    """cSearch: devdefO slots, dpara / oldD, the calpoint's CTF per defocus
+    sample, wD -- against orc.local_phase_d on orc.ctf_search's table."""
+    s = small_stack(orc, N=48, nImg=3, nR=4, nT=3, seed=13)
+    L = lib()
+    px = s["px"]
+    npxl = px.n
+    mR, mT, mD, cpy, gpu = 60, 5, 4, 2, 0
+    iCol, iRow = px.iCol.copy(), px.iRow.copy()
+    dCol, dRow = vp(), vp()
+    assert L.thx_ExpectPreidx(gpu, ctypes.byref(dCol), ctypes.byref(dRow), P(iCol), P(iRow), npxl) == 0
+    attrs = synth.ctf_attrs(3, seed=14)
+    attrs[:, 7] = [0.0, 0.2, -0.1]
+    pre = [orc.defocus_pre(px, a, s["N"]) for a in attrs]
+    freq = pre[0][0]
+    defO = np.ascontiguousarray(np.stack([p[1] for p in pre]))
+    dF = vp()
+    assert L.thx_ExpectPrefre(gpu, ctypes.byref(dF), P(freq), npxl) == 0
+    mgr = vp()
+    assert L.thx_tex_create(1, s["vdim"], gpu, ctypes.byref(mgr)) == 0
+    vol = np.ascontiguousarray(s["vol"])
+    assert L.thx_ExpectLocalV3D(gpu, mgr, P(vol), s["vdim"]) == 0
+    dat = np.ascontiguousarray(s["dat"]).view(np.float32)
+    sig = np.ascontiguousarray(s["sig"])
+    dD, dC, dO, dS = vp(), vp(), vp(), vp()
+    assert L.thx_ExpectLocalIn(gpu, ctypes.byref(dD), ctypes.byref(dC), ctypes.byref(dO),
+                               ctypes.byref(dS), npxl, cpy, 2) == 0
+    host = [vp() for _ in range(10)]
+    assert L.thx_ExpectLocalHostA(gpu, *[ctypes.byref(h) for h in host], mR, mT, mD, 1) == 0
+    f32 = lambda h, k: np.ctypeslib.as_array(ctypes.cast(h, ctypes.POINTER(ctypes.c_float)), (k,))
+    f64 = lambda h, k: np.ctypeslib.as_array(ctypes.cast(h, ctypes.POINTER(ctypes.c_double)), (k,))
+    wC, wR, wT, wD = f32(host[0], 1), f32(host[1], mR), f32(host[2], mT), f32(host[3], mD)
+    oldR, oldT, oldD = f64(host[4], mR), f64(host[5], mT), f64(host[6], mD)
+    trans, rot, dpara = f64(host[7], 2 * mT), f64(host[8], 4 * mR), f64(host[9], mD)
+    mcp = vp()
+    assert L.thx_calpoint_create(1, 2, gpu, mR, mT, mD, npxl, ctypes.byref(mcp)) == 0
+    rng = np.random.default_rng(6)
+    for img in range(3):
+        slot = img % cpy
+        assert L.thx_ExpectLocalP(gpu, dD, dC, dO, dS, P(dat), None, P(defO), P(sig), slot, img,
+                                  npxl, 1) == 0, L.thx_last_error()
+        q = synth.clustered_quaternions(1, mR, 3.0, rng)[0]
+        t = rng.standard_normal((mT, 2))
+        pR = rng.uniform(0.5, 1.5, mR)
+        pT = np.full(mT, 1.0 / mT)
+        pD = rng.uniform(0.5, 1.5, mD)
+        d = 1 + rng.standard_normal(mD) * 0.02
+        oldR[:], oldT[:], oldD[:], dpara[:] = pR, pT, pD, d
+        rot[:], trans[:] = q.reshape(-1), t.reshape(-1)
+        oldC = 0.9
+        assert L.thx_ExpectLocalRTD(gpu, mcp, host[4], host[5], host[6], host[7], host[8],
+                                    host[9]) == 0
+        a = attrs[img]
+        assert L.thx_ExpectLocalPreI3D(gpu, slot, mgr, mcp, dO, dF, dCol, dRow, float(a[7]),
+                                       float(a[6]), float(pre[img][2]), float(pre[img][3]),
+                                       s["pf"], s["N"], s["vdim"], npxl, 1) == 0, L.thx_last_error()
+        assert L.thx_ExpectLocalM(gpu, slot, mcp, dD, dC, dS, host[0], host[1], host[2], host[3],
+                                  oldC, npxl) == 0, L.thx_last_error()
+        ctfD = orc.ctf_search(pre[img][1], freq, d, pre[img][2], pre[img][3], a[7], a[6])
+        rC, rR, rT, rDd, rb, rd = orc.local_phase_d(s["vol"], s["vdim"], s["pf"], q, t, oldC, pR, pT,
+                                                    pD, s["dat"][img], ctfD, s["sig"][img], px,
+                                                    s["N"])
+        for got, want in ((wR, rR), (wT, rT), (wD, rDd)):
+            m = want >= 1e-4 * want.max()
+            assert np.max(np.abs(got - want)[m] / want[m]) < 1e-3
+        assert abs(wC[0] - rC) <= 1e-3 * abs(rC)
+    assert L.thx_calpoint_destroy(mcp) == 0
+    assert L.thx_ExpectLocalHostF(gpu, *[ctypes.byref(h) for h in host], 1) == 0
+    assert L.thx_ExpectLocalFin(gpu, ctypes.byref(dD), ctypes.byref(dC), ctypes.byref(dO),
+                                ctypes.byref(dF), ctypes.byref(dS), 1) == 0
+    assert L.thx_tex_destroy(mgr) == 0
+    assert L.thx_ExpectFreeIdx(gpu, ctypes.byref(dCol), ctypes.byref(dRow)) == 0
+
+
+def test_insert_ft_ctf_search(orc):
+    """InsertFT with cSearch (thx_InsertFTCS, host buffers) against the
+    CTF-search restatement of the insert."""
+    s = small_stack(orc, N=32, nImg=3, seed=15)
+    L = lib()
+    px = s["px"]
+    nImg, mReco, vdim = 3, 20, s["vdim"]
+    rng = np.random.default_rng(16)
+    quat = synth.clustered_quaternions(nImg, mReco, 3.0, rng)
+    trans = rng.standard_normal((nImg, mReco, 2))
+    off = rng.standard_normal((nImg, 2)) * 0.5
+    w = np.full(nImg, 1.0 / mReco, np.float32)
+    attrs = synth.ctf_attrs(nImg, seed=17)
+    nD = 1 + rng.standard_normal((nImg, mReco)) * 0.02
+    F0, T0, O0, c0 = orc.insert_batch_d(vdim, s["pf"], s["dat"], attrs, nD, quat, trans, off, w, px,
+                                        s["N"])
+    size = (vdim // 2 + 1) * vdim * vdim
+    F = np.zeros(2 * size, np.float32)
+    Tm = np.zeros(size, np.float32)
+    O = np.zeros(3)
+    cnt = np.zeros(1, np.int32)
+    ctfa = np.ascontiguousarray(attrs[:, 1:8])
+    dat = np.ascontiguousarray(s["dat"]).view(np.float32)
+    q, t, o, nd = (np.ascontiguousarray(x) for x in (quat, trans, off, nD))
+    iColP = np.ascontiguousarray(px.iCol * s["pf"], np.int32)
+    iRowP = np.ascontiguousarray(px.iRow * s["pf"], np.int32)
+    assert L.thx_InsertFTCS(P(F), P(Tm), P(O), P(cnt), P(dat), P(ctfa), P(o), P(w), P(q), P(t),
+                            P(nd), None, P(iColP), P(iRowP), float(attrs[0, 0]), s["pf"], px.n,
+                            mReco, s["N"], vdim, nImg, None) == 0, L.thx_last_error()
+    F0 = F0.view(np.float32)
+    assert np.max(np.abs(F - F0)) <= 1e-5 * np.max(np.abs(F0))
+    assert np.max(np.abs(Tm - T0)) <= 1e-5 * np.max(np.abs(T0))
+    assert np.allclose(O, O0, rtol=1e-12, atol=1e-12) and int(cnt[0]) == c0 == nImg * mReco

@@ -57,6 +57,11 @@ SIGNATURES = {
     "thx_insert3d_binned": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _p,
                                      _c_int, _c_int, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p,
                                      _c_size, _p]),
+    "thx_insert3d_binned_d": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _p,
+                                       _p, _c_int, _c_int, _p, _p, _p, _c_int, _c_int, _c_int,
+                                       _c_int, _p, _c_size, _p]),
+    "thx_InsertFTCS": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_float,
+                                _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _p]),
     "thx_rccl_unique_id": (_c_int, [_p]),
     "thx_rccl_comm_init": (_c_int, [_c_int, _p, _c_int, _p]),
     "thx_rccl_comm_destroy": (_c_int, [_p]),

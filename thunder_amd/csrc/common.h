@@ -192,6 +192,18 @@ THX_DEV float ctf_at(const float* a, float dU, float dV, int ic, int ir, int idi
     return -w1 * sinf(ki) + ampC * cosf(ki);
 }
 
+// The CTF-search CTF of one pixel (kernel_CalCTFL, gpu/src/Kernel.cu:481-515;
+// src/Optimiser.cpp:1258-1270): ki = K1 defocusP d f^2 + K2 f^4 - phaseShift,
+// -sqrt(1 - conT^2) sin(ki) + conT cos(ki).
+THX_DEV float ctf_search_at(float k1, float dfo, double d, float f, float k2, float ps,
+                            float conT)
+{
+    const float w1 = sqrtf(1.f - (float)((double)conT * conT));
+    const double f2 = (double)f * f;
+    const float ki = (float)((double)(k1 * dfo) * d * f2 + k2 * (f2 * f2) - ps);
+    return -w1 * sinf(ki) + conT * cosf(ki);
+}
+
 // rotate3D, src/Geometry/Euler.cpp:181-189: R = I + 2 q0 A + 2 A A with
 // A = [[0,-q3,q2],[q3,0,-q1],[-q2,q1,0]], stored column-major.
 THX_DEV void quat_to_mat(const double* q, double* m)

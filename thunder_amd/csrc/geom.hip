@@ -184,16 +184,12 @@ __global__ void __launch_bounds__(256) k_ctf_search(const float* __restrict__ de
 {
     const int l = blockIdx.y / nD, iD = blockIdx.y % nD;
     const float conT = attr[8 * l + 6], ps = attr[8 * l + 7];
-    const float w1 = sqrtf(1.f - (float)((double)conT * conT));
     const float k1 = K1[l], k2 = K2[l];
     const double d = dD[(size_t)l * nD + iD];
     const float* dfo = defocusP + (size_t)l * nPxl;
     float* out = ctfD + ((size_t)l * nD + iD) * nPxl;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nPxl; i += gridDim.x * blockDim.x) {
-        const double f2 = (double)freq[i] * freq[i];
-        const float ki = (float)((double)(k1 * dfo[i]) * d * f2 + k2 * (f2 * f2) - ps);
-        out[i] = -w1 * sinf(ki) + conT * cosf(ki);
-    }
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nPxl; i += gridDim.x * blockDim.x)
+        out[i] = ctf_search_at(k1, dfo[i], d, freq[i], k2, ps, conT);
 }
 
 extern "C" int thx_defocus_pre(const float* attr, int nImg, const int* iCol, const int* iRow,

@@ -105,7 +105,9 @@ __global__ void __launch_bounds__(G_THREADS) k_bin_groups(const double* __restri
                                                           double* __restrict__ gMat,
                                                           float2* __restrict__ mShift,
                                                           double* __restrict__ O,
-                                                          int* __restrict__ counter)
+                                                          int* __restrict__ counter,
+                                                          const double* __restrict__ dS,
+                                                          double* __restrict__ mDef)
 {
     __shared__ int sLead[BIN_MAXM];
     __shared__ int sGid[BIN_MAXM];
@@ -150,6 +152,7 @@ __global__ void __launch_bounds__(G_THREADS) k_bin_groups(const double* __restri
         quat_to_mat(q, R);
         const double dx = trans[2 * sIdx] - offx, dy = trans[2 * sIdx + 1] - offy;
         ms[start + pos] = make_float2((float)(-dx) / idim, (float)(-dy) / idim);
+        if (dS) mDef[(size_t)b * mReco + start + pos] = dS[sIdx];
         if (lead == m) {
             const int g = sGid[m];
             gs[g] = start;
@@ -219,7 +222,10 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
                                                         Entry* __restrict__ ent,
                                                         unsigned* __restrict__ vmaxBits,
                                                         float2* __restrict__ F,
-                                                        float* __restrict__ T)
+                                                        float* __restrict__ T,
+                                                        const float* __restrict__ attr,
+                                                        const double* __restrict__ mDef,
+                                                        int idim)
 {
     extern __shared__ int sHist[];
     const int b = blockIdx.x, l = l0 + b, tid = threadIdx.x;
@@ -261,7 +267,9 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
         if (sHist[t]) sHist[t] = atomicAdd(cursor + t, sHist[t]);
     __syncthreads();
     const float2* D = dat + (size_t)l * nPxl;
-    const float* C = ctf + (size_t)l * nPxl;
+    const float* C = attr ? nullptr : ctf + (size_t)l * nPxl;
+    const float* A = attr ? attr + 8 * (size_t)l : nullptr;
+    const double* md = mDef + (size_t)b * mReco;
     const float2* ms = mShift + (size_t)b * mReco;
     const float wl = w[l];
     float vmax = 0.f;
@@ -281,18 +289,34 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
                 bool cj;
                 folded(m, ic, ir, pf, en.x, en.y, en.z, cj);
                 const float2 d = D[p];
-                const float c = C[p];
                 float vr = 0.f, vi = 0.f;
                 const int s0 = gs[g], s1 = gs[g + 1];
-                for (int s = s0; s < s1; s++) {
-                    const float2 sh = ms[s];
-                    const float2 src = cmul(d, phase_shift(ic, ir, sh.x, sh.y));
-                    vr += (src.x * c) * wl;
-                    vi += (src.y * c) * wl;
+                if (!A) {
+                    const float c = C[p];
+                    for (int s = s0; s < s1; s++) {
+                        const float2 sh = ms[s];
+                        const float2 src = cmul(d, phase_shift(ic, ir, sh.x, sh.y));
+                        vr += (src.x * c) * wl;
+                        vi += (src.y * c) * wl;
+                    }
+                    en.tv = ((float)((double)c * c) * wl) * (float)(s1 - s0);
+                } else {
+                    // CTF search: each member's CTF at its own defocus factor,
+                    // CTF(dU d, dV d) (src/Optimiser.cpp:7101-7120)
+                    float tv = 0.f;
+                    for (int s = s0; s < s1; s++) {
+                        const float2 sh = ms[s];
+                        const float c = ctf_at(A, (float)(A[2] * md[s]), (float)(A[3] * md[s]), ic,
+                                               ir, idim);
+                        const float2 src = cmul(d, phase_shift(ic, ir, sh.x, sh.y));
+                        vr += (src.x * c) * wl;
+                        vi += (src.y * c) * wl;
+                        tv += (float)((double)c * c) * wl;
+                    }
+                    en.tv = tv;
                 }
                 en.vr = vr;
                 en.vi = cj ? -vi : vi;
-                en.tv = ((float)((double)c * c) * wl) * (float)(s1 - s0);
                 vmax = fmaxf(vmax, fmaxf(fabsf(en.vr), fmaxf(fabsf(en.vi), fabsf(en.tv))));
                 if (!(fabsf(en.vr) + fabsf(en.vi) + fabsf(en.tv) <= 3.4e38f)) vmax = INFINITY;
                 t = G.tile((int)floorf(en.x), (int)floorf(en.y), (int)floorf(en.z));
@@ -445,12 +469,14 @@ BinPlan plan(int nImg, int mReco, int nOrd, int pf, int rMax)
 }
 
 size_t carve(thx::Carver& cv, const BinPlan& P, int mReco, int** nG, int** gStart, double** gMat,
-             float2** mShift, int** count, int** cursor, int4** chunks, int** ctl, Entry** ent)
+             float2** mShift, double** mDef, int** count, int** cursor, int4** chunks, int** ctl,
+             Entry** ent)
 {
     *nG = cv.take<int>(P.nB);
     *gStart = cv.take<int>((size_t)P.nB * (mReco + 1));
     *gMat = cv.take<double>((size_t)P.nB * mReco * 6);
     *mShift = cv.take<float2>((size_t)P.nB * mReco);
+    *mDef = cv.take<double>((size_t)P.nB * mReco);
     *count = cv.take<int>(P.nt);
     *cursor = cv.take<int>(P.nt);
     *chunks = cv.take<int4>(P.maxChunks);
@@ -467,20 +493,22 @@ extern "C" size_t thx_insert3d_binned_workspace(int nImg, int mReco, int nOrd, i
     const BinPlan P = plan(nImg, mReco, nOrd, pf, rMax);
     thx::Carver cv(nullptr, 0);
     int *a, *b, *c, *d, *e;
-    double* gm;
+    double *gm, *md;
     float2* ms;
     int4* ch;
     Entry* en;
-    return carve(cv, P, mReco, &a, &b, &gm, &ms, &c, &d, &ch, &e, &en);
+    return carve(cv, P, mReco, &a, &b, &gm, &ms, &md, &c, &d, &ch, &e, &en);
 }
 
-extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, int vdim, int pf,
-                                   const float* dat, const float* ctf, const double* quat,
-                                   const double* trans, const double* offS, const float* w,
-                                   const int* nC, int nImg, int mReco, const int* iCol,
-                                   const int* iRow, const int* pxOrder, int nOrd, int nPxl,
-                                   int idim, int rMax, void* workspace, size_t wsBytes,
-                                   thx_stream_t stream)
+// attr / nD (CTF search, both or neither): sample (l, m) inserts with the CTF
+// of image l's attributes at defocus factor nD[l][m]; ctf is then unused.
+static int insert_binned_impl(float* F, float* T, double* O, int* counter, int vdim, int pf,
+                              const float* dat, const float* ctf, const float* attr,
+                              const double* nD, const double* quat, const double* trans,
+                              const double* offS, const float* w, const int* nC, int nImg,
+                              int mReco, const int* iCol, const int* iRow, const int* pxOrder,
+                              int nOrd, int nPxl, int idim, int rMax, void* workspace,
+                              size_t wsBytes, thx_stream_t stream)
 {
     THX_CHECK_ARG(vdim > 0 && vdim % 2 == 0 && pf > 0 && nImg >= 0 && mReco >= 0 && nPxl >= 0 &&
                       idim > 0 && rMax > 0,
@@ -495,16 +523,16 @@ extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, 
     THX_CHECK_ARG(P.nt <= BIN_MAX_TILES,
                   "thx_insert3d_binned: %d tiles exceed the %d-tile histogram (use thx_insert3d_tiled)",
                   P.nt, BIN_MAX_TILES);
-    THX_CHECK_ARG(F && T && O && counter && dat && ctf && quat && trans && offS && w && iCol &&
-                      iRow && workspace,
+    THX_CHECK_ARG(F && T && O && counter && dat && (ctf || attr) && quat && trans && offS && w &&
+                      iCol && iRow && workspace && (!ctf || !attr) && !attr == !nD,
                   "thx_insert3d_binned: null argument");
     thx::Carver cv(workspace, wsBytes);
     int *nG, *gStart, *count, *cursor, *ctl;
-    double* gMat;
+    double *gMat, *mDef;
     float2* mShift;
     int4* chunks;
     Entry* ent;
-    carve(cv, P, mReco, &nG, &gStart, &gMat, &mShift, &count, &cursor, &chunks, &ctl, &ent);
+    carve(cv, P, mReco, &nG, &gStart, &gMat, &mShift, &mDef, &count, &cursor, &chunks, &ctl, &ent);
     THX_CHECK_ARG(cv.ok() && wsBytes >= cv.off, "thx_insert3d_binned: workspace too small");
     hipStream_t s = thx::as_stream(stream);
     const size_t hist = (size_t)P.nt * sizeof(int);
@@ -521,13 +549,14 @@ extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, 
         const int nb = nImg - l0 < P.nB ? nImg - l0 : P.nB;
         THX_HIP(hipMemsetAsync(count, 0, hist, s));
         hipLaunchKernelGGL(k_bin_groups, dim3(nb), dim3(G_THREADS), 0, s, quat, trans, offS, nC,
-                           mReco, l0, idim, nG, gStart, gMat, mShift, O, counter);
+                           mReco, l0, idim, nG, gStart, gMat, mShift, O, counter, nD, mDef);
         THX_LAUNCH_CHECK();
         const dim3 pg(nb, (nOrd + BIN_KCH - 1) / BIN_KCH);
         hipLaunchKernelGGL(k_bin_pass<false>, pg, dim3(C_THREADS), hist, s, P.G, vdim, pf,
                            mReco, l0, nG, gStart, gMat, mShift, iCol, iRow, pxOrder, nOrd, nPxl,
                            reinterpret_cast<const float2*>(dat), ctf, w, count, cursor, ent,
-                           reinterpret_cast<unsigned*>(ctl + 2), reinterpret_cast<float2*>(F), T);
+                           reinterpret_cast<unsigned*>(ctl + 2), reinterpret_cast<float2*>(F), T,
+                           attr, mDef, idim);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_bin_scan, dim3(1), dim3(1024), 0, s, count, P.nt, cursor, chunks,
                            P.maxChunks, ctl);
@@ -535,11 +564,38 @@ extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, 
         hipLaunchKernelGGL(k_bin_pass<true>, pg, dim3(C_THREADS), hist, s, P.G, vdim, pf,
                            mReco, l0, nG, gStart, gMat, mShift, iCol, iRow, pxOrder, nOrd, nPxl,
                            reinterpret_cast<const float2*>(dat), ctf, w, count, cursor, ent,
-                           reinterpret_cast<unsigned*>(ctl + 2), reinterpret_cast<float2*>(F), T);
+                           reinterpret_cast<unsigned*>(ctl + 2), reinterpret_cast<float2*>(F), T,
+                           attr, mDef, idim);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_bin_deposit, dim3(P.maxChunks), dim3(D_THREADS), DEP_LDS, s, P.G, vdim,
                            chunks, ctl, ent, F, T);
         THX_LAUNCH_CHECK();
     }
     return THX_OK;
+}
+
+extern "C" int thx_insert3d_binned(float* F, float* T, double* O, int* counter, int vdim, int pf,
+                                   const float* dat, const float* ctf, const double* quat,
+                                   const double* trans, const double* offS, const float* w,
+                                   const int* nC, int nImg, int mReco, const int* iCol,
+                                   const int* iRow, const int* pxOrder, int nOrd, int nPxl,
+                                   int idim, int rMax, void* workspace, size_t wsBytes,
+                                   thx_stream_t stream)
+{
+    return insert_binned_impl(F, T, O, counter, vdim, pf, dat, ctf, nullptr, nullptr, quat, trans,
+                              offS, w, nC, nImg, mReco, iCol, iRow, pxOrder, nOrd, nPxl, idim,
+                              rMax, workspace, wsBytes, stream);
+}
+
+extern "C" int thx_insert3d_binned_d(float* F, float* T, double* O, int* counter, int vdim,
+                                     int pf, const float* dat, const float* attr,
+                                     const double* nD, const double* quat, const double* trans,
+                                     const double* offS, const float* w, const int* nC, int nImg,
+                                     int mReco, const int* iCol, const int* iRow,
+                                     const int* pxOrder, int nOrd, int nPxl, int idim, int rMax,
+                                     void* workspace, size_t wsBytes, thx_stream_t stream)
+{
+    return insert_binned_impl(F, T, O, counter, vdim, pf, dat, nullptr, attr, nD, quat, trans,
+                              offS, w, nC, nImg, mReco, iCol, iRow, pxOrder, nOrd, nPxl, idim,
+                              rMax, workspace, wsBytes, stream);
 }

@@ -127,7 +127,7 @@ extern "C" int thx_ExpectGlobal3D(const float* rotP, const float* traP,
     THX_HIP(hipMemcpy(dRot.p, rotP, sizeof(float) * 2 * (size_t)nR * npxl, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dTra.p, traP, sizeof(float) * 2 * (size_t)nT * npxl, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dDat.p, datP, sizeof(float) * 2 * nPx, hipMemcpyHostToDevice));
-    THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
+    if (ctfP) THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dSig.p, sigRcpP, sizeof(float) * nPx, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dPR.p, pR, sizeof(double) * nR, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dPT.p, pT, sizeof(double) * nT, hipMemcpyHostToDevice));
@@ -149,18 +149,25 @@ extern "C" int thx_ExpectGlobal3D(const float* rotP, const float* traP,
     return THX_OK;
 }
 
+// ctfa / nD (CTF search, both or neither): CTFAttr[imgNum] (7 RFLOAT:
+// voltage, defocusU, defocusV, defocusTheta, Cs, amplitudeContrast,
+// phaseShift; include/Database.h:302-327) and the samples' defocus factors
+// nD[imgNum * mReco]; ctfP is then unused.
 static int insert_ft(float* F3D, float* T3D, double* O3D, int* counter, const float* datP,
                      const float* ctfP, const double* offS, const float* w, const double* nR,
                      const double* nT, const int* nC, const int* iCol, const int* iRow, int opf,
-                     int npxl, int mReco, int idim, int vdim, int imgNum, void* comm)
+                     int npxl, int mReco, int idim, int vdim, int imgNum, void* comm,
+                     const float* ctfa = nullptr, const double* nD = nullptr,
+                     float pixelSize = 0.f)
 {
-    THX_CHECK_ARG(F3D && T3D && O3D && counter && datP && ctfP && offS && w && nR &&
-                      nT && iCol && iRow,
+    THX_CHECK_ARG(F3D && T3D && O3D && counter && datP && (ctfP || ctfa) && offS && w && nR &&
+                      nT && iCol && iRow && !ctfa == !nD,
                   "thx_InsertFT: null");
+    THX_CHECK_ARG(!ctfa || pixelSize > 0.f, "thx_InsertFT: CTF search needs the pixel size");
     THX_CHECK_ARG(imgNum >= 0 && mReco >= 0 && npxl >= 0 && opf > 0, "thx_InsertFT: bad sizes");
     const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
     const size_t nPx = (size_t)imgNum * npxl, nS = (size_t)imgNum * mReco;
-    DBuf dF, dT, dO, dC, dDat, dCtf, dOff, dW, dQ, dTr, dIc, dIr, dN;
+    DBuf dF, dT, dO, dC, dDat, dCtf, dOff, dW, dQ, dTr, dIc, dIr, dN, dA, dND;
     THX_DALLOC(dF, sizeof(float) * 2 * dimSize);
     THX_DALLOC(dT, sizeof(float) * dimSize);
     THX_DALLOC(dO, sizeof(double) * 3);
@@ -174,6 +181,18 @@ static int insert_ft(float* F3D, float* T3D, double* O3D, int* counter, const fl
     THX_DALLOC(dIc, sizeof(int) * npxl);
     THX_DALLOC(dIr, sizeof(int) * npxl);
     THX_DALLOC(dN, sizeof(int) * imgNum);
+    if (ctfa) {
+        // the thx_ctf attribute rows {pixelSize, voltage, dU, dV, theta, Cs, ampC, ps}
+        std::vector<float> a(8 * (size_t)imgNum);
+        for (int l = 0; l < imgNum; l++) {
+            a[8 * (size_t)l] = pixelSize;
+            for (int k = 0; k < 7; k++) a[8 * (size_t)l + 1 + k] = ctfa[7 * (size_t)l + k];
+        }
+        THX_DALLOC(dA, sizeof(float) * a.size());
+        THX_DALLOC(dND, sizeof(double) * nS);
+        THX_HIP(hipMemcpy(dA.p, a.data(), sizeof(float) * a.size(), hipMemcpyHostToDevice));
+        THX_HIP(hipMemcpy(dND.p, nD, sizeof(double) * nS, hipMemcpyHostToDevice));
+    }
     // the reference seeds GPU0 with the host F/T and accumulates on top
     // (gpu/src/cuthunder.cu:5422-5555)
     THX_HIP(hipMemcpy(dF.p, F3D, sizeof(float) * 2 * dimSize, hipMemcpyHostToDevice));
@@ -181,7 +200,7 @@ static int insert_ft(float* F3D, float* T3D, double* O3D, int* counter, const fl
     THX_HIP(hipMemcpy(dO.p, O3D, sizeof(double) * 3, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dC.p, counter, sizeof(int), hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dDat.p, datP, sizeof(float) * 2 * nPx, hipMemcpyHostToDevice));
-    THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
+    if (ctfP) THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dOff.p, offS, sizeof(double) * 2 * imgNum, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dW.p, w, sizeof(float) * imgNum, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dQ.p, nR, sizeof(double) * 4 * nS, hipMemcpyHostToDevice));
@@ -220,7 +239,23 @@ static int insert_ft(float* F3D, float* T3D, double* O3D, int* counter, const fl
     const size_t binWs = thx_insert3d_binned_workspace(imgNum, mReco, nOrd, opf, rMax);
     const int R = opf * rMax + 2;
     const long nTiles = (long)((R + 15) / 16) * ((2 * R + 15) / 16) * ((2 * R + 15) / 16);
-    if (mReco <= 1024 && R <= vdim / 2 - 1 && nTiles <= 16384 && imgNum > 0) {
+    const bool binned = mReco <= 1024 && R <= vdim / 2 - 1 && nTiles <= 16384;
+    THX_CHECK_ARG(!ctfa || binned || imgNum == 0,
+                  "thx_InsertFT: the CTF-search insert needs mReco <= 1024 and a tile grid of "
+                  "<= 16384 tiles");
+    if (binned && imgNum > 0 && ctfa) {
+        DBuf dOrd, dWs;
+        THX_DALLOC(dOrd, sizeof(int) * nOrd);
+        THX_DALLOC(dWs, binWs);
+        THX_HIP(hipMemcpy(dOrd.p, order.data(), sizeof(int) * nOrd, hipMemcpyHostToDevice));
+        THX_RET(thx_insert3d_binned_d(dF.as<float>(), dT.as<float>(), dO.as<double>(),
+                                      dC.as<int>(), vdim, opf, dDat.as<float>(), dA.as<float>(),
+                                      dND.as<double>(), dQ.as<double>(), dTr.as<double>(),
+                                      dOff.as<double>(), dW.as<float>(),
+                                      nC ? dN.as<int>() : nullptr, imgNum, mReco, dIc.as<int>(),
+                                      dIr.as<int>(), dOrd.as<int>(), nOrd, npxl, idim, rMax,
+                                      dWs.p, binWs, nullptr));
+    } else if (binned && imgNum > 0) {
         DBuf dOrd, dWs;
         THX_DALLOC(dOrd, sizeof(int) * nOrd);
         THX_DALLOC(dWs, binWs);
@@ -266,6 +301,18 @@ extern "C" int thx_InsertFT(float* F3D, float* T3D, double* O3D, int* counter,
 {
     return insert_ft(F3D, T3D, O3D, counter, datP, ctfP, offS, w, nR, nT, nullptr, iCol, iRow,
                      opf, npxl, mReco, idim, vdim, imgNum, nullptr);
+}
+
+extern "C" int thx_InsertFTCS(float* F3D, float* T3D, double* O3D, int* counter,
+                              const float* datP, const float* ctfaData, const double* offS,
+                              const float* w, const double* nR, const double* nT,
+                              const double* nD, const int* nC, const int* iCol, const int* iRow,
+                              float pixelSize, int opf, int npxl, int mReco, int idim, int vdim,
+                              int imgNum, void* comm)
+{
+    THX_CHECK_ARG(ctfaData && nD, "thx_InsertFTCS: ctfaData and nD are required");
+    return insert_ft(F3D, T3D, O3D, counter, datP, nullptr, offS, w, nR, nT, nC, iCol, iRow, opf,
+                     npxl, mReco, idim, vdim, imgNum, comm, ctfaData, nD, pixelSize);
 }
 
 extern "C" int thx_InsertFTC(float* F3D, float* T3D, double* O3D, int* counter,
@@ -327,7 +374,7 @@ extern "C" int thx_ExpectGlobal2D(const float* vol, const float* datP, const flo
     THX_HIP(hipMemcpy(dRot.p, rot, sizeof(double) * 2 * nR, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dTr.p, trans, sizeof(double) * 2 * nT, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dDat.p, datP, sizeof(float) * 2 * nPx, hipMemcpyHostToDevice));
-    THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
+    if (ctfP) THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dSig.p, sigRcpP, sizeof(float) * nPx, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dPR.p, pR, sizeof(double) * nR, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dPT.p, pT, sizeof(double) * nT, hipMemcpyHostToDevice));
@@ -383,7 +430,7 @@ extern "C" int thx_InsertI2D(float* F2D, float* T2D, double* O2D, int* counter, 
     THX_HIP(hipMemcpy(dO.p, O2D, sizeof(double) * 2 * nk, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dC.p, counter, sizeof(int) * nk, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dDat.p, datP, sizeof(float) * 2 * nPx, hipMemcpyHostToDevice));
-    THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
+    if (ctfP) THX_HIP(hipMemcpy(dCtf.p, ctfP, sizeof(float) * nPx, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dW.p, w, sizeof(float) * imgNum, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dOff.p, offS, sizeof(double) * 2 * imgNum, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(dN.p, nC, sizeof(int) * nS, hipMemcpyHostToDevice));

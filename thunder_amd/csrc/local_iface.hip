@@ -17,7 +17,12 @@
 // volume, pixel set and geometry to the calpoint; ExpectLocalM runs the fused
 // projection + likelihood + marginals (thx_local_phase for one image) and
 // copies wC / wR / wT / wD back, synchronising the calpoint's stream as the
-// reference does (cuthunder.cu:3140).  CTF search (mD > 1) is not supported.
+// reference does (cuthunder.cu:3140).  CTF search (searchType 2 / cSearch):
+// ExpectLocalIn also allocates the per-pixel defocus slots, ExpectLocalP
+// fills them, ExpectLocalRTD uploads the defocus factors (dpara) and their
+// priors (oldD), ExpectLocalPreI3D computes the calpoint's CTF per defocus
+// sample (kernel_CalCTFL, cuthunder.cu:2796-2810) and ExpectLocalM runs the
+// (r, t, d) phase (thx_local_phase_d) and returns wD.
 // This per-image path exists for drop-in compatibility; thx_expectation runs
 // the same phases for the whole batch on device.
 #include <vector>
@@ -32,7 +37,10 @@ struct Tex {
 };
 
 struct CalPoint {
-    int gpu = 0, mR = 0, mT = 0, npxl = 0;
+    int gpu = 0, mR = 0, mT = 0, npxl = 0, mD = 1;
+    bool cs = false;                                      // SEARCH_TYPE_CTF
+    double *dP = nullptr, *pD = nullptr;                  // defocus factors, priors
+    float *ctfD = nullptr, *wD = nullptr;                 // CTF per sample, marginal
     hipStream_t stream = nullptr;
     double *quat = nullptr, *trans = nullptr, *pR = nullptr, *pT = nullptr, *pC = nullptr;
     float *wC = nullptr, *wR = nullptr, *wT = nullptr, *base = nullptr;
@@ -61,6 +69,19 @@ int dalloc(T** p, size_t n)
         int st_ = (call);              \
         if (st_ != THX_OK) return st_; \
     } while (0)
+
+// kernel_CalCTFL for one calpoint: ctfD[d][i] from the image's per-pixel
+// defocus, the frequencies and the calpoint's defocus factors
+__global__ void __launch_bounds__(256) k_calpoint_ctf(const float* __restrict__ dfo,
+                                                      const float* __restrict__ freq,
+                                                      const double* __restrict__ dP, float ps,
+                                                      float conT, float k1, float k2, int npxl,
+                                                      float* __restrict__ ctfD)
+{
+    const double d = dP[blockIdx.y];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npxl; i += gridDim.x * blockDim.x)
+        ctfD[(size_t)blockIdx.y * npxl + i] = ctf_search_at(k1, dfo[i], d, freq[i], k2, ps, conT);
+}
 
 }  // namespace
 
@@ -108,13 +129,14 @@ extern "C" int thx_ExpectLocalIn(int gpuIdx, float** devdatP, float** devctfP, f
 {
     THX_CHECK_ARG(devdatP && devctfP && devsigP && nPxl > 0 && cpyNumL > 0,
                   "thx_ExpectLocalIn: bad arguments");
-    THX_CHECK_ARG(searchType != 2, "thx_ExpectLocalIn: CTF search is not supported");
+    THX_CHECK_ARG(searchType != 2 || devdefO, "thx_ExpectLocalIn: CTF search needs devdefO");
     THX_DEV_SET(gpuIdx);
     const size_t n = (size_t)nPxl * cpyNumL;
     THX_RET(dalloc(devdatP, 2 * n));
     THX_RET(dalloc(devctfP, n));
     THX_RET(dalloc(devsigP, n));
-    if (devdefO) *devdefO = nullptr;
+    if (searchType == 2) THX_RET(dalloc(devdefO, n));
+    else if (devdefO) *devdefO = nullptr;
     return THX_OK;
 }
 
@@ -123,15 +145,17 @@ extern "C" int thx_ExpectLocalP(int gpuIdx, float* devdatP, float* devctfP, floa
                                 const float* defO, const float* sigP, int threadId, int imgId,
                                 int npxl, int cSearch)
 {
-    (void)devdefO; (void)defO;
-    THX_CHECK_ARG(devdatP && devctfP && devsigP && datP && ctfP && sigP && threadId >= 0 &&
-                      imgId >= 0 && npxl > 0,
+    THX_CHECK_ARG(devdatP && devctfP && devsigP && datP && (ctfP || cSearch) && sigP &&
+                      threadId >= 0 && imgId >= 0 && npxl > 0 &&
+                      (!cSearch || (devdefO && defO)),
                   "thx_ExpectLocalP: bad arguments");
-    THX_CHECK_ARG(!cSearch, "thx_ExpectLocalP: CTF search is not supported");
     THX_DEV_SET(gpuIdx);
     const size_t d = (size_t)threadId * npxl, s = (size_t)imgId * npxl;
     THX_HIP(hipMemcpy(devdatP + 2 * d, datP + 2 * s, sizeof(float) * 2 * npxl, hipMemcpyHostToDevice));
-    THX_HIP(hipMemcpy(devctfP + d, ctfP + s, sizeof(float) * npxl, hipMemcpyHostToDevice));
+    if (ctfP)
+        THX_HIP(hipMemcpy(devctfP + d, ctfP + s, sizeof(float) * npxl, hipMemcpyHostToDevice));
+    if (cSearch)
+        THX_HIP(hipMemcpy(devdefO + d, defO + s, sizeof(float) * npxl, hipMemcpyHostToDevice));
     THX_HIP(hipMemcpy(devsigP + d, sigP + s, sizeof(float) * npxl, hipMemcpyHostToDevice));
     return THX_OK;
 }
@@ -235,13 +259,16 @@ extern "C" int thx_calpoint_create(int mode, int searchType, int gpuIdx, int mR,
 {
     THX_CHECK_ARG(mcp && mR > 0 && mT > 0 && npxl > 0, "thx_calpoint_create: bad arguments");
     THX_CHECK_ARG(mode == 1, "thx_calpoint_create: only MODE_3D (1) is supported");
-    THX_CHECK_ARG(searchType != 2 && mD <= 1, "thx_calpoint_create: CTF search is not supported");
+    THX_CHECK_ARG(searchType != 2 || (mD >= 1 && (long)mT * mD <= 1024),
+                  "thx_calpoint_create: CTF search needs 1 <= mD, mT * mD <= 1024");
     THX_DEV_SET(gpuIdx);
     CalPoint* c = new CalPoint;
     c->gpu = gpuIdx;
     c->mR = mR;
     c->mT = mT;
     c->npxl = npxl;
+    c->cs = searchType == 2;
+    c->mD = c->cs ? mD : 1;
     int st = THX_OK;
     auto chk = [&](hipError_t e) {
         if (e != hipSuccess && st == THX_OK) {
@@ -262,8 +289,14 @@ extern "C" int thx_calpoint_create(int mode, int searchType, int gpuIdx, int mR,
     // the tile order of a pixel set has at most ~1.25 npxl + 16 entries
     const int ordCap = (npxl * 2 + 31) / 16 * 16;
     chk(hipMalloc(&c->order, sizeof(int) * ordCap));
-    c->wsBytes = thx_local_phase_workspace(1, mR, mT, ordCap > npxl ? ordCap : npxl);
+    c->wsBytes = thx_local_phase_workspace(1, mR, mT * c->mD, ordCap > npxl ? ordCap : npxl);
     chk(hipMalloc(&c->ws, c->wsBytes));
+    if (c->cs) {
+        chk(hipMalloc(&c->dP, sizeof(double) * c->mD));
+        chk(hipMalloc(&c->pD, sizeof(double) * c->mD));
+        chk(hipMalloc(&c->ctfD, sizeof(float) * c->mD * npxl));
+        chk(hipMalloc(&c->wD, sizeof(float) * c->mD));
+    }
     *mcp = c;
     return st;
 }
@@ -273,7 +306,8 @@ extern "C" int thx_calpoint_destroy(void* mcp)
     CalPoint* c = static_cast<CalPoint*>(mcp);
     if (!c) return THX_OK;
     THX_DEV_SET(c->gpu);
-    void* all[] = {c->quat, c->trans, c->pR, c->pT, c->pC, c->wC, c->wR, c->wT, c->base, c->order, c->ws};
+    void* all[] = {c->quat, c->trans, c->pR, c->pT, c->pC, c->wC, c->wR, c->wT, c->base, c->order,
+                   c->ws, c->dP, c->pD, c->ctfD, c->wD};
     for (void* p : all)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -285,10 +319,15 @@ extern "C" int thx_ExpectLocalRTD(int gpuIdx, void* mcp, const double* oldR, con
                                   const double* oldD, const double* trans, const double* rot,
                                   const double* dpara)
 {
-    (void)oldD; (void)dpara;
     CalPoint* c = static_cast<CalPoint*>(mcp);
-    THX_CHECK_ARG(c && oldR && oldT && trans && rot && gpuIdx == c->gpu,
+    THX_CHECK_ARG(c && oldR && oldT && trans && rot && gpuIdx == c->gpu &&
+                      (!c->cs || (oldD && dpara)),
                   "thx_ExpectLocalRTD: bad arguments");
+    if (c->cs) {
+        THX_DEV_SET(gpuIdx);
+        THX_HIP(hipMemcpyAsync(c->dP, dpara, sizeof(double) * c->mD, hipMemcpyHostToDevice, c->stream));
+        THX_HIP(hipMemcpyAsync(c->pD, oldD, sizeof(double) * c->mD, hipMemcpyHostToDevice, c->stream));
+    }
     THX_DEV_SET(gpuIdx);
     THX_HIP(hipMemcpyAsync(c->pR, oldR, sizeof(double) * c->mR, hipMemcpyHostToDevice, c->stream));
     THX_HIP(hipMemcpyAsync(c->pT, oldT, sizeof(double) * c->mT, hipMemcpyHostToDevice, c->stream));
@@ -303,15 +342,22 @@ extern "C" int thx_ExpectLocalPreI3D(int gpuIdx, int datShift, void* mgr, void* 
                                      float conT, float k1, float k2, int pf, int idim, int vdim,
                                      int npxl, int interp)
 {
-    (void)datShift; (void)devdefO; (void)devfreQ; (void)phaseShift; (void)conT;
     CalPoint* c = static_cast<CalPoint*>(mcp);
     const Tex* t = static_cast<const Tex*>(mgr);
     THX_CHECK_ARG(c && t && deviCol && deviRow && gpuIdx == c->gpu && npxl == c->npxl &&
                       vdim == t->vdim && vdim == pf * idim,
                   "thx_ExpectLocalPreI3D: bad arguments");
     THX_CHECK_ARG(interp == 1, "thx_ExpectLocalPreI3D: only LINEAR_INTERP (1) is supported");
-    THX_CHECK_ARG(k1 == 0.f && k2 == 0.f, "thx_ExpectLocalPreI3D: CTF search is not supported");
+    THX_CHECK_ARG(!c->cs || (devdefO && devfreQ && datShift >= 0),
+                  "thx_ExpectLocalPreI3D: a CTF search needs devdefO and devfreQ");
     THX_DEV_SET(gpuIdx);
+    if (c->cs) {
+        hipLaunchKernelGGL(k_calpoint_ctf, dim3(thx::cdiv(npxl, 256) > 16 ? 16 : thx::cdiv(npxl, 256),
+                                                c->mD),
+                           dim3(256), 0, c->stream, devdefO + (size_t)datShift * npxl, devfreQ,
+                           c->dP, phaseShift, conT, k1, k2, npxl, c->ctfD);
+        THX_LAUNCH_CHECK();
+    }
     if (c->boundCol != deviCol) {
         // the pixel set's local-phase visiting order, once per calpoint and set
         std::vector<int> hc(npxl), hr(npxl);
@@ -342,11 +388,25 @@ extern "C" int thx_ExpectLocalM(int gpuIdx, int datShift, void* mcp, const float
 {
     CalPoint* c = static_cast<CalPoint*>(mcp);
     THX_CHECK_ARG(c && c->tex && devdatP && devctfP && devsigP && wC && wR && wT &&
-                      gpuIdx == c->gpu && npxl == c->npxl && datShift >= 0,
+                      gpuIdx == c->gpu && npxl == c->npxl && datShift >= 0 && (!c->cs || wD),
                   "thx_ExpectLocalM: bad arguments (ExpectLocalPreI3D must come first)");
     THX_DEV_SET(gpuIdx);
     const size_t off = (size_t)datShift * npxl;
     THX_HIP(hipMemcpyAsync(c->pC, &oldC, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (c->cs) {
+        // kernel_logDataVSLC + kernel_UpdateWLC (cuthunder.cu:2915-3140)
+        THX_RET(thx_local_phase_d(nullptr, c->tex->vol, 0, c->vdim, c->pf, c->quat, c->mR,
+                                  c->trans, c->mT, c->mD, c->pC, c->pR, c->pT, c->pD,
+                                  devdatP + 2 * off, c->ctfD, devsigP + off, c->iCol, c->iRow,
+                                  c->order, c->nOrd, npxl, c->idim, 1, c->wC, c->wR, c->wT, c->wD,
+                                  c->base, nullptr, c->ws, c->wsBytes, c->stream));
+        THX_HIP(hipMemcpyAsync(wC, c->wC, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipMemcpyAsync(wR, c->wR, sizeof(float) * c->mR, hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipMemcpyAsync(wT, c->wT, sizeof(float) * c->mT, hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipMemcpyAsync(wD, c->wD, sizeof(float) * c->mD, hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipStreamSynchronize(c->stream));
+        return THX_OK;
+    }
     THX_RET(thx_local_phase(c->tex->vol, 0, c->vdim, c->pf, c->quat, c->mR, c->trans, c->mT, c->pC,
                             c->pR, c->pT, devdatP + 2 * off, devctfP + off, devsigP + off, c->iCol,
                             c->iRow, c->order, c->nOrd, npxl, c->idim, 1, c->wC, c->wR, c->wT,

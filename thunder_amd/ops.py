@@ -411,6 +411,36 @@ def insert3d(hm, dat, ctf_, quat, trans, offS, w, px, tiled=True, nC=None, metho
     return hm
 
 
+def insert3d_ctf(hm, dat, attr, nD, quat, trans, offS, w, px, nC=None):
+    """CTF-search insert (thx_insert3d_binned_d): sample (l, m) with the CTF of
+    attr[l] at defocus factor nD[l, m]."""
+    nImg, nPxl = dat.shape
+    mReco = quat.shape[1]
+    _req(dat, torch.complex64, (nImg, nPxl), "dat")
+    _req(attr, torch.float32, (nImg, 8), "attr")
+    _req(nD, torch.float64, (nImg, mReco), "nD")
+    _req(quat, torch.float64, (nImg, mReco, 4), "quat")
+    _req(trans, torch.float64, (nImg, mReco, 2), "trans")
+    _req(offS, torch.float64, (nImg, 2), "offS")
+    _req(w, torch.float32, (nImg,), "w")
+    if nC is not None:
+        _req(nC, torch.int32, (nImg,), "nC")
+    if nPxl != px.n:
+        raise ValueError("pixel set / image size mismatch")
+    if insert_method(hm, mReco, px) != "binned":
+        raise ValueError("CTF-search insert needs the binned deposition's limits "
+                         "(mReco <= 1024, tile grid <= 16384)")
+    dev = dat.device
+    rMax = int(math.ceil(px.rU))
+    ws = workspace(lib().thx_insert3d_binned_workspace(nImg, mReco, len(px.order), px.pf, rMax), dev)
+    check(lib().thx_insert3d_binned_d(
+        _ptr(hm.F), _ptr(hm.T), _ptr(hm.O), _ptr(hm.counter), hm.vdim, px.pf, _ptr(dat),
+        _ptr(attr), _ptr(nD), _ptr(quat), _ptr(trans), _ptr(offS), _ptr(w), _ptr(nC), nImg, mReco,
+        _ptr(px.d_iCol), _ptr(px.d_iRow), _ptr(px.d_order), len(px.order), nPxl, px.idim, rMax,
+        _ptr(ws), ws.numel(), _stream(dev)), "thx_insert3d_binned_d")
+    return hm
+
+
 # ------------------------------------------------------------------ a13
 class RcclComm:
     """RCCL communicator of one hemisphere for thx_halfmap_allreduce, built
