@@ -289,7 +289,10 @@ def main():
     mR, mT = 125, 9
     log(rank, f"[bench] building synthetic volume N={N} pf={pf}")
     vol = synth.projectee(synth.blob_volume(N, seed=1, device=dev), pf)
-    gset = synth.global_sample_set(a.nr, seed=2)
+    # a3 on device (Particle::reset through thx_global_sample_set); sizes by the
+    # reference's rules (thx_global_sample_sizes: nT = 151 at transS 10)
+    _, nR, nT = ops.global_sample_sizes(a.nr)
+    gset = tuple(x.cpu().numpy() for x in ops.global_sample_set(nR, nT, 10.0, 2, dev))
     px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, rL, a.images, dev, seed=5 + 101 * rank,
                                                  vol=vol)
     mk = lambda algo: ex.Expectation(vol, px, gset, n_phase=a.phases, algo=algo, seed=7 + rank,

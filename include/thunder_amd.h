@@ -81,6 +81,21 @@ int thx_pixel_tile_order(const int* iCol, const int* iRow, int nPxl, int cap,
 int thx_ctf(const float* attr, int nImg, const int* iCol, const int* iRow,
             int nPxl, int idim, float* ctfP, thx_stream_t stream);
 
+/* ------------------------------------------------------------------ a3 ---
+ * The global-search sample set.  thx_global_sample_sizes (host): the 3D
+ * clamp mS >= 1500 (1 + nSymElem) (src/Optimiser.cpp:170-175), nR = mS /
+ * (1 + nSymElem) in 3D (mode 1) or mS in 2D (mode 0), nT = max(30,
+ * AROUND(pi (transS chi2Qinv(0.5, 2))^2 transSearchFactor)) (:1724-1745).
+ * thx_global_sample_set (device): Particle::reset (src/Particle.cpp:87-169)
+ * for 3D, C1 -- quat[nR*4] uniform on S^3 (sampleACG with the identity),
+ * trans[nT*2] ~ N(0, transS^2 I), pR = 1/nR, pT = balanceWeight(PAR_T)
+ * normalised; counter RNG (seed). */
+int thx_global_sample_sizes(int mode, int mS, int nSymElem, double transS,
+                            double transSearchFactor, int* mSOut, int* nR, int* nT);
+int thx_global_sample_set(int nR, int nT, double transS, unsigned long long seed,
+                          double* quat, double* trans, double* pR, double* pT,
+                          thx_stream_t stream);
+
 /* ------------------------------------------------------------------ a4 ---
  * Translation phase table traP[t][i] = exp(-2 pi i (iCol tx + iRow ty)/idim)
  * (translate(), src/Image/ImageFunctions.cpp:233-252; kernel_Translate,

@@ -222,3 +222,18 @@ def test_insert_ctf_search(orc, stack, spread, mReco, dup):
     assert np.max(np.abs(gT - Tm)) <= 1e-5 * np.max(np.abs(Tm))
     assert np.allclose(hm.O.cpu().numpy(), O, rtol=1e-12, atol=1e-12)
     assert int(hm.counter.item()) == cnt == nImg * mReco
+
+
+def test_global_sample_set_on_device():
+    """a3: Particle::reset's global set from the C-ABI producer."""
+    nR, nT, transS = 4000, 151, 10.0
+    q, t, pR, pT = [x.cpu().numpy() for x in ops.global_sample_set(nR, nT, transS, 7, DEV)]
+    assert np.allclose(np.linalg.norm(q, axis=1), 1, atol=1e-14)
+    assert np.allclose(q.T @ q / nR, np.eye(4) / 4, atol=0.02)        # uniform on S^3
+    assert abs(t.mean()) < 1.5 and abs(t.std() - transS) < 1.5
+    assert np.allclose(pR, 1.0 / nR)
+    m, s = t.mean(0), t.std(0, ddof=1)
+    ref = 1.0 / (np.exp(-0.5 * (((t - m) / s) ** 2).sum(1)) / (2 * np.pi * s[0] * s[1]))
+    assert np.allclose(pT, ref / ref.sum(), rtol=1e-12, atol=0)
+    q2 = ops.global_sample_set(nR, nT, transS, 7, DEV)[0].cpu().numpy()
+    assert np.array_equal(q, q2)

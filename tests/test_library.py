@@ -158,3 +158,16 @@ def test_round2_entry_points_validate_without_gpu(L):
     assert L.thx_reconstruct(None, None, 32, 2, 1.9, 15.0, 1, 0, 0, None, 0, 0, None, None, None,
                              None, None, 0, None) == bad
     assert L.thx_halfmap_allreduce(None, None, None, None, None, 10, 1, None) == bad
+
+
+def test_global_sample_sizes_match_survey():
+    """a3 sizes (host function, no GPU): nT = 151 at transS 10, tsf 0.25
+    (SURVEY 8a), the 3D clamp 500 -> 1500 (C2), nR = mS / (1 + nSym)."""
+    from thunder_amd import ops, synth
+    assert ops.global_sample_sizes(2000) == (2000, 2000, 151)
+    assert ops.global_sample_sizes(500) == (1500, 1500, 151)
+    assert ops.global_sample_sizes(500, n_sym_elem=3) == (6000, 1500, 151)
+    assert ops.global_sample_sizes(500, mode=0) == (500, 500, 151)
+    assert ops.global_sample_sizes(2000, trans_s=2.0)[2] == 30
+    for ts in (3.0, 10.0, 17.5):
+        assert ops.global_sample_sizes(2000, trans_s=ts)[2] == synth.n_trans_global(ts, 0.25)

@@ -41,6 +41,9 @@ SIGNATURES = {
     "thx_expectation_ctf_workspace": (_c_size, [_p, _p, _c_int, _c_int, _c_int]),
     "thx_expectation_ctf": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _p, _p,
                                      _p, _p, _p, _p, _p, _p, _c_size, _p]),
+    "thx_global_sample_sizes": (_c_int, [_c_int, _c_int, _c_int, _c_double, _c_double, _p, _p, _p]),
+    "thx_global_sample_set": (_c_int, [_c_int, _c_int, _c_double, ctypes.c_ulonglong, _p, _p, _p, _p,
+                                       _p]),
     "thx_resample": (_c_int, [_c_int, _c_int, _p, _p, _c_int, _p, _p, _p, _p, _p]),
     "thx_pf_resample_workspace": (_c_size, [_c_int, _c_int]),
     "thx_pf_resample": (_c_int, [_c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, ctypes.c_ulonglong,

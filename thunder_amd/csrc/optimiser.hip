@@ -23,6 +23,8 @@
 // k_pf_resample).  Not replicated: the generator -- sampling is counter-based
 // (Philox4x32-10), so a run is reproducible for a given seed, where the
 // reference draws from an urandom-seeded GSL mt19937.
+#include <cmath>
+
 #include "common.h"
 
 namespace thx {
@@ -926,6 +928,74 @@ __global__ void __launch_bounds__(256) k_pf_defocus(int nImg, int mD, int op, do
     balance_d(D, mD, lane, pD + (size_t)l * mD);
 }
 
+// ---- a3: the global sample set of Particle::reset (src/Particle.cpp:87-169)
+// for 3D, C1: rotations from sampleACG with the identity (a normalised 4D
+// Gaussian: uniform on S^3), translations from a bivariate Gaussian of width
+// transS (PARTICLE_TRANS_INIT_GAUSSIAN), pR = 1/nR, pT = balanceWeight(PAR_T)
+// (:2342-2375: 1 / N2(t - m; s0, s1, rho = 0) with the sample mean and
+// gsl_stats_sd_m, normalised).  Counter RNG; one workgroup does T.
+__global__ void __launch_bounds__(256) k_sample_set(int nR, int nT, double transS, uint64_t seed,
+                                                    double* __restrict__ quat,
+                                                    double* __restrict__ trans,
+                                                    double* __restrict__ pR,
+                                                    double* __restrict__ pT)
+{
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < nR) {
+        Philox rng(seed, (uint32_t)i, 0x5a3u, 0u);
+        const double2 g0 = rng.gauss2(), g1 = rng.gauss2();
+        const double n = sqrt(g0.x * g0.x + g0.y * g0.y + g1.x * g1.x + g1.y * g1.y);
+        quat[4 * (size_t)i] = g0.x / n;
+        quat[4 * (size_t)i + 1] = g0.y / n;
+        quat[4 * (size_t)i + 2] = g1.x / n;
+        quat[4 * (size_t)i + 3] = g1.y / n;
+        pR[i] = 1.0 / nR;
+    }
+    if (blockIdx.x != 0) return;
+    __shared__ double sRed[4][4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    auto block_sum2 = [&](double a, double b, double& ra, double& rb) {
+        a = wave_sum(a);
+        b = wave_sum(b);
+        __syncthreads();
+        if (lane == 0) { sRed[wv][0] = a; sRed[wv][1] = b; }
+        __syncthreads();
+        ra = sRed[0][0] + sRed[1][0] + sRed[2][0] + sRed[3][0];
+        rb = sRed[0][1] + sRed[1][1] + sRed[2][1] + sRed[3][1];
+    };
+    double sx = 0.0, sy = 0.0;
+    for (int t = threadIdx.x; t < nT; t += 256) {
+        Philox rng(seed, (uint32_t)t, 0x5a4u, 0u);
+        const double2 g = rng.gauss2();
+        trans[2 * (size_t)t] = g.x * transS;
+        trans[2 * (size_t)t + 1] = g.y * transS;
+        sx += g.x * transS;
+        sy += g.y * transS;
+    }
+    double m0, m1;
+    block_sum2(sx, sy, m0, m1);
+    m0 /= nT;
+    m1 /= nT;
+    double vx = 0.0, vy = 0.0;
+    for (int t = threadIdx.x; t < nT; t += 256) {
+        vx += (trans[2 * (size_t)t] - m0) * (trans[2 * (size_t)t] - m0);
+        vy += (trans[2 * (size_t)t + 1] - m1) * (trans[2 * (size_t)t + 1] - m1);
+    }
+    double v0, v1;
+    block_sum2(vx, vy, v0, v1);
+    const double s0 = sqrt(v0 / (nT - 1)), s1 = sqrt(v1 / (nT - 1));
+    double tot = 0.0;
+    for (int t = threadIdx.x; t < nT; t += 256) {
+        const double u = (trans[2 * (size_t)t] - m0) / s0, v = (trans[2 * (size_t)t + 1] - m1) / s1;
+        const double x = 1.0 / (exp(-(u * u + v * v) / 2) / (2 * M_PI * s0 * s1));
+        pT[t] = x;
+        tot += x;
+    }
+    double tt, unused;
+    block_sum2(tot, 0.0, tt, unused);
+    for (int t = threadIdx.x; t < nT; t += 256) pT[t] /= tt;
+}
+
 struct Plan {
     // carve of the driver workspace
     float* rotP; double* gMat; float* traP;
@@ -1055,6 +1125,36 @@ extern "C" int thx_pf_balance_rot(int nImg, int mR, const double* quat, double* 
     if (nImg == 0) return THX_OK;
     hipLaunchKernelGGL(k_pf_balance_rot, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0,
                        thx::as_stream(stream), nImg, mR, quat, pR);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" int thx_global_sample_sizes(int mode, int mS, int nSymElem, double transS,
+                                       double transSearchFactor, int* mSOut, int* nR, int* nT)
+{
+    THX_CHECK_ARG((mode == 0 || mode == 1) && mS > 0 && nSymElem >= 0 && transS > 0.0 &&
+                      transSearchFactor > 0.0 && nR && nT,
+                  "thx_global_sample_sizes: bad arguments");
+    // the 3D clamp of Optimiser::init (src/Optimiser.cpp:170-175, MIN_M_S = 1500)
+    const int m = mode == 1 ? (mS > 1500 * (1 + nSymElem) ? mS : 1500 * (1 + nSymElem)) : mS;
+    if (mSOut) *mSOut = m;
+    *nR = mode == 1 ? m / (1 + nSymElem) : m;                       // :1724-1738
+    // nT = max(30, AROUND(pi (transS chi2Qinv(0.5, 2))^2 tsf)), chi2Qinv(0.5, 2) = 2 ln 2
+    const double r = transS * (2.0 * std::log(2.0));
+    const int t = (int)std::floor(M_PI * r * r * transSearchFactor + 0.5);
+    *nT = t > 30 ? t : 30;
+    return THX_OK;
+}
+
+extern "C" int thx_global_sample_set(int nR, int nT, double transS, unsigned long long seed,
+                                     double* quat, double* trans, double* pR, double* pT,
+                                     thx_stream_t stream)
+{
+    THX_CHECK_ARG(nR > 0 && nT > 1 && transS > 0.0 && quat && trans && pR && pT,
+                  "thx_global_sample_set: bad arguments");
+    hipLaunchKernelGGL(k_sample_set, dim3(thx::cdiv(nR, 256)), dim3(256), 0,
+                       thx::as_stream(stream), nR, nT, transS, (uint64_t)seed, quat, trans, pR,
+                       pT);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }

@@ -128,6 +128,28 @@ def ctf_search(dfo, freq, dD, k1, k2, attr):
     return out
 
 
+# ------------------------------------------------------------------- a3
+def global_sample_sizes(mS, trans_s=10.0, trans_search_factor=0.25, n_sym_elem=0, mode=1):
+    """(mS after the 3D clamp, nR, nT) of the global search (host function)."""
+    out = [ctypes.c_int() for _ in range(3)]
+    check(lib().thx_global_sample_sizes(mode, mS, n_sym_elem, float(trans_s),
+                                        float(trans_search_factor),
+                                        *[ctypes.byref(o) for o in out]), "thx_global_sample_sizes")
+    return tuple(o.value for o in out)
+
+
+def global_sample_set(nR, nT, trans_s, seed, device):
+    """Particle::reset's global set on device: (quat [nR,4], trans [nT,2], pR, pT)."""
+    quat = torch.empty(nR, 4, dtype=torch.float64, device=device)
+    trans = torch.empty(nT, 2, dtype=torch.float64, device=device)
+    pR = torch.empty(nR, dtype=torch.float64, device=device)
+    pT = torch.empty(nT, dtype=torch.float64, device=device)
+    check(lib().thx_global_sample_set(nR, nT, float(trans_s), seed, _ptr(quat), _ptr(trans),
+                                      _ptr(pR), _ptr(pT), _stream(quat.device)),
+          "thx_global_sample_set")
+    return quat, trans, pR, pT
+
+
 # ------------------------------------------------------------------- a4
 def trans_table(trans, px):
     nT = trans.shape[0]
