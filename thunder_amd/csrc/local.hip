@@ -481,9 +481,13 @@ __device__ unsigned long long g_local_stamps[12];
 // image tile takes its CTF from ctfD[l][d] (thx_ctf_search) per column, and
 // the bias sum_i s c_d^2 |P|^2 now depends on the column, so it runs on the
 // MFMA as well: A = (re^2, im^2) regrouped like (re, im), B = (b_j, b_j).
-template <bool CELLS, bool CS = false>
-// two workgroups per CU (LDS-bound): 4 waves per SIMD, 128 VGPRs
-__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(4)))
+// A CS workgroup covers NCT column tiles of 16 (up to 96 (t, d) columns), so
+// the projection -- the expensive part -- is gathered once for all of them;
+// each step then issues 4 NCT MFMAs against NCT accumulators.
+template <bool CELLS, bool CS = false, int NCT = 1>
+// non-CS: two workgroups per CU (LDS-bound), 4 waves per SIMD, 128 VGPRs;
+// CS: the NCT accumulators and CTF prefetches need the 256-VGPR budget
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(CS ? 2 : 4)))
 k_local_fused(const float2* __restrict__ vol,
                                                             int vdim, int pf,
                                                             const double* __restrict__ quat,
@@ -511,15 +515,17 @@ k_local_fused(const float2* __restrict__ vol,
     }
     // classification: image l projects its own class's volume
     if (cls) vol += (size_t)cls[l] * volStride;
-    const int r0 = blockIdx.y * RT, t0 = blockIdx.z * TT;
+    static_assert(CS || NCT == 1, "column tiles per workgroup: CTF search only");
+    constexpr int NC = NCT * TT;   // columns per workgroup
+    const int r0 = blockIdx.y * RT, t0 = blockIdx.z * NC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nRl = min(RT, nR - r0);
     __shared__ __attribute__((aligned(16))) float2 sBox[BOX_CAP];
-    __shared__ __attribute__((aligned(16))) float sB[KC * 2 * TT];   // [px][U, V][t]
+    __shared__ __attribute__((aligned(16))) float sB[KC * 2 * NC];   // [px][U, V][t]
     __shared__ __attribute__((aligned(16))) double2 sXY[KC];        // (iCol pf, iRow pf)
-    __shared__ float sBq[CS ? KC * TT : KC];                         // b = s c^2 ([px][col] for CS)
+    __shared__ float sBq[CS ? KC * NC : KC];                         // b = s c^2 ([px][col] for CS)
     __shared__ int sValid[KC];                                       // 0: padding entry
-    __shared__ float sTr[TT][2];
+    __shared__ float sTr[NC][2];
     __shared__ float sRed[NWAVE];
     __shared__ float sBias[RT];
     __shared__ unsigned sKey[RT];
@@ -539,7 +545,7 @@ k_local_fused(const float2* __restrict__ vol,
         for (int k = 0; k < 6; k++) m[k] = mm[k];
     }
     // columns: translations, or (t, d) pairs for CS (nT counts the columns)
-    if (tid < TT) {
+    if (tid < NC) {
         const int t = CS ? (t0 + tid) / nD : t0 + tid;
         float tx = 0.f, ty = 0.f;
         if (t0 + tid < nT) {
@@ -553,12 +559,24 @@ k_local_fused(const float2* __restrict__ vol,
 
     const float2* D = dat + (size_t)l * nPxl;
     const int bpx = tid / TT, bt = tid % TT;
-    // CS: a staging thread's column has one defocus sample, so its CTF row is fixed
+    // CS: a staging thread's columns bt + 16 ct have fixed defocus samples, so
+    // their CTF rows are fixed (row of column tile 0 here, the rest in cRow)
     const float* C = ctf + ((size_t)l * nD + (CS ? (t0 + bt) % nD : 0)) * nPxl;
+    int cRow[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ct++) cRow[ct] = CS ? (l * nD + (t0 + ct * TT + bt) % nD) : 0;
+    float cc[NCT];      // CS: the CTF of this thread's (next) pixel per column tile
+    auto load_cc = [&](int p) {
+        if (CS)
+#pragma unroll
+            for (int ct = 0; ct < NCT; ct++) cc[ct] = p >= 0 ? ctf[(size_t)cRow[ct] * nPxl + p] : 0.f;
+    };
     const float* S = sig + (size_t)l * nPxl;
     const int nC = (nVisit + KC - 1) / KC;
     const int* R = rec + ((size_t)l * gridDim.y + blockIdx.y) * nC * REC;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[NCT];
+#pragma unroll
+    for (int ct = 0; ct < NCT; ct++) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
     float bias = 0.f, aConst = 0.f;
     // image-tile element staged by threads tid < KC * TT
     const bool stager = tid < KC * TT;
@@ -567,6 +585,7 @@ k_local_fused(const float2* __restrict__ vol,
 
     // pipeline prologue: patch 0 data + box, patch 1 order entry + record
     Pix px = load_pix(stager ? patch_pixel(order, nVisit, bpx) : -1, iCol, iRow, D, C, S);
+    load_cc(px.p);
     int pNext = stager ? patch_pixel(order, nVisit, KC + bpx) : -1;
     Rec rc = load_rec(R);
     Rec rn = nC > 1 ? load_rec(R + REC) : rc;
@@ -595,18 +614,23 @@ k_local_fused(const float2* __restrict__ vol,
             }
         }
         if (stager) {
-            float U = 0.f, V = 0.f;
             const bool ok = px.p >= 0;
-            if (ok && t0 + bt < nT) {
-                const float k2 = -2.f * px.s * px.c;
-                const float yr = k2 * px.d.x, yi = k2 * px.d.y;
-                const float2 T = phase_shift(px.ic, px.ir, sTr[bt][0], sTr[bt][1]);
-                U = yr * T.x + yi * T.y;
-                V = yi * T.x - yr * T.y;
+#pragma unroll
+            for (int ct = 0; ct < NCT; ct++) {
+                const int col = ct * TT + bt;
+                const float cv = CS ? cc[ct] : px.c;
+                float U = 0.f, V = 0.f;
+                if (ok && t0 + col < nT) {
+                    const float k2 = -2.f * px.s * cv;
+                    const float yr = k2 * px.d.x, yi = k2 * px.d.y;
+                    const float2 T = phase_shift(px.ic, px.ir, sTr[col][0], sTr[col][1]);
+                    U = yr * T.x + yi * T.y;
+                    V = yi * T.x - yr * T.y;
+                }
+                sB[(bpx * 2) * NC + col] = U;
+                sB[(bpx * 2 + 1) * NC + col] = V;
+                if (CS) sBq[bpx * NC + col] = ok && t0 + col < nT ? px.s * cv * cv : 0.f;
             }
-            sB[(bpx * 2) * TT + bt] = U;
-            sB[(bpx * 2 + 1) * TT + bt] = V;
-            if (CS) sBq[bpx * TT + bt] = ok && t0 + bt < nT ? px.s * px.c * px.c : 0.f;
             if (bt == 0) {
                 if (ok) aConst += px.s * (px.d.x * px.d.x + px.d.y * px.d.y);
                 if (!CS) sBq[bpx] = ok ? px.s * px.c * px.c : 0.f;
@@ -624,6 +648,7 @@ k_local_fused(const float2* __restrict__ vol,
         if (c + 1 < nC) {
             if (stager) {
                 px = load_pix(pNext, iCol, iRow, D, C, S);
+                load_cc(pNext);
                 pNext = patch_pixel(order, nVisit, (c + 2) * KC + bpx);
             }
             fetch_box<CELLS>(pre, dst, rn, vol, vdim, tid);
@@ -638,17 +663,25 @@ k_local_fused(const float2* __restrict__ vol,
             const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(P.x),
                                                              __float_as_uint(P.y), false, false);
             const int q0 = 4 * s + (kk < 2 ? 0 : 2), q1 = q0 + 1;
-            const float b0 = sB[(q0 * 2 + (kk & 1)) * TT + tc];
-            const float b1 = sB[(q1 * 2 + (kk & 1)) * TT + tc];
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[0]), b0, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[1]), b1, acc, 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < NCT; ct++) {
+                const float b0 = sB[(q0 * 2 + (kk & 1)) * NC + ct * TT + tc];
+                const float b1 = sB[(q1 * 2 + (kk & 1)) * NC + ct * TT + tc];
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[0]), b0, acc[ct],
+                                                               0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sw[1]), b1, acc[ct],
+                                                               0, 0, 0);
+            }
             if (CS) {
                 const auto sq = __builtin_amdgcn_permlane16_swap(
                     __float_as_uint(P.x * P.x), __float_as_uint(P.y * P.y), false, false);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sq[0]),
-                                                           sBq[q0 * TT + tc], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(sq[1]),
-                                                           sBq[q1 * TT + tc], acc, 0, 0, 0);
+#pragma unroll
+                for (int ct = 0; ct < NCT; ct++) {
+                    acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        __uint_as_float(sq[0]), sBq[q0 * NC + ct * TT + tc], acc[ct], 0, 0, 0);
+                    acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        __uint_as_float(sq[1]), sBq[q1 * NC + ct * TT + tc], acc[ct], 0, 0, 0);
+                }
             }
         };
         // a step whose four pixels are all padding adds exactly zero (U = V = b
@@ -709,12 +742,15 @@ k_local_fused(const float2* __restrict__ vol,
     float Al = 0.f;
     for (int k = 0; k < NWAVE; k++) Al += sRed[k];
     // C layout of 16x16x4: col = lane & 15 (translation), row = 4 (lane >> 4) + j
-    const int t = t0 + tc;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int rr = wv * 16 + 4 * kk + j;
-        if (t < nT && rr < nRl)
-            dvp[((size_t)l * nR + r0 + sPerm[rr]) * nT + t] = Al + sBias[rr] + acc[j];
+    for (int ct = 0; ct < NCT; ct++) {
+        const int t = t0 + ct * TT + tc;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int rr = wv * 16 + 4 * kk + j;
+            if (t < nT && rr < nRl)
+                dvp[((size_t)l * nR + r0 + sPerm[rr]) * nT + t] = Al + sBias[rr] + acc[ct][j];
+        }
     }
 }
 
@@ -999,7 +1035,22 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     const long vs = cls ? (long)sel->volStride : 0L;
     if (evBeg) THX_HIP(hipEventRecord(evBeg, s));
     if (nD) {
-        auto kern = volLayout == 1 ? k_local_fused<true, true> : k_local_fused<false, true>;
+        // all (t, d) columns of a workgroup in NCT tiles (one gather of the
+        // projection), up to 96 per workgroup; THX_CS_NCT caps it (A/B builds)
+#ifndef THX_CS_NCT
+#define THX_CS_NCT 6
+#endif
+        const int need = (int)thx::cdiv(nCol, TT);
+        const int nct = THX_CS_NCT == 1 ? 1 : need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 6;
+        auto pick = [&](auto c1, auto c2, auto c4, auto c6) {
+            return nct == 1 ? c1 : nct == 2 ? c2 : nct == 4 ? c4 : c6;
+        };
+        auto kern = volLayout == 1
+                        ? pick(k_local_fused<true, true, 1>, k_local_fused<true, true, 2>,
+                               k_local_fused<true, true, 4>, k_local_fused<true, true, 6>)
+                        : pick(k_local_fused<false, true, 1>, k_local_fused<false, true, 2>,
+                               k_local_fused<false, true, 4>, k_local_fused<false, true, 6>);
+        grid.z = thx::cdiv(nCol, TT * nct);
         hipLaunchKernelGGL(kern, grid, dim3(THREADS), 0, s, reinterpret_cast<const float2*>(vol),
                            vdim, pf, quat, nR, trans, nCol, reinterpret_cast<const float2*>(dat),
                            ctf, sigRcp, iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, d, act, nAct,

@@ -61,6 +61,8 @@ def main():
                    help="local: 1 = tile visiting order (LDS-staged patches), 0 = set order")
     p.add_argument("--stats", type=int, default=0,
                    help="local: report patch-box sizes (voxels per LDS neighbourhood)")
+    p.add_argument("--nd", type=int, default=0,
+                   help="local: CTF search over nd defocus samples (thx_local_phase_d), 0 = off")
     p.add_argument("--spread", type=float, default=3.0,
                    help="local: rotation spread (deg) of each image's cloud, 0 = uniform")
     a = p.parse_args()
@@ -83,8 +85,19 @@ def main():
         pR = torch.full((a.images, mR), 1.0 / mR, dtype=torch.float64, device=dev)
         pT = torch.full((a.images, mT), 1.0 / mT, dtype=torch.float64, device=dev)
         cells = ops.volume_cells(vol) if a.cells else None
-        sec = timed_events(lambda: ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px,
-                                                   cells=cells, tiled=bool(a.tiled)), a.reps, st)
+        if a.nd > 0:
+            dD = torch.as_tensor(1 + rng.standard_normal((a.images, a.nd)) * 0.01, device=dev)
+            ctfD = (ctf[:, None, :] * (1 + 0.01 * torch.arange(a.nd, device=dev)[None, :, None]))
+            ctfD = ctfD.float().contiguous()
+            pD = torch.full((a.images, a.nd), 1.0 / a.nd, dtype=torch.float64, device=dev)
+            sec = timed_events(lambda: ops.local_phase_d(vol, quat, trans, pC, pR, pT, pD, dat, ctfD,
+                                                         sig, px, cells=cells), a.reps, st)
+            out["nd"] = a.nd
+            del dD
+        else:
+            sec = timed_events(lambda: ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig,
+                                                       px, cells=cells, tiled=bool(a.tiled)),
+                               a.reps, st)
         if a.stats:
             out.update(box_stats(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px))
         out.update(ms=sec * 1e3, us_per_image_phase=sec / a.images * 1e6,
