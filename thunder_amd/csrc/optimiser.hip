@@ -146,11 +146,14 @@ THX_DEV double quad10(const double* Mp, const double* q)
     return s;
 }
 
-// Particle statistics run one image per GROUP lanes (4 images per wave): the
-// 4x4 algebra is repeated by every lane anyway, so narrower groups mean 4x
-// fewer waves for the same latency-bound FP64 chains.
+// Particle statistics run one image per GROUP lanes (8 images per wave): the
+// 4x4 algebra is repeated by every lane anyway, so narrower groups mean
+// fewer waves for the same latency-bound FP64 chains, and each lane's 16
+// register-resident particles give the fixed point's quadratic forms ILP.
+// Measured on 12 500 x 125 (tools/pf_bench.py, profiles/r02_pf_group_ab.jsonl):
+// calVari 0.145 / 0.105 ms at GROUP 16 / 8 on 3-degree clouds, 32 and 64 slower.
 #ifndef THX_PF_GROUP
-#define THX_PF_GROUP 16
+#define THX_PF_GROUP 8
 #endif
 constexpr int GROUP = THX_PF_GROUP;
 
