@@ -171,3 +171,37 @@ def test_global_sample_sizes_match_survey():
     assert ops.global_sample_sizes(2000, trans_s=2.0)[2] == 30
     for ts in (3.0, 10.0, 17.5):
         assert ops.global_sample_sizes(2000, trans_s=ts)[2] == synth.n_trans_global(ts, 0.25)
+
+
+def test_ctf_search_entry_points_validate_without_gpu(L):
+    """CTF-search and sample-set entry points check their arguments before any
+    device work; empty batches are no-ops."""
+    ok, bad = 0, 1
+    dummy = ctypes.c_void_p(1)
+    # thx_local_phase_d: nD must be positive; an empty batch is a no-op
+    args = lambda nD, nImg: (None, dummy, 0, 64, 2, dummy, 10, dummy, 9, nD, dummy, dummy, dummy,
+                             dummy, dummy, dummy, dummy, dummy, dummy, None, 0, 200, 32, nImg,
+                             dummy, dummy, dummy, dummy, dummy, None, None, 0, None)
+    assert L.thx_local_phase_d(*args(0, 4)) == bad
+    assert L.thx_local_phase_d(*args(3, 0)) == ok
+    assert L.thx_local_phase_d(*args(200, 4)) == bad        # nT * nD > 1024 columns
+    # thx_ctf_search / thx_defocus_pre: sizes, then empty batches
+    assert L.thx_ctf_search(None, None, None, 0, None, None, None, 4, 10, None, None) == bad
+    assert L.thx_ctf_search(None, None, None, 9, None, None, None, 0, 10, None, None) == ok
+    assert L.thx_defocus_pre(None, 4, None, None, 10, 0, None, None, None, None, None) == bad
+    assert L.thx_defocus_pre(None, 0, None, None, 10, 32, None, None, None, None, None) == ok
+    # defocus particles: bad op, empty batch
+    assert L.thx_pf_defocus(4, 9, 3, 0.0, 1, 0, dummy, dummy, dummy, None) == bad
+    assert L.thx_pf_defocus(0, 9, 0, 0.01, 1, 0, None, None, None, None) == ok
+    # the CTF-search driver: no configuration, wrong search type
+    assert L.thx_expectation_ctf(None, None, None, None, None, None, None, None, 0, 10, 4,
+                                 *([None] * 7), None, 0, None) == bad
+    assert b"CTF-search configuration" in L.thx_last_error()
+    # the insert with per-sample defocus: attr without nD
+    a = (None, None, None, None, 64, 2, None, dummy, None, None, None, None, None, None, 4, 10,
+         None, None, dummy, 944, 870, 32, 15, dummy, 1 << 20, None)
+    assert L.thx_insert3d_binned_d(*a) == bad
+    assert L.thx_InsertFTCS(*([None] * 14), ctypes.c_float(1.32), 2, 10, 5, 32, 64, 1, None) == bad
+    # the global sample set producer
+    assert L.thx_global_sample_set(0, 151, 10.0, 1, dummy, dummy, dummy, dummy, None) == bad
+    assert L.thx_global_sample_set(10, 1, 10.0, 1, dummy, dummy, dummy, dummy, None) == bad
