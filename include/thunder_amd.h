@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define THX_ABI_VERSION 3
+#define THX_ABI_VERSION 4
 
 enum {
     THX_OK = 0,
@@ -527,6 +527,12 @@ typedef struct thx_expect_cfg {
     void* phaseEvents;        /* optional hipEvent_t[2 * phases]: events recorded on `stream`
                                  around every phase's k_local_fused launch (begin, end), for
                                  in-process kernel timing (bench.py); NULL: none */
+    /* ABI 4 */
+    const float* volCells;    /* optional cell-expanded copy of vol (thx_volume_cells, nK == 1):
+                                 the phases gather one 64-B cell per sample instead of four row
+                                 pieces -- the layout for large boxes at full resolution, where
+                                 the projectee is far beyond L2 / MALL and the patch boxes do not
+                                 fit LDS; NULL: the half-complex projectee */
 } thx_expect_cfg;
 
 /* nOrd: length of pxOrder (<= 0 when pxOrder is NULL). */

@@ -202,3 +202,26 @@ def test_global_converge_matches_fixed_quality(local_stack):
         res[conv] = (angle_deg(ex.cloud_mode(quat), qtrue), nph.cpu().numpy())
     assert float(res[True][0].median()) < 2.0 and float(res[False][0].median()) < 2.0
     assert res[True][1].min() >= 11 and res[True][1].max() <= 99
+
+
+def test_local_search_with_cell_projectee(local_stack):
+    """thx_expect_cfg.volCells: the phases gather 64-B cells; the same state,
+    seed and phases give the same refinement quality and, phase by phase, the
+    same likelihood baselines up to the gathers' rounding."""
+    s = local_stack
+    cells = ops.volume_cells(s["vol"])
+    res = {}
+    for name, c in (("halfcomplex", None), ("cells", cells)):
+        state = _start_state(s, 3.0)
+        e = ex.Expectation(s["vol"], s["px"], None, search="local", n_phase=1, seed=8, cells=c)
+        quat, trans, pR, pT, score, cls, nph = e.run(s["dat"], s["ctf"], s["sig"], state=state)
+        res[name] = (score.clone(), quat.clone())
+        state = _start_state(s, 3.0)
+        e3 = ex.Expectation(s["vol"], s["px"], None, search="local", n_phase=4, seed=8, cells=c)
+        q3 = e3.run(s["dat"], s["ctf"], s["sig"], state=state)[0]
+        res[name + "_err"] = angle_deg(ex.cloud_mode(q3), s["qtrue"])
+    # one phase from the same state and seed: the same samples, baselines to FP32 rounding
+    a, b = res["halfcomplex"][0], res["cells"][0]
+    assert torch.allclose(a, b, rtol=1e-5, atol=0)
+    for name in ("halfcomplex", "cells"):
+        assert float(res[name + "_err"].median()) < 1.5

@@ -1131,7 +1131,7 @@ extern "C" int thx_local_phase_d(const thx_local_sel* sel, const float* vol, int
 namespace thx {
 // the driver's phase launch, with optional events around k_local_fused
 int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
-                      const float* vol, int vdim, int pf, const double* quat, int nR,
+                      const float* vol, int volLayout, int vdim, int pf, const double* quat, int nR,
                       const double* trans, int nT, const double* pC, const double* pR,
                       const double* pT, const float* dat, const float* ctf, const float* sigRcp,
                       const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
@@ -1139,8 +1139,8 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       void* workspace, size_t wsBytes, thx_stream_t stream, int nD,
                       const double* pD, float* wD)
 {
-    return local_phase_impl(sel, evBeg, evEnd, vol, 0, vdim, pf, quat, nR, trans, nT, pC, pR, pT,
-                            dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg, wC, wR,
-                            wT, baseL, nullptr, workspace, wsBytes, stream, nD, pD, wD);
+    return local_phase_impl(sel, evBeg, evEnd, vol, volLayout, vdim, pf, quat, nR, trans, nT, pC,
+                            pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg,
+                            wC, wR, wT, baseL, nullptr, workspace, wsBytes, stream, nD, pD, wD);
 }
 }  // namespace thx

@@ -29,7 +29,7 @@
 
 namespace thx {
 int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
-                      const float* vol, int vdim, int pf, const double* quat, int nR,
+                      const float* vol, int volLayout, int vdim, int pf, const double* quat, int nR,
                       const double* trans, int nT, const double* pC, const double* pR,
                       const double* pT, const float* dat, const float* ctf, const float* sigRcp,
                       const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
@@ -1274,6 +1274,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                       nPxl > 0 && (!global || (c.nR > 0 && c.nT > 0)),
                   "thx_expectation: bad configuration");
     THX_CHECK_ARG(c.nK >= 1 && c.nK <= KMAX_CLASS, "thx_expectation: nK must be in [1, 64]");
+    THX_CHECK_ARG(!c.volCells || c.nK == 1, "thx_expectation: volCells needs nK == 1");
     THX_CHECK_ARG(global || c.nK == 1 || cls,
                   "thx_expectation: a K-class local search needs the particles' classes (cls)");
     THX_CHECK_ARG(c.converge ? (c.minPhase >= 0 && c.maxPhase > c.minPhase && c.maxPhase <= 1000)
@@ -1409,7 +1410,8 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipEvent_t* ev = static_cast<hipEvent_t*>(c.phaseEvents);
         const int pi = phase - phase0;
         THX_RET(thx::local_phase_timed(&sel, ev ? ev[2 * pi] : nullptr, ev ? ev[2 * pi + 1] : nullptr,
-                                       vol, c.vdim, c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT,
+                                       c.volCells ? c.volCells : vol, c.volCells ? 1 : 0, c.vdim,
+                                       c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT,
                                        dat, cs ? p.ctfD : ctf, sigRcp, iCol, iRow, pxOrder, nOrd,
                                        nPxl, c.idim, nImg, p.wC, p.wR, p.wT, p.base, p.localWs,
                                        p.localWsBytes, stream, mLD, cs ? cs->pD : nullptr, p.wD));

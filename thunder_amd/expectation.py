@@ -39,7 +39,9 @@ class ExpectCfg(ctypes.Structure):
                 ("minPhase", ctypes.c_int), ("maxPhase", ctypes.c_int),
                 ("perturbMean", ctypes.c_int), ("acgIters", ctypes.c_int),
                 ("perturbFactorL", ctypes.c_double), ("largeFirst", ctypes.c_int),
-                ("phaseEvents", ctypes.c_void_p)]
+                ("phaseEvents", ctypes.c_void_p),
+                # ABI 4
+                ("volCells", ctypes.c_void_p)]
 
 
 class CtfSearchCfg(ctypes.Structure):
@@ -66,13 +68,15 @@ class Expectation:
                   PARTICLE_ROT_MEAN_USING_STAT_PERTURB), "top" = top particle.
     large_first: OPTIMISER_GLOBAL_PERTURB_LARGE (off in the reference's
                  include/Config.h): the first global phase perturbs by perturbFactorL.
+    cells: optional ops.volume_cells(vol) (K = 1): the phases gather one 64-B
+           cell per sample (large boxes at full resolution, thx_expect_cfg.volCells).
     """
 
     def __init__(self, vol, px, gset=None, mLR=125, mLT=9, n_phase=10, perturb=0.5,
                  trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7, shuffle=True,
                  search="global", converge=False, perturb_mean="acg", acg_iters=100,
                  perturb_large=2.0, large_first=False, min_phase=None, max_phase=None,
-                 mLD=9, ctf_refine_s=0.01, perturb_ctf=0.5):
+                 mLD=9, ctf_refine_s=0.01, perturb_ctf=0.5, cells=None):
         dev = vol.device
         self.vol, self.px, self.dev = vol, px, dev
         nK = vol.shape[0] if vol.dim() == 4 else 1
@@ -104,7 +108,13 @@ class Expectation:
                              k_floor, s_floor, trans_s, trans_m, seed, int(bool(shuffle)),
                              nK, self.search, int(bool(converge)), min_phase, max_phase,
                              {"top": 0, "acg": 1}[perturb_mean], acg_iters, perturb_large,
-                             int(bool(large_first)), None)
+                             int(bool(large_first)), None, None)
+        self.cells = cells     # optional thx_volume_cells copy (kept alive here)
+        if cells is not None:
+            if nK != 1:
+                raise ValueError("cells: single-class projectee only")
+            ops._req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
+            self.cfg.volCells = cells.data_ptr()
         self.mLR, self.mLT, self.nK = mLR, mLT, nK
         self.cs = CtfSearchCfg(mLD, ctf_refine_s, perturb_ctf, None, None, None)
 

@@ -57,8 +57,9 @@ def global_cfg(name, N, mS, rU, rL, n_img, K, dev):
             "images": n_img, "phases": 10, "s_per_call": sec, "images_per_s": n_img / sec}
 
 
-def local_cfg(name, N, rU, rL, n_img, mR, mT, dev, mLD=0, spread=3.0):
+def local_cfg(name, N, rU, rL, n_img, mR, mT, dev, mLD=0, spread=3.0, cells=False):
     vol = synth.projectee(synth.blob_volume(N, seed=21, device=dev), 2)
+    vc = ops.volume_cells(vol) if cells else None
     px, dat, ctf, sig, qtrue, ttrue = make_stack(N, 2, rU, rL, n_img, dev, vol=vol)
     rng = np.random.default_rng(5)
     q0 = torch.as_tensor(synth.clustered_quaternions(n_img, mR, spread, rng), device=dev)
@@ -66,7 +67,7 @@ def local_cfg(name, N, rU, rL, n_img, mR, mT, dev, mLD=0, spread=3.0):
     pR0 = torch.full((n_img, mR), 1.0 / mR, dtype=torch.float64, device=dev)
     pT0 = torch.full((n_img, mT), 1.0 / mT, dtype=torch.float64, device=dev)
     e = ex.Expectation(vol, px, None, mLR=mR, mLT=mT, n_phase=3, seed=7,
-                       search="ctf" if mLD else "local", mLD=max(mLD, 1))
+                       search="ctf" if mLD else "local", mLD=max(mLD, 1), cells=vc)
     attrs = torch.as_tensor(synth.ctf_attrs(n_img, seed=6), device=dev)
 
     def run():
@@ -76,20 +77,25 @@ def local_cfg(name, N, rU, rL, n_img, mR, mT, dev, mLD=0, spread=3.0):
         else:
             e.run(dat, ctf, sig, state=st)
     sec = wall(run)
+    algo = n_img * 3 * (64.0 * mR * px.n + 16.0 * px.n)   # SURVEY 8(d) bytes, 3 phases
     return {"config": name, "box": N, "search": "ctf" if mLD else "local", "mLR": mR, "mLT": mT,
             "mLD": mLD, "nPxl": px.n, "images": n_img, "phases": 3, "cloud_spread_deg": spread,
-            "s_per_call": sec, "images_per_s": n_img / sec}
+            "projectee": "cells" if cells else "half-complex", "s_per_call": sec,
+            "images_per_s": n_img / sec, "algorithmic_GBps_incl_pf": algo / sec / 1e9}
 
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--only", default="C2,C4,C5,CS")
+    p.add_argument("--only", default="C2,C4,C5,C5cells,C5n,C5ncells,CS")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     jobs = {
         "C2": lambda: global_cfg("C2", 128, 500, 12, 0, 8192, 1, dev),
         "C4": lambda: global_cfg("C4", 200, 2000, 19, 1, 4096, 4, dev),
         "C5": lambda: local_cfg("C5", 512, 254, 3, 256, 200, 9, dev),
+        "C5cells": lambda: local_cfg("C5", 512, 254, 3, 256, 200, 9, dev, cells=True),
+        "C5n": lambda: local_cfg("C5", 512, 254, 3, 256, 200, 9, dev, spread=1.0),
+        "C5ncells": lambda: local_cfg("C5", 512, 254, 3, 256, 200, 9, dev, spread=1.0, cells=True),
         "CS": lambda: local_cfg("CS (C3 shape)", 256, 24, 1, 4096, 125, 9, dev, mLD=9),
     }
     for k in a.only.split(","):
