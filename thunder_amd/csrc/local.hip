@@ -37,6 +37,8 @@
 // two pixels), so the projection tile never goes through LDS.
 #include <climits>
 
+#include <cmath>
+
 #include "common.h"
 #include "patch.h"
 
@@ -47,8 +49,13 @@ constexpr int NWAVE = THREADS / 64;
 constexpr int RT = 16 * NWAVE;   // rotations per workgroup (one 16-row M-tile per wave)
 constexpr int TT = 16;           // translations per workgroup (one N-tile)
 constexpr int KC = thx::PATCH_KC;          // pixels per stage: one patch of the tile order
-constexpr int BOX_CAP = thx::PATCH_BOX_CAP; // LDS voxels (64 KiB) for a patch neighbourhood
+constexpr int BOX_CAP = 8192;               // LDS voxels (64 KiB) for a patch neighbourhood
 constexpr int NIT = BOX_CAP / 4 / THREADS;   // 32-B box items in flight per thread
+// the big-box variant (one workgroup per CU, 128 KiB of box): the
+// neighbourhoods of a 1-3 degree cloud at full resolution of a large box
+// (box 512: radius ~508 voxels) exceed 64 KiB
+constexpr int BOX_CAP_BIG = thx::PATCH_BOX_CAP;
+static_assert(BOX_CAP_BIG == 2 * BOX_CAP, "records carry offsets for the big boxes");
 constexpr int REC = thx::PATCH_REC;         // ints per patch record
 static_assert(RT == thx::PATCH_RT, "one record tile per workgroup");
 static_assert(KC * TT <= THREADS, "one (pixel, translation) of the image tile per thread");
@@ -167,7 +174,7 @@ THX_DEV void store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __re
     o[12] = (int)min((any[0] ? ni : 0) + (any[1] ? ni : 0), (long)BIG);
     o[13] = (int)magic((unsigned)nx / 4);
     o[14] = (int)magic((unsigned)ny);
-    if (nv0 + nv1 <= BOX_CAP) {
+    if (nv0 + nv1 <= BOX_CAP_BIG) {
         o[15] = -(lo[0][2] * o[7] + lo[0][1] * nx + lo[0][0]);
         o[16] = o[9] - (lo[1][2] * o[7] + lo[1][1] * nx + lo[1][0]);
     }
@@ -324,15 +331,15 @@ THX_DEV Pix load_pix(int p, const int* __restrict__ iCol, const int* __restrict_
 
 // The items (4 consecutive voxels of a box row, 32 B) of a staged patch this
 // thread moves: item it = tid + j THREADS, LDS voxel dst[j].
-template <bool CELLS>
-THX_DEV void fetch_box(f32x4 (&pre)[NIT][2], int (&dst)[NIT], const Rec& b,
+template <bool CELLS, int NI = NIT, int CAP = BOX_CAP>
+THX_DEV void fetch_box(f32x4 (&pre)[NI][2], int (&dst)[NI], const Rec& b,
                        const float2* __restrict__ vol, int vdim, int tid)
 {
-    if (!b.staged()) return;
+    if (!(b.v[10] <= CAP)) return;
     const int nColFT = vdim / 2 + 1;
     const int nq = b.v[6] >> 2, ny = b.v[8];
 #pragma unroll
-    for (int j = 0; j < NIT; j++) {
+    for (int j = 0; j < NI; j++) {
         const int it = tid + j * THREADS;
         if (it < b.v[12]) {
             const bool s1 = it >= b.v[11];
@@ -484,10 +491,12 @@ __device__ unsigned long long g_local_stamps[12];
 // A CS workgroup covers NCT column tiles of 16 (up to 96 (t, d) columns), so
 // the projection -- the expensive part -- is gathered once for all of them;
 // each step then issues 4 NCT MFMAs against NCT accumulators.
-template <bool CELLS, bool CS = false, int NCT = 1>
+template <bool CELLS, bool CS = false, int NCT = 1, bool BIGBOX = false>
 // non-CS: two workgroups per CU (LDS-bound), 4 waves per SIMD, 128 VGPRs;
-// CS: the NCT accumulators and CTF prefetches need the 256-VGPR budget
-__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(CS ? 2 : 4)))
+// CS: the NCT accumulators and CTF prefetches need the 256-VGPR budget;
+// BIGBOX: 128 KiB of box, one workgroup per CU, twice the prefetch registers
+__global__ void __launch_bounds__(THREADS)
+__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : 4)))
 k_local_fused(const float2* __restrict__ vol,
                                                             int vdim, int pf,
                                                             const double* __restrict__ quat,
@@ -516,11 +525,14 @@ k_local_fused(const float2* __restrict__ vol,
     // classification: image l projects its own class's volume
     if (cls) vol += (size_t)cls[l] * volStride;
     static_assert(CS || NCT == 1, "column tiles per workgroup: CTF search only");
+    constexpr int BOXC = BIGBOX ? BOX_CAP_BIG : BOX_CAP;
+    constexpr int NITC = BOXC / 4 / THREADS;
+    auto staged = [](const Rec& r) { return r.v[10] <= BOXC; };
     constexpr int NC = NCT * TT;   // columns per workgroup
     const int r0 = blockIdx.y * RT, t0 = blockIdx.z * NC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nRl = min(RT, nR - r0);
-    __shared__ __attribute__((aligned(16))) float2 sBox[BOX_CAP];
+    __shared__ __attribute__((aligned(16))) float2 sBox[BOXC];
     __shared__ __attribute__((aligned(16))) float sB[KC * 2 * NC];   // [px][U, V][t]
     __shared__ __attribute__((aligned(16))) double2 sXY[KC];        // (iCol pf, iRow pf)
     __shared__ float sBq[CS ? KC * NC : KC];                         // b = s c^2 ([px][col] for CS)
@@ -589,23 +601,23 @@ k_local_fused(const float2* __restrict__ vol,
     int pNext = stager ? patch_pixel(order, nVisit, KC + bpx) : -1;
     Rec rc = load_rec(R);
     Rec rn = nC > 1 ? load_rec(R + REC) : rc;
-    f32x4 pre[NIT][2];
-    int dst[NIT];
-    fetch_box<CELLS>(pre, dst, rc, vol, vdim, tid);
+    f32x4 pre[NITC][2];
+    int dst[NITC];
+    fetch_box<CELLS, NITC, BOXC>(pre, dst, rc, vol, vdim, tid);
 
     __syncthreads();
 #ifdef THX_LOCAL_STAMPS
     unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tp = __builtin_amdgcn_s_memtime(), tq;
-#define STAMP(k) do { tq = __builtin_amdgcn_s_memtime(); if (rc.staged()) st[k] += tq - tp; tp = tq; } while (0)
+#define STAMP(k) do { tq = __builtin_amdgcn_s_memtime(); if (staged(rc)) st[k] += tq - tp; tp = tq; } while (0)
 #else
 #define STAMP(k) do {} while (0)
 #endif
     for (int c = 0; c < nC; c++) {
         // ---- stage patch c: box voxels, image tile B[px][U, V][t], b, (iCol, iRow) pf
-        if (rc.staged()) {
+        if (staged(rc)) {
             f32x4* box4 = reinterpret_cast<f32x4*>(sBox);
 #pragma unroll
-            for (int j = 0; j < NIT; j++) {
+            for (int j = 0; j < NITC; j++) {
                 const int it = tid + j * THREADS;
                 if (it < rc.v[12]) {
                     box4[dst[j] / 2] = pre[j][0];
@@ -651,7 +663,7 @@ k_local_fused(const float2* __restrict__ vol,
                 load_cc(pNext);
                 pNext = patch_pixel(order, nVisit, (c + 2) * KC + bpx);
             }
-            fetch_box<CELLS>(pre, dst, rn, vol, vdim, tid);
+            fetch_box<CELLS, NITC, BOXC>(pre, dst, rn, vol, vdim, tid);
             if (c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
         }
         STAMP(2);
@@ -690,7 +702,7 @@ k_local_fused(const float2* __restrict__ vol,
             return THX_SKIP_PAD &&
                    !(sValid[4 * s] | sValid[4 * s + 1] | sValid[4 * s + 2] | sValid[4 * s + 3]);
         };
-        if (rc.staged()) {
+        if (staged(rc)) {
             const int nx = rc.v[6], sp = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
 #pragma unroll
             for (int s = 0; s < 4; s++) {
@@ -716,7 +728,7 @@ k_local_fused(const float2* __restrict__ vol,
         }
         STAMP(3);
 #ifdef THX_LOCAL_STAMPS
-        const bool stg = rc.staged();
+        const bool stg = staged(rc);
 #endif
         rc = rn;
         rn = r2;
@@ -1062,16 +1074,17 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         THX_LAUNCH_CHECK();
         return THX_OK;
     }
-    if (volLayout == 1)
-        hipLaunchKernelGGL(k_local_fused<true>, grid, dim3(THREADS), 0, s,
-                           reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
-                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
-                           nVisit, nPxl, idim, rec, d, act, nAct, cls, vs);
-    else
-        hipLaunchKernelGGL(k_local_fused<false>, grid, dim3(THREADS), 0, s,
-                           reinterpret_cast<const float2*>(vol), vdim, pf, quat, nR, trans, nT,
-                           reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
-                           nVisit, nPxl, idim, rec, d, act, nAct, cls, vs);
+    // big LDS boxes for large full-resolution pixel sets: the ring's outer
+    // radius in projectee voxels, pf sqrt(2 nPxl / pi), past THX_BIGBOX_MIN_R
+#ifndef THX_BIGBOX_MIN_R
+#define THX_BIGBOX_MIN_R 300
+#endif
+    const bool big = pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R;
+    auto kern = volLayout == 1 ? (big ? k_local_fused<true, false, 1, true> : k_local_fused<true>)
+                               : (big ? k_local_fused<false, false, 1, true> : k_local_fused<false>);
+    hipLaunchKernelGGL(kern, grid, dim3(THREADS), 0, s, reinterpret_cast<const float2*>(vol), vdim,
+                       pf, quat, nR, trans, nT, reinterpret_cast<const float2*>(dat), ctf, sigRcp,
+                       iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, d, act, nAct, cls, vs, 1);
     THX_LAUNCH_CHECK();
     if (evEnd) THX_HIP(hipEventRecord(evEnd, s));
     hipLaunchKernelGGL(k_local_weights, dim3(nImg), dim3(256), 0, s, d, nR, nT, pC, pR, pT, wC,

@@ -21,7 +21,7 @@ namespace thx {
 constexpr int PATCH_KC = 16;        // pixels per patch
 constexpr int PATCH_RT = 128;       // rotations per record tile
 constexpr int PATCH_REC = 20;       // ints per record
-constexpr int PATCH_BOX_CAP = 8192; // largest box the records carry LDS offsets for
+constexpr int PATCH_BOX_CAP = 16384; // largest box the records carry LDS offsets for
 
 size_t patch_rec_bytes(int nImg, int nR, int nVisit);
 // records for quat [nImg][nR][4] (device), one per (image, rotation tile, patch)
