@@ -615,7 +615,10 @@ int thx_ExpectGlobal3D(const float* rotP, const float* traP, const float* datP,
  * *Fin / *FreeIdx call.  The ManagedArrayTexture / ManagedCalPoint objects
  * become opaque handles: thx_tex_create / thx_calpoint_create mirror their
  * Init(mode, vdim, gpu) / Init(mode, searchType, gpu, mLR, mLT, mLD, nPxl).
- * MODE_3D only.  CTF search (searchType 2 / cSearch): ExpectLocalIn also
+ * MODE_3D, and MODE_2D through thx_ExpectLocalV2D / thx_ExpectLocalPreI2D (the
+ * class image of thx_tex_create(0, vdim, ...); the 2D calpoint takes (cos,
+ * sin) = the first two entries of each particle's 4-double rotation row, as
+ * Optimiser packs them; no 2D CTF search).  CTF search (searchType 2 / cSearch): ExpectLocalIn also
  * allocates devdefO, ExpectLocalP copies defO (the image's per-pixel defocus,
  * thx_defocus_pre), ExpectLocalRTD takes dpara (mLD defocus factors) and oldD
  * (their priors), ExpectLocalPreI3D builds the CTF per defocus sample from
@@ -630,6 +633,7 @@ int thx_ExpectLocalIn(int gpuIdx, float** devdatP, float** devctfP, float** devd
 int thx_tex_create(int mode, int vdim, int gpuIdx, void** mgr);
 int thx_tex_destroy(void* mgr);
 int thx_ExpectLocalV3D(int gpuIdx, void* mgr, const float* volume, int vdim);   /* :44 */
+int thx_ExpectLocalV2D(int gpuIdx, void* mgr, const float* volume, int dimSize); /* :40 */
 int thx_ExpectLocalP(int gpuIdx, float* devdatP, float* devctfP, float* devdefO,
                      float* devsigP, const float* datP, const float* ctfP,
                      const float* defO, const float* sigP, int threadId, int imgId,
@@ -648,6 +652,10 @@ int thx_ExpectLocalPreI3D(int gpuIdx, int datShift, void* mgr, void* mcp,
                           const float* devdefO, const float* devfreQ, const int* deviCol,
                           const int* deviRow, float phaseShift, float conT, float k1,
                           float k2, int pf, int idim, int vdim, int npxl, int interp); /* :106 */
+int thx_ExpectLocalPreI2D(int gpuIdx, int datShift, void* mgr, void* mcp,
+                          const float* devdefO, const float* devfreQ, const int* deviCol,
+                          const int* deviRow, float phaseShift, float conT, float k1,
+                          float k2, int pf, int idim, int vdim, int npxl, int interp); /* :89 */
 int thx_ExpectLocalM(int gpuIdx, int datShift, void* mcp, const float* devdatP,
                      const float* devctfP, const float* devsigP, float* wC, float* wR,
                      float* wT, float* wD, double oldC, int npxl);                /* :124 */

@@ -190,3 +190,69 @@ def test_insert2d_matches_restatement(orc, nK):
     assert rc == 0, lib().thx_last_error()
     assert np.max(np.abs(hF.view(np.complex64) - F)) <= 1e-5 * np.abs(F).max()
     assert np.array_equal(hc, cnt.astype(np.int32))
+
+
+def test_local_2d_through_interface_forwards(orc):
+    """MODE_2D through the per-image local surface (ExpectLocalV2D ->
+    ExpectLocalRTD with 4-double rotation rows -> ExpectLocalPreI2D ->
+    ExpectLocalM), against the restatement's 2D phase per image."""
+    s = _stack(orc, nImg=3, nK=2, seed=9)
+    N, pf, vdim, px = s["N"], s["pf"], s["vdim"], s["px"]
+    L = lib()
+    npxl, mR, mT, gpu, cpy = px.n, 20, 6, 0, 2
+    iCol, iRow = px.iCol.copy(), px.iRow.copy()
+    dCol, dRow = vp(), vp()
+    assert L.thx_ExpectPreidx(gpu, ctypes.byref(dCol), ctypes.byref(dRow), P(iCol), P(iRow), npxl) == 0
+    mgr = vp()
+    assert L.thx_tex_create(0, vdim, gpu, ctypes.byref(mgr)) == 0
+    dat = np.ascontiguousarray(s["dat"]).view(np.float32)
+    ctf, sig = np.ascontiguousarray(s["ctf"]), np.ascontiguousarray(s["sig"])
+    dD, dC, dO, dS = vp(), vp(), vp(), vp()
+    assert L.thx_ExpectLocalIn(gpu, ctypes.byref(dD), ctypes.byref(dC), ctypes.byref(dO),
+                               ctypes.byref(dS), npxl, cpy, 1) == 0
+    mcp = vp()
+    assert L.thx_calpoint_create(0, 1, gpu, mR, mT, 1, npxl, ctypes.byref(mcp)) == 0
+    rng = np.random.default_rng(3)
+    wC, wR, wT, wD = (np.zeros(n, np.float32) for n in (1, mR, mT, 1))
+    for img in range(3):
+        k = int(s["k"][img])
+        cl = np.ascontiguousarray(s["cl"][k]).view(np.float32)
+        assert L.thx_ExpectLocalV2D(gpu, mgr, P(cl), (vdim // 2 + 1) * vdim) == 0, L.thx_last_error()
+        slot = img % cpy
+        assert L.thx_ExpectLocalP(gpu, dD, dC, dO, dS, P(dat), P(ctf), None, P(sig), slot, img,
+                                  npxl, 0) == 0
+        th = s["th"][img] + rng.standard_normal(mR) * 0.05
+        rot4 = np.zeros((mR, 4))
+        rot4[:, 0], rot4[:, 1] = np.cos(th), np.sin(th)
+        trans = s["t"][img][None, :] + rng.standard_normal((mT, 2)) * 0.5
+        pR = rng.uniform(0.5, 1.5, mR)
+        pR /= pR.sum()
+        pT = np.full(mT, 1.0 / mT)
+        oldD, dpara = np.ones(1), np.ones(1)
+        rot4c, transc = np.ascontiguousarray(rot4), np.ascontiguousarray(trans)
+        assert L.thx_ExpectLocalRTD(gpu, mcp, P(pR), P(pT), P(oldD), P(transc), P(rot4c),
+                                    P(dpara)) == 0
+        assert L.thx_ExpectLocalPreI2D(gpu, slot, mgr, mcp, None, None, dCol, dRow, 0.0, 0.1, 0.0,
+                                       0.0, pf, N, vdim, npxl, 1) == 0, L.thx_last_error()
+        oldC = 0.8
+        assert L.thx_ExpectLocalM(gpu, slot, mcp, dD, dC, dS, P(wC), P(wR), P(wT), P(wD), oldC,
+                                  npxl) == 0, L.thx_last_error()
+        ref = np.empty((mR, mT), np.float32)
+        for r in range(mR):
+            pri = orc.project2d(s["cl"][k], vdim, pf, _rot(th[r]), px)
+            for t in range(mT):
+                pt = (orc.translate(px, *trans[t], N) * pri).astype(np.complex64)
+                ref[r, t] = orc.logdatavs(s["dat"][img], pt, s["ctf"][img], s["sig"][img])
+        e = np.exp((ref - ref.max()).astype(np.float64))
+        rR = (e * pT[None, :]).sum(1) * oldC
+        rT = (e * pR[:, None]).sum(0) * oldC
+        rC = (e * pR[:, None] * pT[None, :]).sum()
+        for got, want in ((wR, rR), (wT, rT)):
+            m = want >= 1e-4 * want.max()
+            assert np.max(np.abs(got - want)[m] / want[m]) < 2e-3
+        assert abs(wC[0] - rC) <= 2e-3 * rC
+    assert L.thx_calpoint_destroy(mcp) == 0
+    assert L.thx_ExpectLocalFin(gpu, ctypes.byref(dD), ctypes.byref(dC), ctypes.byref(dO), None,
+                                ctypes.byref(dS), 0) == 0
+    assert L.thx_tex_destroy(mgr) == 0
+    assert L.thx_ExpectFreeIdx(gpu, ctypes.byref(dCol), ctypes.byref(dRow)) == 0

@@ -101,6 +101,9 @@ SIGNATURES = {
     "thx_tex_create": (_c_int, [_c_int, _c_int, _c_int, _p]),
     "thx_tex_destroy": (_c_int, [_p]),
     "thx_ExpectLocalV3D": (_c_int, [_c_int, _p, _p, _c_int]),
+    "thx_ExpectLocalV2D": (_c_int, [_c_int, _p, _p, _c_int]),
+    "thx_ExpectLocalPreI2D": (_c_int, [_c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_float, _c_float,
+                                       _c_float, _c_float, _c_int, _c_int, _c_int, _c_int, _c_int]),
     "thx_ExpectLocalP": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int,
                                   _c_int]),
     "thx_ExpectLocalHostA": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,

@@ -32,12 +32,13 @@
 namespace {
 
 struct Tex {
-    int vdim = 0, gpu = 0;
+    int vdim = 0, gpu = 0, mode = 1;   // mode 1: 3D projectee, 0: one 2D class image
     float* vol = nullptr;   // dimSize Complex
 };
 
 struct CalPoint {
-    int gpu = 0, mR = 0, mT = 0, npxl = 0, mD = 1;
+    int gpu = 0, mR = 0, mT = 0, npxl = 0, mD = 1, mode = 1;
+    double* rot2 = nullptr;                               // 2D: (cos, sin) per rotation
     bool cs = false;                                      // SEARCH_TYPE_CTF
     double *dP = nullptr, *pD = nullptr;                  // defocus factors, priors
     float *ctfD = nullptr, *wD = nullptr;                 // CTF per sample, marginal
@@ -69,6 +70,14 @@ int dalloc(T** p, size_t n)
         int st_ = (call);              \
         if (st_ != THX_OK) return st_; \
     } while (0)
+
+__global__ void k_rot2_from_quat(const double* __restrict__ quat, int n, double* __restrict__ rot2)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    rot2[2 * k] = quat[4 * k];
+    rot2[2 * k + 1] = quat[4 * k + 1];
+}
 
 // kernel_CalCTFL for one calpoint: ctfD[d][i] from the image's per-pixel
 // defocus, the frequencies and the calpoint's defocus factors
@@ -217,12 +226,13 @@ extern "C" int thx_ExpectLocalHostF(int gpuIdx, float** wC, float** wR, float** 
 extern "C" int thx_tex_create(int mode, int vdim, int gpuIdx, void** mgr)
 {
     THX_CHECK_ARG(mgr && vdim > 0 && vdim % 2 == 0, "thx_tex_create: bad arguments");
-    THX_CHECK_ARG(mode == 1, "thx_tex_create: only MODE_3D (1) is supported");
+    THX_CHECK_ARG(mode == 0 || mode == 1, "thx_tex_create: mode must be MODE_2D (0) or MODE_3D (1)");
     THX_DEV_SET(gpuIdx);
     Tex* t = new Tex;
     t->vdim = vdim;
     t->gpu = gpuIdx;
-    const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
+    t->mode = mode;
+    const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * (mode == 1 ? vdim : 1);
     if (hipMalloc(&t->vol, sizeof(float) * 2 * dimSize) != hipSuccess) {
         delete t;
         thx::set_error("thx_tex_create: device allocation failed");
@@ -245,11 +255,23 @@ extern "C" int thx_tex_destroy(void* mgr)
 extern "C" int thx_ExpectLocalV3D(int gpuIdx, void* mgr, const float* volume, int vdim)
 {
     Tex* t = static_cast<Tex*>(mgr);
-    THX_CHECK_ARG(t && volume && vdim == t->vdim && gpuIdx == t->gpu,
-                  "thx_ExpectLocalV3D: volume handle / size / device mismatch");
+    THX_CHECK_ARG(t && volume && vdim == t->vdim && gpuIdx == t->gpu && t->mode == 1,
+                  "thx_ExpectLocalV3D: volume handle / size / device / mode mismatch");
     THX_DEV_SET(gpuIdx);
     const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
     THX_HIP(hipMemcpy(t->vol, volume, sizeof(float) * 2 * dimSize, hipMemcpyHostToDevice));
+    return THX_OK;
+}
+
+// ExpectLocalV2D (Interface.h:40-43): one class image, dimSize = (vdim/2+1) vdim
+extern "C" int thx_ExpectLocalV2D(int gpuIdx, void* mgr, const float* volume, int dimSize)
+{
+    Tex* t = static_cast<Tex*>(mgr);
+    THX_CHECK_ARG(t && volume && t->mode == 0 && gpuIdx == t->gpu &&
+                      (long)dimSize == (long)(t->vdim / 2 + 1) * t->vdim,
+                  "thx_ExpectLocalV2D: image handle / size / device / mode mismatch");
+    THX_DEV_SET(gpuIdx);
+    THX_HIP(hipMemcpy(t->vol, volume, sizeof(float) * 2 * (size_t)dimSize, hipMemcpyHostToDevice));
     return THX_OK;
 }
 
@@ -258,7 +280,9 @@ extern "C" int thx_calpoint_create(int mode, int searchType, int gpuIdx, int mR,
                                    int npxl, void** mcp)
 {
     THX_CHECK_ARG(mcp && mR > 0 && mT > 0 && npxl > 0, "thx_calpoint_create: bad arguments");
-    THX_CHECK_ARG(mode == 1, "thx_calpoint_create: only MODE_3D (1) is supported");
+    THX_CHECK_ARG(mode == 0 || mode == 1, "thx_calpoint_create: mode must be 0 (2D) or 1 (3D)");
+    THX_CHECK_ARG(mode == 1 || searchType != 2,
+                  "thx_calpoint_create: 2D CTF search is not supported");
     THX_CHECK_ARG(searchType != 2 || (mD >= 1 && (long)mT * mD <= 1024),
                   "thx_calpoint_create: CTF search needs 1 <= mD, mT * mD <= 1024");
     THX_DEV_SET(gpuIdx);
@@ -269,6 +293,7 @@ extern "C" int thx_calpoint_create(int mode, int searchType, int gpuIdx, int mR,
     c->npxl = npxl;
     c->cs = searchType == 2;
     c->mD = c->cs ? mD : 1;
+    c->mode = mode;
     int st = THX_OK;
     auto chk = [&](hipError_t e) {
         if (e != hipSuccess && st == THX_OK) {
@@ -289,8 +314,10 @@ extern "C" int thx_calpoint_create(int mode, int searchType, int gpuIdx, int mR,
     // the tile order of a pixel set has at most ~1.25 npxl + 16 entries
     const int ordCap = (npxl * 2 + 31) / 16 * 16;
     chk(hipMalloc(&c->order, sizeof(int) * ordCap));
-    c->wsBytes = thx_local_phase_workspace(1, mR, mT * c->mD, ordCap > npxl ? ordCap : npxl);
+    c->wsBytes = mode == 1 ? thx_local_phase_workspace(1, mR, mT * c->mD, ordCap > npxl ? ordCap : npxl)
+                           : thx_local_phase2d_workspace(1, mR, mT);
     chk(hipMalloc(&c->ws, c->wsBytes));
+    if (mode == 0) chk(hipMalloc(&c->rot2, sizeof(double) * 2 * mR));
     if (c->cs) {
         chk(hipMalloc(&c->dP, sizeof(double) * c->mD));
         chk(hipMalloc(&c->pD, sizeof(double) * c->mD));
@@ -307,7 +334,7 @@ extern "C" int thx_calpoint_destroy(void* mcp)
     if (!c) return THX_OK;
     THX_DEV_SET(c->gpu);
     void* all[] = {c->quat, c->trans, c->pR, c->pT, c->pC, c->wC, c->wR, c->wT, c->base, c->order,
-                   c->ws, c->dP, c->pD, c->ctfD, c->wD};
+                   c->ws, c->dP, c->pD, c->ctfD, c->wD, c->rot2};
     for (void* p : all)
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -333,6 +360,17 @@ extern "C" int thx_ExpectLocalRTD(int gpuIdx, void* mcp, const double* oldR, con
     THX_HIP(hipMemcpyAsync(c->pT, oldT, sizeof(double) * c->mT, hipMemcpyHostToDevice, c->stream));
     THX_HIP(hipMemcpyAsync(c->trans, trans, sizeof(double) * 2 * c->mT, hipMemcpyHostToDevice, c->stream));
     THX_HIP(hipMemcpyAsync(c->quat, rot, sizeof(double) * 4 * c->mR, hipMemcpyHostToDevice, c->stream));
+    if (c->mode == 0) {
+        // 2D: rotation k is (r(k, 0), r(k, 1)) = (cos, sin) of the particle's
+        // quaternion row (Particle::rot(dmat22&), src/Particle.cpp:850-854), as
+        // Optimiser packs it (4 doubles per rotation, src/Optimiser.cpp:
+        // 2468-2476); cuthunder's 2D RTD copies 2 nR doubles and reads them with
+        // stride 2 (gpu/src/cuthunder.cu:2700-2717, Kernel.cu:762) -- quirk q9,
+        // not replicated
+        hipLaunchKernelGGL(k_rot2_from_quat, dim3(thx::cdiv(c->mR, 256)), dim3(256), 0, c->stream,
+                           c->quat, c->mR, c->rot2);
+        THX_LAUNCH_CHECK();
+    }
     return THX_OK;
 }
 
@@ -345,7 +383,7 @@ extern "C" int thx_ExpectLocalPreI3D(int gpuIdx, int datShift, void* mgr, void* 
     CalPoint* c = static_cast<CalPoint*>(mcp);
     const Tex* t = static_cast<const Tex*>(mgr);
     THX_CHECK_ARG(c && t && deviCol && deviRow && gpuIdx == c->gpu && npxl == c->npxl &&
-                      vdim == t->vdim && vdim == pf * idim,
+                      c->mode == 1 && t->mode == 1 && vdim == t->vdim && vdim == pf * idim,
                   "thx_ExpectLocalPreI3D: bad arguments");
     THX_CHECK_ARG(interp == 1, "thx_ExpectLocalPreI3D: only LINEAR_INTERP (1) is supported");
     THX_CHECK_ARG(!c->cs || (devdefO && devfreQ && datShift >= 0),
@@ -382,6 +420,31 @@ extern "C" int thx_ExpectLocalPreI3D(int gpuIdx, int datShift, void* mgr, void* 
     return THX_OK;
 }
 
+// ExpectLocalPreI2D (Interface.h:89-105; cuthunder.cu:2762-2825): binds the
+// class image, pixel set and geometry (the 2D phase projects on the fly from
+// the image in LDS); no CTF search in 2D.
+extern "C" int thx_ExpectLocalPreI2D(int gpuIdx, int datShift, void* mgr, void* mcp,
+                                     const float* devdefO, const float* devfreQ,
+                                     const int* deviCol, const int* deviRow, float phaseShift,
+                                     float conT, float k1, float k2, int pf, int idim, int vdim,
+                                     int npxl, int interp)
+{
+    (void)datShift; (void)devdefO; (void)devfreQ; (void)phaseShift; (void)conT; (void)k1; (void)k2;
+    CalPoint* c = static_cast<CalPoint*>(mcp);
+    const Tex* t = static_cast<const Tex*>(mgr);
+    THX_CHECK_ARG(c && t && deviCol && deviRow && gpuIdx == c->gpu && npxl == c->npxl &&
+                      c->mode == 0 && t->mode == 0 && vdim == t->vdim && vdim == pf * idim,
+                  "thx_ExpectLocalPreI2D: bad arguments");
+    THX_CHECK_ARG(interp == 1, "thx_ExpectLocalPreI2D: only LINEAR_INTERP (1) is supported");
+    c->tex = t;
+    c->iCol = deviCol;
+    c->iRow = deviRow;
+    c->pf = pf;
+    c->idim = idim;
+    c->vdim = vdim;
+    return THX_OK;
+}
+
 extern "C" int thx_ExpectLocalM(int gpuIdx, int datShift, void* mcp, const float* devdatP,
                                 const float* devctfP, const float* devsigP, float* wC, float* wR,
                                 float* wT, float* wD, double oldC, int npxl)
@@ -393,6 +456,20 @@ extern "C" int thx_ExpectLocalM(int gpuIdx, int datShift, void* mcp, const float
     THX_DEV_SET(gpuIdx);
     const size_t off = (size_t)datShift * npxl;
     THX_HIP(hipMemcpyAsync(c->pC, &oldC, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (c->mode == 0) {
+        // the 2D phase (kernel_logDataVSL + kernel_UpdateWL on the 2D
+        // projections, cuthunder.cu:2915-3140)
+        THX_RET(thx_local_phase2d(c->tex->vol, c->vdim, c->pf, nullptr, c->rot2, c->mR, c->trans,
+                                  c->mT, c->pC, c->pR, c->pT, devdatP + 2 * off, devctfP + off,
+                                  devsigP + off, c->iCol, c->iRow, npxl, c->idim, 1, c->wC, c->wR,
+                                  c->wT, c->base, nullptr, c->ws, c->wsBytes, c->stream));
+        THX_HIP(hipMemcpyAsync(wC, c->wC, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipMemcpyAsync(wR, c->wR, sizeof(float) * c->mR, hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipMemcpyAsync(wT, c->wT, sizeof(float) * c->mT, hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipStreamSynchronize(c->stream));
+        if (wD) wD[0] = (float)(oldC * (double)wC[0]);
+        return THX_OK;
+    }
     if (c->cs) {
         // kernel_logDataVSLC + kernel_UpdateWLC (cuthunder.cu:2915-3140)
         THX_RET(thx_local_phase_d(nullptr, c->tex->vol, 0, c->vdim, c->pf, c->quat, c->mR,
