@@ -264,6 +264,11 @@ PEAK_FP32_TFLOPS = PEAK_FP32_MFMA_TFLOPS
 
 def main():
     a = parse()
+    # gloo and RCCL print banners on the process's C stdout; the contract is ONE
+    # JSON line there, so fd 1 points at stderr until rank 0 prints the line
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -529,7 +534,10 @@ def main():
                            "scan_algo": a.algo, "perturb_mean": a.perturb_mean,
                            "parallelism": f"dp{a.gpus} (hemisphere = rank % 2)"},
                 **res, **extras}
+        sys.stdout.flush()
+        os.dup2(json_fd, 1)
         print(json.dumps(line), flush=True)
+        os.dup2(2, 1)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
