@@ -515,7 +515,14 @@ k_local_fused(const float2* __restrict__ vol,
                                                             const int* __restrict__ act,
                                                             const int* __restrict__ nAct,
                                                             const int* __restrict__ cls,
-                                                            long volStride, int nD = 1)
+                                                            long volStride, int nD = 1,
+                                                            const double* __restrict__ pC = nullptr,
+                                                            const double* __restrict__ pR = nullptr,
+                                                            const double* __restrict__ pT = nullptr,
+                                                            float* __restrict__ wC = nullptr,
+                                                            float* __restrict__ wR = nullptr,
+                                                            float* __restrict__ wT = nullptr,
+                                                            float* __restrict__ baseL = nullptr)
 {
     int l = blockIdx.x;
     if (act) {
@@ -753,6 +760,70 @@ k_local_fused(const float2* __restrict__ vol,
     __syncthreads();
     float Al = 0.f;
     for (int k = 0; k < NWAVE; k++) Al += sRed[k];
+    if (!CS && wR) {
+        // one workgroup holds the image's whole (r, t) table (nR <= 128, nT <=
+        // 16): the per-image normalisation of k_local_weights
+        // (src/Optimiser.cpp:1383-1402) in the epilogue, no dvp round trip
+        __shared__ float sMax[NWAVE];
+        __shared__ double sWT[NWAVE][TT];
+        __shared__ double sWC[NWAVE];
+        const int t = tc;
+        const bool tv = t < nT;
+        float v[4];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int rr = wv * 16 + 4 * kk + j;
+            v[j] = Al + sBias[rr] + acc[0][j];
+            if (tv && rr < nRl) {
+                mx = fmaxf(mx, v[j]);
+                if (dvp) dvp[((size_t)l * nR + r0 + sPerm[rr]) * nT + t] = v[j];
+            }
+        }
+        mx = wave_max(mx);
+        if (lane == 0) sMax[wv] = mx;
+        __syncthreads();
+        float base = sMax[0];
+        for (int w = 1; w < NWAVE; w++) base = fmaxf(base, sMax[w]);
+        const double c = pC[l];
+        const double ptl = tv ? pT[(size_t)l * nT + t] : 0.0;
+        double colT = 0.0, cw = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int rr = wv * 16 + 4 * kk + j;
+            const bool ok = tv && rr < nRl;
+            const int r = r0 + sPerm[rr < nRl ? rr : 0];
+            const double pr = pR[(size_t)l * nR + r];
+            const double e = ok ? (double)expf(v[j] - base) : 0.0;
+            double rs = e * ptl;          // the row's sum over its 16 translation lanes
+            rs += __shfl_xor(rs, 1, 64);
+            rs += __shfl_xor(rs, 2, 64);
+            rs += __shfl_xor(rs, 4, 64);
+            rs += __shfl_xor(rs, 8, 64);
+            if (tc == 0 && rr < nRl) wR[(size_t)l * nR + r] = (float)(rs * c);
+            if (rr < nRl) cw += rs * pr;
+            colT += e * pr;
+        }
+        colT += __shfl_xor(colT, 16, 64);
+        colT += __shfl_xor(colT, 32, 64);
+        cw += __shfl_xor(cw, 16, 64);
+        cw += __shfl_xor(cw, 32, 64);
+        if (lane < TT) sWT[wv][lane] = colT;
+        if (lane == 0) sWC[wv] = cw;
+        __syncthreads();
+        if (tid < nT) {
+            double a = 0.0;
+            for (int w = 0; w < NWAVE; w++) a += sWT[w][tid];
+            wT[(size_t)l * nT + tid] = (float)(a * c);
+        }
+        if (tid == 0) {
+            double a = 0.0;
+            for (int w = 0; w < NWAVE; w++) a += sWC[w];
+            wC[l] = (float)a;
+            baseL[l] = base;
+        }
+        return;
+    }
     // C layout of 16x16x4: col = lane & 15 (translation), row = 4 (lane >> 4) + j
 #pragma unroll
     for (int ct = 0; ct < NCT; ct++) {
@@ -1066,7 +1137,7 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         hipLaunchKernelGGL(kern, grid, dim3(THREADS), 0, s, reinterpret_cast<const float2*>(vol),
                            vdim, pf, quat, nR, trans, nCol, reinterpret_cast<const float2*>(dat),
                            ctf, sigRcp, iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, d, act, nAct,
-                           cls, vs, nD);
+                           cls, vs, nD, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
         THX_LAUNCH_CHECK();
         if (evEnd) THX_HIP(hipEventRecord(evEnd, s));
         hipLaunchKernelGGL(k_local_weights_d, dim3(nImg), dim3(256), 0, s, d, nR, nT, nD, pC, pR,
@@ -1082,14 +1153,22 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     const bool big = pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R;
     auto kern = volLayout == 1 ? (big ? k_local_fused<true, false, 1, true> : k_local_fused<true>)
                                : (big ? k_local_fused<false, false, 1, true> : k_local_fused<false>);
+    // one workgroup per image (nR <= 128, nT <= 16, the phases' 125 x 9):
+    // the normalisation runs in the kernel's epilogue and dvp is only written
+    // when the caller asks for it
+    const bool fuse = grid.y == 1 && grid.z == 1;
     hipLaunchKernelGGL(kern, grid, dim3(THREADS), 0, s, reinterpret_cast<const float2*>(vol), vdim,
                        pf, quat, nR, trans, nT, reinterpret_cast<const float2*>(dat), ctf, sigRcp,
-                       iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, d, act, nAct, cls, vs, 1);
+                       iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, fuse ? dvp : d, act, nAct, cls,
+                       vs, 1, pC, pR, pT, fuse ? wC : nullptr, fuse ? wR : nullptr,
+                       fuse ? wT : nullptr, fuse ? baseL : nullptr);
     THX_LAUNCH_CHECK();
     if (evEnd) THX_HIP(hipEventRecord(evEnd, s));
-    hipLaunchKernelGGL(k_local_weights, dim3(nImg), dim3(256), 0, s, d, nR, nT, pC, pR, pT, wC,
-                       wR, wT, baseL, act, nAct);
-    THX_LAUNCH_CHECK();
+    if (!fuse) {
+        hipLaunchKernelGGL(k_local_weights, dim3(nImg), dim3(256), 0, s, d, nR, nT, pC, pR, pT, wC,
+                           wR, wT, baseL, act, nAct);
+        THX_LAUNCH_CHECK();
+    }
     return THX_OK;
 }
 
