@@ -7,7 +7,7 @@ A "launch" is the whole launch sequence the bench times with HIP events
 (local_bench: the single k_local_fused<false> dispatch of a bench phase):
   scan  : k_prep_aconst .. k_scan_combine_bf of one thx_global_scan call whose
           k_scan_split grid is the 4096-image grid (bench.scan_roofline);
-  local : k_patch_boxes .. k_local_weights of one thx_local_phase call of
+  local : k_patch_boxes .. k_local_fused of one thx_local_phase call of
           bench.local_roofline (full resolution, 512 images): the clustered
           cloud in the half-complex layout (first four 512-image
           k_local_fused<false> sequences), and the uniform cloud in the cell
@@ -86,10 +86,10 @@ def main():
                                              for n, gr, _ in g)),
         # bench.local_roofline: 4 clustered-cloud launches (half-complex), then
         # 4 uniform ones, then 4 uniform in the cell-expanded layout
-        "local_fullres_512": summarise(rd, wr, "k_patch_boxes", "k_local_weights",
+        "local_fullres_512": summarise(rd, wr, "k_patch_boxes", "k_local_fused",
                                        lambda g: any("k_local_fused<false" in n and gr == 512 * 512
                                                      for n, gr, _ in g), first=4),
-        "local_fullres_512_uniform_cells": summarise(rd, wr, "k_patch_boxes", "k_local_weights",
+        "local_fullres_512_uniform_cells": summarise(rd, wr, "k_patch_boxes", "k_local_fused",
                                                      lambda g: any("k_local_fused<true" in n
                                                                    for n, _, _ in g)),
         # the bench step's dominant kernel: one k_local_fused<false> launch per
