@@ -256,3 +256,49 @@ def test_local_2d_through_interface_forwards(orc):
                                 ctypes.byref(dS), 0) == 0
     assert L.thx_tex_destroy(mgr) == 0
     assert L.thx_ExpectFreeIdx(gpu, ctypes.byref(dCol), ctypes.byref(dRow)) == 0
+
+
+def test_c1_shape_phase_and_insert(orc):
+    """Config C1 (script/demo_2D.json): box 64, 8 classes, the full-resolution
+    ring rU 30 (nPxl 1367): the 2D phase per image against the restatement and
+    the 8-class insert with per-sample classes."""
+    N, pf, nK = 64, 2, 8
+    s = _stack(orc, N=N, pf=pf, rU=30, nImg=3, nK=nK, seed=21)
+    vdim, px = s["vdim"], s["px"]
+    # SURVEY 8's C1 count 1367 is the rL 0 ring; the stack's rL 1 drops the origin
+    assert px.n == 1366
+    nImg, mR, mT = 3, 16, 5
+    rng = s["rng"]
+    th = s["th"][:, None] + rng.standard_normal((nImg, mR)) * 0.05
+    rot = _rot(th)
+    trans = s["t"][:, None, :] + rng.standard_normal((nImg, mT, 2)) * 0.5
+    pC = np.full(nImg, 0.9)
+    pR = np.full((nImg, mR), 1.0 / mR)
+    pT = np.full((nImg, mT), 1.0 / mT)
+    cls = s["k"].astype(np.int32)
+    _, _, _, _, d = ops.local_phase2d(T_(s["cl"]), T_(rot), T_(trans), T_(pC), T_(pR), T_(pT),
+                                      T_(s["dat"]), T_(s["ctf"]), T_(s["sig"]), s["gpx"],
+                                      cls=T_(cls), want_dvp=True)
+    d = d.cpu().numpy()
+    for l in range(nImg):
+        ref = np.empty((mR, mT), np.float32)
+        for r in range(mR):
+            pri = orc.project2d(s["cl"][cls[l]], vdim, pf, rot[l, r], px)
+            for t in range(mT):
+                pt = (orc.translate(px, *trans[l, t], N) * pri).astype(np.complex64)
+                ref[r, t] = orc.logdatavs(s["dat"][l], pt, s["ctf"][l], s["sig"][l])
+        assert np.max(np.abs(d[l] - ref)) <= 1e-5 * np.abs(ref).max()
+    mReco = 20
+    irot = _rot(rng.uniform(0, 2 * np.pi, (nImg, mReco)))
+    itr = rng.standard_normal((nImg, mReco, 2))
+    off = rng.standard_normal((nImg, 2)) * 0.2
+    w = np.full(nImg, 1.0 / mReco, np.float32)
+    nc = rng.integers(0, nK, (nImg, mReco)).astype(np.int32)
+    F, Tm, O, cnt = orc.insert2d_batch(vdim, pf, s["dat"], s["ctf"], irot, itr, off, w, nc, px, N,
+                                       nK=nK)
+    hm = ops.HalfMap2D(vdim, nK, DEV)
+    ops.insert2d(hm, T_(s["dat"]), T_(s["ctf"]), T_(irot), T_(itr), T_(off), T_(w), s["gpx"],
+                 nc=T_(nc))
+    assert np.max(np.abs(hm.F.cpu().numpy().reshape(-1) - F)) <= 1e-5 * np.abs(F).max()
+    assert np.max(np.abs(hm.T.cpu().numpy().reshape(-1) - Tm)) <= 1e-5 * np.abs(Tm).max()
+    assert np.array_equal(hm.counter.cpu().numpy(), cnt.astype(np.int32))
