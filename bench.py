@@ -68,7 +68,8 @@ def parse():
     p.add_argument("--large-first", type=int, default=0,
                    help="1: OPTIMISER_GLOBAL_PERTURB_LARGE (off in the reference's Config.h)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-images", type=int, default=4096,
+                   help="images of the CPU-baseline sample (median of 3 runs)")
     p.add_argument("--no-extras", action="store_true", help="skip insert / all-reduce / local roofline")
     return p.parse_args()
 
@@ -216,28 +217,68 @@ def cpu_info():
     return model, os.cpu_count()
 
 
-def cpu_baseline(vol_np, N, pf, gset, dat, ctf, sig, px, seconds, phases):
+def cpu_share():
+    """The host CPUs this process may use: the affinity mask, the cgroup CPU
+    quota (cgroup v2 cpu.max or v1 cfs_quota/period) and OMP_NUM_THREADS (the
+    per-GPU share the box exports).  Threads = the smallest of them."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() else None
+    threads = aff
+    if quota:
+        threads = min(threads, max(1, int(math.floor(quota))))
+    if omp:
+        threads = min(threads, omp)
+    return {"threads": threads, "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+            "omp_num_threads": omp, "nproc": os.cpu_count()}
+
+
+def cpu_baseline(vol_np, N, pf, gset, dat, ctf, sig, px, phases, n_img=4096, runs=3):
     """The CPU path (oracle/cpu_fast.c: the reference's expectation loop
     structure, OpenMP, -O3 -march=native, likelihood vectorised over images in
-    the scan and over pixels in the phases) on the host cores, same workload
-    shape per image, on a bounded sample of images."""
+    the scan and over pixels in the phases) on the host cores this process
+    may use (cpu_share), same workload shape per image: the median of `runs`
+    runs over the same n_img-image sample."""
     import ctypes
     from oracle import oracle as orc
     orc.build()
     L = ctypes.CDLL(os.path.join(ROOT, "oracle", "libcpufast.so"))
     P = lambda x: x.ctypes.data_as(ctypes.c_void_p)
-    threads = int(os.environ.get("OMP_NUM_THREADS") or (os.cpu_count() or 1))
+    share = cpu_share()
+    threads = share["threads"]
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    L.cpu_set_threads(threads)
     q, t, pR, pT = (np.ascontiguousarray(x) for x in gset)
     vdim = pf * N
     mR, mT = 125, 9
     rng = np.random.default_rng(0)
     vol_np = np.ascontiguousarray(vol_np)
     iCol, iRow = np.ascontiguousarray(px.iCol), np.ascontiguousarray(px.iRow)
+    n = min(n_img, len(dat))
+    lq = np.ascontiguousarray(synth.clustered_quaternions(n * phases, mR, 3.0, rng))
+    lt = np.ascontiguousarray(rng.standard_normal((n * phases, mT, 2)))
+    d, c, s_ = (np.ascontiguousarray(x[:n]) for x in (dat, ctf, sig))
 
-    def run(n):
-        lq = np.ascontiguousarray(synth.clustered_quaternions(n * phases, mR, 3.0, rng))
-        lt = np.ascontiguousarray(rng.standard_normal((n * phases, mT, 2)))
-        d, c, s_ = (np.ascontiguousarray(x[:n]) for x in (dat, ctf, sig))
+    def run():
         base = np.zeros(n, np.float32)
         lb = np.zeros(n, np.float32)
         t0 = time.perf_counter()
@@ -245,18 +286,16 @@ def cpu_baseline(vol_np, N, pf, gset, dat, ctf, sig, px, seconds, phases):
                    n, P(iCol), P(iRow), px.n, N, P(lq), mR, P(lt), mT, phases, P(base), P(lb))
         return time.perf_counter() - t0
 
-    n = 16
-    dt = run(n)
-    n2 = max(16, min(len(dat), int(n * seconds / max(dt, 1e-3))))
-    if n2 > n:
-        dt = run(n2)
-        n = n2
+    dts = sorted(run() for _ in range(runs))
+    dt = dts[len(dts) // 2]
     model, ncpu = cpu_info()
     return {"value": n / dt, "unit": "particle-images/s", "cores": threads, "kind": "port",
             "cpu_model": model, "nproc": ncpu, "build": "gcc -O3 -march=native -fopenmp",
+            "cpu_share": share, "runs_s": [round(x, 2) for x in dts],
+            "spread": (dts[-1] - dts[0]) / dt,
             "sample": f"{n} images x (global scan nR={len(q)} nT={len(t)} nPxl={px.n} + "
                       f"{phases} local phases {mR}x{mT}), oracle/cpu_fast.c, OpenMP {threads} "
-                      f"threads, {dt:.1f} s"}
+                      f"threads, median of {runs} runs ({dt:.1f} s)"}
 
 
 PEAK_FP32_TFLOPS = PEAK_FP32_MFMA_TFLOPS
@@ -514,10 +553,10 @@ def main():
 
     if rank == 0 and not a.no_cpu_baseline:
         vol_np = vol.cpu().numpy()
-        n_cpu = min(4096, dat.shape[0])   # room for the --cpu-seconds target (~12 s)
+        n_cpu = min(a.cpu_images, dat.shape[0])
         extras["cpu_baseline"] = cpu_baseline(vol_np, N, pf, gset, dat[:n_cpu].cpu().numpy(),
                                               ctf[:n_cpu].cpu().numpy(), sig[:n_cpu].cpu().numpy(),
-                                              px, a.cpu_seconds, a.phases)
+                                              px, a.phases, n_img=n_cpu)
 
     if rank == 0:
         line = {"metric": "particle-images/sec through expectation (box 256, 2000 rot samples)",

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define THX_ABI_VERSION 4
+#define THX_ABI_VERSION 5
 
 enum {
     THX_OK = 0,
@@ -394,6 +394,13 @@ int thx_rccl_comm_init(int nranks, const void* id, int rank, void** comm);
 int thx_rccl_comm_destroy(void* comm);
 int thx_halfmap_allreduce(void* comm, float* F, float* T, double* O, int* counter,
                           long long dimSize, int nK, thx_stream_t stream);
+/* The hemispheres' hand-over for the FSC of Model::compareTwoHemispheres
+ * (src/Model.cpp:307-852, MPI_Recv_Large of the A and B maps on the master):
+ * send nSend floats to rank peerSend and receive nRecv floats from rank
+ * peerRecv of `comm` (a communicator over both hemispheres' leads), one RCCL
+ * group on `stream`; either side may be NULL. */
+int thx_halfmap_sendrecv(void* comm, const float* send, long long nSend, int peerSend,
+                         float* recv, long long nRecv, int peerRecv, thx_stream_t stream);
 
 /* ------------------------------------------------------------------ f4 ---
  * The 2D classification path (MODE_2D).  2D projectees / half-maps are
@@ -533,6 +540,8 @@ typedef struct thx_expect_cfg {
                                  pieces -- the layout for large boxes at full resolution, where
                                  the projectee is far beyond L2 / MALL and the patch boxes do not
                                  fit LDS; NULL: the half-complex projectee */
+    /* ABI 5 */
+    int nPhaseEvents;         /* event pairs phaseEvents holds: phases past it are not timed */
 } thx_expect_cfg;
 
 /* nOrd: length of pxOrder (<= 0 when pxOrder is NULL). */

@@ -32,6 +32,16 @@
 
 typedef struct { float re, im; } cpx;
 
+/* OpenMP threads of the parallel regions below (the caller's CPU share). */
+void cpu_set_threads(int n)
+{
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
 static void rotmat(const double* q, double* m)
 {
     /* rotate3D, src/Geometry/Euler.cpp:181-189 (column-major) */

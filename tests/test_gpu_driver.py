@@ -204,6 +204,48 @@ def test_global_converge_matches_fixed_quality(local_stack):
     assert res[True][1].min() >= 11 and res[True][1].max() <= 99
 
 
+def test_concurrent_sub_batches_on_three_streams(local_stack):
+    """Three sub-batches of a global search enqueued from three host threads on
+    three HIP streams at once give bit-identical particles, priors, scores and
+    phase counts to the same sub-batches run one after the other on one
+    stream.  Every call gets its own scratch (ops.workspace is per stream):
+    the per-device buffer the driver used to share let concurrent calls
+    overwrite each other's patch records and active lists."""
+    import threading
+    s = local_stack
+    gset = s["gset"]
+    dat, ctf, sig, _, _ = grid_images(s["vol"][None], s["px"], gset, 3 * 96, seed=81, snr=1.0)
+    e = ex.Expectation(s["vol"], s["px"], gset, n_phase=10, seed=5)
+    parts = [slice(96 * k, 96 * (k + 1)) for k in range(3)]
+    args = [(dat[p].contiguous(), ctf[p].contiguous(), sig[p].contiguous()) for p in parts]
+    torch.cuda.synchronize()
+    serial = [[x.clone() for x in e.run(*a)] for a in args]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(DEV) for _ in range(3)]
+    got, errs = [None] * 3, []
+    go = threading.Barrier(3)
+
+    def worker(k):
+        try:
+            go.wait()
+            with torch.cuda.stream(streams[k]):
+                got[k] = e.run(*args[k])
+        except Exception as exc:      # noqa: BLE001 -- reported below
+            errs.append(exc)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for k in range(3):
+        for a, b in zip(serial[k], got[k]):
+            assert torch.equal(a, b), k
+    ops.release_workspaces()
+
+
 def test_local_search_with_cell_projectee(local_stack):
     """thx_expect_cfg.volCells: the phases gather 64-B cells; the same state,
     seed and phases give the same refinement quality and, phase by phase, the

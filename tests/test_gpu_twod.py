@@ -258,6 +258,66 @@ def test_local_2d_through_interface_forwards(orc):
     assert L.thx_ExpectFreeIdx(gpu, ctypes.byref(dCol), ctypes.byref(dRow)) == 0
 
 
+def test_c1_shape_global_scan(orc):
+    """Config C1's global scan (script/demo_2D.json: box 64, 8 classes, 2D
+    global sampling mS 100 -> nR 100, transS 10 -> nT 151, global-search ring
+    rU 7 -> nPxl 69) through thx_ExpectGlobal2D on 16 images against the
+    restatement: orc.project2d / orc.translate per sample, the likelihood of
+    every (image, class, rotation, translation) in float64 (the FP32 sum of
+    orc.logdatavs over 69 pixels agrees with it to ~1e-7 relative; 1.9 M
+    ctypes calls would take minutes), and orc.weights_global(kIdx, nK) for the
+    running baseline and marginals over the 8 classes."""
+    N, pf, nK, rU, nImg = 64, 2, 8, 7, 16
+    s = _stack(orc, N=N, pf=pf, rU=rU, nImg=nImg, nK=nK, seed=31)
+    vdim = s["vdim"]
+    px = orc.pixel_set(N, pf, rU, 0)
+    assert px.n == 69                       # SURVEY 8's C1 global-search count
+    mS, nR, nT = ops.global_sample_sizes(100, mode=0)
+    assert (nR, nT) == (100, 151)
+    rng = np.random.default_rng(32)
+    # the images on the rL 0 ring (the stack's own set is rL 1)
+    k_true = rng.integers(0, nK, nImg)
+    th_true = rng.uniform(0, 2 * np.pi, nImg)
+    t_true = rng.standard_normal((nImg, 2)) * 2
+    dat = np.stack([orc.project2d(s["cl"][k_true[l]], vdim, pf, _rot(th_true[l]), px) *
+                    orc.translate(px, *t_true[l], N) for l in range(nImg)])
+    dat = (dat + 0.5 * (rng.standard_normal(dat.shape) + 1j * rng.standard_normal(dat.shape))
+           ).astype(np.complex64)
+    ctf = rng.uniform(0.3, 1.0, (nImg, px.n)).astype(np.float32)
+    sig = -rng.uniform(0.5, 2.0, (nImg, px.n)).astype(np.float32)
+    rot = _rot(rng.uniform(0, 2 * np.pi, nR))
+    trans = rng.standard_normal((nT, 2)) * 10.0
+    pR = np.full(nR, 1.0 / nR)
+    pT = rng.uniform(0.5, 1.5, nT)
+    pT /= pT.sum()
+    tra = np.stack([orc.translate(px, *trans[t], N) for t in range(nT)]).astype(np.complex128)
+    state = None
+    for k in range(nK):
+        pri = np.stack([orc.project2d(s["cl"][k], vdim, pf, rot[r], px) for r in range(nR)])
+        pt = (pri.astype(np.complex128)[:, None, :] * tra[None, :, :]).astype(np.complex64)
+        dvp = np.empty((nImg, nR, nT), np.float32)
+        for l in range(nImg):
+            e = dat[l].astype(np.complex128) - ctf[l].astype(np.float64) * pt.astype(np.complex128)
+            dvp[l] = (sig[l].astype(np.float64) * (e.real ** 2 + e.imag ** 2)).sum(-1)
+        state = orc.weights_global(dvp, pR, pT, k, nK, state)
+    rC, rR, rT, rb = state
+    wC = np.zeros(nImg * nK, np.float32)
+    wR = np.zeros(nImg * nK * nR, np.float32)
+    wT = np.zeros(nImg * nK * nT, np.float32)
+    cl = np.ascontiguousarray(s["cl"]).view(np.float32)
+    datf = np.ascontiguousarray(dat).view(np.float32)
+    rc = lib().thx_ExpectGlobal2D(P(cl), P(datf), P(ctf), P(sig), P(np.ascontiguousarray(trans)),
+                                  P(wC), P(wR), P(wT), P(pR), P(pT), P(np.ascontiguousarray(rot)),
+                                  P(px.iCol), P(px.iRow), nK, nR, nT, pf, 1, N, vdim, px.n, nImg)
+    assert rc == 0, lib().thx_last_error()
+    for got, want in ((wC, rC), (wR, rR), (wT, rT)):
+        got, want = got.reshape(nImg, -1), want.reshape(nImg, -1)
+        m = want >= 1e-4 * want.max(axis=1, keepdims=True)
+        assert np.max(np.abs(got - want)[m] / want[m]) < 2e-3
+    # the classes the scan puts the weight on are the images' true classes
+    assert np.mean(wC.reshape(nImg, nK).argmax(1) == k_true) >= 0.75
+
+
 def test_c1_shape_phase_and_insert(orc):
     """Config C1 (script/demo_2D.json): box 64, 8 classes, the full-resolution
     ring rU 30 (nPxl 1367): the 2D phase per image against the restatement and

@@ -69,6 +69,8 @@ SIGNATURES = {
     "thx_rccl_comm_init": (_c_int, [_c_int, _p, _c_int, _p]),
     "thx_rccl_comm_destroy": (_c_int, [_p]),
     "thx_halfmap_allreduce": (_c_int, [_p, _p, _p, _p, _p, ctypes.c_longlong, _c_int, _p]),
+    "thx_halfmap_sendrecv": (_c_int, [_p, _p, ctypes.c_longlong, _c_int, _p, ctypes.c_longlong,
+                                      _c_int, _p]),
     "thx_project2d": (_c_int, [_p, _c_int, _c_int, _p, _c_int, _p, _p, _c_int, _p, _p]),
     "thx_local_phase2d_workspace": (_c_size, [_c_int, _c_int, _c_int]),
     "thx_local_phase2d": (_c_int, [_p, _c_int, _c_int, _p, _p, _c_int, _p, _c_int, _p, _p, _p, _p, _p,

@@ -58,6 +58,31 @@ extern "C" int thx_rccl_comm_destroy(void* comm)
     return THX_OK;
 }
 
+// Inside a group the first failure is kept and the group is still closed, so
+// the calling thread never keeps an open ncclGroup after an error.
+#define THX_NCCL_GROUPED(call)                                                 \
+    do {                                                                       \
+        ncclResult_t r_ = (call);                                              \
+        if (r_ != ncclSuccess && first == ncclSuccess) {                       \
+            first = r_;                                                        \
+            what = #call;                                                      \
+        }                                                                      \
+    } while (0)
+
+static int group_end(ncclResult_t first, const char* what)
+{
+    const ncclResult_t e = ncclGroupEnd();
+    if (first == ncclSuccess && e != ncclSuccess) {
+        first = e;
+        what = "ncclGroupEnd()";
+    }
+    if (first != ncclSuccess) {
+        ::thx::set_error("halfmap.hip %s: %s", what, ncclGetErrorString(first));
+        return THX_ERR_HIP;
+    }
+    return THX_OK;
+}
+
 extern "C" int thx_halfmap_allreduce(void* comm, float* F, float* T, double* O, int* counter,
                                      long long dimSize, int nK, thx_stream_t stream)
 {
@@ -66,10 +91,35 @@ extern "C" int thx_halfmap_allreduce(void* comm, float* F, float* T, double* O, 
     hipStream_t s = thx::as_stream(stream);
     const size_t n = (size_t)dimSize * nK;
     THX_NCCL(ncclGroupStart());
-    THX_NCCL(ncclAllReduce(F, F, 2 * n, ncclFloat32, ncclSum, c, s));
-    THX_NCCL(ncclAllReduce(T, T, n, ncclFloat32, ncclSum, c, s));
-    if (O) THX_NCCL(ncclAllReduce(O, O, 3 * (size_t)nK, ncclFloat64, ncclSum, c, s));
-    if (counter) THX_NCCL(ncclAllReduce(counter, counter, nK, ncclInt32, ncclSum, c, s));
-    THX_NCCL(ncclGroupEnd());
-    return THX_OK;
+    ncclResult_t first = ncclSuccess;
+    const char* what = "";
+    THX_NCCL_GROUPED(ncclAllReduce(F, F, 2 * n, ncclFloat32, ncclSum, c, s));
+    THX_NCCL_GROUPED(ncclAllReduce(T, T, n, ncclFloat32, ncclSum, c, s));
+    if (O) THX_NCCL_GROUPED(ncclAllReduce(O, O, 3 * (size_t)nK, ncclFloat64, ncclSum, c, s));
+    if (counter) THX_NCCL_GROUPED(ncclAllReduce(counter, counter, nK, ncclInt32, ncclSum, c, s));
+    return group_end(first, what);
+}
+
+// The half-map hand-over of Model::compareTwoHemispheres (src/Model.cpp:
+// 307-852: MPI_Recv_Large of hemisphere A's and B's maps on the master):
+// one point-to-point step on a communicator that spans both hemispheres'
+// leads -- `send` (nSend floats) goes to rank peerSend, `recv` (nRecv floats)
+// comes from rank peerRecv; either side may be absent (NULL / peer < 0).  Over
+// xGMI this is one peer copy; no host staging.
+extern "C" int thx_halfmap_sendrecv(void* comm, const float* send, long long nSend, int peerSend,
+                                    float* recv, long long nRecv, int peerRecv,
+                                    thx_stream_t stream)
+{
+    THX_CHECK_ARG(comm, "thx_halfmap_sendrecv: null communicator");
+    THX_CHECK_ARG(!send || (nSend > 0 && peerSend >= 0), "thx_halfmap_sendrecv: bad send side");
+    THX_CHECK_ARG(!recv || (nRecv > 0 && peerRecv >= 0), "thx_halfmap_sendrecv: bad receive side");
+    if (!send && !recv) return THX_OK;
+    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    hipStream_t s = thx::as_stream(stream);
+    THX_NCCL(ncclGroupStart());
+    ncclResult_t first = ncclSuccess;
+    const char* what = "";
+    if (send) THX_NCCL_GROUPED(ncclSend(send, (size_t)nSend, ncclFloat32, peerSend, c, s));
+    if (recv) THX_NCCL_GROUPED(ncclRecv(recv, (size_t)nRecv, ncclFloat32, peerRecv, c, s));
+    return group_end(first, what);
 }

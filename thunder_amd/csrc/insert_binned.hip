@@ -32,8 +32,10 @@
 // records the batch's largest |value|, and the deposit scales by 2^e with
 // |value * weight * 2^e| < 2^47, so <= 2^15 entries of a chunk sum without
 // overflow and the tap products (the float products of the float path) are
-// rounded once, at 2^-48 of the largest value; the tile sums are exact and
-// independent of order.  Non-finite values take a float-atomic path so NaN /
+// rounded once, at 2^-48 of the largest value of their own kind: F (re, im)
+// and T carry separate maxima and exponents, so T far below the data's scale
+// (data >> ctf^2, pixels near CTF zeros) keeps its own 2^-48 relative grid;
+// the tile sums are exact and independent of order.  Non-finite values take a float-atomic path so NaN /
 // Inf propagate as in the reference.
 // Entries live in the caller's workspace; images are processed in batches
 // so the entry buffer stays bounded (thx_insert3d_binned_workspace).
@@ -220,7 +222,7 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
                                                         int* __restrict__ count,
                                                         int* __restrict__ cursor,
                                                         Entry* __restrict__ ent,
-                                                        unsigned* __restrict__ vmaxBits,
+                                                        unsigned* __restrict__ vmaxBits,   // [F, T]
                                                         float2* __restrict__ F,
                                                         float* __restrict__ T,
                                                         const float* __restrict__ attr,
@@ -272,7 +274,7 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
     const double* md = mDef + (size_t)b * mReco;
     const float2* ms = mShift + (size_t)b * mReco;
     const float wl = w[l];
-    float vmax = 0.f;
+    float vmaxF = 0.f, vmaxT = 0.f;
     for (long e0 = 0; e0 < nE; e0 += C_THREADS) {
         const long e = e0 + tid;
         int t = -1;
@@ -317,8 +319,9 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
                 }
                 en.vr = vr;
                 en.vi = cj ? -vi : vi;
-                vmax = fmaxf(vmax, fmaxf(fabsf(en.vr), fmaxf(fabsf(en.vi), fabsf(en.tv))));
-                if (!(fabsf(en.vr) + fabsf(en.vi) + fabsf(en.tv) <= 3.4e38f)) vmax = INFINITY;
+                vmaxF = fmaxf(vmaxF, fmaxf(fabsf(en.vr), fabsf(en.vi)));
+                vmaxT = fmaxf(vmaxT, fabsf(en.tv));
+                if (!(fabsf(en.vr) + fabsf(en.vi) + fabsf(en.tv) <= 3.4e38f)) vmaxF = INFINITY;
                 t = G.tile((int)floorf(en.x), (int)floorf(en.y), (int)floorf(en.z));
             }
         }
@@ -330,9 +333,11 @@ __global__ void __launch_bounds__(C_THREADS) k_bin_pass(TileGrid G, int vdim, in
             scatter_ft(F, T, vdim, en.x, en.y, en.z, en.vr, en.vi, en.tv);
         }
     }
-    // the batch's largest |value| (non-negative float bits order like uints)
-    vmax = wave_max(vmax);
-    if ((tid & 63) == 0 && vmax > 0.f) atomicMax(vmaxBits, __float_as_uint(vmax));
+    // the batch's largest |F| and |T| (non-negative float bits order like uints)
+    vmaxF = wave_max(vmaxF);
+    vmaxT = wave_max(vmaxT);
+    if ((tid & 63) == 0 && vmaxF > 0.f) atomicMax(vmaxBits, __float_as_uint(vmaxF));
+    if ((tid & 63) == 0 && vmaxT > 0.f) atomicMax(vmaxBits + 1, __float_as_uint(vmaxT));
 }
 
 // 3. tile offsets, cursors and deposit chunks (one workgroup)
@@ -374,7 +379,7 @@ __global__ void __launch_bounds__(1024) k_bin_scan(const int* __restrict__ count
         if (tid == 1023) { carryE += sA[1023]; carryC += sB[1023]; }
         __syncthreads();
     }
-    if (tid == 0) { ctl[0] = min(carryC, maxChunks); ctl[1] = (int)carryE; ctl[2] = 0; }
+    if (tid == 0) { ctl[0] = min(carryC, maxChunks); ctl[1] = (int)carryE; ctl[2] = 0; ctl[3] = 0; }
 }
 
 // 5. one chunk of one tile: 64-bit fixed-point LDS accumulation, row-contiguous flush
@@ -393,8 +398,9 @@ __global__ void __launch_bounds__(D_THREADS) k_bin_deposit(TileGrid G, int vdim,
     const int tx = t % G.ntx, ty = (t / G.ntx) % G.nty, tz = t / (G.ntx * G.nty);
     const int ox = tx * BT, oy = ty * BT - G.R, oz = tz * BT - G.R;
     const int nColFT = vdim / 2 + 1;
-    const float vmax = __uint_as_float((unsigned)ctl[2]);
-    if (!(vmax <= 3.4e38f)) {
+    const float vmaxF = __uint_as_float((unsigned)ctl[2]);
+    const float vmaxT = __uint_as_float((unsigned)ctl[3]);
+    if (!(vmaxF <= 3.4e38f) || !(vmaxT <= 3.4e38f)) {
         // non-finite values: float atomics straight to HBM (NaN / Inf propagate)
         for (int i = tid; i < ch.z; i += D_THREADS) {
             const Entry e = ent[(size_t)ch.y + i];
@@ -402,10 +408,12 @@ __global__ void __launch_bounds__(D_THREADS) k_bin_deposit(TileGrid G, int vdim,
         }
         return;
     }
-    // 2^e with vmax * 2^e < 2^47 (frexp: vmax = m 2^k, m in [0.5, 1))
-    int k = 0;
-    if (vmax > 0.f) frexpf(vmax, &k);
-    const int ex = 47 - k;
+    // 2^e with vmax * 2^e < 2^47 (frexp: vmax = m 2^k, m in [0.5, 1)), one
+    // exponent for F (re, im) and one for T
+    int kF = 0, kT = 0;
+    if (vmaxF > 0.f) frexpf(vmaxF, &kF);
+    if (vmaxT > 0.f) frexpf(vmaxT, &kT);
+    const int exF = 47 - kF, exT = 47 - kT;
     for (int v = tid; v < 3 * BVOX; v += D_THREADS) sQ[v] = 0ull;
     __syncthreads();
     for (int i = tid; i < ch.z; i += D_THREADS) {
@@ -424,9 +432,9 @@ __global__ void __launch_bounds__(D_THREADS) k_bin_deposit(TileGrid G, int vdim,
                     const float wt = wx[ix] * wy[jy] * wz[kz];
                     const int v = 3 * (a + (kz * BH + jy) * BH + ix);
                     // the float products of the float path, scaled exactly, rounded once
-                    atomicAdd(&sQ[v], (unsigned long long)__float2ll_rn(ldexpf(e.vr * wt, ex)));
-                    atomicAdd(&sQ[v + 1], (unsigned long long)__float2ll_rn(ldexpf(e.vi * wt, ex)));
-                    atomicAdd(&sQ[v + 2], (unsigned long long)__float2ll_rn(ldexpf(e.tv * wt, ex)));
+                    atomicAdd(&sQ[v], (unsigned long long)__float2ll_rn(ldexpf(e.vr * wt, exF)));
+                    atomicAdd(&sQ[v + 1], (unsigned long long)__float2ll_rn(ldexpf(e.vi * wt, exF)));
+                    atomicAdd(&sQ[v + 2], (unsigned long long)__float2ll_rn(ldexpf(e.tv * wt, exT)));
                 }
     }
     __syncthreads();
@@ -440,7 +448,7 @@ __global__ void __launch_bounds__(D_THREADS) k_bin_deposit(TileGrid G, int vdim,
         if (lane < 2 * BH) { xi = lane >> 1; q = (long long)sQ[3 * (row * BH + xi) + (lane & 1)]; }
         else if (lane < 3 * BH) { xi = lane - 2 * BH; q = (long long)sQ[3 * (row * BH + xi) + 2]; }
         if (xi < 0 || q == 0 || ox + xi >= nColFT) continue;
-        const float v = (float)ldexp((double)q, -ex);
+        const float v = (float)ldexp((double)q, lane < 2 * BH ? -exF : -exT);
         const int gy = wrap_idx(oy + y, vdim), gz = wrap_idx(oz + z, vdim);
         const size_t g = ((size_t)gz * vdim + gy) * nColFT + ox + xi;
         if (lane < 2 * BH) atomicAdd(F + 2 * g + (lane & 1), v);
@@ -517,8 +525,8 @@ static int insert_binned_impl(float* F, float* T, double* O, int* counter, int v
                   BIN_MAXM);
     THX_CHECK_ARG(pf * rMax + 2 <= vdim / 2 - 1,
                   "thx_insert3d_binned: rMax * pf reaches the volume edge");
-    THX_CHECK_ARG(pxOrder && nOrd > 0, "thx_insert3d_binned: pxOrder required");
     if (nImg == 0 || mReco == 0 || nPxl == 0) return THX_OK;
+    THX_CHECK_ARG(pxOrder && nOrd > 0, "thx_insert3d_binned: pxOrder required");
     const BinPlan P = plan(nImg, mReco, nOrd, pf, rMax);
     THX_CHECK_ARG(P.nt <= BIN_MAX_TILES,
                   "thx_insert3d_binned: %d tiles exceed the %d-tile histogram (use thx_insert3d_tiled)",

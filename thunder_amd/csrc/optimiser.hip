@@ -1407,8 +1407,9 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             THX_RET(thx_ctf_search(p.dfo, p.freq, cs->d, mLD, p.K1, p.K2, cs->attr, nImg, nPxl,
                                    p.ctfD, stream));
         }
-        hipEvent_t* ev = static_cast<hipEvent_t*>(c.phaseEvents);
         const int pi = phase - phase0;
+        // phases past the caller's event pairs run untimed
+        hipEvent_t* ev = pi < c.nPhaseEvents ? static_cast<hipEvent_t*>(c.phaseEvents) : nullptr;
         THX_RET(thx::local_phase_timed(&sel, ev ? ev[2 * pi] : nullptr, ev ? ev[2 * pi + 1] : nullptr,
                                        c.volCells ? c.volCells : vol, c.volCells ? 1 : 0, c.vdim,
                                        c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT,

@@ -41,7 +41,9 @@ class ExpectCfg(ctypes.Structure):
                 ("perturbFactorL", ctypes.c_double), ("largeFirst", ctypes.c_int),
                 ("phaseEvents", ctypes.c_void_p),
                 # ABI 4
-                ("volCells", ctypes.c_void_p)]
+                ("volCells", ctypes.c_void_p),
+                # ABI 5
+                ("nPhaseEvents", ctypes.c_int)]
 
 
 class CtfSearchCfg(ctypes.Structure):
@@ -109,7 +111,7 @@ class Expectation:
                              k_floor, s_floor, trans_s, trans_m, seed, int(bool(shuffle)),
                              nK, self.search, int(bool(converge)), min_phase, max_phase,
                              {"top": 0, "acg": 1}[perturb_mean], acg_iters, perturb_large,
-                             int(bool(large_first)), None, None)
+                             int(bool(large_first)), None, None, 0)
         if isinstance(cells, str):
             if cells != "auto":
                 raise ValueError("cells: a thx_volume_cells tensor, None or 'auto'")
@@ -222,11 +224,15 @@ class PhaseTimer:
         check(lib().thx_event_pairs_create(n_pairs, ctypes.byref(self.ev)), "thx_event_pairs_create")
         self.e = expectation
         expectation.cfg.phaseEvents = self.ev
+        expectation.cfg.nPhaseEvents = n_pairs
 
     def select(self, first_pair):
         """Record the next run's phases into pairs first_pair, first_pair + 1, ..."""
+        if not 0 <= first_pair <= self.n:
+            raise ValueError("first_pair outside the timer's event pairs")
         self.e.cfg.phaseEvents = ctypes.c_void_p(self.ev.value + 2 * first_pair *
                                                  ctypes.sizeof(ctypes.c_void_p))
+        self.e.cfg.nPhaseEvents = self.n - first_pair
 
     def ms(self):
         out = (ctypes.c_float * self.n)()
@@ -235,6 +241,7 @@ class PhaseTimer:
 
     def close(self):
         self.e.cfg.phaseEvents = None
+        self.e.cfg.nPhaseEvents = 0
         lib().thx_event_pairs_destroy(self.ev, self.n)
 
 

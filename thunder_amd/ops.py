@@ -7,6 +7,7 @@ is enqueued (a mis-shaped launch must never reach the GPU).
 """
 import ctypes
 import math
+import threading
 
 import numpy as np
 import torch
@@ -14,6 +15,7 @@ import torch
 from ._lib import check, lib
 
 _ws_cache = {}
+_ws_lock = threading.Lock()
 
 
 def _ptr(t):
@@ -38,13 +40,31 @@ def _req(t, dtype, shape, name):
     return t
 
 
-def workspace(nbytes, device):
-    key = torch.device(device)
-    buf = _ws_cache.get(key)
-    if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=key)
-        _ws_cache[key] = buf
-    return buf
+def workspace(nbytes, device, stream=None):
+    """Scratch for one call enqueued on ``stream`` (default: the device's
+    current stream).  One buffer per (device, stream): calls on one stream are
+    ordered, so they may share it, while calls on different streams (concurrent
+    sub-batches, several host threads) never do -- a shared buffer would let
+    one call's patch records, active lists and particle scratch overwrite
+    another's.  The buffer is allocated with its stream current, so the
+    caching allocator reuses its memory only in that stream's order."""
+    dev = torch.device(device)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    key = (dev, stream.cuda_stream)
+    with _ws_lock:
+        buf = _ws_cache.get(key)
+        if buf is None or buf.numel() < nbytes:
+            with torch.cuda.stream(stream):
+                buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=dev)
+            _ws_cache[key] = buf
+        return buf
+
+
+def release_workspaces():
+    """Drop the cached per-stream scratch buffers (e.g. before destroying streams)."""
+    with _ws_lock:
+        _ws_cache.clear()
 
 
 # ------------------------------------------------------------------- a1

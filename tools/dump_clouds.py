@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Dump the bench's particle clouds (C3 stack, 12 500 images) after k phases
-for a sample of images, for CPU-side analysis of the local phase's patch
-boxes (tools/box_model.py): gpurun_out/clouds.npz with quat_k{k} [n, 125, 4]."""
+(all images, float16) for CPU-side analysis of the local phase's patch boxes
+(tools/box_model.py, tools/group_model.py): gpurun_out/clouds.npz with
+quat_k{k} [12500, 125, 4]."""
 import os
 import sys
 
@@ -21,11 +22,11 @@ def main():
     gset = synth.global_sample_set(2000, seed=2)
     px, dat, ctf, sig, *_ = make_stack(N, pf, 24, 1, 12500, dev, seed=5, vol=vol)
     out = {"iCol": px.iCol, "iRow": px.iRow, "order": px.order}
-    sel = torch.arange(0, 12500, 25, device=dev)
-    for k in (0, 1, 3, 6, 9):
+    sel = torch.arange(0, 12500, 1, device=dev)
+    for k in (0, 2, 5, 9):
         e = ex.Expectation(vol, px, gset, n_phase=k, seed=7)
         q = e.run(dat, ctf, sig)[0]
-        out[f"quat_k{k}"] = q[sel].cpu().numpy()
+        out[f"quat_k{k}"] = q[sel].cpu().numpy().astype(np.float16)
         print(k, flush=True)
     np.savez_compressed(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                      "gpurun_out", "clouds.npz"), **out)
