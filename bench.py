@@ -516,17 +516,40 @@ def main():
         extras["insert_images_per_s"] = a.gpus * nI / isec
         hm_bytes = recs[0].hm.F.numel() * 8 + recs[0].hm.T.numel() * 4
         if dist:
-            groups = ex.hemisphere_groups(world)
-            comm = ops.RcclComm.from_group(groups[rank % 2], cdev)
+            # the round end across ranks (thunder_amd.hemisphere): RCCL sum of
+            # each hemisphere's half-maps, reconstruction on the hemisphere
+            # leads, B's map handed to A's lead (xGMI peer transfer), FSC there
+            from thunder_amd import hemisphere as hs
+            re_ = hs.RoundEnd(world, rank, transport="rccl" if backend == "nccl" else "torch",
+                              device=cdev)
             torch.cuda.synchronize()
             dist.barrier()
             t1 = time.perf_counter()
-            comm.allreduce(recs[0].hm)
+            re_.reduce(recs[0].hm)
             torch.cuda.synchronize()
             extras["allreduce_ms"] = (time.perf_counter() - t1) * 1e3
             extras["allreduce_bytes"] = hm_bytes
-            extras["allreduce_ranks_per_hemisphere"] = comm.nranks
-            comm.close()
+            extras["allreduce_ranks_per_hemisphere"] = len([r for r in range(world)
+                                                            if r % 2 == rank % 2])
+            extras["allreduce_transport"] = re_.transport
+            if re_.is_lead:
+                ops.reconstruct(recs[0].hm, N, pf, want_ft=False)   # hipFFT plans (first call)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                mine = ops.reconstruct(recs[0].hm, N, pf)[1]
+                torch.cuda.synchronize()
+                extras["reconstruct_ms_per_halfmap"] = (time.perf_counter() - t1) * 1e3
+                t1 = time.perf_counter()
+                got = re_.exchange(mine)
+                torch.cuda.synchronize()
+                extras["exchange_ms"] = (time.perf_counter() - t1) * 1e3
+                extras["exchange_bytes"] = mine.numel() * 8
+                if got is not None:
+                    fsc = ops.fsc(got[0], got[1], N // 2)
+                    extras["reconstructed_fsc_shells_4_16_32_64"] = [
+                        round(float(fsc[k]), 4) for k in (4, 16, 32, 64) if k < fsc.numel()]
+            dist.barrier()
+            re_.close()
         else:
             extras["allreduce_ms"] = 0.0
             extras["allreduce_note"] = "1 GPU: both hemispheres on one device, no all-reduce"

@@ -434,6 +434,14 @@ int thx_insert2d(float* F, float* T, double* O, int* counter, int vdim, int pf,
                  const float* dat, const float* ctf, const double* rot, const double* trans,
                  const double* offS, const float* w, const int* nc, int nImg, int mReco,
                  const int* iCol, const int* iRow, int nPxl, int idim, thx_stream_t stream);
+/* The 2D insert with CTF search (InsertI2D's cSearch, kernel_CalculateCTF per
+ * sample, gpu/src/cuthunder.cu:3753): sample (l, m) inserts with the CTF of
+ * attr[l] (nImg x 8, as thx_ctf) at defocus factor nD[l*mReco + m]. */
+int thx_insert2d_d(float* F, float* T, double* O, int* counter, int vdim, int pf,
+                   const float* dat, const float* attr, const double* nD, const double* rot,
+                   const double* trans, const double* offS, const float* w, const int* nc,
+                   int nImg, int mReco, const int* iCol, const int* iRow, int nPxl, int idim,
+                   thx_stream_t stream);
 
 /* ------------------------------------------------------------------ f1 ---
  * The reconstruction solve of one half-map, Reconstructor::reconstruct
@@ -595,6 +603,22 @@ int thx_event_pairs_destroy(void* events, int n);
  * Reference-shaped host adapters (host pointers, stateless, synchronous).  *
  * ====================================================================== */
 
+/* The batch adapters (ExpectGlobal3D / 2D, InsertFT*, InsertI2D) deal their
+ * images out over several GPUs in contiguous blocks, one host thread per
+ * device, as cuthunder deals batches round-robin over every visible GPU
+ * (gpu/src/cuthunder.cu:2002-2198, 5570-5826); insert partial half-maps are
+ * summed onto the first device.  The devices (also what thx_getAviDevice
+ * reports to the per-image local path): every visible GPU; or the list in the
+ * environment variable THX_DEVICES ("0,2,5"); THX_DEVICES=local -- device
+ * (local rank % GPU count) from LOCAL_RANK / OMPI_COMM_WORLD_LOCAL_RANK /
+ * MPI_LOCALRANKID / SLURM_LOCALID, one MPI process per GPU without any change
+ * to the caller; THX_DEVICES=current -- the caller's current device.  This
+ * returns the list (devs may be NULL when cap is 0). */
+int thx_adapter_devices(int* devs, int cap, int* n);
+/* hipSetDevice for C++ callers without HIP headers (e.g. before
+ * thx_rccl_comm_init, whose communicator lives on the current device). */
+int thx_set_device(int dev);
+
 /* gpu/interface/Interface.h:199-208 ExpectRotran: traP[nT][npxl] and
  * rotMat[nR][9] from trans[nT*2] and rot[nR*4]. */
 int thx_ExpectRotran(float* traP, const double* trans, const double* rot,
@@ -633,7 +657,7 @@ int thx_ExpectGlobal3D(const float* rotP, const float* traP, const float* datP,
  * (their priors), ExpectLocalPreI3D builds the CTF per defocus sample from
  * devdefO + datShift * npxl, devfreQ, phaseShift, conT, k1, k2, and
  * ExpectLocalM returns wD[mLD]. */
-int thx_getAviDevice(int* gpus, int cap, int* n);                               /* :16 */
+int thx_getAviDevice(int* gpus, int cap, int* n);   /* :16 -- the adapter devices */
 int thx_ExpectPreidx(int gpuIdx, int** deviCol, int** deviRow, const int* iCol,
                      const int* iRow, int npxl);                                  /* :18 */
 int thx_ExpectPrefre(int gpuIdx, float** devfreQ, const float* freQ, int npxl); /* :26 */
@@ -685,15 +709,21 @@ int thx_ExpectGlobal2D(const float* vol, const float* datP, const float* ctfP,
                        const int* iCol, const int* iRow, int nK, int nR, int nT, int pf,
                        int interp, int idim, int vdim, int npxl, int imgNum);
 
-/* gpu/interface/Interface.h:239-265 InsertI2D (no CTF search): F2D[nk
- * images], T2D, O2D[nk*2], counter[nk] read-modify-write; nC[imgNum*mReco]
- * the sample classes, nR / nT[imgNum*mReco*2] (cos, sin) / translations;
- * iCol / iRow the padded pixel set.  The hemisphere reduction is the
- * caller's (thx_halfmap_allreduce). */
-int thx_InsertI2D(float* F2D, float* T2D, double* O2D, int* counter, const float* datP,
-                  const float* ctfP, const float* w, const double* offS, const int* nC,
-                  const double* nR, const double* nT, const int* iCol, const int* iRow,
-                  int nk, int opf, int npxl, int mReco, int idim, int vdim, int imgNum);
+/* gpu/interface/Interface.h:239-265 InsertI2D, argument for argument: F2D[nk
+ * images], T2D, O2D[nk*2], counter[nk] read-modify-write host buffers;
+ * nC[imgNum*mReco] the sample classes, nR / nT[imgNum*mReco*2] (cos, sin) /
+ * translations; iCol / iRow the padded pixel set.  The reference's (hemi,
+ * slav) MPI pair becomes `comm`: the hemisphere's RCCL communicator
+ * (thx_rccl_comm_init; NULL = no reduction).  cSearch: sample (l, m) inserts
+ * with the CTF of ctfaData[l] (CTFAttr, 7 floats) at defocus factor
+ * nD[l*mReco + m] and pixelSize (kernel_CalculateCTF); else ctfP[imgNum*npxl].
+ * sigRcpP is unused (OPTIMISER_RECONSTRUCT_SIGMA_REGULARISE is off). */
+int thx_InsertI2D(float* F2D, float* T2D, double* O2D, int* counter, void* comm,
+                  const float* datP, const float* ctfP, const float* sigRcpP, const float* w,
+                  const double* offS, const int* nC, const double* nR, const double* nT,
+                  const double* nD, const float* ctfaData, const int* iCol, const int* iRow,
+                  float pixelSize, int cSearch, int nk, int opf, int npxl, int mReco, int idim,
+                  int vdim, int imgNum);
 
 /* gpu/interface/Interface.h:294-318 InsertFT (K = 1, cSearch off): F3D
  * [dimSize*2], T3D[dimSize] (real), O3D[3], counter[1] are read-modify-write

@@ -69,3 +69,101 @@ def test_halfmap_allreduce_per_hemisphere(world):
     assert allidx == list(range(100))
     for r in range(world):
         assert all(i % 2 == r % 2 for i in out[r][5])
+
+
+# ---- the bench's N > 1 round end on CPU tensors: shard -> insert -> reduce
+# ---- per hemisphere -> reconstruct on the leads -> hand-over -> FSC on rank 0
+N_RE, PF_RE, NIMG_RE, MRECO_RE = 16, 2, 24, 5
+
+
+def _re_inputs(orc):
+    from stacks import small_stack
+    from thunder_amd import synth
+    s = small_stack(orc, N=N_RE, nImg=NIMG_RE, nR=4, nT=3, seed=12)
+    rng = np.random.default_rng(13)
+    quat = synth.clustered_quaternions(NIMG_RE, MRECO_RE, 5.0, rng)
+    trans = rng.standard_normal((NIMG_RE, MRECO_RE, 2))
+    off = np.zeros((NIMG_RE, 2))
+    w = np.full(NIMG_RE, 1.0 / MRECO_RE, np.float32)
+    return s, quat, trans, off, w
+
+
+def _insert_cpu(orc, s, idx, quat, trans, off, w):
+    vdim = N_RE * PF_RE
+    F, T, O, cnt = orc.insert_batch(vdim, PF_RE, s["dat"][idx], s["ctf"][idx], quat[idx], trans[idx],
+                                    off[idx], w[idx], s["px"], N_RE)
+    shape = (vdim, vdim, vdim // 2 + 1)
+
+    class HM:
+        pass
+    hm = HM()
+    hm.F = torch.from_numpy(F.reshape(shape).copy())
+    hm.T = torch.from_numpy(T.reshape(shape).copy())
+    hm.O = torch.from_numpy(np.asarray(O, np.float64).copy())
+    hm.counter = torch.tensor([cnt], dtype=torch.int32)
+    return hm
+
+
+def _reconstruct_cpu(hm):
+    from oracle import reconstruct as orec
+    m, _, _ = orec.reconstruct(hm.F.numpy(), hm.T.numpy(), N_RE, PF_RE)
+    return torch.from_numpy(np.fft.rfftn(m).astype(np.complex64))
+
+
+def _fsc_cpu(A, B):
+    from oracle import oracle as orc
+    return torch.from_numpy(orc.fsc(A.numpy(), B.numpy(), N_RE, N_RE // 2))
+
+
+def _round_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as orc
+    from thunder_amd.expectation import hemisphere_shard
+    from thunder_amd.hemisphere import RoundEnd, round_end
+    orc.lib()
+    s, quat, trans, off, w = _re_inputs(orc)
+    idx = np.asarray(hemisphere_shard(NIMG_RE, world, rank))
+    hm = _insert_cpu(orc, s, idx, quat, trans, off, w)
+    re = RoundEnd(world, rank, transport="torch")
+    fsc = round_end(hm, re, _reconstruct_cpu, _fsc_cpu)
+    out[rank] = (None if fsc is None else fsc.clone(), int(hm.counter.item()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_round_end_fsc_across_ranks(world, orc):
+    """bench.py's N > 1 round end (thunder_amd.hemisphere.round_end) on CPU
+    tensors over gloo, with the restatement's insert / reconstruction / FSC:
+    rank 0's FSC equals the one-process FSC of the two hemispheres' maps
+    (every image inserted once, in its hemisphere), and each lead's counter
+    is its hemisphere's sample count.  Unmeasured on hardware: the GPU run
+    swaps in the RCCL transport and thx_reconstruct / thx_fsc."""
+    port = free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_round_worker, args=(world, port, out), nprocs=world, join=True)
+    from thunder_amd.expectation import hemisphere_shard
+    s, quat, trans, off, w = _re_inputs(orc)
+    maps, maps1 = [], []
+    for h in (0, 1):
+        # the same partial maps summed in one process (float32 a + b, as the
+        # all-reduce does), and the whole hemisphere inserted in one call
+        parts = [_insert_cpu(orc, s, np.asarray(hemisphere_shard(NIMG_RE, world, r)), quat, trans,
+                             off, w) for r in range(world) if r % 2 == h]
+        hm = parts[0]
+        for p_ in parts[1:]:
+            hm.F += p_.F
+            hm.T += p_.T
+        maps.append(_reconstruct_cpu(hm))
+        maps1.append(_reconstruct_cpu(_insert_cpu(orc, s, np.arange(h, NIMG_RE, 2), quat, trans,
+                                                  off, w)))
+    ref = _fsc_cpu(*maps).numpy()
+    got, cnt0 = out[0]
+    assert got is not None and np.allclose(got.numpy(), ref, rtol=0, atol=1e-9), (got, ref)
+    # against one-call hemisphere inserts: the float32 sum order differs, the
+    # balancing iterations may stop one step apart -- the curve agrees to 1e-2
+    assert np.allclose(got.numpy(), _fsc_cpu(*maps1).numpy(), atol=1e-2)
+    assert all(out[r][0] is None for r in range(1, world))
+    assert cnt0 == (NIMG_RE // 2) * MRECO_RE and out[1][1] == (NIMG_RE // 2) * MRECO_RE

@@ -151,3 +151,93 @@ def test_binned_insert_outside_tile_grid_and_single_sample(orc, stack, rmax_div,
     assert np.max(np.abs(gF - F)) <= 1e-5 * np.max(np.abs(F))
     assert np.max(np.abs(gT - Tm)) <= 1e-5 * np.max(np.abs(Tm))
     assert int(hm.counter.item()) == cnt == nImg * mReco
+
+
+def _host_insert_ftc(s, quat, trans, off, w, nC, mReco):
+    size = (s["vdim"] // 2 + 1) * s["vdim"] ** 2
+    F = np.zeros(2 * size, np.float32)
+    Tm = np.zeros(size, np.float32)
+    O = np.zeros(3)
+    cnt = np.zeros(1, np.int32)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    dat = np.ascontiguousarray(s["dat"]).view(np.float32)
+    ctf = np.ascontiguousarray(s["ctf"])
+    iq, it = np.ascontiguousarray(quat), np.ascontiguousarray(trans)
+    iColP = (s["px"].iCol * s["pf"]).astype(np.int32)
+    iRowP = (s["px"].iRow * s["pf"]).astype(np.int32)
+    st = lib().thx_InsertFTC(P(F), P(Tm), P(O), P(cnt), P(dat), P(ctf), P(off), P(w), P(iq), P(it),
+                             P(nC), P(iColP), P(iRowP), s["pf"], s["px"].n, mReco, s["N"], s["vdim"],
+                             len(nC))
+    assert st == 0, lib().thx_last_error()
+    return F, Tm, O, cnt
+
+
+def test_host_adapters_split_images_over_devices(orc, stack, monkeypatch):
+    """The batch adapters deal contiguous image blocks over the devices of
+    THX_DEVICES, one host thread each, and sum the insert's partial half-maps
+    onto the first device (cuthunder's round-robin over every GPU,
+    gpu/src/cuthunder.cu:2002-2198, 5570-5826).  On a one-GPU box the list
+    "0,0,0" runs that whole path -- three workers, the peer-copy reduction --
+    on one device: the insert matches the restatement and the scan's weights
+    are bit-identical to the one-device call."""
+    s = stack
+    nImg, mReco = 6, 12
+    nC = np.array([3, 0, 12, 7, 1, 12], np.int32)
+    quat, trans, off, w = _samples(nImg, mReco, 33)
+    rF, rT, rO, rc = _oracle_truncated(orc, s, quat, trans, off, w, nC)
+    L = lib()
+    for devs in ("current", "0,0,0", "local"):
+        monkeypatch.setenv("THX_DEVICES", devs)
+        monkeypatch.setenv("LOCAL_RANK", "0")
+        buf = (ctypes.c_int * 8)()
+        n = ctypes.c_int()
+        assert L.thx_adapter_devices(buf, 8, ctypes.byref(n)) == 0
+        assert list(buf[:n.value]) == ([0, 0, 0] if devs == "0,0,0" else [0])
+        F, Tm, O, cnt = _host_insert_ftc(s, quat, trans, off, w, nC, mReco)
+        assert np.max(np.abs(F - rF.view(np.float32))) <= 1e-5 * np.max(np.abs(rF.view(np.float32)))
+        assert np.max(np.abs(Tm - rT)) <= 1e-5 * np.max(np.abs(rT))
+        assert np.allclose(O, rO, rtol=1e-12, atol=1e-12) and int(cnt[0]) == rc
+    # ExpectGlobal3D: per-image work, so the split is exact
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    nR, nT = len(s["quat"]), len(s["trans"])
+    px = ops.PixelSet(s["N"], s["pf"], s["rU"], s["rL"], device=DEV)
+    rotP = ops.project3d(T(s["vol"]), ops.rotmat(T(s["quat"])), px).cpu().numpy()
+    traP = ops.trans_table(T(s["trans"]), px).cpu().numpy()
+    pR, pT = np.full(nR, 1.0 / nR), np.full(nT, 1.0 / nT)
+    outs = {}
+    for devs in ("current", "0,0,0"):
+        monkeypatch.setenv("THX_DEVICES", devs)
+        wC, wR, wT = (np.zeros(nImg * k, np.float32) for k in (1, nR, nT))
+        base = np.zeros(nImg, np.float32)
+        assert L.thx_ExpectGlobal3D(P(rotP.view(np.float32)), P(traP.view(np.float32)),
+                                    P(np.ascontiguousarray(s["dat"]).view(np.float32)),
+                                    P(np.ascontiguousarray(s["ctf"])),
+                                    P(np.ascontiguousarray(s["sig"])), P(wC), P(wR), P(wT), P(pR),
+                                    P(pT), P(base), 0, 1, nR, nT, px.n, nImg) == 0, L.thx_last_error()
+        outs[devs] = (wC, wR, wT, base)
+    for a, b in zip(outs["current"], outs["0,0,0"]):
+        assert np.array_equal(a, b)
+
+
+def test_binned_insert_keeps_small_t_per_voxel(orc, stack):
+    """F and T carry separate fixed-point exponents in the binned deposit:
+    with data 1e6 x the CTF scale and CTF values spanning four decades, every
+    T voxel above 1e-7 of the largest keeps 1e-5 relative accuracy against
+    the restatement (a shared exponent set by |F| would round T to 2^-48 of
+    max |F| ~ the whole T signal)."""
+    s = stack
+    nImg, mReco = 6, 9
+    quat, trans, off, w = _samples(nImg, mReco, 42)
+    rng = np.random.default_rng(43)
+    dat = (s["dat"] * 1e6).astype(np.complex64)
+    ctf = (10.0 ** rng.uniform(-4, 0, s["ctf"].shape) * np.sign(s["ctf"])).astype(np.float32)
+    px = ops.PixelSet(s["N"], s["pf"], s["rU"], s["rL"], device=DEV)
+    hm = ops.HalfMap(s["vdim"], DEV)
+    ops.insert3d(hm, T(dat), T(ctf), T(quat), T(trans), T(off), T(w), px, method="binned")
+    F, Tm, O, cnt = orc.insert_batch(s["vdim"], s["pf"], dat, ctf, quat, trans, off, w, s["px"], s["N"])
+    gT = hm.T.cpu().numpy().reshape(-1)
+    m = Tm > 1e-7 * Tm.max()
+    assert m.sum() > 100
+    assert np.max(np.abs(gT - Tm)[m] / Tm[m]) < 1e-5
+    gF = hm.F.cpu().numpy().reshape(-1)
+    assert np.max(np.abs(gF - F)) <= 1e-5 * np.max(np.abs(F))

@@ -184,9 +184,10 @@ def test_insert2d_matches_restatement(orc, nK):
     hO = np.zeros(2 * nK)
     hc = np.zeros(nK, np.int32)
     ncl = nc if nc is not None else np.zeros((nImg, mReco), np.int32)
-    rc = lib().thx_InsertI2D(P(hF), P(hT), P(hO), P(hc), P(dat.view(np.float32)), P(ctf), P(w),
-                             P(off), P(ncl), P(np.ascontiguousarray(rot)), P(trans),
-                             P(px.iColPad), P(px.iRowPad), nK, pf, px.n, mReco, N, vdim, nImg)
+    rc = lib().thx_InsertI2D(P(hF), P(hT), P(hO), P(hc), None, P(dat.view(np.float32)), P(ctf),
+                             None, P(w), P(off), P(ncl), P(np.ascontiguousarray(rot)), P(trans),
+                             None, None, P(px.iColPad), P(px.iRowPad), 0.0, 0, nK, pf, px.n,
+                             mReco, N, vdim, nImg)
     assert rc == 0, lib().thx_last_error()
     assert np.max(np.abs(hF.view(np.complex64) - F)) <= 1e-5 * np.abs(F).max()
     assert np.array_equal(hc, cnt.astype(np.int32))
@@ -362,3 +363,60 @@ def test_c1_shape_phase_and_insert(orc):
     assert np.max(np.abs(hm.F.cpu().numpy().reshape(-1) - F)) <= 1e-5 * np.abs(F).max()
     assert np.max(np.abs(hm.T.cpu().numpy().reshape(-1) - Tm)) <= 1e-5 * np.abs(Tm).max()
     assert np.array_equal(hm.counter.cpu().numpy(), cnt.astype(np.int32))
+
+
+def test_insert_i2d_ctf_search_and_devices(orc, monkeypatch):
+    """thx_InsertI2D with cSearch (Interface.h:239-265's argument list): every
+    sample inserts with its own CTF, CTFAttr at defocus factor nD (CTF.cpp at
+    (dU d, dV d)), per-sample classes, read-modify-write of the caller's
+    buffers -- against the restatement inserting sample by sample with
+    orc.ctf; once on the current device and once dealt over THX_DEVICES
+    "0,0" (two workers, the peer-copy reduction)."""
+    N, pf, nK = 32, 2, 3
+    vdim = N * pf
+    px = orc.pixel_set(N, pf, N // 2 - 2, 0)
+    rng = np.random.default_rng(17)
+    nImg, mReco = 5, 4
+    dat = (rng.standard_normal((nImg, px.n)) + 1j * rng.standard_normal((nImg, px.n))).astype(np.complex64)
+    rot = _rot(rng.uniform(0, 2 * np.pi, (nImg, mReco)))
+    trans = rng.standard_normal((nImg, mReco, 2))
+    off = rng.standard_normal((nImg, 2)) * 0.2
+    w = rng.uniform(0.1, 0.3, nImg).astype(np.float32)
+    nc = rng.integers(0, nK, (nImg, mReco)).astype(np.int32)
+    nD = rng.uniform(0.97, 1.03, (nImg, mReco))
+    pixel = 1.32
+    # CTFAttr: voltage, defocusU, defocusV, defocusTheta, Cs, amplitudeContrast, phaseShift
+    ca = np.stack([np.full(nImg, 300e3), rng.uniform(1.5e4, 3e4, nImg), rng.uniform(1.5e4, 3e4, nImg),
+                   rng.uniform(0, np.pi, nImg), np.full(nImg, 2.7e7), np.full(nImg, 0.1),
+                   np.zeros(nImg)], 1).astype(np.float32)
+    size = (vdim // 2 + 1) * vdim
+    rF = np.zeros(nK * size, np.complex64)
+    rT = np.zeros(nK * size, np.float32)
+    rO = np.zeros(2 * nK)
+    rc = np.zeros(nK, np.int64)
+    for l in range(nImg):
+        for m in range(mReco):
+            a = ca[l]
+            c = orc.ctf(px, (pixel, a[0], a[1] * nD[l, m], a[2] * nD[l, m], a[3], a[4], a[5], a[6]), N)
+            F, Tm, O, cnt = orc.insert2d_batch(vdim, pf, dat[l:l + 1], c[None], rot[l:l + 1, m:m + 1],
+                                               trans[l:l + 1, m:m + 1], off[l:l + 1], w[l:l + 1],
+                                               nc[l:l + 1, m:m + 1].copy(), px, N, nK=nK)
+            rF += F.reshape(-1)
+            rT += Tm.reshape(-1)
+            rO += O.reshape(-1)
+            rc += np.asarray(cnt).reshape(-1)
+    for devs in ("current", "0,0"):
+        monkeypatch.setenv("THX_DEVICES", devs)
+        hF = np.zeros(2 * nK * size, np.float32)
+        hT = np.zeros(nK * size, np.float32)
+        hO = np.zeros(2 * nK)
+        hc = np.zeros(nK, np.int32)
+        rc_ = lib().thx_InsertI2D(P(hF), P(hT), P(hO), P(hc), None, P(dat.view(np.float32)), None,
+                                  None, P(w), P(off), P(nc), P(np.ascontiguousarray(rot)),
+                                  P(trans), P(nD), P(ca), P(px.iColPad), P(px.iRowPad), pixel, 1,
+                                  nK, pf, px.n, mReco, N, vdim, nImg)
+        assert rc_ == 0, lib().thx_last_error()
+        assert np.max(np.abs(hF.view(np.complex64) - rF)) <= 1e-5 * np.abs(rF).max()
+        assert np.max(np.abs(hT - rT)) <= 1e-5 * np.abs(rT).max()
+        assert np.allclose(hO, rO, rtol=1e-12, atol=1e-12)
+        assert np.array_equal(hc, rc.astype(np.int32))

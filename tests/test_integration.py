@@ -33,7 +33,8 @@ def test_integration_blocks_present():
     for fn in ("getAviDevice", "ExpectRotran", "ExpectProject", "ExpectGlobal3D", "ExpectPreidx",
                "ExpectPrefre", "ExpectLocalIn", "ExpectLocalV3D", "ExpectLocalP",
                "ExpectLocalHostA", "ExpectLocalRTD", "ExpectLocalPreI3D", "ExpectLocalM",
-               "ExpectLocalHostF", "ExpectLocalFin", "ExpectFreeIdx", "InsertFT"):
+               "ExpectLocalHostF", "ExpectLocalFin", "ExpectFreeIdx", "InsertFT",
+               "ExpectGlobal2D", "ExpectLocalV2D", "ExpectLocalPreI2D", "InsertI2D"):
         assert re.search(rf"\bvoid {fn}\(", iface), fn
     assert "thx_tex_create" in handles and "thx_calpoint_create" in handles
 
@@ -44,9 +45,12 @@ def test_forwards_compile_and_link(tmp_path):
     lib = build.build()
     iface, handles = blocks()
     src = tmp_path / "Interface_thx.cpp"
-    src.write_text('#include "thunder_restated.h"\n' + iface + "\n" + handles)
+    # the reference's prototypes first: -Werror=missing-declarations turns any
+    # forward whose signature differs from Interface.h's into a build error
+    src.write_text('#include "interface_restated.h"\n' + iface + "\n" + handles)
     out = tmp_path / "libinterface_thx.so"
     cmd = ["g++", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Werror", "-Wno-unused-parameter",
+           "-Werror=missing-declarations",
            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "tests", "integration"),
            "-I", MPI_INC, str(src), "-o", str(out), "-Wl,--no-undefined",
            "-L", os.path.dirname(lib), "-lthunder_amd", os.path.join(MPI_LIB, "libmpi.so"),
@@ -56,5 +60,21 @@ def test_forwards_compile_and_link(tmp_path):
     nm = subprocess.run(["nm", "-D", "--defined-only", "-C", str(out)], capture_output=True,
                         text=True).stdout
     for sig in ("ExpectLocalM(int, int, ManagedCalPoint*", "InsertFT(Volume&, Volume&, double*, int*",
-                "ManagedCalPoint::Init(int, int, int, int, int, int, int)", "getAviDevice("):
-        assert sig in nm, sig
+                "ManagedCalPoint::Init(int, int, int, int, int, int, int)", "getAviDevice(",
+                "InsertI2D(Complex*, float*, double*, int*, ompi_communicator_t*&",
+                "ExpectGlobal2D(Complex*, Complex*, float*"):
+        assert sig.split("ompi")[0] in nm, sig
+
+
+def test_drifted_forward_fails_to_compile(tmp_path):
+    """The guard itself: a forward with one argument type changed from
+    Interface.h's declaration does not compile."""
+    if not (os.path.exists(os.path.join(MPI_INC, "mpi.h")) and shutil.which("g++")):
+        pytest.skip("needs g++ and MPICH's mpi.h")
+    src = tmp_path / "drift.cpp"
+    src.write_text('#include "interface_restated.h"\n'
+                   "void ExpectFreeIdx(int gpuIdx, int** deviCol, long** deviRow) {}\n")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Werror=missing-declarations",
+                        "-I", os.path.join(ROOT, "tests", "integration"), "-I", MPI_INC, str(src)],
+                       capture_output=True, text=True)
+    assert r.returncode != 0 and "missing-declarations" in r.stderr

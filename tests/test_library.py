@@ -147,8 +147,9 @@ def test_round2_entry_points_validate_without_gpu(L):
     tr = np.zeros(2 * nImg * mReco)
     ic = np.array([2, 4, 6, 8], np.int32)
     ir = np.zeros(4, np.int32)
-    assert L.thx_InsertI2D(P(F), P(T), P(O), P(cnt), P(dat), P(ctf), P(w), P(off), P(nc), P(rot),
-                           P(tr), P(ic), P(ir), nk, 2, npxl, mReco, 32, 64, nImg) == bad
+    assert L.thx_InsertI2D(P(F), P(T), P(O), P(cnt), None, P(dat), P(ctf), None, P(w), P(off),
+                           P(nc), P(rot), P(tr), None, None, P(ic), P(ir), 0.0, 0, nk, 2, npxl,
+                           mReco, 32, 64, nImg) == bad
     assert b"class index" in L.thx_last_error()
     # ExpectGlobal2D supports the reference's linear interpolation only
     assert L.thx_ExpectGlobal2D(P(F), P(dat), P(ctf), P(ctf), P(tr), P(w), P(w), P(w), P(off),

@@ -80,8 +80,13 @@ SIGNATURES = {
                               _c_int, _p, _p, _c_int, _c_int, _p]),
     "thx_ExpectGlobal2D": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
                                     _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int]),
-    "thx_InsertI2D": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
-                               _c_int, _c_int, _c_int, _c_int, _c_int]),
+    "thx_InsertI2D": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                               _c_float, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
+                               _c_int]),
+    "thx_insert2d_d": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _p, _p,
+                                _c_int, _c_int, _p, _p, _c_int, _c_int, _p]),
+    "thx_adapter_devices": (_c_int, [_p, _c_int, _p]),
+    "thx_set_device": (_c_int, [_c_int]),
     "thx_reconstruct_workspace": (_c_size, [_c_int, _c_int]),
     "thx_reconstruct": (_c_int, [_p, _p, _c_int, _c_int, _c_float, _c_float, _c_int, _c_int, _c_int, _p,
                                  _c_int, _c_int, _p, _p, _p, _p, _p, _c_size, _p]),

@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <vector>
 
 #include "../../include/thunder_amd.h"
 
@@ -52,6 +53,13 @@ inline int set_max_lds(const void* fn, int bytes, std::atomic<unsigned>& done)
     done.fetch_or(bit, std::memory_order_release);
     return THX_OK;
 }
+
+// the devices the host adapters use and getAviDevice reports (interface.hip)
+int adapter_devices(std::vector<int>& devs);
+
+// the RCCL half-map all-reduce with oDim doubles of O per class (halfmap.hip)
+int halfmap_allreduce_impl(void* comm, float* F, float* T, double* O, int oDim, int* counter,
+                           long long dimSize, int nK, hipStream_t s);
 
 inline hipStream_t as_stream(thx_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -83,21 +83,31 @@ static int group_end(ncclResult_t first, const char* what)
     return THX_OK;
 }
 
-extern "C" int thx_halfmap_allreduce(void* comm, float* F, float* T, double* O, int* counter,
-                                     long long dimSize, int nK, thx_stream_t stream)
+namespace thx {
+// oDim doubles of O per class (3 in 3D, 2 for the 2D InsertI2D's O2D)
+int halfmap_allreduce_impl(void* comm, float* F, float* T, double* O, int oDim, int* counter,
+                           long long dimSize, int nK, hipStream_t s)
 {
-    THX_CHECK_ARG(comm && F && T && dimSize > 0 && nK >= 1, "thx_halfmap_allreduce: bad arguments");
+    THX_CHECK_ARG(comm && F && T && dimSize > 0 && nK >= 1 && oDim > 0,
+                  "thx_halfmap_allreduce: bad arguments");
     ncclComm_t c = static_cast<ncclComm_t>(comm);
-    hipStream_t s = thx::as_stream(stream);
     const size_t n = (size_t)dimSize * nK;
     THX_NCCL(ncclGroupStart());
     ncclResult_t first = ncclSuccess;
     const char* what = "";
     THX_NCCL_GROUPED(ncclAllReduce(F, F, 2 * n, ncclFloat32, ncclSum, c, s));
     THX_NCCL_GROUPED(ncclAllReduce(T, T, n, ncclFloat32, ncclSum, c, s));
-    if (O) THX_NCCL_GROUPED(ncclAllReduce(O, O, 3 * (size_t)nK, ncclFloat64, ncclSum, c, s));
+    if (O) THX_NCCL_GROUPED(ncclAllReduce(O, O, (size_t)oDim * nK, ncclFloat64, ncclSum, c, s));
     if (counter) THX_NCCL_GROUPED(ncclAllReduce(counter, counter, nK, ncclInt32, ncclSum, c, s));
     return group_end(first, what);
+}
+}  // namespace thx
+
+extern "C" int thx_halfmap_allreduce(void* comm, float* F, float* T, double* O, int* counter,
+                                     long long dimSize, int nK, thx_stream_t stream)
+{
+    return thx::halfmap_allreduce_impl(comm, F, T, O, 3, counter, dimSize, nK,
+                                       thx::as_stream(stream));
 }
 
 // The half-map hand-over of Model::compareTwoHemispheres (src/Model.cpp:

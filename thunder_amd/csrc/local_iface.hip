@@ -97,10 +97,12 @@ __global__ void __launch_bounds__(256) k_calpoint_ctf(const float* __restrict__ 
 extern "C" int thx_getAviDevice(int* gpus, int cap, int* n)
 {
     THX_CHECK_ARG(n && (cap == 0 || gpus), "thx_getAviDevice: bad arguments");
-    int c = 0;
-    THX_HIP(hipGetDeviceCount(&c));
-    for (int i = 0; i < c && i < cap; i++) gpus[i] = i;
-    *n = c;
+    // the adapter devices (every GPU, or THX_DEVICES: one per process with "local")
+    std::vector<int> d;
+    const int st = thx::adapter_devices(d);
+    if (st != THX_OK) return st;
+    for (int i = 0; i < (int)d.size() && i < cap; i++) gpus[i] = d[i];
+    *n = (int)d.size();
     return THX_OK;
 }
 

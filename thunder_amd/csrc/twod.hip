@@ -197,7 +197,9 @@ __global__ void __launch_bounds__(256) k_insert2d(float2* __restrict__ F, float*
                                                   const float* __restrict__ w,
                                                   const int* __restrict__ nc, int mReco,
                                                   const int* __restrict__ iCol,
-                                                  const int* __restrict__ iRow, int nPxl, int idim)
+                                                  const int* __restrict__ iRow, int nPxl, int idim,
+                                                  const float* __restrict__ attr,
+                                                  const double* __restrict__ nD)
 {
     const int m = blockIdx.y, l = blockIdx.z;
     const size_t sIdx = (size_t)l * mReco + m;
@@ -217,11 +219,15 @@ __global__ void __launch_bounds__(256) k_insert2d(float2* __restrict__ F, float*
         atomicAdd(counter + k, 1);
     }
     const float2* D = dat + (size_t)l * nPxl;
-    const float* C = ctf + (size_t)l * nPxl;
+    const float* C = attr ? nullptr : ctf + (size_t)l * nPxl;
+    // CTF search (InsertI2D with cSearch): the sample's own CTF at (dU d, dV d)
+    // (kernel_CalculateCTF, gpu/src/cuthunder.cu:3753; src/Optimiser.cpp:7101-7120)
+    const float* A = attr ? attr + 8 * (size_t)l : nullptr;
+    const float dU = A ? (float)(A[2] * nD[sIdx]) : 0.f, dV = A ? (float)(A[3] * nD[sIdx]) : 0.f;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nPxl; i += gridDim.x * blockDim.x) {
         const int ic = iCol[i], ir = iRow[i];
         const float2 src = cmul(D[i], phase_shift(ic, ir, rCol, rRow));
-        const float c = C[i];
+        const float c = A ? ctf_at(A, dU, dV, ic, ir, idim) : C[i];
         const float vr = (src.x * c) * wl, vi = (src.y * c) * wl;
         const float tv = (float)((double)c * c) * wl;
         float x, y;
@@ -286,23 +292,46 @@ extern "C" int thx_local_phase2d(const float* vol, int vdim, int pf, const int* 
     return thx::launch_local_weights(d, nR, nT, pC, pR, pT, wC, wR, wT, baseL, nImg, s);
 }
 
+static int insert2d_impl(float* F, float* T, double* O, int* counter, int vdim, int pf,
+                         const float* dat, const float* ctf, const float* attr, const double* nD,
+                         const double* rot, const double* trans, const double* offS,
+                         const float* w, const int* nc, int nImg, int mReco, const int* iCol,
+                         const int* iRow, int nPxl, int idim, thx_stream_t stream)
+{
+    THX_CHECK_ARG(vdim > 0 && vdim % 2 == 0 && pf > 0 && nImg >= 0 && mReco >= 0 && nPxl >= 0 &&
+                      idim > 0 && nImg <= 65535 && mReco <= 65535,
+                  "thx_insert2d: bad sizes");
+    if (nImg == 0 || mReco == 0 || nPxl == 0) return THX_OK;
+    THX_CHECK_ARG(F && T && O && counter && dat && (ctf || (attr && nD)) && rot && trans && offS &&
+                      w && iCol && iRow,
+                  "thx_insert2d: null argument");
+    const unsigned gx = thx::cdiv(nPxl, 256) > 8 ? 8 : thx::cdiv(nPxl, 256);
+    hipLaunchKernelGGL(k_insert2d, dim3(gx, mReco, nImg), dim3(256), 0, thx::as_stream(stream),
+                       reinterpret_cast<float2*>(F), T, O, counter, vdim, pf,
+                       reinterpret_cast<const float2*>(dat), ctf, rot, trans, offS, w, nc, mReco,
+                       iCol, iRow, nPxl, idim, attr, nD);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 extern "C" int thx_insert2d(float* F, float* T, double* O, int* counter, int vdim, int pf,
                             const float* dat, const float* ctf, const double* rot,
                             const double* trans, const double* offS, const float* w,
                             const int* nc, int nImg, int mReco, const int* iCol, const int* iRow,
                             int nPxl, int idim, thx_stream_t stream)
 {
-    THX_CHECK_ARG(vdim > 0 && vdim % 2 == 0 && pf > 0 && nImg >= 0 && mReco >= 0 && nPxl >= 0 &&
-                      idim > 0 && nImg <= 65535 && mReco <= 65535,
-                  "thx_insert2d: bad sizes");
-    if (nImg == 0 || mReco == 0 || nPxl == 0) return THX_OK;
-    THX_CHECK_ARG(F && T && O && counter && dat && ctf && rot && trans && offS && w && iCol && iRow,
-                  "thx_insert2d: null argument");
-    const unsigned gx = thx::cdiv(nPxl, 256) > 8 ? 8 : thx::cdiv(nPxl, 256);
-    hipLaunchKernelGGL(k_insert2d, dim3(gx, mReco, nImg), dim3(256), 0, thx::as_stream(stream),
-                       reinterpret_cast<float2*>(F), T, O, counter, vdim, pf,
-                       reinterpret_cast<const float2*>(dat), ctf, rot, trans, offS, w, nc, mReco,
-                       iCol, iRow, nPxl, idim);
-    THX_LAUNCH_CHECK();
-    return THX_OK;
+    THX_CHECK_ARG(ctf || nImg == 0, "thx_insert2d: null ctf");
+    return insert2d_impl(F, T, O, counter, vdim, pf, dat, ctf, nullptr, nullptr, rot, trans, offS,
+                         w, nc, nImg, mReco, iCol, iRow, nPxl, idim, stream);
+}
+
+extern "C" int thx_insert2d_d(float* F, float* T, double* O, int* counter, int vdim, int pf,
+                              const float* dat, const float* attr, const double* nD,
+                              const double* rot, const double* trans, const double* offS,
+                              const float* w, const int* nc, int nImg, int mReco, const int* iCol,
+                              const int* iRow, int nPxl, int idim, thx_stream_t stream)
+{
+    THX_CHECK_ARG((attr && nD) || nImg == 0, "thx_insert2d_d: null attr / nD");
+    return insert2d_impl(F, T, O, counter, vdim, pf, dat, nullptr, attr, nD, rot, trans, offS, w,
+                         nc, nImg, mReco, iCol, iRow, nPxl, idim, stream);
 }

@@ -525,6 +525,16 @@ class RcclComm:
               "thx_halfmap_allreduce")
         return hm
 
+    def sendrecv(self, send=None, peer_send=-1, recv=None, peer_recv=-1, n_recv=0):
+        """thx_halfmap_sendrecv: float32 device tensors, ranks of this communicator."""
+        ns = send.numel() if send is not None else 0
+        nr = n_recv if recv is not None else 0
+        if recv is not None and recv.numel() < nr:
+            raise ValueError("recv buffer smaller than n_recv")
+        dev = (send if send is not None else recv).device
+        check(lib().thx_halfmap_sendrecv(self.comm, _ptr(send), ns, peer_send, _ptr(recv), nr,
+                                         peer_recv, _stream(dev)), "thx_halfmap_sendrecv")
+
     def close(self):
         if self.comm:
             check(lib().thx_rccl_comm_destroy(self.comm), "thx_rccl_comm_destroy")
