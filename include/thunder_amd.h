@@ -443,6 +443,36 @@ int thx_insert2d_d(float* F, float* T, double* O, int* counter, int vdim, int pf
                    int nImg, int mReco, const int* iCol, const int* iRow, int nPxl, int idim,
                    thx_stream_t stream);
 
+/* ------------------------------------------------------------------ f2 ---
+ * Image preprocessing of Optimiser::initImg (src/Optimiser.cpp:4608-5024),
+ * the re-mask of reMaskImg / ReMask (:6093-6190; gpu/src/cuthunder.cu:9406)
+ * and GCTFinit's CTF images (cuthunder.cu:9641), for a device stack of nImg
+ * real-space idim x idim float images.
+ * thx_img_stats -- substractBgImg + the per-image terms of statImg: img in
+ *   (centred = 1: as stored in an MRC stack; 0: the reference's corner-origin
+ *   Image layout), out (corner origin) = (x - bgMean) / bgSd over the pixels
+ *   outside rMask (pixels); stats[nImg][5] = {bgMean, bgSd, bgStddev(0)
+ *   after, stddev(0) after, mean inside rMask after}.  stdN = the mean of
+ *   stats[.][2] over the hemisphere's images (the caller's all-reduce).
+ * thx_img_finish -- maskImg + normaliseImg + fwImg: ori (optional) = img /
+ *   stdN; img = softMask(img, rMask, edge = EDGE_WIDTH_RL 6) / stdN with a zero
+ *   background (zeroMask) or N(0, stdN) noise; imgFT / oriFT = forward r2c
+ *   FFTs (unnormalised), [nImg][idim][idim/2+1] Complex.  img is overwritten.
+ * thx_remask -- imgFT in place: backward FFT / idim^2, x soft mask, forward;
+ *   rl: nImg x idim^2 floats of scratch.
+ * thx_img_gather -- allocPreCal's datP[l][i] = imgFT_l[iPxl[i]] (a1's iPxl).
+ * thx_ctf_image -- ctf[nImg][idim][idim/2+1] over the whole half-complex grid. */
+int thx_img_stats(const float* img, int centred, int nImg, int idim, float rMask, float* out,
+                  float* stats, thx_stream_t stream);
+int thx_img_finish(float* img, int nImg, int idim, float rMask, float edge, int zeroMask,
+                   float stdN, unsigned long long seed, float* imgFT, float* ori, float* oriFT,
+                   thx_stream_t stream);
+int thx_remask(float* imgFT, int nImg, int idim, float rMask, float edge, float* rl,
+               thx_stream_t stream);
+int thx_img_gather(const float* imgFT, int nImg, int idim, const int* iPxl, int nPxl,
+                   float* datP, thx_stream_t stream);
+int thx_ctf_image(const float* attr, int nImg, int idim, float* ctf, thx_stream_t stream);
+
 /* ------------------------------------------------------------------ f1 ---
  * The reconstruction solve of one half-map, Reconstructor::reconstruct
  * (src/Reconstructor.cpp:1129-1831; GPU twin reconstructG :1835), 3D,

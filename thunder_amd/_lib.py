@@ -87,6 +87,12 @@ SIGNATURES = {
                                 _c_int, _c_int, _p, _p, _c_int, _c_int, _p]),
     "thx_adapter_devices": (_c_int, [_p, _c_int, _p]),
     "thx_set_device": (_c_int, [_c_int]),
+    "thx_img_stats": (_c_int, [_p, _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
+    "thx_img_finish": (_c_int, [_p, _c_int, _c_int, _c_float, _c_float, _c_int, _c_float,
+                                ctypes.c_ulonglong, _p, _p, _p, _p]),
+    "thx_remask": (_c_int, [_p, _c_int, _c_int, _c_float, _c_float, _p, _p]),
+    "thx_img_gather": (_c_int, [_p, _c_int, _c_int, _p, _c_int, _p, _p]),
+    "thx_ctf_image": (_c_int, [_p, _c_int, _c_int, _p, _p]),
     "thx_reconstruct_workspace": (_c_size, [_c_int, _c_int]),
     "thx_reconstruct": (_c_int, [_p, _p, _c_int, _c_int, _c_float, _c_float, _c_int, _c_int, _c_int, _p,
                                  _c_int, _c_int, _p, _p, _p, _p, _p, _c_size, _p]),

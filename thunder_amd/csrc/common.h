@@ -259,6 +259,48 @@ THX_DEV void scatter_ft(float2* __restrict__ F, float* __restrict__ T, int vdim,
         }
 }
 
+// Philox-4x32-10 counter RNG (reproducible per (seed, counter); the reference
+// draws from an urandom-seeded GSL mt19937, src/Functions/Random.cpp:51-73)
+struct Philox {
+    uint4 ctr;
+    uint2 key;
+    THX_DEV Philox(uint64_t seed, uint32_t a, uint32_t b, uint32_t c)
+    {
+        key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+        ctr = make_uint4(a, b, c, 0);
+    }
+    THX_DEV uint4 next()
+    {
+        uint4 x = ctr;
+        uint2 k = key;
+#pragma unroll
+        for (int r = 0; r < 10; r++) {
+            const uint64_t p0 = (uint64_t)0xD2511F53u * x.x;
+            const uint64_t p1 = (uint64_t)0xCD9E8D57u * x.z;
+            x = make_uint4((uint32_t)(p1 >> 32) ^ x.y ^ k.x, (uint32_t)p1,
+                           (uint32_t)(p0 >> 32) ^ x.w ^ k.y, (uint32_t)p0);
+            k.x += 0x9E3779B9u;
+            k.y += 0xBB67AE85u;
+        }
+        ctr.w++;
+        return x;
+    }
+    THX_DEV double uniform()   // (0, 1)
+    {
+        const uint4 v = next();
+        const uint64_t m = ((uint64_t)v.x << 21) ^ (uint64_t)v.y;
+        return ((double)(m & ((1ull << 53) - 1)) + 0.5) * (1.0 / 9007199254740992.0);
+    }
+    THX_DEV double2 gauss2()   // Box-Muller
+    {
+        const double u1 = uniform(), u2 = uniform();
+        const double r = sqrt(-2.0 * log(u1));
+        double s, c;
+        sincos(2.0 * M_PI * u2, &s, &c);
+        return make_double2(r * c, r * s);
+    }
+};
+
 // 2^56 fixed point for LDS sums of a few values in [0, 8): ds_add_u64 retires
 // a wave-instruction in 7-12 CU cycles where ds_add_f32 takes ~193 on gfx950
 // (tools/probes/lds_atomic.hip); the integer sum is exact and order-free.

@@ -40,47 +40,6 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
 
 namespace {
 
-// ------------------------------------------------------------- Philox RNG
-struct Philox {
-    uint4 ctr;
-    uint2 key;
-    THX_DEV Philox(uint64_t seed, uint32_t a, uint32_t b, uint32_t c)
-    {
-        key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-        ctr = make_uint4(a, b, c, 0);
-    }
-    THX_DEV uint4 next()
-    {
-        uint4 x = ctr;
-        uint2 k = key;
-#pragma unroll
-        for (int r = 0; r < 10; r++) {
-            const uint64_t p0 = (uint64_t)0xD2511F53u * x.x;
-            const uint64_t p1 = (uint64_t)0xCD9E8D57u * x.z;
-            x = make_uint4((uint32_t)(p1 >> 32) ^ x.y ^ k.x, (uint32_t)p1,
-                           (uint32_t)(p0 >> 32) ^ x.w ^ k.y, (uint32_t)p0);
-            k.x += 0x9E3779B9u;
-            k.y += 0xBB67AE85u;
-        }
-        ctr.w++;
-        return x;
-    }
-    THX_DEV double uniform()   // (0, 1)
-    {
-        const uint4 v = next();
-        const uint64_t m = ((uint64_t)v.x << 21) ^ (uint64_t)v.y;
-        return ((double)(m & ((1ull << 53) - 1)) + 0.5) * (1.0 / 9007199254740992.0);
-    }
-    THX_DEV double2 gauss2()   // Box-Muller
-    {
-        const double u1 = uniform(), u2 = uniform();
-        const double r = sqrt(-2.0 * log(u1));
-        double s, c;
-        sincos(2.0 * M_PI * u2, &s, &c);
-        return make_double2(r * c, r * s);
-    }
-};
-
 THX_DEV void qmul(const double* a, const double* b, double* o)
 {
     // quaternion_mul (src/Geometry/Euler.cpp), Hamilton product

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include <map>
+#include <memory>
 #include <mutex>
 #include <tuple>
 
@@ -50,6 +51,8 @@
 namespace {
 
 constexpr int TAB_N = 100000;   // _kernelRL.init(MKB_RL_R2, 0, 1, 1e5) (src/Reconstructor.cpp:77-88)
+
+inline unsigned cdiv_i(int a, int b) { return (unsigned)((a + b - 1) / b); }
 
 // k of a half-complex index: i in [0, vdim/2], j, k wrapped to [-vdim/2, vdim/2)
 THX_DEV void ft_coord(long q, int vdim, int& i, int& j, int& k)
@@ -110,7 +113,7 @@ __global__ void k_w_from_t(float* __restrict__ W, const float* __restrict__ T, i
     }
 }
 
-// C = T W (T real, so C is real)
+// C = T W (T real, so C is real): the first iteration's C
 __global__ void k_c_from_tw(float2* __restrict__ C, const float* __restrict__ T,
                             const float* __restrict__ W, long n)
 {
@@ -118,41 +121,48 @@ __global__ void k_c_from_tw(float2* __restrict__ C, const float* __restrict__ T,
 }
 
 // convoluteC in real space: c(i,j,k) * kernelRL(QUAD_3 / (N pf)^2) / nf,
-// scaled by 1/size of FFT::bw
-__global__ void k_kernel_mul(float* __restrict__ c, int vdim, const float* __restrict__ tab,
-                             float nf, float scale)
+// scaled by 1/size of FFT::bw.  Grid: x over rows' i, y = j, z = k (no
+// per-element index decode).
+__global__ void __launch_bounds__(256) k_kernel_mul(float* __restrict__ c, int vdim,
+                                                    const float* __restrict__ tab, float nf,
+                                                    float scale)
 {
-    const long n = (long)vdim * vdim * vdim;
+    const int j = blockIdx.y, k = blockIdx.z;
+    const int jj = j >= vdim / 2 ? j - vdim : j, kk = k >= vdim / 2 ? k - vdim : k;
     const float inv = 1.f / ((float)vdim * (float)vdim);
-    GRID_STRIDE(q, n)
-    {
-        int i = (int)(q % vdim);
-        const long r = q / vdim;
-        int j = (int)(r % vdim), k = (int)(r / vdim);
-        if (i >= vdim / 2) i -= vdim;
-        if (j >= vdim / 2) j -= vdim;
-        if (k >= vdim / 2) k -= vdim;
-        const float x = (float)(i * i + j * j + k * k) * inv;
+    const int jk2 = jj * jj + kk * kk;
+    float* row = c + ((size_t)k * vdim + j) * vdim;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < vdim; i += gridDim.x * blockDim.x) {
+        const int ii = i >= vdim / 2 ? i - vdim : i;
+        const float x = (float)(ii * ii + jk2) * inv;
         const int t = min(TAB_N, (int)rintf(x / 1e-5f));          // TabFunction: _tab[AROUND((x - a) / s)]
-        c[q] = (c[q] * scale) * tab[t] / nf;
+        row[i] = (row[i] * scale) * tab[t] / nf;
     }
 }
 
-// W /= max(|C|, 1e-6) inside the sphere; max | |C| - 1 | over the sphere
-__global__ void __launch_bounds__(256) k_update_w(float* __restrict__ W, const float2* __restrict__ C,
-                                                  int vdim, long r2, unsigned* __restrict__ diffBits)
+// W /= max(|C|, 1e-6) inside the sphere; max | |C| - 1 | over the sphere;
+// fused with the next iteration's C = T W (the same pass over W)
+__global__ void __launch_bounds__(256) k_update_w(float* __restrict__ W, float2* __restrict__ C,
+                                                  const float* __restrict__ T, int vdim, long r2,
+                                                  unsigned* __restrict__ diffBits)
 {
-    const long n = (long)(vdim / 2 + 1) * vdim * vdim;
+    const int nc = vdim / 2 + 1;
+    const int j = blockIdx.y, k = blockIdx.z;
+    const int jj = j >= vdim / 2 ? j - vdim : j, kk = k >= vdim / 2 ? k - vdim : k;
+    const long jk2 = (long)jj * jj + (long)kk * kk;
+    const size_t row = ((size_t)k * vdim + j) * nc;
     float dmax = 0.f;
-    GRID_STRIDE(q, n)
-    {
-        int i, j, k;
-        ft_coord(q, vdim, i, j, k);
-        if ((long)i * i + (long)j * j + (long)k * k >= r2) continue;
-        const float2 c = C[q];
-        const float a = sqrtf(c.x * c.x + c.y * c.y);
-        W[q] = W[q] / fmaxf(a, 1e-6f);
-        dmax = fmaxf(dmax, fabsf(a - 1.f));
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nc; i += gridDim.x * blockDim.x) {
+        const size_t q = row + i;
+        float w = W[q];
+        if ((long)i * i + jk2 < r2) {
+            const float2 c = C[q];
+            const float a = sqrtf(c.x * c.x + c.y * c.y);
+            w = w / fmaxf(a, 1e-6f);
+            W[q] = w;
+            dmax = fmaxf(dmax, fabsf(a - 1.f));
+        }
+        C[q] = make_float2(T[q] * w, 0.f);
     }
     dmax = wave_max(dmax);
     __shared__ float s[4];
@@ -160,7 +170,7 @@ __global__ void __launch_bounds__(256) k_update_w(float* __restrict__ W, const f
     __syncthreads();
     if (threadIdx.x == 0) {
         const float m = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
-        atomicMax(diffBits, __float_as_uint(m));   // non-negative floats order as their bits
+        if (m > 0.f) atomicMax(diffBits, __float_as_uint(m));   // non-negative floats order as their bits
     }
 }
 
@@ -262,12 +272,21 @@ int make_plans(Plans& p, int vdim, int N)
     return THX_OK;
 }
 
-// Plans per (device, vdim, N), made once: creating a 512^3 hipFFT plan costs
-// hundreds of ms, the transforms themselves ~0.6 ms.  Calls using the same
-// plans are serialised (the work area and stream are bound per call).
+// Plans per (device, vdim, N, stream), made once: creating a 512^3 hipFFT
+// plan costs hundreds of ms, the transforms themselves ~0.6 ms.  A plan binds
+// one stream and work area, so every stream has its own; calls on one stream
+// take its entry's mutex (host threads sharing a stream), calls on different
+// streams -- the two hemispheres, several GPUs -- run concurrently.  The
+// cache's own mutex covers only the lookup.
+struct PlanEntry {
+    std::mutex mu;
+    Plans p;
+    bool made = false;
+};
+
 struct PlanCache {
     std::mutex mu;
-    std::map<std::tuple<int, int, int>, Plans> plans;
+    std::map<std::tuple<int, int, int, hipStream_t>, std::unique_ptr<PlanEntry>> plans;
 };
 
 PlanCache& plan_cache()
@@ -276,21 +295,44 @@ PlanCache& plan_cache()
     return *c;
 }
 
-int cached_plans(int vdim, int N, Plans** out)
+// the entry for (current device, vdim, N, s), its plans made; returned locked
+int cached_plans(int vdim, int N, hipStream_t s, PlanEntry** out,
+                 std::unique_lock<std::mutex>& lock)
 {
     int dev = 0;
     THX_HIP(hipGetDevice(&dev));
     PlanCache& c = plan_cache();
-    const auto key = std::make_tuple(dev, vdim, N);
-    auto it = c.plans.find(key);
-    if (it == c.plans.end()) {
-        Plans p;
-        const int st = make_plans(p, vdim, N);
-        if (st != THX_OK) return st;
-        it = c.plans.emplace(key, p).first;
+    PlanEntry* e = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(c.mu);
+        auto& slot = c.plans[std::make_tuple(dev, vdim, N, s)];
+        if (!slot) slot.reset(new PlanEntry);
+        e = slot.get();
     }
-    *out = &it->second;
+    lock = std::unique_lock<std::mutex>(e->mu);
+    if (!e->made) {
+        const int st = make_plans(e->p, vdim, N);
+        if (st != THX_OK) return st;
+        e->made = true;
+    }
+    *out = e;
     return THX_OK;
+}
+
+// the tabulated real-space kernel per (a, alpha), computed once (1e5 Bessel
+// evaluations) under its own lock
+const std::vector<float>& kernel_table(float a, float alpha)
+{
+    static std::mutex mu;
+    static std::map<std::pair<float, float>, std::vector<float>>* tabs =
+        new std::map<std::pair<float, float>, std::vector<float>>;
+    std::lock_guard<std::mutex> lk(mu);
+    std::vector<float>& t = (*tabs)[std::make_pair(a, alpha)];
+    if (t.empty()) {
+        t.resize(TAB_N + 1);
+        for (int q = 0; q <= TAB_N; q++) t[q] = (float)mkb_rl_r2(q * 1e-5, a, alpha);
+    }
+    return t;
 }
 
 }  // namespace
@@ -301,10 +343,10 @@ extern "C" size_t thx_reconstruct_workspace(int N, int pf)
     const int vdim = N * pf;
     size_t work = 0;
     {
-        std::lock_guard<std::mutex> lk(plan_cache().mu);
-        Plans* p = nullptr;
-        if (cached_plans(vdim, N, &p) != THX_OK) return 0;
-        work = p->work;
+        std::unique_lock<std::mutex> lk;
+        PlanEntry* e = nullptr;
+        if (cached_plans(vdim, N, nullptr, &e, lk) != THX_OK) return 0;
+        work = e->p.work;
     }
     thx::Carver k(nullptr, ~size_t(0));
     const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
@@ -331,13 +373,13 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
     const size_t need = thx_reconstruct_workspace(N, pf);
     THX_CHECK_ARG(need > 0 && workspace && wsBytes >= need, "thx_reconstruct: workspace too small");
     hipStream_t s = thx::as_stream(stream);
-    std::lock_guard<std::mutex> lk(plan_cache().mu);
-    Plans* pp = nullptr;
+    std::unique_lock<std::mutex> lk;     // this stream's plans, held for the solve
+    PlanEntry* pe = nullptr;
     {
-        const int st = cached_plans(vdim, N, &pp);
+        const int st = cached_plans(vdim, N, s, &pe, lk);
         if (st != THX_OK) return st;
     }
-    Plans& pl = *pp;
+    Plans& pl = pe->p;
     const size_t work = pl.work;
     const size_t dimSize = (size_t)(vdim / 2 + 1) * vdim * vdim;
     thx::Carver k(workspace, wsBytes);
@@ -356,13 +398,7 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
         THX_FFT(hipfftSetStream(pl.r2cN, s));
     }
     // the tabulated real-space kernel (float, as the reference's RFLOAT table)
-    // (computed once per (a, alpha) and kept: 1e5 Bessel evaluations)
-    static std::map<std::pair<float, float>, std::vector<float>> tabs;
-    std::vector<float>& htab = tabs[std::make_pair(a, alpha)];
-    if (htab.empty()) {
-        htab.resize(TAB_N + 1);
-        for (int t = 0; t <= TAB_N; t++) htab[t] = (float)mkb_rl_r2(t * 1e-5, a, alpha);
-    }
+    const std::vector<float>& htab = kernel_table(a, alpha);
     const float nf = (float)mkb_rl_r2(0.0, a, alpha);   // MKB_RL(0, a, alpha)
     THX_HIP(hipMemcpyAsync(tab, htab.data(), sizeof(float) * (TAB_N + 1), hipMemcpyHostToDevice, s));
 
@@ -382,21 +418,24 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
         float diffPrev = 3.4e38f;
         diffC = 3.4e38f;
         int nNoDec = 0;
+        const dim3 gRow(1, vdim, vdim), gRowRL(cdiv_i(vdim, 256), vdim, vdim);
+        hipLaunchKernelGGL(k_c_from_tw, g, b, 0, s, C, T, W, nFT);
+        THX_LAUNCH_CHECK();
+        unsigned* bits = nullptr;
+        THX_HIP(hipHostMalloc(reinterpret_cast<void**>(&bits), sizeof(unsigned), 0));
         for (m = 0; m < 30; m++) {                                // MAX_N_ITER_BALANCE
-            hipLaunchKernelGGL(k_c_from_tw, g, b, 0, s, C, T, W, nFT);
-            THX_LAUNCH_CHECK();
             THX_FFT(hipfftExecC2R(pl.c2r, reinterpret_cast<hipfftComplex*>(C), rl));
-            hipLaunchKernelGGL(k_kernel_mul, g, b, 0, s, rl, vdim, tab, nf, scaleBw);
+            hipLaunchKernelGGL(k_kernel_mul, gRowRL, b, 0, s, rl, vdim, tab, nf, scaleBw);
             THX_LAUNCH_CHECK();
             THX_FFT(hipfftExecR2C(pl.r2c, rl, reinterpret_cast<hipfftComplex*>(C)));
             THX_HIP(hipMemsetAsync(diff, 0, sizeof(unsigned), s));
-            hipLaunchKernelGGL(k_update_w, g, b, 0, s, W, C, vdim, r2, diff);
+            // W update + the next iteration's C in one pass
+            hipLaunchKernelGGL(k_update_w, gRow, b, 0, s, W, C, T, vdim, r2, diff);
             THX_LAUNCH_CHECK();
-            unsigned bits = 0;
-            THX_HIP(hipMemcpyAsync(&bits, diff, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+            THX_HIP(hipMemcpyAsync(bits, diff, sizeof(unsigned), hipMemcpyDeviceToHost, s));
             THX_HIP(hipStreamSynchronize(s));
             diffPrev = diffC;
-            diffC = __builtin_bit_cast(float, bits);
+            diffC = __builtin_bit_cast(float, *bits);
             if (diffOut) diffOut[m] = diffC;
             if (diffC > diffPrev * 0.95f) nNoDec += 1;            // DIFF_C_DECREASE_THRES
             else nNoDec = 0;
@@ -405,6 +444,7 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
                 break;
             }
         }
+        (void)hipHostFree(bits);
     } else {
         hipLaunchKernelGGL(k_w_from_t, g, b, 0, s, W, T, vdim, r2);
         THX_LAUNCH_CHECK();
