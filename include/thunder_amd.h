@@ -64,8 +64,9 @@ int thx_pixel_set(int idim, int pf, float rU, float rL, int cap, int* iCol,
 /* Visiting order of the pixel set for the local phases (no reference
  * counterpart; the reference walks the set in allocPreCalIdx order): the
  * set is cut into 4 x 4 squares of (iCol, iRow), squares in serpentine row
- * order, consecutive partial squares (the disc edge) merged while they fit in
- * 16 entries, every group padded to 16 with -1.  Each 16-entry group of
+ * order, inside a square its four 2 x 2 quads in turn, consecutive partial
+ * squares (the disc edge) merged while they fit in 16 entries, every group
+ * padded to 16 with -1.  Each 16-entry group of
  * `order` is then a compact patch whose slice neighbourhood fits in LDS
  * (thx_local_phase).  Host function; order: cap ints, *nOrd receives the
  * length (a multiple of 16; every pixel index appears exactly once). */
@@ -167,6 +168,8 @@ int thx_global_scan(const float* rotP, int nR, const float* traP, int nT,
  * volLayout 0: `vol` is the half-complex projectee; 1: `vol` is its
  * cell-expanded copy from thx_volume_cells (8x the bytes, one aligned 64-B
  * segment per trilinear gather -- the layout for HBM-bound full-resolution
+ * phases); 2: `vol` is its bricked copy from thx_volume_bricks (the same
+ * bytes, fewer cache lines per gather -- the layout for L2-resident
  * phases).
  * pxOrder (device, nOrd ints, may be NULL = set order, nOrd ignored): the
  * pixel visiting order from thx_pixel_tile_order (-1 entries skipped).
@@ -248,6 +251,17 @@ int thx_local_phase_d(const thx_local_sel* sel, const float* vol, int volLayout,
  * i + 1 past the half plane zero.  cells: 8 * dimSize Complex. */
 int thx_volume_cells(const float* vol, int vdim, float* cells,
                      thx_stream_t stream);
+
+/* Bricked copy of a half-complex volume, the same bytes: 128-B bricks of
+ * 4 x 2 x 2 (x, y, z) voxels, brick (bx, by, bz) at float2 offset
+ * 16 ((bz vdim/2 + by) nxB + bx), nxB = ceil((vdim/2 + 1) / 4), voxel
+ * (x & 3) + 4 (y & 1) + 8 (z & 1) inside; rows / slices wrapped like
+ * iFTHalf, x >= vdim/2 + 1 zero.  The four rows of a trilinear cell share a
+ * brick when y0, z0 are even, so a sample touches ~2.8 cache lines instead
+ * of ~4.25 (thx_local_phase volLayout 2; thx_expectation builds one per
+ * class in its workspace).  bricks: thx_volume_bricks_bytes(vdim) bytes. */
+size_t thx_volume_bricks_bytes(int vdim);
+int thx_volume_bricks(const float* vol, int vdim, float* bricks, thx_stream_t stream);
 
 /* ----------------------------------------------------------------- a10 ---
  * Systematic resampling of Particle::resample (src/Particle.cpp:1291-1478)

@@ -55,13 +55,14 @@ def _scan_vs_oracle(orc, vol, px, pxh, N, pf, gset, dat, ctf, sig, algo):
     assert np.allclose(wC.reshape(-1), rC, rtol=1e-3, atol=0)
 
 
-def _phase_vs_oracle(orc, vol, px, pxh, N, pf, quat, trans, dat, ctf, sig, cells=None, tol=1e-5):
+def _phase_vs_oracle(orc, vol, px, pxh, N, pf, quat, trans, dat, ctf, sig, cells=None, tol=1e-5,
+                     bricks=None):
     nImg, mR = quat.shape[:2]
     mT = trans.shape[1]
     pR = np.full((nImg, mR), 1.0 / mR)
     pT = np.full((nImg, mT), 1.0 / mT)
     wC, wR, wT, base, d = ops.local_phase(vol, T(quat), T(trans), T(np.ones(nImg)), T(pR), T(pT),
-                                          dat, ctf, sig, px, want_dvp=True, cells=cells)
+                                          dat, ctf, sig, px, want_dvp=True, cells=cells, bricks=bricks)
     d, wR, base = d.cpu().numpy(), wR.cpu().numpy(), base.cpu().numpy()
     vnp = vol.cpu().numpy()
     for l in range(nImg):
@@ -106,16 +107,18 @@ def test_c3_fp32_scan_matches_oracle(orc, c3):
                     c3["ctf"][:n].contiguous(), c3["sig"][:n].contiguous(), algo=1)
 
 
-def test_c3_local_phase_bench_clouds_match_oracle(orc, c3):
-    """The driver's layout (half-complex, LDS patch boxes) at the bench's
-    cloud widths (3 and 10 degrees), 125 x 9."""
+@pytest.mark.parametrize("bricks", [False, True])
+def test_c3_local_phase_bench_clouds_match_oracle(orc, c3, bricks):
+    """The half-complex layout and the driver's bricked copy (LDS patch
+    boxes) at the bench's cloud widths (3, 10 and 30 degrees), 125 x 9."""
     rng = np.random.default_rng(8)
     pxh = orc.pixel_set(256, 2, 24, 1)
-    for spread in (3.0, 10.0):
+    br = ops.volume_bricks(c3["vol"]) if bricks else None
+    for spread in (3.0, 10.0, 30.0):
         quat = synth.clustered_quaternions(4, 125, spread, rng)
         trans = rng.standard_normal((4, 9, 2)) * 2
         _phase_vs_oracle(orc, c3["vol"], c3["px"], pxh, 256, 2, quat, trans, c3["dat"][:4].contiguous(),
-                         c3["ctf"][:4].contiguous(), c3["sig"][:4].contiguous())
+                         c3["ctf"][:4].contiguous(), c3["sig"][:4].contiguous(), bricks=br)
 
 
 # ---------------------------------------------------------------------- C2

@@ -251,6 +251,8 @@ def test_local_phase_staged_patches(orc, stack64, spread, lo, hi):
     b = ops.local_phase(vol, *args, want_dvp=True, tiled=False)
     c = ops.local_phase(vol, *args, want_dvp=True, cells=ops.volume_cells(vol))
     assert torch.equal(a[4], c[4])
+    e = ops.local_phase(vol, *args, want_dvp=True, bricks=ops.volume_bricks(vol))
+    assert torch.equal(a[4], e[4])      # the same taps in the same order from bricks
     da, db = a[4].cpu().numpy(), b[4].cpu().numpy()
     assert np.max(np.abs(da - db) / np.abs(db)) < 2e-6      # pixel summation order only
     for l in range(nImg):
@@ -453,3 +455,23 @@ def test_empty_batches(orc, stack):
     k, sd = ops.pf_calvari(q, t)
     assert k.shape == (0, 3) and sd.shape == (0, 2)
     torch.cuda.synchronize()
+
+
+def test_volume_bricks_layout():
+    """thx_volume_bricks against the layout its header states: voxel (x, y, z)
+    at 16 ((z/2 vdim/2 + y/2) nxB + x/4) + (x & 3) + 4 (y & 1) + 8 (z & 1),
+    zeros past the half-plane edge; the bytes equal the half-complex volume's
+    rounded up to whole bricks."""
+    vdim = 24
+    g = torch.Generator().manual_seed(3)
+    vol = torch.complex(torch.randn(vdim, vdim, vdim // 2 + 1, generator=g),
+                        torch.randn(vdim, vdim, vdim // 2 + 1, generator=g)).to(DEV)
+    b = ops.volume_bricks(vol).cpu()
+    nxB = (vdim // 2 + 1 + 3) // 4
+    assert b.numel() == nxB * 16 * (vdim // 2) ** 2
+    z, y, x = torch.meshgrid(torch.arange(vdim), torch.arange(vdim), torch.arange(nxB * 4),
+                             indexing="ij")
+    idx = 16 * (((z // 2) * (vdim // 2) + y // 2) * nxB + x // 4) + (x & 3) + 4 * (y & 1) + 8 * (z & 1)
+    got = b[idx.reshape(-1)].reshape(vdim, vdim, nxB * 4)
+    assert torch.equal(got[..., :vdim // 2 + 1], vol.cpu())
+    assert torch.count_nonzero(got[..., vdim // 2 + 1:]) == 0

@@ -84,9 +84,21 @@ extern "C" int thx_pixel_tile_order(const int* iCol, const int* iRow, int nPxl, 
         const long tc = (tr & 1) ? nTc - 1 - tc0 : tc0;   // serpentine square rows
         key[i] = tr * nTc + tc;
     }
+    // inside a square: its 2x2 quads in turn, so that every 4 consecutive
+    // entries (one step of the local phase's lanes) are a compact quad
+#ifndef THX_QUAD_ORDER
+#define THX_QUAD_ORDER 1
+#endif
+    std::vector<int> sub(nPxl, 0);
+    for (int i = 0; THX_QUAD_ORDER && i < nPxl; i++) {
+        const int lc = (iCol[i] - cMin) % TILE, lr = (iRow[i] - rMin) % TILE;
+        sub[i] = ((lr / 2) * 2 + lc / 2) * 4 + (lr % 2) * 2 + lc % 2;
+    }
     std::vector<int> idx(nPxl);
     for (int i = 0; i < nPxl; i++) idx[i] = i;
-    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return key[a] < key[b]; });
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) {
+        return key[a] != key[b] ? key[a] < key[b] : sub[a] < sub[b];
+    });
     // groups of <= 16: whole squares, consecutive partial squares merged
     std::vector<int> out;
     out.reserve(nPxl + GROUP);

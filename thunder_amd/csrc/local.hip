@@ -92,6 +92,77 @@ THX_DEV float2 interp_cells(const float4* __restrict__ cells, int vdim, float x,
     return make_float2(re, conj ? -im : im);
 }
 
+// Bricked projectee (thx_volume_bricks): the half-complex volume in 128-B
+// bricks of 4 x 2 x 2 (x, y, z) voxels, x fastest inside a brick row, so the
+// four rows (y0, y0 + 1) x (z0, z0 + 1) of a trilinear cell share a brick
+// whenever y0 and z0 are even.  A sample then touches (1 + 1/4)(1 + 1/2)
+// (1 + 1/2) = 2.8 128-B lines on average instead of the half-complex rows'
+// (1 + 1/16) 2 2 = 4.25, at the same footprint (the L2-resident working set
+// of a phase stays L2-resident).  Rows / slices wrapped like iFTHalf; bricks
+// past the half-plane edge (x >= nColFT) hold zeros.
+enum { LAYOUT_FT = 0, LAYOUT_CELLS = 1, LAYOUT_BRICKS = 2 };
+
+THX_DEV int bricks_nx(int vdim) { return (vdim / 2 + 1 + 3) / 4; }
+
+// float2 index of voxel 0 of the brick row holding wrapped row (yw, zw)
+THX_DEV size_t brick_row(int yw, int zw, int vdim, int nxB)
+{
+    return (((size_t)(zw >> 1) * (vdim >> 1) + (yw >> 1)) * nxB << 4) + ((((zw & 1) << 1) | (yw & 1)) << 2);
+}
+
+THX_DEV int brick_x(int x) { return ((x >> 2) << 4) + (x & 3); }
+
+// interp_ft's taps, weights and summation order from the bricked layout
+THX_DEV float2 interp_bricks(const float2* __restrict__ vol, int vdim, float x, float y, float z)
+{
+    const bool conj = !(x >= 0.f);
+    if (conj) { x = -x; y = -y; z = -z; }
+    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+    const float dx = x - fx, dy = y - fy, dz = z - fz;
+    const float vx[2] = {1.f - dx, dx};
+    const float vy[2] = {1.f - dy, dy};
+    const float vz[2] = {1.f - dz, dz};
+    const int nxB = bricks_nx(vdim);
+    const int ya = wrap_idx(y0, vdim), yb = wrap_idx(y0 + 1, vdim);
+    const int za = wrap_idx(z0, vdim), zb = wrap_idx(z0 + 1, vdim);
+    const int o0 = brick_x(x0), o1 = brick_x(x0 + 1);
+    const size_t r00 = brick_row(ya, za, vdim, nxB), r01 = brick_row(yb, za, vdim, nxB);
+    const size_t r10 = brick_row(ya, zb, vdim, nxB), r11 = brick_row(yb, zb, vdim, nxB);
+#ifdef THX_BRICK_PAIR
+    // the x pair is one 16-B piece unless x0 ends a brick row (1 in 4):
+    // then the upper half is re-read from the next brick
+    const bool split = (x0 & 3) == 3;
+    auto pair = [&](size_t r, float2& lo, float2& hi) {
+        const f32x4u v = *reinterpret_cast<const f32x4u*>(vol + r + o0);
+        lo = make_float2(v.x, v.y);
+        hi = make_float2(v.z, v.w);
+        if (split) hi = vol[r + o1];
+    };
+    float2 a0, a1, b0, b1, c0, c1, d0, d1;
+    pair(r00, a0, a1);
+    pair(r01, b0, b1);
+    pair(r10, c0, c1);
+    pair(r11, d0, d1);
+#else
+    const float2 a0 = vol[r00 + o0], a1 = vol[r00 + o1];
+    const float2 b0 = vol[r01 + o0], b1 = vol[r01 + o1];
+    const float2 c0 = vol[r10 + o0], c1 = vol[r10 + o1];
+    const float2 d0 = vol[r11 + o0], d1 = vol[r11 + o1];
+#endif
+    float re = 0.f, im = 0.f;
+    float w;
+    w = vx[0] * vy[0] * vz[0]; re += a0.x * w; im += a0.y * w;
+    w = vx[1] * vy[0] * vz[0]; re += a1.x * w; im += a1.y * w;
+    w = vx[0] * vy[1] * vz[0]; re += b0.x * w; im += b0.y * w;
+    w = vx[1] * vy[1] * vz[0]; re += b1.x * w; im += b1.y * w;
+    w = vx[0] * vy[0] * vz[1]; re += c0.x * w; im += c0.y * w;
+    w = vx[1] * vy[0] * vz[1]; re += c1.x * w; im += c1.y * w;
+    w = vx[0] * vy[1] * vz[1]; re += d0.x * w; im += d0.y * w;
+    w = vx[1] * vy[1] * vz[1]; re += d1.x * w; im += d1.y * w;
+    return make_float2(re, conj ? -im : im);
+}
+
 // Patch record (k_patch_boxes -> k_local_fused): layout in patch.h.
 struct Rec {
     int v[REC];
@@ -139,7 +210,7 @@ THX_DEV void store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __re
     bool any[2];
     for (int s = 0; s < 2; s++) {
         // clamp into the half volume (rows / slices wrap once at most)
-        lo[s][0] = max(e[6 * s], 0);
+        lo[s][0] = max(e[6 * s], 0) & ~3;   // whole 4-voxel items (32 B, a brick row)
         lo[s][1] = max(e[6 * s + 1], -half);
         lo[s][2] = max(e[6 * s + 2], -half);
         n[s][0] = min(e[6 * s + 3], nColFT - 1) - lo[s][0] + 1;
@@ -185,13 +256,90 @@ THX_DEV void store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __re
         dst[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
 }
 
+#ifndef THX_SKIP_PAD
+#define THX_SKIP_PAD 1
+#endif
+#ifndef THX_LOCAL_SORT
+#define THX_LOCAL_SORT 1
+#endif
+
+// 3D Morton code of three 10-bit coordinates.
+THX_DEV unsigned morton3(unsigned x, unsigned y, unsigned z)
+{
+    auto spread = [](unsigned v) {
+        v &= 0x3ffu;
+        v = (v | (v << 16)) & 0x030000ffu;
+        v = (v | (v << 8)) & 0x0300f00fu;
+        v = (v | (v << 4)) & 0x030c30c3u;
+        v = (v | (v << 2)) & 0x09249249u;
+        return v;
+    };
+    return spread(x) | (spread(y) << 1) | (spread(z) << 2);
+}
+
+// Lane slot -> rotation of the tile.  A particle cloud arrives in resampling
+// order (copies of one ancestor adjacent, ancestors in no spatial order), so
+// the 16 rotations a wave gathers for one pixel can land anywhere in the
+// cloud.  Ranking the tile's rotations by the Morton code of their vector
+// part relative to the tile's first rotation (10 bits per axis, 0.22 deg)
+// gives each wave a compact group of rotations: its 16 lanes then read
+// neighbouring voxels (shared cache lines on the L2 gathers, spread banks on
+// the LDS taps).  Per-rotation arithmetic is unchanged, only which lane does
+// it; rows past nRl keep key ~0u and sort last.
+THX_DEV void rotation_slots(const double* __restrict__ q4, int nRl, int tid,
+                            unsigned* __restrict__ sKey, int* __restrict__ sPerm)
+{
+    if (tid < RT) {
+        unsigned key = ~0u;
+        if (THX_LOCAL_SORT && tid < nRl) {
+            const double a0 = q4[0], a1 = -q4[1], a2 = -q4[2], a3 = -q4[3];   // conj(q_0)
+            const double* b = q4 + 4 * tid;
+            double w = a0 * b[0] - a1 * b[1] - a2 * b[2] - a3 * b[3];
+            double x = a0 * b[1] + a1 * b[0] + a2 * b[3] - a3 * b[2];
+            double y = a0 * b[2] - a1 * b[3] + a2 * b[0] + a3 * b[1];
+            double z = a0 * b[3] + a1 * b[2] - a2 * b[1] + a3 * b[0];
+            if (w < 0.0) { x = -x; y = -y; z = -z; }
+            auto qz = [](double v) { return (unsigned)min(1023.0, max(0.0, (v + 1.0) * 512.0)); };
+            key = morton3(qz(x), qz(y), qz(z)) ;
+        } else if (tid < nRl) {
+            key = (unsigned)tid;
+        }
+        sKey[tid] = key;
+    }
+    __syncthreads();
+    if (tid < RT) {
+        const unsigned k = sKey[tid];
+        int rank = 0;
+        for (int j = 0; j < RT; j++) {
+            const unsigned kj = sKey[j];
+            rank += (kj < k) || (kj == k && j < tid);
+        }
+        sPerm[rank] = tid;
+    }
+    __syncthreads();
+}
+
+// Slot -> rotation of the tile (rotation_slots' sPerm): slots past nRl (the
+// tile's padding rows, never stored) take their wave group's first rotation,
+// so the 16 rotations a wave gathers for stay one compact group; a group of
+// padding only takes the tile's first.
+THX_DEV int slot_rotation(const int* __restrict__ sPerm, int slot, int nRl)
+{
+    const int rp = sPerm[slot];
+    if (rp < nRl) return rp;
+    const int g0 = sPerm[slot & ~15];
+    return g0 < nRl ? g0 : 0;
+}
+
 // One workgroup per (image, rotation tile), one lane per patch, the tile's
-// rotations split over the 4 waves: the LDS boxes that hold every tap of the
-// patch's samples under the tile's rotations.  The matrices sit in LDS and
-// are read as broadcasts; per rotation and axis the extremes of the rotated
-// patch rectangle are its corners picked by the signs of the two matrix
-// entries.  The waves' partial bounds meet in LDS.
+// rotation slots (rotation_slots: the Morton-ranked order k_local_fused's
+// waves take them in) split over the 4 waves: the LDS boxes that hold every
+// tap of the patch's samples under the tile's rotations.  The matrices sit
+// in LDS and are read as broadcasts; per rotation and axis the extremes of
+// the rotated patch rectangle are its corners picked by the signs of the two
+// matrix entries.  The waves' partial bounds meet in LDS.
 constexpr int PB_WAVES = 4;
+constexpr int PB_SLOTS = RT / PB_WAVES;   // 32 slots per wave
 
 __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __restrict__ quat,
                                                                int nR,
@@ -205,6 +353,8 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
 {
     __shared__ float sM[RT][6];
     __shared__ int sE[PB_WAVES][12][64];
+    __shared__ unsigned sKey[RT];
+    __shared__ int sPerm[RT];
     const int nC = (nVisit + KC - 1) / KC, nRT = (nR + RT - 1) / RT;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ry = blockIdx.x % nRT;
@@ -214,28 +364,37 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
         l = act[l];
     }
     const int nRl = min(RT, nR - ry * RT);
-    for (int k = threadIdx.x; k < nRl; k += 64 * PB_WAVES) {
+    const double* Q = quat + ((size_t)l * nR + ry * RT) * 4;
+    rotation_slots(Q, nRl, threadIdx.x, sKey, sPerm);
+    for (int k = threadIdx.x; k < RT; k += 64 * PB_WAVES) {
+        const int r = slot_rotation(sPerm, k, nRl);
         double q[4], m[9];
-        for (int a = 0; a < 4; a++) q[a] = quat[((size_t)l * nR + ry * RT + k) * 4 + a];
+        for (int a = 0; a < 4; a++) q[a] = Q[(size_t)r * 4 + a];
         quat_to_mat(q, m);
         for (int a = 0; a < 6; a++) sM[k][a] = (float)m[a];
     }
     __syncthreads();
-    const int rPer = (nRl + PB_WAVES - 1) / PB_WAVES;
-    const int rBeg = wv * rPer, rEnd = min(nRl, rBeg + rPer);
+    const int rBeg = wv * PB_SLOTS, rEnd = rBeg + PB_SLOTS;
+    // every rotated point lies in the corner hull; the bounds are FP32
+    // (|error| < 1e-4 voxel against the FP64-then-rounded sample coordinates),
+    // widened by EPS before the floor; a cell spans floor(c) .. floor(c) + 1.
+    // The extremes are tracked in FP32 and floored once: floor and the clamp
+    // at 0 are monotone, so this equals flooring every rotation's bound.
+    constexpr float EPS = 1e-3f;
     for (int c0 = 0; c0 < nC; c0 += 64) {
         const int c = c0 + lane;
         int cLo = BIG, cHi = -BIG, rLo = BIG, rHi = -BIG, ic0 = 0, ir0 = 0;
-        int pk[KC];
+        int pk[KC], pc[KC], pr[KC];
 #pragma unroll
         for (int k = 0; k < KC; k++) pk[k] = patch_pixel(order, nVisit, c * KC + k);
 #pragma unroll
         for (int k = KC - 1; k >= 0; k--) {
-            const int ic = iCol[max(pk[k], 0)], ir = iRow[max(pk[k], 0)];   // loads in flight together
+            pc[k] = iCol[max(pk[k], 0)];    // loads in flight together
+            pr[k] = iRow[max(pk[k], 0)];
             if (pk[k] >= 0) {
-                cLo = min(cLo, ic); cHi = max(cHi, ic);
-                rLo = min(rLo, ir); rHi = max(rHi, ir);
-                ic0 = ic; ir0 = ir;          // ends on the patch's first pixel
+                cLo = min(cLo, pc[k]); cHi = max(cHi, pc[k]);
+                rLo = min(rLo, pr[k]); rHi = max(rHi, pr[k]);
+                ic0 = pc[k]; ir0 = pr[k];   // ends on the patch's first pixel
             }
         }
         int e[12];
@@ -244,13 +403,6 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
         if (cLo <= cHi) {
             const float X0 = (float)(cLo * pf), X1 = (float)(cHi * pf);
             const float Y0 = (float)(rLo * pf), Y1 = (float)(rHi * pf);
-            // every rotated patch point lies in the corner hull; the bounds
-            // are FP32 (|error| < 1e-4 voxel against the FP64-then-rounded
-            // sample coordinates), widened by EPS before the floor; a cell
-            // spans floor(c) .. floor(c) + 1.  The extremes are tracked in
-            // FP32 and floored once: floor and the clamp at 0 are monotone,
-            // so this equals flooring every rotation's bound.
-            constexpr float EPS = 1e-3f;
             float f[12];
 #pragma unroll
             for (int k = 0; k < 12; k++) f[k] = (k % 6) < 3 ? INFINITY : -INFINITY;
@@ -331,7 +483,7 @@ THX_DEV Pix load_pix(int p, const int* __restrict__ iCol, const int* __restrict_
 
 // The items (4 consecutive voxels of a box row, 32 B) of a staged patch this
 // thread moves: item it = tid + j THREADS, LDS voxel dst[j].
-template <bool CELLS, int NI = NIT, int CAP = BOX_CAP>
+template <int LAYOUT, int NI = NIT, int CAP = BOX_CAP>
 THX_DEV void fetch_box(f32x4 (&pre)[NI][2], int (&dst)[NI], const Rec& b,
                        const float2* __restrict__ vol, int vdim, int tid)
 {
@@ -352,8 +504,15 @@ THX_DEV void fetch_box(f32x4 (&pre)[NI][2], int (&dst)[NI], const Rec& b,
             const int gx = (s1 ? b.v[3] : b.v[0]) + 4 * xq;
             const int gy = wrap_idx((s1 ? b.v[4] : b.v[1]) + y, vdim);
             const int gz = wrap_idx((s1 ? b.v[5] : b.v[2]) + z, vdim);
+            if (LAYOUT == LAYOUT_BRICKS) {   // gx % 4 == 0: one 32-B brick row piece
+                const f32x4* p = reinterpret_cast<const f32x4*>(
+                    vol + brick_row(gy, gz, vdim, bricks_nx(vdim)) + brick_x(gx));
+                pre[j][0] = p[0];
+                pre[j][1] = p[1];
+                continue;
+            }
             const unsigned g = ((unsigned)gz * vdim + gy) * nColFT + gx;
-            if (!CELLS && gx + 3 < nColFT) {
+            if (LAYOUT == LAYOUT_FT && gx + 3 < nColFT) {
                 const f32x4u* p = reinterpret_cast<const f32x4u*>(vol + g);
                 const f32x4u lo = p[0], hi = p[1];
                 pre[j][0] = f32x4{lo.x, lo.y, lo.z, lo.w};
@@ -365,7 +524,7 @@ THX_DEV void fetch_box(f32x4 (&pre)[NI][2], int (&dst)[NI], const Rec& b,
             for (int k = 0; k < 4; k++) {
                 e[k] = make_float2(0.f, 0.f);
                 if (gx + k < nColFT) {
-                    if (CELLS) {
+                    if (LAYOUT == LAYOUT_CELLS) {
                         const float4 q = reinterpret_cast<const float4*>(vol)[(size_t)(g + k) * 4];
                         e[k] = make_float2(q.x, q.y);
                     } else {
@@ -380,6 +539,7 @@ THX_DEV void fetch_box(f32x4 (&pre)[NI][2], int (&dst)[NI], const Rec& b,
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 
 // Trilinear gather of getByInterpolationFT (the taps and weights of
 // interp_ft, common.h) from the staged boxes, on packed FP32: the weights are
@@ -415,72 +575,18 @@ THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int sp, int of
     return make_float2(s.x, conj ? -s.y : s.y);
 }
 
-#ifndef THX_SKIP_PAD
-#define THX_SKIP_PAD 1
-#endif
-#ifndef THX_LOCAL_SORT
-#define THX_LOCAL_SORT 1
-#endif
-
-// 3D Morton code of three 10-bit coordinates.
-THX_DEV unsigned morton3(unsigned x, unsigned y, unsigned z)
-{
-    auto spread = [](unsigned v) {
-        v &= 0x3ffu;
-        v = (v | (v << 16)) & 0x030000ffu;
-        v = (v | (v << 8)) & 0x0300f00fu;
-        v = (v | (v << 4)) & 0x030c30c3u;
-        v = (v | (v << 2)) & 0x09249249u;
-        return v;
-    };
-    return spread(x) | (spread(y) << 1) | (spread(z) << 2);
-}
-
-// Lane slot -> rotation of the tile.  A particle cloud arrives in resampling
-// order (copies of one ancestor adjacent, ancestors in no spatial order), so
-// the 16 rotations a wave gathers for one pixel can land anywhere in the
-// cloud.  Ranking the tile's rotations by the Morton code of their vector
-// part relative to the tile's first rotation (10 bits per axis, 0.22 deg)
-// gives each wave a compact group of rotations: its 16 lanes then read
-// neighbouring voxels (shared cache lines on the L2 gathers, spread banks on
-// the LDS taps).  Per-rotation arithmetic is unchanged, only which lane does
-// it; rows past nRl keep key ~0u and sort last.
-THX_DEV void rotation_slots(const double* __restrict__ q4, int nRl, int tid,
-                            unsigned* __restrict__ sKey, int* __restrict__ sPerm)
-{
-    if (tid < RT) {
-        unsigned key = ~0u;
-        if (THX_LOCAL_SORT && tid < nRl) {
-            const double a0 = q4[0], a1 = -q4[1], a2 = -q4[2], a3 = -q4[3];   // conj(q_0)
-            const double* b = q4 + 4 * tid;
-            double w = a0 * b[0] - a1 * b[1] - a2 * b[2] - a3 * b[3];
-            double x = a0 * b[1] + a1 * b[0] + a2 * b[3] - a3 * b[2];
-            double y = a0 * b[2] - a1 * b[3] + a2 * b[0] + a3 * b[1];
-            double z = a0 * b[3] + a1 * b[2] - a2 * b[1] + a3 * b[0];
-            if (w < 0.0) { x = -x; y = -y; z = -z; }
-            auto qz = [](double v) { return (unsigned)min(1023.0, max(0.0, (v + 1.0) * 512.0)); };
-            key = morton3(qz(x), qz(y), qz(z)) ;
-        } else if (tid < nRl) {
-            key = (unsigned)tid;
-        }
-        sKey[tid] = key;
-    }
-    __syncthreads();
-    if (tid < RT) {
-        const unsigned k = sKey[tid];
-        int rank = 0;
-        for (int j = 0; j < RT; j++) {
-            const unsigned kj = sKey[j];
-            rank += (kj < k) || (kj == k && j < tid);
-        }
-        sPerm[rank] = tid;
-    }
-    __syncthreads();
-}
 
 #ifdef THX_LOCAL_STAMPS
 // diagnostic: per-iteration phase cycles of staged patches, waves 0 and 7
 __device__ unsigned long long g_local_stamps[12];
+#endif
+#ifdef THX_STEP_COUNT
+// diagnostic: wave-steps gathered from the shared box, straight from vol,
+// and skipped (padding); slot 1 unused
+__device__ unsigned long long g_step_counts[4];
+#define MCOUNT(k) (mc[k] += 1)
+#else
+#define MCOUNT(k) ((void)0)
 #endif
 
 // CS (CTF search, SEARCH_TYPE_CTF): the columns are the nT x nD (t, d) pairs
@@ -491,7 +597,7 @@ __device__ unsigned long long g_local_stamps[12];
 // A CS workgroup covers NCT column tiles of 16 (up to 96 (t, d) columns), so
 // the projection -- the expensive part -- is gathered once for all of them;
 // each step then issues 4 NCT MFMAs against NCT accumulators.
-template <bool CELLS, bool CS = false, int NCT = 1, bool BIGBOX = false>
+template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false>
 // non-CS: two workgroups per CU (LDS-bound), 4 waves per SIMD, 128 VGPRs;
 // CS: the NCT accumulators and CTF prefetches need the 256-VGPR budget;
 // BIGBOX: 128 KiB of box, one workgroup per CU, twice the prefetch registers
@@ -556,8 +662,7 @@ k_local_fused(const float2* __restrict__ vol,
     const int rl = wv * 16 + (lane & 15);
     double m[6];
     {
-        const int rp = sPerm[rl];
-        const int r = r0 + (rp < nRl ? rp : 0);
+        const int r = r0 + slot_rotation(sPerm, rl, nRl);
         double q[4], mm[9];
         for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
         quat_to_mat(q, mm);
@@ -610,9 +715,12 @@ k_local_fused(const float2* __restrict__ vol,
     Rec rn = nC > 1 ? load_rec(R + REC) : rc;
     f32x4 pre[NITC][2];
     int dst[NITC];
-    fetch_box<CELLS, NITC, BOXC>(pre, dst, rc, vol, vdim, tid);
+    fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rc, vol, vdim, tid);
 
     __syncthreads();
+#ifdef THX_STEP_COUNT
+    unsigned long long mc[4] = {0, 0, 0, 0};
+#endif
 #ifdef THX_LOCAL_STAMPS
     unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tp = __builtin_amdgcn_s_memtime(), tq;
 #define STAMP(k) do { tq = __builtin_amdgcn_s_memtime(); if (staged(rc)) st[k] += tq - tp; tp = tq; } while (0)
@@ -670,7 +778,7 @@ k_local_fused(const float2* __restrict__ vol,
                 load_cc(pNext);
                 pNext = patch_pixel(order, nVisit, (c + 2) * KC + bpx);
             }
-            fetch_box<CELLS, NITC, BOXC>(pre, dst, rn, vol, vdim, tid);
+            fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rn, vol, vdim, tid);
             if (c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
         }
         STAMP(2);
@@ -713,7 +821,8 @@ k_local_fused(const float2* __restrict__ vol,
             const int nx = rc.v[6], sp = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
 #pragma unroll
             for (int s = 0; s < 4; s++) {
-                if (pad_step(s)) continue;
+                if (pad_step(s)) { MCOUNT(3); continue; }
+                MCOUNT(0);
                 const double2 xy = sXY[4 * s + g];
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
@@ -723,14 +832,16 @@ k_local_fused(const float2* __restrict__ vol,
         } else {
 #pragma unroll 2
             for (int s = 0; s < 4; s++) {
-                if (pad_step(s)) continue;
+                if (pad_step(s)) { MCOUNT(3); continue; }
+                MCOUNT(2);
                 const double2 xy = sXY[4 * s + g];
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
                 const float z = (float)(m[2] * xy.x + m[5] * xy.y);
-                reduce_step(s, CELLS ? interp_cells(reinterpret_cast<const float4*>(vol), vdim,
-                                                    x, y, z)
-                                     : interp_ft(vol, vdim, x, y, z));
+                reduce_step(s, LAYOUT == LAYOUT_CELLS
+                                   ? interp_cells(reinterpret_cast<const float4*>(vol), vdim, x, y, z)
+                               : LAYOUT == LAYOUT_BRICKS ? interp_bricks(vol, vdim, x, y, z)
+                                                         : interp_ft(vol, vdim, x, y, z));
             }
         }
         STAMP(3);
@@ -746,6 +857,10 @@ k_local_fused(const float2* __restrict__ vol,
         tp = tq;
 #endif
     }
+#ifdef THX_STEP_COUNT
+    if (lane == 0)
+        for (int k = 0; k < 4; k++) atomicAdd(&g_step_counts[k], mc[k]);
+#endif
 #ifdef THX_LOCAL_STAMPS
     if (lane == 0 && (wv == 0 || wv == 7))
         for (int k = 0; k < 6; k++) atomicAdd(&g_local_stamps[(wv == 7) * 6 + k], st[k]);
@@ -1011,6 +1126,24 @@ __global__ void __launch_bounds__(256) k_volume_cells(const float2* __restrict__
     }
 }
 
+// One thread per 8-B voxel of the bricked copy (its own write coalesced).
+__global__ void __launch_bounds__(256) k_volume_bricks(const float2* __restrict__ vol,
+                                                       int vdim, float2* __restrict__ out)
+{
+    const int nColFT = vdim / 2 + 1, nxB = (nColFT + 3) / 4;
+    const long n = (long)nxB * 16 * (vdim / 2) * (vdim / 2);
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
+         q += (long)gridDim.x * blockDim.x) {
+        const int in = (int)(q & 15);
+        const long b = q >> 4;
+        const int bx = (int)(b % nxB);
+        const long yz = b / nxB;
+        const int by = (int)(yz % (vdim / 2)), bz = (int)(yz / (vdim / 2));
+        const int x = 4 * bx + (in & 3), y = 2 * by + ((in >> 2) & 1), z = 2 * bz + (in >> 3);
+        out[q] = x < nColFT ? vol[((size_t)z * vdim + y) * nColFT + x] : make_float2(0.f, 0.f);
+    }
+}
+
 size_t dvp_bytes(int nImg, int nR, int nT) { return (size_t)nImg * nR * nT * sizeof(float); }
 
 size_t rec_bytes(int nImg, int nR, int nVisit)
@@ -1058,6 +1191,21 @@ extern "C" int thx_volume_cells(const float* vol, int vdim, float* cells,
     return THX_OK;
 }
 
+extern "C" size_t thx_volume_bricks_bytes(int vdim)
+{
+    if (vdim <= 0 || vdim % 2) return 0;
+    return (size_t)((vdim / 2 + 1 + 3) / 4) * 16 * (vdim / 2) * (vdim / 2) * 2 * sizeof(float);
+}
+
+extern "C" int thx_volume_bricks(const float* vol, int vdim, float* bricks, thx_stream_t stream)
+{
+    THX_CHECK_ARG(vol && bricks && vdim > 0 && vdim % 2 == 0, "thx_volume_bricks: bad arguments");
+    hipLaunchKernelGGL(k_volume_bricks, dim3(8192), dim3(256), 0, thx::as_stream(stream),
+                       reinterpret_cast<const float2*>(vol), vdim, reinterpret_cast<float2*>(bricks));
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 #ifdef THX_LOCAL_STAMPS
 extern "C" int thx_debug_local_stamps(unsigned long long* out, int reset)
 {
@@ -1065,6 +1213,18 @@ extern "C" int thx_debug_local_stamps(unsigned long long* out, int reset)
     if (reset) {
         const unsigned long long z[12] = {0};
         THX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_local_stamps), z, sizeof(z)));
+    }
+    return THX_OK;
+}
+#endif
+
+#ifdef THX_STEP_COUNT
+extern "C" int thx_debug_step_counts(unsigned long long* out, int reset)
+{
+    THX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_counts), sizeof(unsigned long long) * 4));
+    if (reset) {
+        const unsigned long long z[4] = {0};
+        THX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_step_counts), z, sizeof(z)));
     }
     return THX_OK;
 }
@@ -1092,7 +1252,7 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     THX_CHECK_ARG(!nD || (pD && wD && (long)nT * nD <= LOCAL_D_MAXCOL),
                   "thx_local_phase_d: needs pD, wD and nT * nD <= 1024");
     const int nCol = nD ? nT * nD : nT;
-    THX_CHECK_ARG(volLayout == 0 || volLayout == 1, "thx_local_phase: volLayout must be 0 or 1");
+    THX_CHECK_ARG(volLayout >= 0 && volLayout <= 2, "thx_local_phase: volLayout must be 0, 1 or 2");
     THX_CHECK_ARG((long)nImg * ((nR + RT - 1) / RT) <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 &&
                       (nCol + TT - 1) / TT <= 65535,
                   "thx_local_phase: grid too large");
@@ -1128,11 +1288,14 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         auto pick = [&](auto c1, auto c2, auto c4, auto c6) {
             return nct == 1 ? c1 : nct == 2 ? c2 : nct == 4 ? c4 : c6;
         };
-        auto kern = volLayout == 1
-                        ? pick(k_local_fused<true, true, 1>, k_local_fused<true, true, 2>,
-                               k_local_fused<true, true, 4>, k_local_fused<true, true, 6>)
-                        : pick(k_local_fused<false, true, 1>, k_local_fused<false, true, 2>,
-                               k_local_fused<false, true, 4>, k_local_fused<false, true, 6>);
+        auto kern = volLayout == LAYOUT_CELLS
+                        ? pick(k_local_fused<LAYOUT_CELLS, true, 1>, k_local_fused<LAYOUT_CELLS, true, 2>,
+                               k_local_fused<LAYOUT_CELLS, true, 4>, k_local_fused<LAYOUT_CELLS, true, 6>)
+                    : volLayout == LAYOUT_BRICKS
+                        ? pick(k_local_fused<LAYOUT_BRICKS, true, 1>, k_local_fused<LAYOUT_BRICKS, true, 2>,
+                               k_local_fused<LAYOUT_BRICKS, true, 4>, k_local_fused<LAYOUT_BRICKS, true, 6>)
+                        : pick(k_local_fused<LAYOUT_FT, true, 1>, k_local_fused<LAYOUT_FT, true, 2>,
+                               k_local_fused<LAYOUT_FT, true, 4>, k_local_fused<LAYOUT_FT, true, 6>);
         grid.z = thx::cdiv(nCol, TT * nct);
         hipLaunchKernelGGL(kern, grid, dim3(THREADS), 0, s, reinterpret_cast<const float2*>(vol),
                            vdim, pf, quat, nR, trans, nCol, reinterpret_cast<const float2*>(dat),
@@ -1151,8 +1314,12 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
 #define THX_BIGBOX_MIN_R 300
 #endif
     const bool big = pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R;
-    auto kern = volLayout == 1 ? (big ? k_local_fused<true, false, 1, true> : k_local_fused<true>)
-                               : (big ? k_local_fused<false, false, 1, true> : k_local_fused<false>);
+    auto kern =
+        volLayout == LAYOUT_CELLS
+            ? (big ? k_local_fused<LAYOUT_CELLS, false, 1, true> : k_local_fused<LAYOUT_CELLS>)
+        : volLayout == LAYOUT_BRICKS
+            ? (big ? k_local_fused<LAYOUT_BRICKS, false, 1, true> : k_local_fused<LAYOUT_BRICKS>)
+            : (big ? k_local_fused<LAYOUT_FT, false, 1, true> : k_local_fused<LAYOUT_FT>);
     // one workgroup per image (nR <= 128, nT <= 16, the phases' 125 x 9):
     // the normalisation runs in the kernel's epilogue and dvp is only written
     // when the caller asks for it

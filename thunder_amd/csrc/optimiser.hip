@@ -27,6 +27,17 @@
 
 #include "common.h"
 
+#ifdef THX_DUMP_QUAT
+static double* g_quat_sink = nullptr;   // [popcount(mask)][nImg][mLR][4], device
+static unsigned g_quat_mask = 0;
+extern "C" int thx_debug_quat_sink(double* dst, unsigned phaseMask)
+{
+    g_quat_sink = dst;
+    g_quat_mask = phaseMask;
+    return 0;
+}
+#endif
+
 namespace thx {
 int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
                       const float* vol, int volLayout, int vdim, int pf, const double* quat, int nR,
@@ -972,6 +983,7 @@ struct Plan {
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
     double* bestR; double* bestT;                        // convergence: smallest variR / variT
     void* localWs; size_t localWsBytes;
+    float* bricks; size_t brickStride;   // bricked projectees (thx_volume_bricks), per class
     // CTF search: defocus precalculation, per-phase CTF table, D statistics
     float* freq; float* dfo; float* K1; float* K2; float* ctfD; float* wD;
     double* sdD; double* bestD; double* tmpD; int* topD;
@@ -1036,6 +1048,13 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.bestD = k.take<double>(on * nImg);
     p.tmpD = k.take<double>(nd * nImg);
     p.topD = k.take<int>(on * nImg);
+    // the phases gather from a bricked copy of every class's projectee
+    // (thx_volume_bricks, 1x the bytes) unless the caller gave volCells
+#ifndef THX_BRICKS
+#define THX_BRICKS 1
+#endif
+    p.brickStride = thx_volume_bricks_bytes(c.vdim) / sizeof(float);
+    p.bricks = THX_BRICKS && !c.volCells ? k.take<float>(p.brickStride * nK) : nullptr;
     p.bytes = k.off + 256;
     return p;
 }
@@ -1256,6 +1275,10 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     int* clsD = cls ? cls : p.cls;
     int* nPD = nPhaseOut ? nPhaseOut : p.nP;
     const int* clsSel = nK > 1 ? clsD : nullptr;    // rows / volumes picked per image
+    if (p.bricks)
+        for (int k = 0; k < nK; k++)
+            THX_RET(thx_volume_bricks(vol + 2 * dimSize * k, c.vdim, p.bricks + p.brickStride * k,
+                                      stream));
 
     if (global) {
         // ---- global scan of every class (ExpectRotran + ExpectProject + ExpectGlobal3D
@@ -1333,7 +1356,11 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     const int phase0 = global ? 1 : 0;
     const int nPh = c.converge ? c.maxPhase - phase0 : c.nPhase;
     const int* done = nullptr;
-    thx_local_sel sel{nullptr, nullptr, clsSel, (long long)dimSize};
+    // the phases' volume: the caller's cell copy, the bricked copies, or vol
+    const float* phaseVol = c.volCells ? c.volCells : p.bricks ? p.bricks : vol;
+    const int phaseLayout = c.volCells ? 1 : p.bricks ? 2 : 0;
+    thx_local_sel sel{nullptr, nullptr, clsSel,
+                      (long long)(p.bricks ? p.brickStride / 2 : dimSize)};
     if (c.converge) {
         THX_HIP(hipMemsetAsync(p.done, 0, sizeof(int) * nImg, s));
         hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
@@ -1367,10 +1394,18 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                    p.ctfD, stream));
         }
         const int pi = phase - phase0;
+#ifdef THX_DUMP_QUAT
+        // diagnostic build: the clouds the local phase evaluates (after perturb)
+        if (g_quat_sink && pi < 32 && ((g_quat_mask >> pi) & 1u)) {
+            const int slot = __builtin_popcount(g_quat_mask & ((1u << pi) - 1u));
+            THX_HIP(hipMemcpyAsync(g_quat_sink + (size_t)slot * nImg * c.mLR * 4, quat,
+                                   sizeof(double) * nImg * c.mLR * 4, hipMemcpyDeviceToDevice, s));
+        }
+#endif
         // phases past the caller's event pairs run untimed
         hipEvent_t* ev = pi < c.nPhaseEvents ? static_cast<hipEvent_t*>(c.phaseEvents) : nullptr;
         THX_RET(thx::local_phase_timed(&sel, ev ? ev[2 * pi] : nullptr, ev ? ev[2 * pi + 1] : nullptr,
-                                       c.volCells ? c.volCells : vol, c.volCells ? 1 : 0, c.vdim,
+                                       phaseVol, phaseLayout, c.vdim,
                                        c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT,
                                        dat, cs ? p.ctfD : ctf, sigRcp, iCol, iRow, pxOrder, nOrd,
                                        nPxl, c.idim, nImg, p.wC, p.wR, p.wT, p.base, p.localWs,

@@ -275,15 +275,38 @@ def volume_cells(vol):
     return out
 
 
-def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False, cells=None,
-                tiled=True):
-    """cells: optional thx_volume_cells copy of vol (used for the gathers).
-    tiled: visit pixels in px.order (LDS-staged neighbourhoods) instead of set order."""
-    vdim = _vol_dim(vol)
-    layout = 0
+def _layout(vol, cells, bricks):
+    """(volLayout, volume argument) of thx_local_phase for the given copies."""
+    if cells is not None and bricks is not None:
+        raise ValueError("cells and bricks are alternatives")
     if cells is not None:
         _req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
-        layout = 1
+        return 1, cells
+    if bricks is not None:
+        vdim = _vol_dim(vol)
+        _req(bricks, torch.complex64, (lib().thx_volume_bricks_bytes(vdim) // 8,), "bricks")
+        return 2, bricks
+    return 0, vol
+
+
+def volume_bricks(vol):
+    """Bricked copy (4 x 2 x 2 voxels per 128-B brick, the same bytes as vol):
+    the trilinear rows of a sample share cache lines (thx_volume_bricks)."""
+    vdim = _vol_dim(vol)
+    out = torch.empty(lib().thx_volume_bricks_bytes(vdim) // 8, dtype=torch.complex64,
+                      device=vol.device)
+    check(lib().thx_volume_bricks(_ptr(vol), vdim, _ptr(out), _stream(vol.device)),
+          "thx_volume_bricks")
+    return out
+
+
+def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False, cells=None,
+                tiled=True, bricks=None):
+    """cells / bricks: optional thx_volume_cells / thx_volume_bricks copy of
+    vol (used for the gathers and the staged boxes).
+    tiled: visit pixels in px.order (LDS-staged neighbourhoods) instead of set order."""
+    vdim = _vol_dim(vol)
+    layout, src = _layout(vol, cells, bricks)
     nImg, nPxl = _images(dat, ctf_, sig)
     if nPxl != px.n:
         raise ValueError("pixel set / image size mismatch")
@@ -303,7 +326,8 @@ def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False
                                                    len(px.order) if tiled else nPxl), dev)
     for l0 in range(0, nImg, 65535):
         nb = min(65535, nImg - l0)
-        check(lib().thx_local_phase(_ptr(cells if layout else vol), layout, vdim, px.pf, _ptr(quat[l0:]), nR, _ptr(trans[l0:]),
+        check(lib().thx_local_phase(_ptr(src), layout, vdim, px.pf, _ptr(quat[l0:]), nR,
+                                    _ptr(trans[l0:]),
                                     nT, _ptr(pC[l0:]), _ptr(pR[l0:]), _ptr(pT[l0:]), _ptr(dat[l0:]),
                                     _ptr(ctf_[l0:]), _ptr(sig[l0:]), _ptr(px.d_iCol),
                                     _ptr(px.d_iRow), _ptr(px.d_order) if tiled else None,
@@ -315,14 +339,11 @@ def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False
 
 
 def local_phase_d(vol, quat, trans, pC, pR, pT, pD, dat, ctfD, sig, px, want_dvp=False,
-                  cells=None, tiled=True):
+                  cells=None, tiled=True, bricks=None):
     """CTF-search phase (thx_local_phase_d): ctfD [nImg, nD, nPxl], pD [nImg, nD];
     returns wC, wR, wT, wD, baseL, dvp [nImg, nR, nT, nD] (or None)."""
     vdim = _vol_dim(vol)
-    layout = 0
-    if cells is not None:
-        _req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
-        layout = 1
+    layout, src = _layout(vol, cells, bricks)
     nImg, nPxl = dat.shape
     nR, nT, nD = quat.shape[1], trans.shape[1], pD.shape[1]
     dev = dat.device
@@ -347,7 +368,7 @@ def local_phase_d(vol, quat, trans, pC, pR, pT, pD, dat, ctfD, sig, px, want_dvp
     d = torch.empty(nImg, nR, nT, nD, dtype=torch.float32, device=dev) if want_dvp else None
     ws = workspace(lib().thx_local_phase_workspace(nImg, nR, nT * nD,
                                                    len(px.order) if tiled else nPxl), dev)
-    check(lib().thx_local_phase_d(None, _ptr(cells if layout else vol), layout, vdim, px.pf,
+    check(lib().thx_local_phase_d(None, _ptr(src), layout, vdim, px.pf,
                                   _ptr(quat), nR, _ptr(trans), nT, nD, _ptr(pC), _ptr(pR),
                                   _ptr(pT), _ptr(pD), _ptr(dat), _ptr(ctfD), _ptr(sig),
                                   _ptr(px.d_iCol), _ptr(px.d_iRow),

@@ -12,8 +12,18 @@ A "launch" is the whole launch sequence the bench times with HIP events
           cloud in the half-complex layout (first four 512-image
           k_local_fused<false> sequences), and the uniform cloud in the cell
           layout (k_local_fused<true>).
-Bytes: FETCH_SIZE x 1024 x 2 (FETCH_SIZE is in KiB and reads half of a wide
-read on gfx950) + WRITE_SIZE x 1024 -- MI355X_MICROARCH.md, HBM section.
+Bytes: FETCH_SIZE is 64 B per memory-side read request (TCC_EA0_RDREQ x 64),
+whatever the request's size.  profiles/r02_fetch_calibration.json measured
+what that means per access shape on gfx950: wide coalesced reads (128-B
+requests: streaming loads, LDS DMA, the staged box rows) are counted at half
+their bytes (x2), 64-B cell gathers exactly (x1), and 16-B pieces on separate
+rows (the half-complex interp_ft taps) as one 64-B request each -- 64 B
+moved per piece, so x1 is the HBM traffic there too.  Each summary carries the
+factor of its dominant access shape plus the two bounds (x1 .. x2) when the
+launch mixes shapes; WRITE_SIZE x 1024 is exact for streaming stores
+(MI355X_MICROARCH.md, HBM section).  When a pmc3 pass with TCC_EA0_RDREQ and
+TCC_EA0_RDREQ_128B (if the box lists it) exists, the split is exact:
+64 B x (RDREQ - RDREQ_128B) + 128 B x RDREQ_128B.
 
   python tools/traffic.py gpurun_out/TAG profiles/rNN_traffic.json
 """
@@ -50,27 +60,46 @@ def groups(disp, start, end):
     return out
 
 
-def summarise(rd, wr, start, end, pick, first=None):
+def _entry(fetch_kib, write_kib, factor, launches, kernels, shape):
+    r = fetch_kib * 1024 * factor
+    w = write_kib * 1024
+    return {"read_bytes": r, "write_bytes": w, "traffic_bytes": r + w, "launches": launches,
+            "fetch_factor": factor, "access_shape": shape,
+            "traffic_bytes_bounds": [fetch_kib * 1024 + w, fetch_kib * 2048 + w],
+            "kernels": kernels}
+
+
+def summarise(rd, wr, start, end, pick, factor, shape, first=None):
     gr = [g for g in groups(rd, start, end) if pick(g)][:first]
     gw = [g for g in groups(wr, start, end) if pick(g)][:first]
     if not gr or not gw:
         return None
-    r = sum(sum(v for _, _, v in g) for g in gr) / len(gr) * 1024 * 2
-    w = sum(sum(v for _, _, v in g) for g in gw) / len(gw) * 1024
-    return {"read_bytes": r, "write_bytes": w, "traffic_bytes": r + w, "launches": len(gr),
-            "kernels": [n.split("(")[0] for n, _, _ in gr[-1]]}
+    f = sum(sum(v for _, _, v in g) for g in gr) / len(gr)
+    w = sum(sum(v for _, _, v in g) for g in gw) / len(gw)
+    return _entry(f, w, factor, len(gr), [n.split("(")[0] for n, _, _ in gr[-1]], shape)
 
 
-def single(rd, wr, name, grid):
+def single(rd, wr, name, grid, factor, shape):
     """Average bytes per dispatch of one kernel at one grid size."""
     r = [v for n, g, v in rd if name in n and g == grid]
     w = [v for n, g, v in wr if name in n and g == grid]
     if not r or not w:
         return None
-    rb = sum(r) / len(r) * 1024 * 2
-    wb = sum(w) / len(w) * 1024
-    return {"read_bytes": rb, "write_bytes": wb, "traffic_bytes": rb + wb, "launches": len(r),
-            "kernels": [name]}
+    return _entry(sum(r) / len(r), sum(w) / len(w), factor, len(r), [name], shape)
+
+
+def exact_split(tag, name, grid):
+    """64 B x (RDREQ - RDREQ_128B) + 128 B x RDREQ_128B per dispatch, from a
+    pmc3 pass, or None."""
+    p = os.path.join(tag, "pmc3", "run_counter_collection.csv")
+    if not os.path.exists(p):
+        return None
+    req = [v for n, g, v in dispatches(p, "TCC_EA0_RDREQ_sum") if name in n and g == grid]
+    big = [v for n, g, v in dispatches(p, "TCC_EA0_RDREQ_128B_sum") if name in n and g == grid]
+    if not req or not big:
+        return None
+    a, b = sum(req) / len(req), sum(big) / len(big)
+    return {"read_bytes": 64 * (a - b) + 128 * b, "requests": a, "requests_128B": b}
 
 
 def main():
@@ -83,19 +112,25 @@ def main():
                   "FETCH_SIZE x2 on gfx950",
         "scan_4096": summarise(rd, wr, "k_prep_aconst", "k_scan_combine_bf",
                                lambda g: any("k_scan_split" in n and gr == scan_grid
-                                             for n, gr, _ in g)),
+                                             for n, gr, _ in g), 2, "streaming (128-B requests)"),
         # bench.local_roofline: 4 clustered-cloud launches (half-complex), then
         # 4 uniform ones, then 4 uniform in the cell-expanded layout
         "local_fullres_512": summarise(rd, wr, "k_patch_boxes", "k_local_fused",
                                        lambda g: any("k_local_fused<false" in n and gr == 512 * 512
-                                                     for n, gr, _ in g), first=4),
+                                                     for n, gr, _ in g), 2,
+                                       "staged box rows (128-B requests) + 16-B row taps", first=4),
         "local_fullres_512_uniform_cells": summarise(rd, wr, "k_patch_boxes", "k_local_fused",
                                                      lambda g: any("k_local_fused<true" in n
-                                                                   for n, _, _ in g)),
+                                                                   for n, _, _ in g), 1,
+                                                     "64-B cell gathers"),
         # the bench step's dominant kernel: one k_local_fused<false> launch per
         # phase over the whole 12 500-image batch (grid 12500 x 1 x 1 of 512)
-        "local_bench": single(rd, wr, "k_local_fused<false", 12500 * 512),
+        "local_bench": single(rd, wr, "k_local_fused<false", 12500 * 512, 2,
+                              "staged box rows + LDS DMA micro boxes (128-B requests)"),
     }
+    ex = exact_split(tag, "k_local_fused<false", 12500 * 512)
+    if ex and res["local_bench"]:
+        res["local_bench"]["exact_read"] = ex
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
