@@ -11,13 +11,18 @@ no collective on the expectation path.  Insert (mReco = 100), the RCCL
 half-map all-reduce (thx_halfmap_allreduce over each hemisphere's ranks) and
 the FSC are timed separately and reported as extra fields.
 
-`roofline` is the dominant kernel of the timed step, k_local_fused<false>
+`roofline` is the dominant kernel of the timed step, k_local_fused<0>
 (the particle-filter phase at global resolution), timed by HIP events the
 driver records around every one of its launches inside the timed region
-(thx_expect_cfg.phaseEvents) and priced at SURVEY §8(d)'s algorithmic FLOP
-(56 mLR nPxl + 15 mLR mLT nPxl per image-phase) against the FP32 peak.  The
-global scan and the full-resolution phase are reported beside it
-(roofline_scan, roofline_local).
+(thx_expect_cfg.phaseEvents).  It gathers its taps from the 1.9 MB
+low-resolution ball of the projectee, which stays in L2, so it is priced
+against the L2 -> L1 line bandwidth measured by tools/probes/l2_roof.hip
+(random 16-B row pieces, one 128-B line each: 34.4 TB/s, the guide's L2
+figure): `achieved` = SURVEY §8(d)'s 64 B of taps per rotation-pixel per
+launch / launch time, and the PMC line traffic of the same launches
+(tools/l2_lines.py: TCP_TCC_READ_REQ x 128 B) against the same roof says how
+close the kernel runs to it.  The global scan and the full-resolution phase
+are reported beside it (roofline_scan, roofline_local).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -107,6 +112,37 @@ def pmc_traffic():
         return {}, None
     with open(files[-1]) as f:
         return json.load(f), os.path.relpath(files[-1], ROOT)
+
+
+def newest_profile(pattern):
+    """The newest round's profiles/<pattern> file (rNN sorts by round), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    return files[-1] if files else None
+
+
+def l2_gather_roof():
+    """L2 -> L1 line bandwidth (TB/s) for random 16-B row pieces from an
+    L2-resident 2 MB table: tools/probes/l2_roof.hip, profiles/rNN_l2_roof.jsonl."""
+    f = newest_profile("r*_l2_roof.jsonl")
+    if not f:
+        return None, None
+    with open(f) as fh:
+        for line in fh:
+            d = json.loads(line)
+            if d["pattern"] == "line16" and abs(d["table_MB"] - 2.0) < 1e-6:
+                return d["line_TBps"], os.path.relpath(f, ROOT)
+    return None, None
+
+
+def l2_lines():
+    """Per-phase L1 -> L2 line requests of the bench's k_local_fused launches
+    (rocprofv3 --pmc TCP_TCC_READ_REQ, tools/l2_lines.py)."""
+    f = newest_profile("r*_l2_lines.json")
+    if not f:
+        return None, None
+    with open(f) as fh:
+        return json.load(fh), os.path.relpath(f, ROOT)
 
 
 def timed_events(fn, reps, stream):
@@ -408,7 +444,7 @@ def main():
         t = traffic.get(key) if ok else None
         return (t["traffic_bytes"], f"{traffic_src}: {key}") if t else (None, None)
 
-    # ---- dominant kernel of the timed step: k_local_fused<false>
+    # ---- dominant kernel of the timed step: k_local_fused<0> (half-complex layout)
     if local_ms:
         nL = chunks[0][1] - chunks[0][0]
         per_img = 56.0 * mR * px.n + 15.0 * mR * mT * px.n        # SURVEY §8(d), per image-phase
@@ -416,24 +452,47 @@ def main():
         t_launch = float(np.mean(local_ms)) / 1e3
         achieved = flop / t_launch / 1e12
         tr, tr_src = launch_traffic("local_bench", N == 256 and a.nr == 2000 and nL == 12500)
+        tap_bytes = 64.0 * mR * px.n * nL
+        roof, roof_src = l2_gather_roof()
+        roof = roof or 34.5           # MI355X_MICROARCH.md, L2 per XCD x 8
+        by_phase = ([float(np.mean(local_ms[k::a.phases])) for k in range(a.phases)]
+                    if len(local_ms) == a.phases * a.steps else None)
+        lines, lines_src = l2_lines() if (N == 256 and a.nr == 2000 and nL == 12500) else (None, None)
+        line_fields = {}
+        if lines and by_phase and len(lines["per_phase"]) == a.phases:
+            lb = [p["TCP_TCC_READ_REQ_sum"] * 128.0 for p in lines["per_phase"]]
+            rate = [b / (ms / 1e3) / 1e12 for b, ms in zip(lb, by_phase)]
+            line_fields = {
+                "l2_line_bytes_per_launch": float(np.mean(lb)),
+                "l2_line_TBps_by_phase": [round(r, 2) for r in rate],
+                "l2_line_frac_by_phase": [round(r / roof, 3) for r in rate],
+                "l2_line_frac": float(np.sum(lb) / (np.sum(by_phase) / 1e3) / 1e12 / roof),
+                "l2_lines_per_sample_by_phase": [round(p["TCP_TCC_READ_REQ_sum"] / (mR * px.n * nL), 2)
+                                                 for p in lines["per_phase"]],
+                "l2_hit_rate": float(lines["mean"]["TCC_HIT_sum"] /
+                                     (lines["mean"]["TCC_HIT_sum"] + lines["mean"]["TCC_MISS_sum"])),
+                "l2_lines_source": lines_src}
         extras["roofline"] = {
-            "bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved / PEAK_FP32_TFLOPS, "traffic": tr,
+            "bound": "l2", "achieved": tap_bytes / t_launch / 1e12, "peak": roof, "unit": "TB/s",
+            "frac": tap_bytes / t_launch / 1e12 / roof, "traffic": tr,
             "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
-            "kernel": f"k_local_fused<false> (particle-filter phase, nPxl={px.n}, {mR}x{mT}, "
+            "peak_source": roof_src or "MI355X_MICROARCH.md L2", **line_fields,
+            "kernel": f"k_local_fused<0> (particle-filter phase, nPxl={px.n}, {mR}x{mT}, "
                       f"{nL} images per launch)",
             "launch_ms": t_launch * 1e3, "launches_timed": len(local_ms),
             "launch_ms_by_phase": [round(float(np.mean(local_ms[k::a.phases])), 3)
                                    for k in range(a.phases)] if len(local_ms) == a.phases * a.steps else None,
             "share_of_step": float(np.sum(local_ms)) / (a.steps * ms_per_step),
             "algorithmic_flop_per_launch": flop,
-            "tap_bytes_per_launch": 64.0 * mR * px.n * nL,
-            "tap_rate_TBps": 64.0 * mR * px.n * nL / t_launch / 1e12,
+            "fp32_TFLOPs": achieved, "fp32_frac": achieved / PEAK_FP32_TFLOPS,
+            "tap_bytes_per_launch": tap_bytes,
             "note": "HIP events recorded by the driver on its launch stream around every "
-                    "k_local_fused launch of the timed steps; FP32 peak (the f32 MFMA rate equals "
-                    "the vector rate); algorithmic FLOP = 56 mLR nPxl (FP64 rotate, weights, 8-tap "
-                    "complex FMA) + 15 mLR mLT nPxl (direct likelihood) per image-phase, SURVEY 8(d); "
-                    "the 8 taps per rotation-pixel (64 B) come from LDS patch boxes, not HBM"}
+                    "k_local_fused launch of the timed steps; achieved = 64 B of taps per "
+                    "rotation-pixel (SURVEY 8(d)) per launch / launch time, peak = the L2 -> L1 "
+                    "line bandwidth for random 16-B row pieces (tools/probes/l2_roof.hip, = the "
+                    "guide's L2 figure); each tap row piece costs a 128-B line unless L1 or the "
+                    "LDS patch box serves it, so the line traffic (PMC, l2_line_*) runs at the roof "
+                    "while the algorithmic rate is a fraction of it"}
 
     if not a.no_extras:
         # ---- secondary: the global scan (bf16x3 MFMA) and its FP32-MFMA twin

@@ -52,7 +52,6 @@ namespace {
 
 constexpr int TAB_N = 100000;   // _kernelRL.init(MKB_RL_R2, 0, 1, 1e5) (src/Reconstructor.cpp:77-88)
 
-inline unsigned cdiv_i(int a, int b) { return (unsigned)((a + b - 1) / b); }
 
 // k of a half-complex index: i in [0, vdim/2], j, k wrapped to [-vdim/2, vdim/2)
 THX_DEV void ft_coord(long q, int vdim, int& i, int& j, int& k)
@@ -120,56 +119,94 @@ __global__ void k_c_from_tw(float2* __restrict__ C, const float* __restrict__ T,
     GRID_STRIDE(q, n) C[q] = make_float2(T[q] * W[q], 0.f);
 }
 
-// convoluteC in real space: c(i,j,k) * kernelRL(QUAD_3 / (N pf)^2) / nf,
-// scaled by 1/size of FFT::bw.  Grid: x over rows' i, y = j, z = k (no
-// per-element index decode).
-__global__ void __launch_bounds__(256) k_kernel_mul(float* __restrict__ c, int vdim,
-                                                    const float* __restrict__ tab, float nf,
-                                                    float scale)
+// Per-iteration passes: a workgroup covers a slab of RB_SPLIT-th of a k-plane
+// (flat over (j, i), i fastest, j by a magic-number division), so there are
+// few workgroups (one atomic each) and every thread streams hundreds of
+// elements.
+constexpr int RB_THREADS = 512, RB_SPLIT = 4;
+
+inline unsigned magic_u(unsigned d) { return d <= 1 ? 0u : 0xFFFFFFFFu / d + 1u; }
+__device__ __forceinline__ int udiv_m(int u, int d, unsigned m)
 {
-    const int j = blockIdx.y, k = blockIdx.z;
-    const int jj = j >= vdim / 2 ? j - vdim : j, kk = k >= vdim / 2 ? k - vdim : k;
+    return d <= 1 ? u : (int)__umulhi((unsigned)u, m);
+}
+
+// The real-space factor of convoluteC, kernelRL(QUAD_3 / (N pf)^2) / nf
+// scaled by 1/size of FFT::bw, per octant voxel (|i|, |j|, |k|), i fastest:
+// it depends on |r|^2 only, so the balancing passes read it coalesced (68 MB
+// at vdim 512) instead of gathering the 1e5-entry table per voxel.
+__global__ void k_kernel_octant(float* __restrict__ oct, int vdim, const float* __restrict__ tab,
+                                float nf, float scale)
+{
+    const int h1 = vdim / 2 + 1;
+    const long n = (long)h1 * h1 * h1;
     const float inv = 1.f / ((float)vdim * (float)vdim);
-    const int jk2 = jj * jj + kk * kk;
-    float* row = c + ((size_t)k * vdim + j) * vdim;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < vdim; i += gridDim.x * blockDim.x) {
-        const int ii = i >= vdim / 2 ? i - vdim : i;
-        const float x = (float)(ii * ii + jk2) * inv;
+    GRID_STRIDE(q, n)
+    {
+        const int a = (int)(q % h1);
+        const long bc = q / h1;
+        const int b = (int)(bc % h1), c = (int)(bc / h1);
+        const float x = (float)(a * a + b * b + c * c) * inv;
         const int t = min(TAB_N, (int)rintf(x / 1e-5f));          // TabFunction: _tab[AROUND((x - a) / s)]
-        row[i] = (row[i] * scale) * tab[t] / nf;
+        oct[q] = scale * tab[t] / nf;
+    }
+}
+
+// convoluteC in real space: c(i,j,k) * the octant factor of (|i|, |j|, |k|)
+__global__ void __launch_bounds__(RB_THREADS) k_kernel_mul(float* __restrict__ c, int vdim,
+                                                           const float* __restrict__ oct,
+                                                           unsigned mVdim)
+{
+    const int k = blockIdx.y;
+    const int h1 = vdim / 2 + 1;
+    const int ak = k > vdim / 2 ? vdim - k : k;
+    const int nPlane = vdim * vdim;
+    const int q0 = (int)((long)nPlane * blockIdx.x / RB_SPLIT);
+    const int q1 = (int)((long)nPlane * (blockIdx.x + 1) / RB_SPLIT);
+    float* plane = c + (size_t)k * nPlane;
+    const float* o = oct + (size_t)ak * h1 * h1;
+    for (int q = q0 + threadIdx.x; q < q1; q += RB_THREADS) {
+        const int j = udiv_m(q, vdim, mVdim), i = q - j * vdim;
+        const int ai = i > vdim / 2 ? vdim - i : i, aj = j > vdim / 2 ? vdim - j : j;
+        plane[q] *= o[aj * h1 + ai];
     }
 }
 
 // W /= max(|C|, 1e-6) inside the sphere; max | |C| - 1 | over the sphere;
 // fused with the next iteration's C = T W (the same pass over W)
-__global__ void __launch_bounds__(256) k_update_w(float* __restrict__ W, float2* __restrict__ C,
-                                                  const float* __restrict__ T, int vdim, long r2,
-                                                  unsigned* __restrict__ diffBits)
+__global__ void __launch_bounds__(RB_THREADS) k_update_w(float* __restrict__ W, float2* __restrict__ C,
+                                                         const float* __restrict__ T, int vdim, long r2,
+                                                         unsigned mNc, unsigned* __restrict__ diffBits)
 {
     const int nc = vdim / 2 + 1;
-    const int j = blockIdx.y, k = blockIdx.z;
-    const int jj = j >= vdim / 2 ? j - vdim : j, kk = k >= vdim / 2 ? k - vdim : k;
-    const long jk2 = (long)jj * jj + (long)kk * kk;
-    const size_t row = ((size_t)k * vdim + j) * nc;
+    const int k = blockIdx.y;
+    const int kk = k >= vdim / 2 ? k - vdim : k;
+    const int nPlane = vdim * nc;
+    const int q0 = (int)((long)nPlane * blockIdx.x / RB_SPLIT);
+    const int q1 = (int)((long)nPlane * (blockIdx.x + 1) / RB_SPLIT);
+    const size_t base = (size_t)k * nPlane;
     float dmax = 0.f;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nc; i += gridDim.x * blockDim.x) {
-        const size_t q = row + i;
-        float w = W[q];
-        if ((long)i * i + jk2 < r2) {
-            const float2 c = C[q];
-            const float a = sqrtf(c.x * c.x + c.y * c.y);
+    for (int q = q0 + threadIdx.x; q < q1; q += RB_THREADS) {
+        const int j = udiv_m(q, nc, mNc), i = q - j * nc;
+        const int jj = j >= vdim / 2 ? j - vdim : j;
+        const size_t e = base + q;
+        float w = W[e];
+        if ((long)i * i + (long)jj * jj + (long)kk * kk < r2) {
+            const float2 cv = C[e];
+            const float a = sqrtf(cv.x * cv.x + cv.y * cv.y);
             w = w / fmaxf(a, 1e-6f);
-            W[q] = w;
+            W[e] = w;
             dmax = fmaxf(dmax, fabsf(a - 1.f));
         }
-        C[q] = make_float2(T[q] * w, 0.f);
+        C[e] = make_float2(T[e] * w, 0.f);
     }
     dmax = wave_max(dmax);
-    __shared__ float s[4];
-    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = dmax;
+    __shared__ float sm[RB_THREADS / 64];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = dmax;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const float m = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
+        float m = sm[0];
+        for (int w = 1; w < RB_THREADS / 64; w++) m = fmaxf(m, sm[w]);
         if (m > 0.f) atomicMax(diffBits, __float_as_uint(m));   // non-negative floats order as their bits
     }
 }
@@ -354,6 +391,7 @@ extern "C" size_t thx_reconstruct_workspace(int N, int pf)
     k.take<float2>(dimSize);                      // C / pad
     k.take<float>((size_t)vdim * vdim * vdim);    // real space
     k.take<float>(TAB_N + 1);                     // kernel table
+    k.take<float>((size_t)(vdim / 2 + 1) * (vdim / 2 + 1) * (vdim / 2 + 1));   // kernel octant
     k.take<unsigned>(64);                         // diff
     k.take<char>(work);                           // hipFFT work area
     return k.off + 256;
@@ -387,6 +425,7 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
     float2* C = k.take<float2>(dimSize);
     float* rl = k.take<float>((size_t)vdim * vdim * vdim);
     float* tab = k.take<float>(TAB_N + 1);
+    float* oct = k.take<float>((size_t)(vdim / 2 + 1) * (vdim / 2 + 1) * (vdim / 2 + 1));
     unsigned* diff = k.take<unsigned>(64);
     void* fftWork = k.take<char>(work);
     THX_FFT(hipfftSetWorkArea(pl.c2r, fftWork));
@@ -418,19 +457,22 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
         float diffPrev = 3.4e38f;
         diffC = 3.4e38f;
         int nNoDec = 0;
-        const dim3 gRow(1, vdim, vdim), gRowRL(cdiv_i(vdim, 256), vdim, vdim);
+        const dim3 gSlab(RB_SPLIT, vdim), bSlab(RB_THREADS);
+        const unsigned mVdim = magic_u((unsigned)vdim), mNc = magic_u((unsigned)(vdim / 2 + 1));
         hipLaunchKernelGGL(k_c_from_tw, g, b, 0, s, C, T, W, nFT);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_kernel_octant, g, b, 0, s, oct, vdim, tab, nf, scaleBw);
         THX_LAUNCH_CHECK();
         unsigned* bits = nullptr;
         THX_HIP(hipHostMalloc(reinterpret_cast<void**>(&bits), sizeof(unsigned), 0));
         for (m = 0; m < 30; m++) {                                // MAX_N_ITER_BALANCE
             THX_FFT(hipfftExecC2R(pl.c2r, reinterpret_cast<hipfftComplex*>(C), rl));
-            hipLaunchKernelGGL(k_kernel_mul, gRowRL, b, 0, s, rl, vdim, tab, nf, scaleBw);
+            hipLaunchKernelGGL(k_kernel_mul, gSlab, bSlab, 0, s, rl, vdim, oct, mVdim);
             THX_LAUNCH_CHECK();
             THX_FFT(hipfftExecR2C(pl.r2c, rl, reinterpret_cast<hipfftComplex*>(C)));
             THX_HIP(hipMemsetAsync(diff, 0, sizeof(unsigned), s));
             // W update + the next iteration's C in one pass
-            hipLaunchKernelGGL(k_update_w, gRow, b, 0, s, W, C, T, vdim, r2, diff);
+            hipLaunchKernelGGL(k_update_w, gSlab, bSlab, 0, s, W, C, T, vdim, r2, mNc, diff);
             THX_LAUNCH_CHECK();
             THX_HIP(hipMemcpyAsync(bits, diff, sizeof(unsigned), hipMemcpyDeviceToHost, s));
             THX_HIP(hipStreamSynchronize(s));
