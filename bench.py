@@ -178,14 +178,15 @@ def scan_roofline(vol, px, gset, dat, ctf, sig, algo, reps=3):
     return sec, issued, algorithmic, peak
 
 
-def local_roofline(vol, N, pf, device, n_img=512, reps=3, spread=1.5):
+def local_roofline(vol, N, pf, device, n_img=512, reps=3, spreads=(1.5, 3.0, 0.0)):
     """Full-resolution particle-filter phase (nPxl = 24746 at box 256,
     mLR = 125, mLT = 9): algorithmic bytes 64 * mLR * nPxl + 16 * nPxl per
-    image-phase.  Two clouds: a local-search cloud (`spread` degrees around
-    one pose per image, the narrow clouds of a C5-style local refinement) in
-    the half-complex layout the driver uses, where the patch boxes stage the
-    taps in LDS; and uniformly random rotations (every tap a gather), in both
-    the half-complex and the cell-expanded layout."""
+    image-phase.  Clouds of `spreads` degrees around one pose per image (the
+    narrow clouds of a C5-style local refinement; 0 = uniformly random
+    rotations, every tap a gather), each in the half-complex layout (taps of
+    compact patches staged in LDS boxes, the rest gathered row by row) and
+    in the cell-expanded layout (every sample one quad-cooperative 64-B cell
+    read)."""
     rU = N // 2 - 2
     px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, 1, n_img, device, seed=17, vol=vol)
     rng = np.random.default_rng(3)
@@ -195,23 +196,21 @@ def local_roofline(vol, N, pf, device, n_img=512, reps=3, spread=1.5):
     pC = torch.ones(n_img, dtype=torch.float64, device=device)
     pR = torch.full((n_img, mR), 1.0 / mR, dtype=torch.float64, device=device)
     pT = torch.full((n_img, mT), 1.0 / mT, dtype=torch.float64, device=device)
-    qc = torch.as_tensor(np.ascontiguousarray(synth.clustered_quaternions(n_img, mR, spread, rng)),
-                         device=device)
-    qu = torch.as_tensor(synth.uniform_quaternions(n_img * mR, rng).reshape(n_img, mR, 4),
-                         device=device)
-    out = {}
-    out["clustered_ms"] = timed_events(lambda: ops.local_phase(vol, qc, trans, pC, pR, pT, dat, ctf,
-                                                               sig, px), reps, st) * 1e3
-    out["uniform_ms"] = timed_events(lambda: ops.local_phase(vol, qu, trans, pC, pR, pT, dat, ctf,
-                                                             sig, px), reps, st) * 1e3
     cells = ops.volume_cells(vol)
-    out["uniform_cells_ms"] = timed_events(lambda: ops.local_phase(vol, qu, trans, pC, pR, pT, dat,
-                                                                   ctf, sig, px, cells=cells),
-                                           reps, st) * 1e3
+    out = {"clouds": []}
+    for sp in spreads:
+        q = (synth.clustered_quaternions(n_img, mR, sp, rng) if sp > 0
+             else synth.uniform_quaternions(n_img * mR, rng).reshape(n_img, mR, 4))
+        q = torch.as_tensor(np.ascontiguousarray(q), device=device)
+        row = {"spread_deg": sp if sp > 0 else "uniform"}
+        for name, cl in (("halfcomplex", None), ("cells", cells)):
+            row[name + "_ms"] = timed_events(lambda: ops.local_phase(vol, q, trans, pC, pR, pT, dat,
+                                                                     ctf, sig, px, cells=cl),
+                                             reps, st) * 1e3
+        out["clouds"].append(row)
     del cells
     out["algo_bytes"] = n_img * (64.0 * mR * px.n + 16.0 * px.n)
     out["nPxl"] = px.n
-    out["spread_deg"] = spread
     out["n_img"] = n_img
     return out
 
@@ -531,21 +530,24 @@ def main():
         lr = local_roofline(vol, N, pf, dev)
         tr, tr_src = launch_traffic("local_fullres_512", N == 256)
         lbytes = lr["algo_bytes"]
-        lsec = lr["clustered_ms"] / 1e3
+        frac = lambda ms: lbytes / (ms / 1e3) / 1e9 / PEAK_HBM_GBS
+        clouds = []
+        for row in lr["clouds"]:
+            best = min(("halfcomplex", "cells"), key=lambda k: row[k + "_ms"])
+            clouds.append({**{k: (round(v, 3) if isinstance(v, float) else v) for k, v in row.items()},
+                           "frac_halfcomplex": round(frac(row["halfcomplex_ms"]), 3),
+                           "frac_cells": round(frac(row["cells_ms"]), 3), "best": best})
+        head = clouds[0]
+        lsec = min(head["halfcomplex_ms"], head["cells_ms"]) / 1e3
         extras["roofline_local"] = {
             "bound": "hbm", "achieved": lbytes / lsec / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": lbytes / lsec / 1e9 / PEAK_HBM_GBS, "traffic": tr,
             "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
             "algorithmic_bytes": lbytes,
             "kernel": f"local phase full-res (nPxl={lr['nPxl']}, 125x9, {lr['n_img']} images), "
-                      f"{lr['spread_deg']} deg local-search clouds, half-complex projectee "
-                      f"(the driver's layout), taps staged in LDS patch boxes",
-            "launch_ms": lr["clustered_ms"],
-            "uniform_rotations": {
-                "launch_ms_halfcomplex": lr["uniform_ms"],
-                "frac_halfcomplex": lbytes / (lr["uniform_ms"] / 1e3) / 1e9 / PEAK_HBM_GBS,
-                "launch_ms_cells": lr["uniform_cells_ms"],
-                "frac_cells": lbytes / (lr["uniform_cells_ms"] / 1e3) / 1e9 / PEAK_HBM_GBS}}
+                      f"{head['spread_deg']} deg local-search clouds, the faster projectee layout "
+                      f"({head['best']}); every cloud and layout in by_cloud",
+            "launch_ms": lsec * 1e3, "by_cloud": clouds}
         extras["insert_fullres"] = insert_fullres(vol, N, pf, dev)
 
         # ---- insert (mReco = 100) into the two hemispheres' half-maps, the

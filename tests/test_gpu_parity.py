@@ -169,8 +169,9 @@ def test_local_phase(orc, stack):
 
 
 def test_local_phase_cells_layout_and_many_rotations(orc, stack):
-    """The cell-expanded projectee gives the same gathers; mR > 128 and
-    mT > 16 exercise the multi-tile grid."""
+    """The cell-expanded projectee gives the same taps and weights (each
+    sample's 8 taps summed as a quad tree instead of in sequence, so equal
+    to FP32 rounding); mR > 128 and mT > 16 exercise the multi-tile grid."""
     s = stack
     px = dev_pixels(s)
     nImg, nR, nT = 2, 150, 20
@@ -186,8 +187,9 @@ def test_local_phase_cells_layout_and_many_rotations(orc, stack):
             T(s["sig"][:nImg]), px)
     a = ops.local_phase(vol, *args, want_dvp=True)
     b = ops.local_phase(vol, *args, want_dvp=True, cells=cells)
-    assert torch.equal(a[4], b[4])
-    d = a[4].cpu().numpy()
+    da, db = a[4].cpu().numpy(), b[4].cpu().numpy()
+    assert np.max(np.abs(da - db) / np.abs(da)) < 2e-6
+    d = db
     for l in range(nImg):
         *_, rd = orc.local_phase(s["vol"], s["vdim"], s["pf"], quat[l], trans[l], 1.0, pR[l],
                                  pT[l], s["dat"][l], s["ctf"][l], s["sig"][l], s["px"], s["N"])
@@ -250,7 +252,7 @@ def test_local_phase_staged_patches(orc, stack64, spread, lo, hi):
     a = ops.local_phase(vol, *args, want_dvp=True)
     b = ops.local_phase(vol, *args, want_dvp=True, tiled=False)
     c = ops.local_phase(vol, *args, want_dvp=True, cells=ops.volume_cells(vol))
-    assert torch.equal(a[4], c[4])
+    assert np.max(np.abs(c[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
     e = ops.local_phase(vol, *args, want_dvp=True, bricks=ops.volume_bricks(vol))
     assert torch.equal(a[4], e[4])      # the same taps in the same order from bricks
     da, db = a[4].cpu().numpy(), b[4].cpu().numpy()

@@ -92,6 +92,38 @@ THX_DEV float2 interp_cells(const float4* __restrict__ cells, int vdim, float x,
     return make_float2(re, conj ? -im : im);
 }
 
+// Quad-cooperative gather from the cell-expanded projectee: lane j (0..3) of
+// the quad that evaluates one sample reads the 16-B piece j of its 64-B cell
+// -- taps (dz, dy) = (j >> 1, j & 1), dx = 0, 1 -- so one wave instruction
+// covers 16 samples with 16 segment accesses (the L1 merges a quad's pieces:
+// tools/probes/l2_roof.hip coop64), against 64 row-piece accesses for 16
+// samples in the half-complex layout.  Returns the piece's weighted part of
+// interp_ft's sum (same weights; the quad sum is a tree).
+THX_DEV float2 interp_cell_piece(const float4* __restrict__ cells, int vdim, float x, float y,
+                                 float z, int j)
+{
+    const bool conj = !(x >= 0.f);
+    if (conj) { x = -x; y = -y; z = -z; }
+    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+    const float dx = x - fx, dy = y - fy, dz = z - fz;
+    const int nColFT = vdim / 2 + 1;
+    const size_t c = (((size_t)wrap_idx(z0, vdim) * vdim + wrap_idx(y0, vdim)) * nColFT + x0) * 4 + j;
+    const float4 q = cells[c];
+    const float wy = (j & 1) ? dy : 1.f - dy, wz = (j >> 1) ? dz : 1.f - dz;
+    const float w0 = (1.f - dx) * wy * wz, w1 = dx * wy * wz;
+    const float re = q.x * w0 + q.z * w1, im = q.y * w0 + q.w * w1;
+    return make_float2(re, conj ? -im : im);
+}
+
+// sum over the lanes of each quad (DPP quad permutations), every lane gets it
+THX_DEV float quad_sum(float v)
+{
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false));
+    return v;
+}
+
 // Bricked projectee (thx_volume_bricks): the half-complex volume in 128-B
 // bricks of 4 x 2 x 2 (x, y, z) voxels, x fastest inside a brick row, so the
 // four rows (y0, y0 + 1) x (z0, z0 + 1) of a trilinear cell share a brick
@@ -487,7 +519,7 @@ template <int LAYOUT, int NI = NIT, int CAP = BOX_CAP>
 THX_DEV void fetch_box(f32x4 (&pre)[NI][2], int (&dst)[NI], const Rec& b,
                        const float2* __restrict__ vol, int vdim, int tid)
 {
-    if (!(b.v[10] <= CAP)) return;
+    if (LAYOUT == LAYOUT_CELLS || !(b.v[10] <= CAP)) return;   // cells: never staged
     const int nColFT = vdim / 2 + 1;
     const int nq = b.v[6] >> 2, ny = b.v[8];
 #pragma unroll
@@ -640,12 +672,16 @@ k_local_fused(const float2* __restrict__ vol,
     static_assert(CS || NCT == 1, "column tiles per workgroup: CTF search only");
     constexpr int BOXC = BIGBOX ? BOX_CAP_BIG : BOX_CAP;
     constexpr int NITC = BOXC / 4 / THREADS;
-    auto staged = [](const Rec& r) { return r.v[10] <= BOXC; };
+    // the cell layout gathers every sample quad-cooperatively: no LDS box, no
+    // patch records (padding entries sample pixel (0, 0)), so a CU holds as
+    // many workgroups as the VGPRs allow
+    constexpr bool COOP = LAYOUT == LAYOUT_CELLS;
+    auto staged = [](const Rec& r) { return !COOP && r.v[10] <= BOXC; };
     constexpr int NC = NCT * TT;   // columns per workgroup
     const int r0 = blockIdx.y * RT, t0 = blockIdx.z * NC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nRl = min(RT, nR - r0);
-    __shared__ __attribute__((aligned(16))) float2 sBox[BOXC];
+    __shared__ __attribute__((aligned(16))) float2 sBox[COOP ? 8 : BOXC];
     __shared__ __attribute__((aligned(16))) float sB[KC * 2 * NC];   // [px][U, V][t]
     __shared__ __attribute__((aligned(16))) double2 sXY[KC];        // (iCol pf, iRow pf)
     __shared__ float sBq[CS ? KC * NC : KC];                         // b = s c^2 ([px][col] for CS)
@@ -662,7 +698,8 @@ k_local_fused(const float2* __restrict__ vol,
     const int rl = wv * 16 + (lane & 15);
     double m[6];
     {
-        const int r = r0 + slot_rotation(sPerm, rl, nRl);
+        // COOP: lane 4 r + j works on rotation slot 16 wv + r (its quad's sample)
+        const int r = r0 + slot_rotation(sPerm, COOP ? wv * 16 + (lane >> 2) : rl, nRl);
         double q[4], mm[9];
         for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
         quat_to_mat(q, mm);
@@ -711,8 +748,8 @@ k_local_fused(const float2* __restrict__ vol,
     Pix px = load_pix(stager ? patch_pixel(order, nVisit, bpx) : -1, iCol, iRow, D, C, S);
     load_cc(px.p);
     int pNext = stager ? patch_pixel(order, nVisit, KC + bpx) : -1;
-    Rec rc = load_rec(R);
-    Rec rn = nC > 1 ? load_rec(R + REC) : rc;
+    Rec rc = COOP ? Rec{} : load_rec(R);
+    Rec rn = COOP || nC <= 1 ? rc : load_rec(R + REC);
     f32x4 pre[NITC][2];
     int dst[NITC];
     fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rc, vol, vdim, tid);
@@ -763,7 +800,7 @@ k_local_fused(const float2* __restrict__ vol,
                 if (!CS) sBq[bpx] = ok ? px.s * px.c * px.c : 0.f;
                 sValid[bpx] = ok;
                 // padding entries sample the patch's first pixel (inside the box)
-                const int ic = ok ? px.ic : rc.v[17], ir = ok ? px.ir : rc.v[18];
+                const int ic = ok ? px.ic : COOP ? 0 : rc.v[17], ir = ok ? px.ir : COOP ? 0 : rc.v[18];
                 sXY[bpx] = make_double2((double)(ic * pf), (double)(ir * pf));
             }
         }
@@ -779,7 +816,7 @@ k_local_fused(const float2* __restrict__ vol,
                 pNext = patch_pixel(order, nVisit, (c + 2) * KC + bpx);
             }
             fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rn, vol, vdim, tid);
-            if (c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
+            if (!COOP && c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
         }
         STAMP(2);
         // ---- projection samples: this lane's rotation x pixels 4s + g
@@ -817,7 +854,64 @@ k_local_fused(const float2* __restrict__ vol,
             return THX_SKIP_PAD &&
                    !(sValid[4 * s] | sValid[4 * s + 1] | sValid[4 * s + 2] | sValid[4 * s + 3]);
         };
-        if (staged(rc)) {
+        // COOP step: quad r of the wave evaluates rotation 16 wv + r at the four
+        // pixels 4s + p, one cooperative cell read each, summed over the quad;
+        // the (re, im) of pixels (4s, 4s+2) and (4s+1, 4s+3) then reach the
+        // MFMA A layout (row r = lane & 15, k = lane >> 4) by ds_bpermute from
+        // lane 4 r + k of the quad layout
+        auto coop_step = [&](int s) {
+            const int j = lane & 3;
+            float2 P[4];
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                const double2 xy = sXY[4 * s + p];
+                const float x = (float)(m[0] * xy.x + m[3] * xy.y);
+                const float y = (float)(m[1] * xy.x + m[4] * xy.y);
+                const float z = (float)(m[2] * xy.x + m[5] * xy.y);
+                const float2 v = interp_cell_piece(reinterpret_cast<const float4*>(vol), vdim, x, y, z, j);
+                P[p] = make_float2(quad_sum(v.x), quad_sum(v.y));
+            }
+            if (!CS)
+#pragma unroll
+                for (int p = 0; p < 4; p++) bias += sBq[4 * s + p] * (P[p].x * P[p].x + P[p].y * P[p].y);
+            const int k = lane & 3;
+            const int src = (4 * (lane & 15) + (lane >> 4)) * 4;     // byte address of the source lane
+            const float v1 = k == 0 ? P[0].x : k == 1 ? P[0].y : k == 2 ? P[2].x : P[2].y;
+            const float v2 = k == 0 ? P[1].x : k == 1 ? P[1].y : k == 2 ? P[3].x : P[3].y;
+            const float a1 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v1)));
+            const float a2 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(v2)));
+            const int q0 = 4 * s + (kk < 2 ? 0 : 2), q1 = q0 + 1;
+#pragma unroll
+            for (int ct = 0; ct < NCT; ct++) {
+                const float b0 = sB[(q0 * 2 + (kk & 1)) * NC + ct * TT + tc];
+                const float b1 = sB[(q1 * 2 + (kk & 1)) * NC + ct * TT + tc];
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, b1, acc[ct], 0, 0, 0);
+            }
+            if (CS) {
+                const float u1 = k == 0 ? P[0].x * P[0].x : k == 1 ? P[0].y * P[0].y
+                               : k == 2 ? P[2].x * P[2].x : P[2].y * P[2].y;
+                const float u2 = k == 0 ? P[1].x * P[1].x : k == 1 ? P[1].y * P[1].y
+                               : k == 2 ? P[3].x * P[3].x : P[3].y * P[3].y;
+                const float c1 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(u1)));
+                const float c2 = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(u2)));
+#pragma unroll
+                for (int ct = 0; ct < NCT; ct++) {
+                    acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(c1, sBq[q0 * NC + ct * TT + tc],
+                                                                   acc[ct], 0, 0, 0);
+                    acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(c2, sBq[q1 * NC + ct * TT + tc],
+                                                                   acc[ct], 0, 0, 0);
+                }
+            }
+        };
+        if (COOP) {
+#pragma unroll 2
+            for (int s = 0; s < 4; s++) {
+                if (pad_step(s)) { MCOUNT(3); continue; }
+                MCOUNT(2);
+                coop_step(s);
+            }
+        } else if (staged(rc)) {
             const int nx = rc.v[6], sp = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
 #pragma unroll
             for (int s = 0; s < 4; s++) {
@@ -838,10 +932,8 @@ k_local_fused(const float2* __restrict__ vol,
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
                 const float z = (float)(m[2] * xy.x + m[5] * xy.y);
-                reduce_step(s, LAYOUT == LAYOUT_CELLS
-                                   ? interp_cells(reinterpret_cast<const float4*>(vol), vdim, x, y, z)
-                               : LAYOUT == LAYOUT_BRICKS ? interp_bricks(vol, vdim, x, y, z)
-                                                         : interp_ft(vol, vdim, x, y, z));
+                reduce_step(s, LAYOUT == LAYOUT_BRICKS ? interp_bricks(vol, vdim, x, y, z)
+                                                       : interp_ft(vol, vdim, x, y, z));
             }
         }
         STAMP(3);
@@ -869,8 +961,13 @@ k_local_fused(const float2* __restrict__ vol,
     aConst = wave_sum(aConst);
     if (lane == 0) sRed[wv] = aConst;
     // B_r: the four pixel slots of a rotation are lanes l, l + 16, l + 32, l + 48
-    bias += __shfl_xor(bias, 16, 64);
-    bias += __shfl_xor(bias, 32, 64);
+    // (COOP: every lane of quad r holds rotation r's whole sum)
+    if (COOP) {
+        bias = __shfl(bias, 4 * (lane & 15), 64);
+    } else {
+        bias += __shfl_xor(bias, 16, 64);
+        bias += __shfl_xor(bias, 32, 64);
+    }
     if (lane < 16) sBias[rl] = CS ? 0.f : bias;
     __syncthreads();
     float Al = 0.f;
@@ -1271,9 +1368,11 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     float* d = dvp ? dvp : ws.take<float>((size_t)nImg * nR * nCol);
     int* rec = ws.take<int>(rec_bytes(nImg, nR, nVisit) / sizeof(int));
     hipStream_t s = thx::as_stream(stream);
-    hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * thx::cdiv(nR, RT)), dim3(64 * PB_WAVES),
-                       0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct);
-    THX_LAUNCH_CHECK();
+    if (volLayout != LAYOUT_CELLS) {   // the cell layout's quad gathers use no patch boxes
+        hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * thx::cdiv(nR, RT)), dim3(64 * PB_WAVES),
+                           0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct);
+        THX_LAUNCH_CHECK();
+    }
     dim3 grid(nImg, thx::cdiv(nR, RT), thx::cdiv(nCol, TT));
     const long vs = cls ? (long)sel->volStride : 0L;
     if (evBeg) THX_HIP(hipEventRecord(evBeg, s));

@@ -5,6 +5,9 @@
 //   line8   : each lane 8 B from a random line (a single voxel)
 //   seg64   : each lane 64 B (4 x 16 B) from one random 64-B segment (a cell)
 //   stream  : 8 lanes per line, every byte of a line used (the L2 -> L1 peak)
+//   coop64  : lanes 4s .. 4s+3 read the four 16-B pieces of one random 64-B
+//             segment in one instruction (does the L1 merge a quad's pieces?)
+// A table that fits L1 (e.g. 0.016 MB) measures the L1 access rate alone.
 // Prints one JSON line per pattern: ms, loads/s, 128-B lines/s, and the line
 // bytes per second (lines x 128 B) -- the roof the local phase's L2 gathers
 // are priced against (bench.py roofline).
@@ -44,6 +47,11 @@ __global__ void __launch_bounds__(THREADS) k_roof(const float* __restrict__ t, u
             } else if (PAT == 2) { // seg64: 4 x 16 B of one 64-B segment
                 const f32x4* p = reinterpret_cast<const f32x4*>(t + (size_t)line * 32 + ((h >> 24) & 1) * 16);
                 v[u] = p[0] + p[1] + p[2] + p[3];
+            } else if (PAT == 4) { // coop64: a quad reads one 64-B segment
+                const unsigned hq = mix((gid >> 2) * 2654435761u + it * 977u + u);
+                const unsigned lq = hq % nLines;
+                v[u] = *reinterpret_cast<const f32x4*>(t + (size_t)lq * 32 + ((hq >> 24) & 1) * 16 +
+                                                       (threadIdx.x & 3) * 4);
             } else {               // stream: lanes 8k..8k+7 share a line
                 const unsigned l8 = mix((gid >> 3) * 977u + it * 31u + u) % nLines;
                 v[u] = *reinterpret_cast<const f32x4*>(t + (size_t)l8 * 32 + (threadIdx.x & 7) * 4);
@@ -68,24 +76,25 @@ int main(int argc, char** argv)
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    const char* names[4] = {"line16", "line8", "seg64", "stream"};
+    const char* names[5] = {"line16", "line8", "seg64", "stream", "coop64"};
     const double loads = (double)blocks * THREADS * ITERS;
     for (int rep = 0; rep < 2; rep++)
-        for (int p = 0; p < 4; p++) {
+        for (int p = 0; p < 5; p++) {
             hipEventRecord(a);
             if (p == 0) hipLaunchKernelGGL(k_roof<0>, dim3(blocks), dim3(THREADS), 0, 0, t, nLines, out);
             if (p == 1) hipLaunchKernelGGL(k_roof<1>, dim3(blocks), dim3(THREADS), 0, 0, t, nLines, out);
             if (p == 2) hipLaunchKernelGGL(k_roof<2>, dim3(blocks), dim3(THREADS), 0, 0, t, nLines, out);
             if (p == 3) hipLaunchKernelGGL(k_roof<3>, dim3(blocks), dim3(THREADS), 0, 0, t, nLines, out);
+            if (p == 4) hipLaunchKernelGGL(k_roof<4>, dim3(blocks), dim3(THREADS), 0, 0, t, nLines, out);
             hipEventRecord(b);
             hipEventSynchronize(b);
             float ms;
             hipEventElapsedTime(&ms, a, b);
             // distinct lines per load: 1 (line16, line8), 1 per 4 loads of a segment
             // counted as one lane-load of 64 B (seg64), 1/8 (stream)
-            const double lines = p == 3 ? loads / 8 : loads;
+            const double lines = p == 3 ? loads / 8 : p == 4 ? loads / 4 : loads;
             if (rep)
-                printf("{\"pattern\": \"%s\", \"table_MB\": %.1f, \"ms\": %.3f, \"lane_loads_per_s\": %.4g, "
+                printf("{\"pattern\": \"%s\", \"table_MB\": %.3f, \"ms\": %.3f, \"lane_loads_per_s\": %.4g, "
                        "\"lines_per_s\": %.4g, \"line_TBps\": %.3f}\n",
                        names[p], mb, ms, loads / ms * 1e3, lines / ms * 1e3, lines * 128 / ms / 1e9);
         }

@@ -116,19 +116,19 @@ def main():
         # bench.local_roofline: 4 clustered-cloud launches (half-complex), then
         # 4 uniform ones, then 4 uniform in the cell-expanded layout
         "local_fullres_512": summarise(rd, wr, "k_patch_boxes", "k_local_fused",
-                                       lambda g: any("k_local_fused<false" in n and gr == 512 * 512
+                                       lambda g: any("k_local_fused<0," in n and gr == 512 * 512
                                                      for n, gr, _ in g), 2,
                                        "staged box rows (128-B requests) + 16-B row taps", first=4),
         "local_fullres_512_uniform_cells": summarise(rd, wr, "k_patch_boxes", "k_local_fused",
-                                                     lambda g: any("k_local_fused<true" in n
+                                                     lambda g: any("k_local_fused<1," in n
                                                                    for n, _, _ in g), 1,
                                                      "64-B cell gathers"),
         # the bench step's dominant kernel: one k_local_fused<false> launch per
         # phase over the whole 12 500-image batch (grid 12500 x 1 x 1 of 512)
-        "local_bench": single(rd, wr, "k_local_fused<false", 12500 * 512, 2,
+        "local_bench": single(rd, wr, "k_local_fused<0,", 12500 * 512, 2,
                               "staged box rows + LDS DMA micro boxes (128-B requests)"),
     }
-    ex = exact_split(tag, "k_local_fused<false", 12500 * 512)
+    ex = exact_split(tag, "k_local_fused<0,", 12500 * 512)
     if ex and res["local_bench"]:
         res["local_bench"]["exact_read"] = ex
     with open(out, "w") as f:
