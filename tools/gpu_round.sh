@@ -1,11 +1,12 @@
 #!/bin/bash
 # One GPU-box pass: parity tests, headline bench, kernel-trace profile and HBM
 # PMC passes of the bench.  Run on the GPU box from the repo root:
-#   tools/gpu_round.sh TAG [tests|bench|prof|pmc ...]   (default: all four)
+#   tools/gpu_round.sh TAG [tests|bench|prof|pmc|lines|probe ...]
+#   (default: tests bench prof pmc lines)
 # Every step has its own time limit; the first failure ends the script.
 set -e
 tag=$1; shift
-steps=${*:-tests bench prof pmc}
+steps=${*:-tests bench prof pmc lines}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$tag
 mkdir -p $O
@@ -36,5 +37,16 @@ for s in $steps; do
             > $O/pmc$i.log 2>&1)
       done
       python3 $R/tools/traffic.py $O $O/traffic.json > /dev/null ;;
+    lines)
+      # L1 -> L2 line requests of the bench's k_local_fused launches (per phase)
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum \
+          TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_local_fused" --output-format csv \
+          -d $O/pmc_lines -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-extras \
+          --no-cpu-baseline > $O/pmc_lines.log 2>&1)
+      python3 $R/tools/l2_lines.py $O/pmc_lines $O/l2_lines.json > /dev/null ;;
+    probe)
+      for mb in 0.016 2 16 4096; do
+        timeout -k 10 120 $R/tools/probes/l2_roof_bin $mb >> $O/l2_roof.jsonl
+      done ;;
   esac
 done

@@ -4,14 +4,14 @@ passes of tools/gpu_round.sh (pmc1 = FETCH_SIZE, pmc2 = WRITE_SIZE, both run
 on `bench.py --steps 1 --warmup 0`).
 
 A "launch" is the whole launch sequence the bench times with HIP events
-(local_bench: the single k_local_fused<false> dispatch of a bench phase):
+(local_bench: the single k_local_fused<0> dispatch of a bench phase):
   scan  : k_prep_aconst .. k_scan_combine_bf of one thx_global_scan call whose
           k_scan_split grid is the 4096-image grid (bench.scan_roofline);
   local : k_patch_boxes .. k_local_fused of one thx_local_phase call of
           bench.local_roofline (full resolution, 512 images): the clustered
           cloud in the half-complex layout (first four 512-image
-          k_local_fused<false> sequences), and the uniform cloud in the cell
-          layout (k_local_fused<true>).
+          k_local_fused<0> sequences), and the 3-degree and uniform clouds in
+          the cell layout (k_local_fused<1>, 4 launches per cloud).
 Bytes: FETCH_SIZE is 64 B per memory-side read request (TCC_EA0_RDREQ x 64),
 whatever the request's size.  profiles/r02_fetch_calibration.json measured
 what that means per access shape on gfx950: wide coalesced reads (128-B
@@ -88,6 +88,17 @@ def single(rd, wr, name, grid, factor, shape):
     return _entry(sum(r) / len(r), sum(w) / len(w), factor, len(r), [name], shape)
 
 
+def sliced(rd, wr, name, grid, k, per, factor, shape):
+    """Average bytes per dispatch of the k-th run of `per` consecutive
+    dispatches of one kernel at one grid (bench.local_roofline: 1 + reps
+    launches per cloud and layout)."""
+    r = [v for n, g, v in rd if name in n and g == grid][k * per:(k + 1) * per]
+    w = [v for n, g, v in wr if name in n and g == grid][k * per:(k + 1) * per]
+    if not r or not w:
+        return None
+    return _entry(sum(r) / len(r), sum(w) / len(w), factor, len(r), [name], shape)
+
+
 def exact_split(tag, name, grid):
     """64 B x (RDREQ - RDREQ_128B) + 128 B x RDREQ_128B per dispatch, from a
     pmc3 pass, or None."""
@@ -113,17 +124,18 @@ def main():
         "scan_4096": summarise(rd, wr, "k_prep_aconst", "k_scan_combine_bf",
                                lambda g: any("k_scan_split" in n and gr == scan_grid
                                              for n, gr, _ in g), 2, "streaming (128-B requests)"),
-        # bench.local_roofline: 4 clustered-cloud launches (half-complex), then
-        # 4 uniform ones, then 4 uniform in the cell-expanded layout
+        # bench.local_roofline: per cloud (1.5 deg, 3 deg, uniform) 4 launches
+        # half-complex (k_patch_boxes + k_local_fused<0>), then 4 cell-layout
+        # launches (k_local_fused<1> alone)
         "local_fullres_512": summarise(rd, wr, "k_patch_boxes", "k_local_fused",
                                        lambda g: any("k_local_fused<0," in n and gr == 512 * 512
                                                      for n, gr, _ in g), 2,
                                        "staged box rows (128-B requests) + 16-B row taps", first=4),
-        "local_fullres_512_uniform_cells": summarise(rd, wr, "k_patch_boxes", "k_local_fused",
-                                                     lambda g: any("k_local_fused<1," in n
-                                                                   for n, _, _ in g), 1,
-                                                     "64-B cell gathers"),
-        # the bench step's dominant kernel: one k_local_fused<false> launch per
+        "local_fullres_512_3deg_cells": sliced(rd, wr, "k_local_fused<1,", 512 * 512, 1, 4, 1,
+                                               "64-B cell gathers"),
+        "local_fullres_512_uniform_cells": sliced(rd, wr, "k_local_fused<1,", 512 * 512, 2, 4, 1,
+                                                  "64-B cell gathers"),
+        # the bench step's dominant kernel: one k_local_fused<0> launch per
         # phase over the whole 12 500-image batch (grid 12500 x 1 x 1 of 512)
         "local_bench": single(rd, wr, "k_local_fused<0,", 12500 * 512, 2,
                               "staged box rows + LDS DMA micro boxes (128-B requests)"),
