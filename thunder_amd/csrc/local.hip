@@ -905,7 +905,12 @@ k_local_fused(const float2* __restrict__ vol,
             }
         };
         if (COOP) {
-#pragma unroll 2
+// all four steps unrolled: 16 cell reads in flight per wave (C5 +3-4 %,
+// full-res 1.5-3 deg 2-5 % over 2; profiles/r03_coop_unroll_ab.jsonl)
+#ifndef THX_COOP_UNROLL
+#define THX_COOP_UNROLL 4
+#endif
+#pragma unroll THX_COOP_UNROLL
             for (int s = 0; s < 4; s++) {
                 if (pad_step(s)) { MCOUNT(3); continue; }
                 MCOUNT(2);
