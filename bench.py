@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--images", type=int, default=12500, help="particle images per GPU per step")
+    p.add_argument("--streams", type=int, default=1,
+                   help="run the --chunk sub-batches concurrently on this many HIP streams "
+                        "(one host thread each)")
     p.add_argument("--chunk", type=int, default=0,
                    help="images per expectation launch (0: the whole batch in one launch; "
                         "288 GB of HBM holds the workspaces of all 12500)")
@@ -385,11 +388,37 @@ def main():
     # per phase when the batch runs as one expectation call)
     timer = ex.PhaseTimer(e, a.phases * max(1, a.steps)) if len(chunks) == 1 and a.phases else None
 
+    streams = [torch.cuda.Stream(dev) for _ in range(a.streams)] if a.streams > 1 else None
+
+    def run_chunks(cs, stream=None):
+        for c in cs:
+            l0, l1 = chunks[c]
+            if stream is None:
+                outs[c] = e.run(dat[l0:l1], ctf[l0:l1], sig[l0:l1], out=outs[c])
+            else:
+                with torch.cuda.stream(stream):
+                    outs[c] = e.run(dat[l0:l1], ctf[l0:l1], sig[l0:l1], out=outs[c])
+
     def step(i=None):
         if timer is not None and i is not None:
             timer.select(i * a.phases)
-        for c, (l0, l1) in enumerate(chunks):
-            outs[c] = e.run(dat[l0:l1], ctf[l0:l1], sig[l0:l1], out=outs[c])
+        if streams is None:
+            run_chunks(range(len(chunks)))
+            return
+        # sub-batches round-robin over the streams, one host thread per stream
+        # (the driver's calls release the GIL); the streams join the default one
+        import threading
+        cur = torch.cuda.current_stream(dev)
+        for st in streams:
+            st.wait_stream(cur)
+        th = [threading.Thread(target=run_chunks, args=(range(k, len(chunks), len(streams)), st))
+              for k, st in enumerate(streams)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for st in streams:
+            cur.wait_stream(st)
 
     log(rank, f"[bench] nPxl={px.n} nR={a.nr} nT={len(gset[1])} images/gpu={a.images}")
     if timer is not None:
