@@ -254,7 +254,9 @@ def test_local_phase_staged_patches(orc, stack64, spread, lo, hi):
     c = ops.local_phase(vol, *args, want_dvp=True, cells=ops.volume_cells(vol))
     assert np.max(np.abs(c[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
     e = ops.local_phase(vol, *args, want_dvp=True, bricks=ops.volume_bricks(vol))
-    assert torch.equal(a[4], e[4])      # the same taps in the same order from bricks
+    # the same taps from bricks; the half-complex phase may take the box-less
+    # route (interp_ft's unfused sum) where the bricked one stages (packed FMA)
+    assert np.max(np.abs(e[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
     da, db = a[4].cpu().numpy(), b[4].cpu().numpy()
     assert np.max(np.abs(da - db) / np.abs(db)) < 2e-6      # pixel summation order only
     for l in range(nImg):

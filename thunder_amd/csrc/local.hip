@@ -234,7 +234,7 @@ THX_DEV int udiv(int u, int d, unsigned m) { return d <= 1 ? u : (int)__umulhi((
 constexpr int BIG = 1 << 29;
 
 // The patch record from the folded-box bounds e (side 0 lo xyz, hi xyz; side 1).
-THX_DEV void store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __restrict__ out)
+THX_DEV int store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __restrict__ out)
 {
     const int nColFT = vdim / 2 + 1, half = vdim / 2;
     int o[REC] = {0};
@@ -286,6 +286,24 @@ THX_DEV void store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __re
     int4* dst = reinterpret_cast<int4*>(out);
     for (int k = 0; k < REC / 4; k++)
         dst[k] = make_int4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    return o[10];
+}
+
+// Route of a phase (FT layout, 64 KiB boxes): a sample of the images' patch
+// records is counted first (route[0] patches whose box fits, route[1]
+// patches); below THX_STAGE_MIN_PCT per cent staged, the phase gathers every
+// patch from L2 with the box-less kernel (6 waves per SIMD instead of 4, no
+// records), otherwise records are built for all images and the staged kernel
+// runs.  Both kernels are launched; the one not chosen exits at entry, so the
+// choice needs no host round trip.
+#ifndef THX_STAGE_MIN_PCT
+#define THX_STAGE_MIN_PCT 50
+#endif
+constexpr int ROUTE_SAMPLE = 16;   // every 16th image's records are counted
+
+THX_DEV bool route_nostage(const int* __restrict__ route)
+{
+    return (long)route[0] * 100 < (long)THX_STAGE_MIN_PCT * route[1];
 }
 
 #ifndef THX_SKIP_PAD
@@ -381,20 +399,26 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
                                                                int nVisit, int pf, int vdim,
                                                                int* __restrict__ rec,
                                                                const int* __restrict__ act,
-                                                               const int* __restrict__ nAct)
+                                                               const int* __restrict__ nAct,
+                                                               int* __restrict__ route = nullptr,
+                                                               int routeMode = 0)
 {
     __shared__ float sM[RT][6];
     __shared__ int sE[PB_WAVES][12][64];
     __shared__ unsigned sKey[RT];
     __shared__ int sPerm[RT];
+    // routeMode 1: count the records of every ROUTE_SAMPLE-th image into
+    // route; 2: build all records unless the count chose the box-less kernel
+    if (routeMode == 2 && route_nostage(route)) return;
     const int nC = (nVisit + KC - 1) / KC, nRT = (nR + RT - 1) / RT;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ry = blockIdx.x % nRT;
-    int l = blockIdx.x / nRT;
+    int l = (blockIdx.x / nRT) * (routeMode == 1 ? ROUTE_SAMPLE : 1);
     if (act) {                     // active-image list: slots past the count exit
         if (l >= *nAct) return;
         l = act[l];
     }
+    int nFit = 0, nAll = 0;
     const int nRl = min(RT, nR - ry * RT);
     const double* Q = quat + ((size_t)l * nR + ry * RT) * 4;
     rotation_slots(Q, nRl, threadIdx.x, sKey, sPerm);
@@ -485,9 +509,19 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
 #pragma unroll
                 for (int k = 0; k < 12; k++)
                     e[k] = (k % 6) < 3 ? min(e[k], sE[w][k][lane]) : max(e[k], sE[w][k][lane]);
-            store_rec(e, ic0, ir0, vdim, rec + (((size_t)l * nRT + ry) * nC + c) * REC);
+            const int nv = store_rec(e, ic0, ir0, vdim, rec + (((size_t)l * nRT + ry) * nC + c) * REC);
+            nFit += nv <= BOX_CAP;
+            nAll += 1;
         }
         __syncthreads();
+    }
+    if (routeMode == 1 && wv == 0) {
+        nFit = wave_sum(nFit);
+        nAll = wave_sum(nAll);
+        if (lane == 0) {
+            atomicAdd(&route[0], nFit);
+            atomicAdd(&route[1], nAll);
+        }
     }
 }
 
@@ -629,12 +663,14 @@ __device__ unsigned long long g_step_counts[4];
 // A CS workgroup covers NCT column tiles of 16 (up to 96 (t, d) columns), so
 // the projection -- the expensive part -- is gathered once for all of them;
 // each step then issues 4 NCT MFMAs against NCT accumulators.
-template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false>
+template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false, bool STAGE = true>
 // non-CS: two workgroups per CU (LDS-bound), 4 waves per SIMD, 128 VGPRs;
 // CS: the NCT accumulators and CTF prefetches need the 256-VGPR budget;
-// BIGBOX: 128 KiB of box, one workgroup per CU, twice the prefetch registers
+// BIGBOX: 128 KiB of box, one workgroup per CU, twice the prefetch registers;
+// no LDS box (cell layout, or STAGE = false): no box prefetch registers, so
+// 6 waves per SIMD (three workgroups per CU) for the L2 gathers
 __global__ void __launch_bounds__(THREADS)
-__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : 4)))
+__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : (LAYOUT == LAYOUT_CELLS || !STAGE) ? 6 : 4)))
 k_local_fused(const float2* __restrict__ vol,
                                                             int vdim, int pf,
                                                             const double* __restrict__ quat,
@@ -660,8 +696,11 @@ k_local_fused(const float2* __restrict__ vol,
                                                             float* __restrict__ wC = nullptr,
                                                             float* __restrict__ wR = nullptr,
                                                             float* __restrict__ wT = nullptr,
-                                                            float* __restrict__ baseL = nullptr)
+                                                            float* __restrict__ baseL = nullptr,
+                                                            const int* __restrict__ route = nullptr)
 {
+    // routed phases launch the staged and the box-less kernel; one exits
+    if (route && route_nostage(route) == STAGE) return;
     int l = blockIdx.x;
     if (act) {
         if (l >= *nAct) return;
@@ -676,12 +715,14 @@ k_local_fused(const float2* __restrict__ vol,
     // patch records (padding entries sample pixel (0, 0)), so a CU holds as
     // many workgroups as the VGPRs allow
     constexpr bool COOP = LAYOUT == LAYOUT_CELLS;
-    auto staged = [](const Rec& r) { return !COOP && r.v[10] <= BOXC; };
+    // STAGE = false: every patch gathered from L2 (no box, no records)
+    constexpr bool NOBOX = COOP || !STAGE;
+    auto staged = [](const Rec& r) { return !NOBOX && r.v[10] <= BOXC; };
     constexpr int NC = NCT * TT;   // columns per workgroup
     const int r0 = blockIdx.y * RT, t0 = blockIdx.z * NC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nRl = min(RT, nR - r0);
-    __shared__ __attribute__((aligned(16))) float2 sBox[COOP ? 8 : BOXC];
+    __shared__ __attribute__((aligned(16))) float2 sBox[NOBOX ? 8 : BOXC];
     __shared__ __attribute__((aligned(16))) float sB[KC * 2 * NC];   // [px][U, V][t]
     __shared__ __attribute__((aligned(16))) double2 sXY[KC];        // (iCol pf, iRow pf)
     __shared__ float sBq[CS ? KC * NC : KC];                         // b = s c^2 ([px][col] for CS)
@@ -748,11 +789,11 @@ k_local_fused(const float2* __restrict__ vol,
     Pix px = load_pix(stager ? patch_pixel(order, nVisit, bpx) : -1, iCol, iRow, D, C, S);
     load_cc(px.p);
     int pNext = stager ? patch_pixel(order, nVisit, KC + bpx) : -1;
-    Rec rc = COOP ? Rec{} : load_rec(R);
-    Rec rn = COOP || nC <= 1 ? rc : load_rec(R + REC);
+    Rec rc = NOBOX ? Rec{} : load_rec(R);
+    Rec rn = NOBOX || nC <= 1 ? rc : load_rec(R + REC);
     f32x4 pre[NITC][2];
     int dst[NITC];
-    fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rc, vol, vdim, tid);
+    if (!NOBOX) fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rc, vol, vdim, tid);
 
     __syncthreads();
 #ifdef THX_STEP_COUNT
@@ -800,7 +841,7 @@ k_local_fused(const float2* __restrict__ vol,
                 if (!CS) sBq[bpx] = ok ? px.s * px.c * px.c : 0.f;
                 sValid[bpx] = ok;
                 // padding entries sample the patch's first pixel (inside the box)
-                const int ic = ok ? px.ic : COOP ? 0 : rc.v[17], ir = ok ? px.ir : COOP ? 0 : rc.v[18];
+                const int ic = ok ? px.ic : NOBOX ? 0 : rc.v[17], ir = ok ? px.ir : NOBOX ? 0 : rc.v[18];
                 sXY[bpx] = make_double2((double)(ic * pf), (double)(ir * pf));
             }
         }
@@ -815,8 +856,8 @@ k_local_fused(const float2* __restrict__ vol,
                 load_cc(pNext);
                 pNext = patch_pixel(order, nVisit, (c + 2) * KC + bpx);
             }
-            fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rn, vol, vdim, tid);
-            if (!COOP && c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
+            if (!NOBOX) fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rn, vol, vdim, tid);
+            if (!NOBOX && c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
         }
         STAMP(2);
         // ---- projection samples: this lane's rotation x pixels 4s + g
@@ -1334,7 +1375,7 @@ extern "C" int thx_debug_step_counts(unsigned long long* out, int reset)
 
 extern "C" size_t thx_local_phase_workspace(int nImg, int nR, int nT, int nVisit)
 {
-    return dvp_bytes(nImg, nR, nT) + rec_bytes(nImg, nR, nVisit) + 512;
+    return dvp_bytes(nImg, nR, nT) + rec_bytes(nImg, nR, nVisit) + 256 + 768;
 }
 
 // nD = 0: the phase without CTF search; nD >= 1: CTF search over nD defocus
@@ -1372,10 +1413,34 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     thx::Carver ws(workspace, wsBytes);
     float* d = dvp ? dvp : ws.take<float>((size_t)nImg * nR * nCol);
     int* rec = ws.take<int>(rec_bytes(nImg, nR, nVisit) / sizeof(int));
+    int* route = ws.take<int>(64);
     hipStream_t s = thx::as_stream(stream);
-    if (volLayout != LAYOUT_CELLS) {   // the cell layout's quad gathers use no patch boxes
-        hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * thx::cdiv(nR, RT)), dim3(64 * PB_WAVES),
-                           0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct);
+    // big LDS boxes for large full-resolution pixel sets: the ring's outer
+    // radius in projectee voxels, pf sqrt(2 nPxl / pi), past THX_BIGBOX_MIN_R
+#ifndef THX_BIGBOX_MIN_R
+#define THX_BIGBOX_MIN_R 300
+#endif
+    const bool big = pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R;
+    // the staged / box-less route of a half-complex phase, chosen on the device
+    // from a sample of the patch records (route_nostage); THX_ROUTE = 0 keeps the
+    // staged kernel (A/B builds)
+#ifndef THX_ROUTE
+#define THX_ROUTE 1
+#endif
+    const bool routed = THX_ROUTE && volLayout == LAYOUT_FT && !nD && !big;
+    const unsigned nRT = thx::cdiv(nR, RT);
+    if (routed) {
+        THX_HIP(hipMemsetAsync(route, 0, 2 * sizeof(int), s));
+        hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)thx::cdiv(nImg, ROUTE_SAMPLE) * nRT),
+                           dim3(64 * PB_WAVES), 0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim,
+                           rec, act, nAct, route, 1);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * nRT), dim3(64 * PB_WAVES), 0, s, quat,
+                           nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct, route, 2);
+        THX_LAUNCH_CHECK();
+    } else if (volLayout != LAYOUT_CELLS) {   // the cell layout's quad gathers use no patch boxes
+        hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * nRT), dim3(64 * PB_WAVES), 0, s, quat,
+                           nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct, nullptr, 0);
         THX_LAUNCH_CHECK();
     }
     dim3 grid(nImg, thx::cdiv(nR, RT), thx::cdiv(nCol, TT));
@@ -1404,7 +1469,8 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         hipLaunchKernelGGL(kern, grid, dim3(THREADS), 0, s, reinterpret_cast<const float2*>(vol),
                            vdim, pf, quat, nR, trans, nCol, reinterpret_cast<const float2*>(dat),
                            ctf, sigRcp, iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, d, act, nAct,
-                           cls, vs, nD, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                           cls, vs, nD, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           nullptr);
         THX_LAUNCH_CHECK();
         if (evEnd) THX_HIP(hipEventRecord(evEnd, s));
         hipLaunchKernelGGL(k_local_weights_d, dim3(nImg), dim3(256), 0, s, d, nR, nT, nD, pC, pR,
@@ -1412,12 +1478,6 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         THX_LAUNCH_CHECK();
         return THX_OK;
     }
-    // big LDS boxes for large full-resolution pixel sets: the ring's outer
-    // radius in projectee voxels, pf sqrt(2 nPxl / pi), past THX_BIGBOX_MIN_R
-#ifndef THX_BIGBOX_MIN_R
-#define THX_BIGBOX_MIN_R 300
-#endif
-    const bool big = pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R;
     auto kern =
         volLayout == LAYOUT_CELLS
             ? (big ? k_local_fused<LAYOUT_CELLS, false, 1, true> : k_local_fused<LAYOUT_CELLS>)
@@ -1428,11 +1488,19 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     // the normalisation runs in the kernel's epilogue and dvp is only written
     // when the caller asks for it
     const bool fuse = grid.y == 1 && grid.z == 1;
-    hipLaunchKernelGGL(kern, grid, dim3(THREADS), 0, s, reinterpret_cast<const float2*>(vol), vdim,
-                       pf, quat, nR, trans, nT, reinterpret_cast<const float2*>(dat), ctf, sigRcp,
-                       iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, fuse ? dvp : d, act, nAct, cls,
-                       vs, 1, pC, pR, pT, fuse ? wC : nullptr, fuse ? wR : nullptr,
-                       fuse ? wT : nullptr, fuse ? baseL : nullptr);
+    auto launch = [&](auto k, const int* rt) {
+        hipLaunchKernelGGL(k, grid, dim3(THREADS), 0, s, reinterpret_cast<const float2*>(vol), vdim,
+                           pf, quat, nR, trans, nT, reinterpret_cast<const float2*>(dat), ctf, sigRcp,
+                           iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, fuse ? dvp : d, act, nAct,
+                           cls, vs, 1, pC, pR, pT, fuse ? wC : nullptr, fuse ? wR : nullptr,
+                           fuse ? wT : nullptr, fuse ? baseL : nullptr, rt);
+    };
+    if (routed) {
+        launch(k_local_fused<LAYOUT_FT, false, 1, false, true>, route);
+        launch(k_local_fused<LAYOUT_FT, false, 1, false, false>, route);
+    } else {
+        launch(kern, nullptr);
+    }
     THX_LAUNCH_CHECK();
     if (evEnd) THX_HIP(hipEventRecord(evEnd, s));
     if (!fuse) {

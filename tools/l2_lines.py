@@ -27,9 +27,31 @@ def main():
                     name = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"])
                     if "k_local_fused" not in name or int(r["Grid_Size"]) != 12500 * 512:
                         continue
-                    d = rows.setdefault(int(r["Dispatch_Id"]), {})
+                    d = rows.setdefault(int(r["Dispatch_Id"]),
+                                        {"_nostage": re.search(r"false, false>", name) is not None})
                     d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    phases = [rows[k] for k in sorted(rows)]
+    # a routed phase is two dispatches (the staged kernel, then the box-less
+    # one; the one not chosen exits at entry): sum consecutive dispatches into
+    # phases, a phase closing on the box-less variant (STAGE = false) or when
+    # the next dispatch is a staged one
+    phases, cur = [], None
+    for k in sorted(rows):
+        d = rows[k]
+        nostage = d.pop("_nostage")
+        if cur is None:
+            cur = dict(d)
+        else:
+            if not nostage:                 # a staged dispatch opens a new phase
+                phases.append(cur)
+                cur = dict(d)
+                continue
+            for c, v in d.items():
+                cur[c] = cur.get(c, 0.0) + v
+        if nostage:
+            phases.append(cur)
+            cur = None
+    if cur is not None:
+        phases.append(cur)
     if not phases:
         sys.exit("no k_local_fused dispatches at the bench grid")
     keys = sorted(phases[0])

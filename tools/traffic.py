@@ -79,13 +79,16 @@ def summarise(rd, wr, start, end, pick, factor, shape, first=None):
     return _entry(f, w, factor, len(gr), [n.split("(")[0] for n, _, _ in gr[-1]], shape)
 
 
-def single(rd, wr, name, grid, factor, shape):
-    """Average bytes per dispatch of one kernel at one grid size."""
+def single(rd, wr, name, grid, factor, shape, per=1):
+    """Average bytes per launch of one kernel at one grid size; `per`
+    consecutive dispatches make one launch (a routed phase dispatches the
+    staged and the box-less variant, one of them exits at entry)."""
     r = [v for n, g, v in rd if name in n and g == grid]
     w = [v for n, g, v in wr if name in n and g == grid]
     if not r or not w:
         return None
-    return _entry(sum(r) / len(r), sum(w) / len(w), factor, len(r), [name], shape)
+    return _entry(sum(r) / len(r) * per, sum(w) / len(w) * per, factor, len(r) // per, [name],
+                  shape)
 
 
 def sliced(rd, wr, name, grid, k, per, factor, shape):
@@ -138,7 +141,7 @@ def main():
         # the bench step's dominant kernel: one k_local_fused<0> launch per
         # phase over the whole 12 500-image batch (grid 12500 x 1 x 1 of 512)
         "local_bench": single(rd, wr, "k_local_fused<0,", 12500 * 512, 2,
-                              "staged box rows + LDS DMA micro boxes (128-B requests)"),
+                              "staged box rows (128-B requests) + 16-B row taps", per=2),
     }
     ex = exact_split(tag, "k_local_fused<0,", 12500 * 512)
     if ex and res["local_bench"]:
