@@ -91,15 +91,17 @@ def single(rd, wr, name, grid, factor, shape, per=1):
                   shape)
 
 
-def sliced(rd, wr, name, grid, k, per, factor, shape):
-    """Average bytes per dispatch of the k-th run of `per` consecutive
-    dispatches of one kernel at one grid (bench.local_roofline: 1 + reps
-    launches per cloud and layout)."""
-    r = [v for n, g, v in rd if name in n and g == grid][k * per:(k + 1) * per]
-    w = [v for n, g, v in wr if name in n and g == grid][k * per:(k + 1) * per]
+def sliced(rd, wr, name, grid, k, per, factor, shape, pair=1):
+    """Average bytes per launch of the k-th run of `per` consecutive launches
+    of one kernel at one grid (bench.local_roofline: 1 + reps launches per
+    cloud and layout); `pair` dispatches make one launch (routed phases)."""
+    n0, n1 = k * per * pair, (k + 1) * per * pair
+    r = [v for n, g, v in rd if name in n and g == grid][n0:n1]
+    w = [v for n, g, v in wr if name in n and g == grid][n0:n1]
     if not r or not w:
         return None
-    return _entry(sum(r) / len(r), sum(w) / len(w), factor, len(r), [name], shape)
+    return _entry(sum(r) / len(r) * pair, sum(w) / len(w) * pair, factor, len(r) // pair, [name],
+                  shape)
 
 
 def exact_split(tag, name, grid):
@@ -130,10 +132,10 @@ def main():
         # bench.local_roofline: per cloud (1.5 deg, 3 deg, uniform) 4 launches
         # half-complex (k_patch_boxes + k_local_fused<0>), then 4 cell-layout
         # launches (k_local_fused<1> alone)
-        "local_fullres_512": summarise(rd, wr, "k_patch_boxes", "k_local_fused",
-                                       lambda g: any("k_local_fused<0," in n and gr == 512 * 512
-                                                     for n, gr, _ in g), 2,
-                                       "staged box rows (128-B requests) + 16-B row taps", first=4),
+        # a routed half-complex phase is two dispatches (staged / box-less
+        # variant, one exits at entry): the grid is 512 workgroups x 512 threads
+        "local_fullres_512": sliced(rd, wr, "k_local_fused<0,", 512 * 512, 0, 4, 2,
+                                    "staged box rows (128-B requests) + 16-B row taps", pair=2),
         "local_fullres_512_3deg_cells": sliced(rd, wr, "k_local_fused<1,", 512 * 512, 1, 4, 1,
                                                "64-B cell gathers"),
         "local_fullres_512_uniform_cells": sliced(rd, wr, "k_local_fused<1,", 512 * 512, 2, 4, 1,
