@@ -663,6 +663,9 @@ __device__ unsigned long long g_step_counts[4];
 // A CS workgroup covers NCT column tiles of 16 (up to 96 (t, d) columns), so
 // the projection -- the expensive part -- is gathered once for all of them;
 // each step then issues 4 NCT MFMAs against NCT accumulators.
+#ifndef THX_NOBOX_WAVES
+#define THX_NOBOX_WAVES 6
+#endif
 template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false, bool STAGE = true>
 // non-CS: two workgroups per CU (LDS-bound), 4 waves per SIMD, 128 VGPRs;
 // CS: the NCT accumulators and CTF prefetches need the 256-VGPR budget;
@@ -670,7 +673,7 @@ template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false, bool ST
 // no LDS box (cell layout, or STAGE = false): no box prefetch registers, so
 // 6 waves per SIMD (three workgroups per CU) for the L2 gathers
 __global__ void __launch_bounds__(THREADS)
-__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : (LAYOUT == LAYOUT_CELLS || !STAGE) ? 6 : 4)))
+__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : (LAYOUT == LAYOUT_CELLS || !STAGE) ? THX_NOBOX_WAVES : 4)))
 k_local_fused(const float2* __restrict__ vol,
                                                             int vdim, int pf,
                                                             const double* __restrict__ quat,
