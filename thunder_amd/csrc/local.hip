@@ -722,14 +722,24 @@ k_local_fused(const float2* __restrict__ vol,
     constexpr bool NOBOX = COOP || !STAGE;
     auto staged = [](const Rec& r) { return !NOBOX && r.v[10] <= BOXC; };
     constexpr int NC = NCT * TT;   // columns per workgroup
+    // box-less kernels stage PP patches' image tiles per barrier pair (fewer
+    // barriers, 4 PP independent steps between them); CS keeps one.  PP 2:
+    // full-res cells -2.5 %, the bench's phases unchanged; PP 4 needs two
+    // image-tile elements per thread and spills (profiles/r03_nobox_pp_ab.jsonl)
+#ifndef THX_NOBOX_PP
+#define THX_NOBOX_PP 2
+#endif
+    constexpr int PP = (LAYOUT == LAYOUT_CELLS || !STAGE) && !CS ? THX_NOBOX_PP : 1;
+    constexpr int PKC = PP * KC;                        // pixels per iteration
+    constexpr int NE = (PKC * TT + THREADS - 1) / THREADS;   // image-tile elements per thread
     const int r0 = blockIdx.y * RT, t0 = blockIdx.z * NC;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nRl = min(RT, nR - r0);
     __shared__ __attribute__((aligned(16))) float2 sBox[NOBOX ? 8 : BOXC];
-    __shared__ __attribute__((aligned(16))) float sB[KC * 2 * NC];   // [px][U, V][t]
-    __shared__ __attribute__((aligned(16))) double2 sXY[KC];        // (iCol pf, iRow pf)
-    __shared__ float sBq[CS ? KC * NC : KC];                         // b = s c^2 ([px][col] for CS)
-    __shared__ int sValid[KC];                                       // 0: padding entry
+    __shared__ __attribute__((aligned(16))) float sB[PKC * 2 * NC];  // [px][U, V][t]
+    __shared__ __attribute__((aligned(16))) double2 sXY[PKC];       // (iCol pf, iRow pf)
+    __shared__ float sBq[CS ? KC * NC : PKC];                        // b = s c^2 ([px][col] for CS)
+    __shared__ int sValid[PKC];                                      // 0: padding entry
     __shared__ float sTr[NC][2];
     __shared__ float sRed[NWAVE];
     __shared__ float sBias[RT];
@@ -783,15 +793,23 @@ k_local_fused(const float2* __restrict__ vol,
 #pragma unroll
     for (int ct = 0; ct < NCT; ct++) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
     float bias = 0.f, aConst = 0.f;
-    // image-tile element staged by threads tid < KC * TT
-    const bool stager = tid < KC * TT;
+    // image-tile elements tid + j THREADS (< PKC TT): pixel bpx + j THREADS / TT
+    // of the iteration's PKC, column bt
+    constexpr int PSTEP = THREADS / TT;
+    auto stager = [&](int j) { return tid + j * THREADS < PKC * TT; };
     const int g = lane >> 4;       // pixel slot of this lane in a step
     const int kk = lane >> 4, tc = lane & 15;   // B-operand row / column
 
-    // pipeline prologue: patch 0 data + box, patch 1 order entry + record
-    Pix px = load_pix(stager ? patch_pixel(order, nVisit, bpx) : -1, iCol, iRow, D, C, S);
-    load_cc(px.p);
-    int pNext = stager ? patch_pixel(order, nVisit, KC + bpx) : -1;
+    // pipeline prologue: patches 0 .. PP-1 data + box, the next PP's order
+    // entries + record
+    Pix px[NE];
+    int pNext[NE];
+#pragma unroll
+    for (int j = 0; j < NE; j++) {
+        px[j] = load_pix(stager(j) ? patch_pixel(order, nVisit, bpx + j * PSTEP) : -1, iCol, iRow, D, C, S);
+        pNext[j] = stager(j) ? patch_pixel(order, nVisit, PKC + bpx + j * PSTEP) : -1;
+    }
+    load_cc(px[0].p);
     Rec rc = NOBOX ? Rec{} : load_rec(R);
     Rec rn = NOBOX || nC <= 1 ? rc : load_rec(R + REC);
     f32x4 pre[NITC][2];
@@ -808,7 +826,7 @@ k_local_fused(const float2* __restrict__ vol,
 #else
 #define STAMP(k) do {} while (0)
 #endif
-    for (int c = 0; c < nC; c++) {
+    for (int c = 0; c < nC; c += PP) {
         // ---- stage patch c: box voxels, image tile B[px][U, V][t], b, (iCol, iRow) pf
         if (staged(rc)) {
             f32x4* box4 = reinterpret_cast<f32x4*>(sBox);
@@ -821,43 +839,49 @@ k_local_fused(const float2* __restrict__ vol,
                 }
             }
         }
-        if (stager) {
-            const bool ok = px.p >= 0;
+#pragma unroll
+        for (int j = 0; j < NE; j++) {
+            if (!stager(j)) continue;
+            const Pix& x = px[j];
+            const int q = bpx + j * PSTEP;      // pixel of the iteration
+            const bool ok = x.p >= 0;
 #pragma unroll
             for (int ct = 0; ct < NCT; ct++) {
                 const int col = ct * TT + bt;
-                const float cv = CS ? cc[ct] : px.c;
+                const float cv = CS ? cc[ct] : x.c;
                 float U = 0.f, V = 0.f;
                 if (ok && t0 + col < nT) {
-                    const float k2 = -2.f * px.s * cv;
-                    const float yr = k2 * px.d.x, yi = k2 * px.d.y;
-                    const float2 T = phase_shift(px.ic, px.ir, sTr[col][0], sTr[col][1]);
+                    const float k2 = -2.f * x.s * cv;
+                    const float yr = k2 * x.d.x, yi = k2 * x.d.y;
+                    const float2 T = phase_shift(x.ic, x.ir, sTr[col][0], sTr[col][1]);
                     U = yr * T.x + yi * T.y;
                     V = yi * T.x - yr * T.y;
                 }
-                sB[(bpx * 2) * NC + col] = U;
-                sB[(bpx * 2 + 1) * NC + col] = V;
-                if (CS) sBq[bpx * NC + col] = ok && t0 + col < nT ? px.s * cv * cv : 0.f;
+                sB[(q * 2) * NC + col] = U;
+                sB[(q * 2 + 1) * NC + col] = V;
+                if (CS) sBq[q * NC + col] = ok && t0 + col < nT ? x.s * cv * cv : 0.f;
             }
             if (bt == 0) {
-                if (ok) aConst += px.s * (px.d.x * px.d.x + px.d.y * px.d.y);
-                if (!CS) sBq[bpx] = ok ? px.s * px.c * px.c : 0.f;
-                sValid[bpx] = ok;
+                if (ok) aConst += x.s * (x.d.x * x.d.x + x.d.y * x.d.y);
+                if (!CS) sBq[q] = ok ? x.s * x.c * x.c : 0.f;
+                sValid[q] = ok;
                 // padding entries sample the patch's first pixel (inside the box)
-                const int ic = ok ? px.ic : NOBOX ? 0 : rc.v[17], ir = ok ? px.ir : NOBOX ? 0 : rc.v[18];
-                sXY[bpx] = make_double2((double)(ic * pf), (double)(ir * pf));
+                const int ic = ok ? x.ic : NOBOX ? 0 : rc.v[17], ir = ok ? x.ir : NOBOX ? 0 : rc.v[18];
+                sXY[q] = make_double2((double)(ic * pf), (double)(ir * pf));
             }
         }
         STAMP(0);
         __syncthreads();
         STAMP(1);
-        // ---- prefetch patch c + 1 (in flight during the gathers below)
+        // ---- prefetch patches c + PP .. (in flight during the gathers below)
         Rec r2 = rn;
-        if (c + 1 < nC) {
-            if (stager) {
-                px = load_pix(pNext, iCol, iRow, D, C, S);
-                load_cc(pNext);
-                pNext = patch_pixel(order, nVisit, (c + 2) * KC + bpx);
+        if (c + PP < nC) {
+#pragma unroll
+            for (int j = 0; j < NE; j++) {
+                if (!stager(j)) continue;
+                px[j] = load_pix(pNext[j], iCol, iRow, D, C, S);
+                if (j == 0) load_cc(pNext[0]);
+                pNext[j] = patch_pixel(order, nVisit, (c + 2 * PP) * KC + bpx + j * PSTEP);
             }
             if (!NOBOX) fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rn, vol, vdim, tid);
             if (!NOBOX && c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
@@ -955,7 +979,7 @@ k_local_fused(const float2* __restrict__ vol,
 #define THX_COOP_UNROLL 4
 #endif
 #pragma unroll THX_COOP_UNROLL
-            for (int s = 0; s < 4; s++) {
+            for (int s = 0; s < 4 * PP; s++) {
                 if (pad_step(s)) { MCOUNT(3); continue; }
                 MCOUNT(2);
                 coop_step(s);
@@ -963,7 +987,7 @@ k_local_fused(const float2* __restrict__ vol,
         } else if (staged(rc)) {
             const int nx = rc.v[6], sp = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
 #pragma unroll
-            for (int s = 0; s < 4; s++) {
+            for (int s = 0; s < 4 * PP; s++) {
                 if (pad_step(s)) { MCOUNT(3); continue; }
                 MCOUNT(0);
                 const double2 xy = sXY[4 * s + g];
@@ -974,7 +998,7 @@ k_local_fused(const float2* __restrict__ vol,
             }
         } else {
 #pragma unroll 2
-            for (int s = 0; s < 4; s++) {
+            for (int s = 0; s < 4 * PP; s++) {
                 if (pad_step(s)) { MCOUNT(3); continue; }
                 MCOUNT(2);
                 const double2 xy = sXY[4 * s + g];
