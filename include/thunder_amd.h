@@ -444,6 +444,19 @@ int thx_local_phase2d(const float* vol, int vdim, int pf, const int* cls, const 
                       const int* iCol, const int* iRow, int nPxl, int idim, int nImg, float* wC,
                       float* wR, float* wT, float* baseL, float* dvp, void* workspace,
                       size_t wsBytes, thx_stream_t stream);
+/* thx_local_phase2d_d -- the 2D phase with CTF search (ExpectLocalPreI2D +
+ *   ExpectLocalM with cSearch; kernel_logDataVSLC / kernel_UpdateWLC,
+ *   gpu/src/Kernel.cu:889-939, 1459-1554, on the 2D projections): columns are
+ *   the nT x nD (t, d) pairs, ctfD [nImg][nD][nPxl] (thx_ctf_search), priors
+ *   pD / marginal wD [nImg][nD]; dvp (optional) [nImg][nR][nT][nD]. */
+size_t thx_local_phase2d_d_workspace(int nImg, int nR, int nT, int nD);
+int thx_local_phase2d_d(const float* vol, int vdim, int pf, const int* cls, const double* rot,
+                        int nR, const double* trans, int nT, int nD, const double* pC,
+                        const double* pR, const double* pT, const double* pD, const float* dat,
+                        const float* ctfD, const float* sigRcp, const int* iCol, const int* iRow,
+                        int nPxl, int idim, int nImg, float* wC, float* wR, float* wT, float* wD,
+                        float* baseL, float* dvp, void* workspace, size_t wsBytes,
+                        thx_stream_t stream);
 int thx_insert2d(float* F, float* T, double* O, int* counter, int vdim, int pf,
                  const float* dat, const float* ctf, const double* rot, const double* trans,
                  const double* offS, const float* w, const int* nc, int nImg, int mReco,
@@ -636,6 +649,56 @@ int thx_expectation_ctf(const thx_expect_cfg* cfg, const thx_ctf_search_cfg* cs,
                         int nPxl, int nImg, double* quat, double* trans, double* pR,
                         double* pT, float* score, int* cls, int* nPhaseOut,
                         void* workspace, size_t wsBytes, thx_stream_t stream);
+
+/* MODE_2D (the _para.mode == MODE_2D branches of Optimiser::expectationG,
+ * src/Optimiser.cpp:646-1079, 1183-1616, 1726-2131): the same driver with
+ *   vol      nK half-complex class images [nK][vdim][vdim/2+1] Complex;
+ *   gRot     the global rotations as Particle::_r rows (cos, sin, 0, 0)
+ *            (nR x 4; thx_global_sample_set2d), gTrans / gPR / gPT as 3D;
+ *   rot      the particles' rotations, nImg x mLR x 4 rows (cos, sin, 0, 0);
+ *   kMin     the reseed floor of k1 ((1 / perturbFactor) MIN_STD_FACTOR / mS,
+ *            :2032-2044);
+ * particle statistics of von Mises rotations (src/Particle.cpp:87-169,
+ * 1013-1016, 1160-1178, 1920-1921, 2317-2329; src/Geometry/DirectionalStat.cpp:
+ * 252-384): calVari k1 = 1 - R (inferVMS), perturb r_i <- r_i d_i with
+ * d_i ~ sampleVMS(k = min(1, k1 pf)), pR = 1 / pdfVMS, peak factor from the
+ * (n / 2)-th largest weight, the stopping rule on variR = k1.  perturbMean
+ * and volCells do not apply (ignored / NULL); pxOrder is not used (the 2D
+ * phase is direct, thx_local_phase2d).  thx_expectation2d_ctf: the
+ * SEARCH_TYPE_CTF local search of thx_expectation_ctf in MODE_2D (the 2D
+ * phase over (r, t, d) columns, thx_local_phase2d_d). */
+size_t thx_expectation2d_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl);
+int thx_expectation2d(const thx_expect_cfg* cfg, const float* vol, const double* gRot,
+                      const double* gTrans, const double* gPR, const double* gPT,
+                      const float* dat, const float* ctf, const float* sigRcp, const int* iCol,
+                      const int* iRow, int nPxl, int nImg, double* rot, double* trans,
+                      double* pR, double* pT, float* score, int* cls, int* nPhaseOut,
+                      void* workspace, size_t wsBytes, thx_stream_t stream);
+size_t thx_expectation2d_ctf_workspace(const thx_expect_cfg* cfg, const thx_ctf_search_cfg* cs,
+                                       int nImg, int nPxl);
+int thx_expectation2d_ctf(const thx_expect_cfg* cfg, const thx_ctf_search_cfg* cs,
+                          const float* vol, const float* dat, const float* sigRcp,
+                          const int* iCol, const int* iRow, int nPxl, int nImg, double* rot,
+                          double* trans, double* pR, double* pT, float* score, int* cls,
+                          int* nPhaseOut, void* workspace, size_t wsBytes, thx_stream_t stream);
+/* MODE_2D particle statistics one image at a time (rows (cos, sin, 0, 0)):
+ * thx_global_sample_set2d -- Particle::reset's 2D rotations (sampleVMS with
+ *   k = 1: uniform angles, src/Particle.cpp:101-103), translations / priors as
+ *   thx_global_sample_set;
+ * thx_pf_calvari2d -- calVari: k[3l..3l+2] = max(kFloor, 1 - R), sd as
+ *   thx_pf_calvari;
+ * thx_pf_balance_rot2d -- balanceWeight(PAR_R): pR = 1 / pdfVMS normalised;
+ * thx_pf_perturb2d -- perturb(pf, PAR_R / PAR_T) + balanceWeight with the
+ *   spreads k / sd of thx_pf_calvari2d (counter RNG: seed, stream_id). */
+int thx_global_sample_set2d(int nR, int nT, double transS, unsigned long long seed, double* rot,
+                            double* trans, double* pR, double* pT, thx_stream_t stream);
+int thx_pf_calvari2d(int nImg, int mR, const double* rot, int mT, const double* trans,
+                     double kFloor, double sFloor, double* k, double* sd, thx_stream_t stream);
+int thx_pf_balance_rot2d(int nImg, int mR, const double* rot, double* pR, thx_stream_t stream);
+int thx_pf_perturb2d(int nImg, int mR, int mT, double* rot, double* trans, double* pR,
+                     double* pT, const double* k, const double* sd, double pf, double transS,
+                     double transM, unsigned long long seed, unsigned stream_id,
+                     thx_stream_t stream);
 
 /* HIP event pairs for thx_expect_cfg.phaseEvents: create n (begin, end)
  * pairs, read back ms[i] per pair (-1: not recorded), destroy. */

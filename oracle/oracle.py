@@ -84,6 +84,8 @@ def lib():
                                     _c_double, _f64p, _f64p, _f64p, _f32p, _f32p, _f32p, _i32p,
                                     _i32p, _c_int, _c_int, _f32p, _f32p, _f32p, _f32p, _f32p,
                                     ctypes.c_void_p]
+    L.orc_local_phase2d_d.restype = None
+    L.orc_local_phase2d_d.argtypes = L.orc_local_phase_d.argtypes
     L.orc_insert_batch_d.restype = None
     L.orc_insert_batch_d.argtypes = [_f32p, _f32p, _f64p, _i64p, _c_int, _c_int, _f32p, _f32p,
                                      _f64p, _f64p, _f64p, _f64p, _f32p, _c_int, _c_int, _i32p,
@@ -221,6 +223,23 @@ def local_phase_d(vol, vdim, pf, quat, trans, pC, pR, pT, pD, dat, ctfD, sig, px
                             _c(pR, np.float64), _c(pT, np.float64), _c(pD, np.float64), _cf(dat),
                             _c(ctfD, np.float32).reshape(-1), _c(sig, np.float32), px.iCol,
                             px.iRow, px.n, idim, wC, wR, wT, wD, base, dvp.ctypes.data)
+    return wC[0], wR, wT, wD, base[0], dvp.reshape(nR, nT, nD)
+
+
+def local_phase2d_d(img, vdim, pf, rot, trans, pC, pR, pT, pD, dat, ctfD, sig, px, idim):
+    """The 2D (r, t, d) phase of one image: rot [nR, 2] (cos, sin)."""
+    nR, nT, nD = len(rot), len(trans), len(pD)
+    wC = np.zeros(1, np.float32)
+    wR = np.zeros(nR, np.float32)
+    wT = np.zeros(nT, np.float32)
+    wD = np.zeros(nD, np.float32)
+    base = np.zeros(1, np.float32)
+    dvp = np.zeros(nR * nT * nD, np.float32)
+    lib().orc_local_phase2d_d(_cf(img).reshape(-1), vdim, pf, _c(rot, np.float64).reshape(-1), nR,
+                              _c(trans, np.float64).reshape(-1), nT, nD, float(pC),
+                              _c(pR, np.float64), _c(pT, np.float64), _c(pD, np.float64),
+                              _cf(dat), _c(ctfD, np.float32).reshape(-1), _c(sig, np.float32),
+                              px.iCol, px.iRow, px.n, idim, wC, wR, wT, wD, base, dvp.ctypes.data)
     return wC[0], wR, wT, wD, base[0], dvp.reshape(nR, nT, nD)
 
 

@@ -111,3 +111,81 @@ def keep_half_height(u, peak):
     u = np.asarray(u, np.float64)
     hh = u.max() * peak
     return np.where(u < hh, 0.0, u - hh)
+
+
+# ---------------------------------------------------------------- MODE_2D
+# 2D rotations are Particle::_r rows (cos, sin, 0, 0) (sampleVMS(dmat4&),
+# src/Geometry/DirectionalStat.cpp:320-332).
+
+def vms_kappa(k):
+    """The concentration of sampleVMS / pdfVMS from the dispersion k
+    (DirectionalStat.cpp:256, 269)."""
+    return (1 - k) * (1 + 2 * k - k * k) / k / (2 - k)
+
+
+def infer_vms(R):
+    """inferVMS(dvec2& mu, double& k, src) (DirectionalStat.cpp:334-357): the
+    normalised resultant mu and k = 1 - |resultant| / n."""
+    R = np.asarray(R, np.float64)
+    mu = np.array([R[:, 0].sum(), R[:, 1].sum()])
+    n = np.hypot(mu[0], mu[1])
+    return mu / n, 1.0 - n / len(R)
+
+
+def cal_vari_rot2d(R):
+    """Particle::calVari(PAR_R), MODE_2D (src/Particle.cpp:1013-1016): k1."""
+    return infer_vms(R)[1]
+
+
+def pdf_vms(x, mu, k):
+    """pdfVMS (DirectionalStat.cpp:252-262), rows x."""
+    from math import factorial
+    kappa = vms_kappa(k)
+    x = np.asarray(x, np.float64)[:, :2]
+    if kappa < 5:
+        i0 = sum((kappa / 2) ** (2 * m) / factorial(m) ** 2 for m in range(40))   # gsl_sf_bessel_I0
+        return np.exp(kappa * (x @ mu)) / (2 * np.pi * i0)
+    sd = np.sqrt(1.0 / kappa)
+    d = np.hypot(x[:, 0] - mu[0], x[:, 1] - mu[1])
+    return np.exp(-d * d / (2 * sd * sd)) / (np.sqrt(2 * np.pi) * sd)
+
+
+def balance_rot2d(R):
+    """Particle::balanceWeight(PAR_R), MODE_2D (src/Particle.cpp:2317-2329):
+    w_i = 1 / pdfVMS(r_i; inferVMS(r)); returned normalised to sum 1."""
+    mu, k = infer_vms(R)
+    w = 1.0 / pdf_vms(R, mu, k)
+    return w / w.sum()
+
+
+def peak_factor_rot2d(u):
+    """Particle::setPeakFactor(PAR_R), MODE_2D (src/Particle.cpp:1920-1921):
+    the (n / PEAK_FACTOR_BASE)-th largest over the largest."""
+    s = np.sort(np.asarray(u, np.float64))[::-1]
+    return max(PEAK_FACTOR_MIN, min(PEAK_FACTOR_MAX, s[len(s) // PEAK_FACTOR_BASE] / s[0]))
+
+
+def sample_vms(rng, kappa, n):
+    """sampleVMS(dmat2&, mu = (1, 0), k, n) (DirectionalStat.cpp:264-318) with
+    numpy's generator: uniform directions below kappa 0.1, else Best & Fisher's
+    rejection sampler for the cosine and a fair sign for the sine.  Returns
+    rows (cos, sin)."""
+    out = np.empty((n, 2))
+    if kappa < 0.1:
+        th = rng.uniform(0, 2 * np.pi, n)
+        out[:, 0], out[:, 1] = np.cos(th), np.sin(th)
+        return out
+    a = 1 + np.sqrt(1 + 4 * kappa * kappa)
+    b = (a - np.sqrt(2 * a)) / (2 * kappa)
+    r = (1 + b * b) / (2 * b)
+    for i in range(n):
+        while True:
+            z = np.cos(np.pi * rng.uniform())
+            f = (1 + r * z) / (r + z)
+            c = kappa * (r - f)
+            u2 = rng.uniform()
+            if c * (2 - c) > u2 or np.log(c / u2) + 1 - c >= 0:
+                break
+        d = np.sqrt((1 - f) * (f + 1))
+        out[i] = (f, -d) if rng.uniform() > 0.5 else (f, d)
+    return out

@@ -368,12 +368,17 @@ void orc_local_phase(const float* vol, int vdim, int pf, const double* quat,
  * sample (ctfD[nD][nPxl], orc_ctf_search) and the defocus priors pD --
  * src/Optimiser.cpp:1225-1427 with nC = 1; dvp[r][t][d] (the layout of
  * kernel_logDataVSLC, gpu/src/Kernel.cu:889-939). */
-void orc_local_phase_d(const float* vol, int vdim, int pf, const double* quat, int nR,
-                       const double* trans, int nT, int nD, double pC, const double* pR,
-                       const double* pT, const double* pD, const float* dat,
-                       const float* ctfD, const float* sigRcp, const int* iCol,
-                       const int* iRow, int nPxl, int idim, float* wC, float* wR, float* wT,
-                       float* wD, float* baseL, float* dvp)
+void orc_project2d(float* dst, const float* img, int vdim, int pf, const double* cs,
+                   const int* iCol, const int* iRow, int nPxl);
+
+/* twoD: the projection of the 2D branch (orc_project2d of the class image
+ * at rotation rows (cos, sin), stride 2) instead of orc_project3d */
+static void local_phase_d_impl(int twoD, const float* vol, int vdim, int pf, const double* quat,
+                               int nR, const double* trans, int nT, int nD, double pC,
+                               const double* pR, const double* pT, const double* pD,
+                               const float* dat, const float* ctfD, const float* sigRcp,
+                               const int* iCol, const int* iRow, int nPxl, int idim, float* wC,
+                               float* wR, float* wT, float* wD, float* baseL, float* dvp)
 {
     float* traP = (float*)malloc(sizeof(float) * 2 * (size_t)nT * nPxl);
     float* priRotP = (float*)malloc(sizeof(float) * 2 * nPxl);
@@ -387,9 +392,13 @@ void orc_local_phase_d(const float* vol, int vdim, int pf, const double* quat, i
     for (int t = 0; t < nT; t++) wT[t] = 0;
     for (int d = 0; d < nD; d++) wD[d] = 0;
     for (int r = 0; r < nR; r++) {
-        double mat[9];
-        orc_rotate3d(mat, quat + 4 * r);
-        orc_project3d(priRotP, vol, vdim, pf, mat, iCol, iRow, nPxl);
+        if (twoD) {
+            orc_project2d(priRotP, vol, vdim, pf, quat + 2 * r, iCol, iRow, nPxl);
+        } else {
+            double mat[9];
+            orc_rotate3d(mat, quat + 4 * r);
+            orc_project3d(priRotP, vol, vdim, pf, mat, iCol, iRow, nPxl);
+        }
         for (int t = 0; t < nT; t++) {
             cmul(priAllP, traP + 2 * (size_t)t * nPxl, priRotP, nPxl);
             for (int d = 0; d < nD; d++) {
@@ -416,6 +425,31 @@ void orc_local_phase_d(const float* vol, int vdim, int pf, const double* quat, i
     free(traP);
     free(priRotP);
     free(priAllP);
+}
+
+void orc_local_phase_d(const float* vol, int vdim, int pf, const double* quat, int nR,
+                       const double* trans, int nT, int nD, double pC, const double* pR,
+                       const double* pT, const double* pD, const float* dat,
+                       const float* ctfD, const float* sigRcp, const int* iCol,
+                       const int* iRow, int nPxl, int idim, float* wC, float* wR, float* wT,
+                       float* wD, float* baseL, float* dvp)
+{
+    local_phase_d_impl(0, vol, vdim, pf, quat, nR, trans, nT, nD, pC, pR, pT, pD, dat, ctfD,
+                       sigRcp, iCol, iRow, nPxl, idim, wC, wR, wT, wD, baseL, dvp);
+}
+
+/* f4 with CTF search: the 2D phase over (r, t, d) (the MODE_2D projection of
+ * src/Optimiser.cpp:1277-1300 in the SEARCH_TYPE_CTF loop); rot: nR rows
+ * (cos, sin) */
+void orc_local_phase2d_d(const float* img, int vdim, int pf, const double* rot, int nR,
+                         const double* trans, int nT, int nD, double pC, const double* pR,
+                         const double* pT, const double* pD, const float* dat,
+                         const float* ctfD, const float* sigRcp, const int* iCol,
+                         const int* iRow, int nPxl, int idim, float* wC, float* wR, float* wT,
+                         float* wD, float* baseL, float* dvp)
+{
+    local_phase_d_impl(1, img, vdim, pf, rot, nR, trans, nT, nD, pC, pR, pT, pD, dat, ctfD,
+                       sigRcp, iCol, iRow, nPxl, idim, wC, wR, wT, wD, baseL, dvp);
 }
 
 /* --------------------------------------------------------------- a10 ---- */

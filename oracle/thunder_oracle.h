@@ -58,6 +58,12 @@ void orc_local_phase_d(const float* vol, int vdim, int pf, const double* quat, i
                        const float* ctfD, const float* sigRcp, const int* iCol,
                        const int* iRow, int nPxl, int idim, float* wC, float* wR, float* wT,
                        float* wD, float* baseL, float* dvp);
+void orc_local_phase2d_d(const float* img, int vdim, int pf, const double* rot, int nR,
+                       const double* trans, int nT, int nD, double pC, const double* pR,
+                       const double* pT, const double* pD, const float* dat,
+                       const float* ctfD, const float* sigRcp, const int* iCol,
+                       const int* iRow, int nPxl, int idim, float* wC, float* wR, float* wT,
+                       float* wD, float* baseL, float* dvp);
 
 /* a12, CTF search: insert with a per-sample CTF(defocus x d)
  * (src/Optimiser.cpp:7101-7120). */

@@ -52,6 +52,22 @@ SIGNATURES = {
                                  ctypes.c_uint, _c_int, _p, _p, _p, _p, _p, _p, _c_size, _p]),
     "thx_pf_calvari": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _c_double, _c_double, _p, _p, _p]),
     "thx_pf_balance_rot": (_c_int, [_c_int, _c_int, _p, _p, _p]),
+    "thx_global_sample_set2d": (_c_int, [_c_int, _c_int, _c_double, ctypes.c_ulonglong, _p, _p, _p,
+                                         _p, _p]),
+    "thx_pf_calvari2d": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _c_double, _c_double, _p, _p, _p]),
+    "thx_pf_balance_rot2d": (_c_int, [_c_int, _c_int, _p, _p, _p]),
+    "thx_pf_perturb2d": (_c_int, [_c_int, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_double,
+                                  _c_double, _c_double, ctypes.c_ulonglong, ctypes.c_uint, _p]),
+    "thx_expectation2d_workspace": (_c_size, [_p, _c_int, _c_int]),
+    "thx_expectation2d_ctf_workspace": (_c_size, [_p, _p, _c_int, _c_int]),
+    "thx_expectation2d_ctf": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p,
+                                       _p, _p, _p, _c_size, _p]),
+    "thx_local_phase2d_d_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "thx_local_phase2d_d": (_c_int, [_p, _c_int, _c_int, _p, _p, _c_int, _p, _c_int, _c_int, _p, _p,
+                                     _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _p, _p, _p,
+                                     _p, _p, _p, _p, _c_size, _p]),
+    "thx_expectation2d": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _p, _p,
+                                   _p, _p, _p, _p, _p, _p, _c_size, _p]),
     "thx_pf_peak": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _c_int, _p]),
     "thx_insert3d": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _p, _c_int,
                               _c_int, _p, _p, _c_int, _c_int, _p]),

@@ -1338,6 +1338,16 @@ int launch_local_weights(const float* dvp, int nR, int nT, const double* pC, con
     return THX_OK;
 }
 
+int launch_local_weights_d(const float* dvp, int nR, int nT, int nD, const double* pC,
+                           const double* pR, const double* pT, const double* pD, float* wC,
+                           float* wR, float* wT, float* wD, float* baseL, int nImg, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_local_weights_d, dim3(nImg), dim3(256), 0, s, dvp, nR, nT, nD, pC, pR,
+                       pT, pD, wC, wR, wT, wD, baseL, nullptr, nullptr);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 int launch_patch_boxes(const double* quat, int nR, const int* iCol, const int* iRow,
                        const int* order, int nVisit, int pf, int vdim, int nImg, int* rec,
                        hipStream_t s)

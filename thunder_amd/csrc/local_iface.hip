@@ -283,8 +283,6 @@ extern "C" int thx_calpoint_create(int mode, int searchType, int gpuIdx, int mR,
 {
     THX_CHECK_ARG(mcp && mR > 0 && mT > 0 && npxl > 0, "thx_calpoint_create: bad arguments");
     THX_CHECK_ARG(mode == 0 || mode == 1, "thx_calpoint_create: mode must be 0 (2D) or 1 (3D)");
-    THX_CHECK_ARG(mode == 1 || searchType != 2,
-                  "thx_calpoint_create: 2D CTF search is not supported");
     THX_CHECK_ARG(searchType != 2 || (mD >= 1 && (long)mT * mD <= 1024),
                   "thx_calpoint_create: CTF search needs 1 <= mD, mT * mD <= 1024");
     THX_DEV_SET(gpuIdx);
@@ -317,7 +315,7 @@ extern "C" int thx_calpoint_create(int mode, int searchType, int gpuIdx, int mR,
     const int ordCap = (npxl * 2 + 31) / 16 * 16;
     chk(hipMalloc(&c->order, sizeof(int) * ordCap));
     c->wsBytes = mode == 1 ? thx_local_phase_workspace(1, mR, mT * c->mD, ordCap > npxl ? ordCap : npxl)
-                           : thx_local_phase2d_workspace(1, mR, mT);
+                           : thx_local_phase2d_d_workspace(1, mR, mT, c->mD);
     chk(hipMalloc(&c->ws, c->wsBytes));
     if (mode == 0) chk(hipMalloc(&c->rot2, sizeof(double) * 2 * mR));
     if (c->cs) {
@@ -424,20 +422,30 @@ extern "C" int thx_ExpectLocalPreI3D(int gpuIdx, int datShift, void* mgr, void* 
 
 // ExpectLocalPreI2D (Interface.h:89-105; cuthunder.cu:2762-2825): binds the
 // class image, pixel set and geometry (the 2D phase projects on the fly from
-// the image in LDS); no CTF search in 2D.
+// the image in LDS); with CTF search the calpoint's CTF per defocus sample
+// (kernel_CalCTFL from devdefO / devfreQ, as ExpectLocalPreI3D).
 extern "C" int thx_ExpectLocalPreI2D(int gpuIdx, int datShift, void* mgr, void* mcp,
                                      const float* devdefO, const float* devfreQ,
                                      const int* deviCol, const int* deviRow, float phaseShift,
                                      float conT, float k1, float k2, int pf, int idim, int vdim,
                                      int npxl, int interp)
 {
-    (void)datShift; (void)devdefO; (void)devfreQ; (void)phaseShift; (void)conT; (void)k1; (void)k2;
     CalPoint* c = static_cast<CalPoint*>(mcp);
     const Tex* t = static_cast<const Tex*>(mgr);
     THX_CHECK_ARG(c && t && deviCol && deviRow && gpuIdx == c->gpu && npxl == c->npxl &&
                       c->mode == 0 && t->mode == 0 && vdim == t->vdim && vdim == pf * idim,
                   "thx_ExpectLocalPreI2D: bad arguments");
     THX_CHECK_ARG(interp == 1, "thx_ExpectLocalPreI2D: only LINEAR_INTERP (1) is supported");
+    THX_CHECK_ARG(!c->cs || (devdefO && devfreQ && datShift >= 0),
+                  "thx_ExpectLocalPreI2D: a CTF search needs devdefO and devfreQ");
+    THX_DEV_SET(gpuIdx);
+    if (c->cs) {
+        hipLaunchKernelGGL(k_calpoint_ctf, dim3(thx::cdiv(npxl, 256) > 16 ? 16 : thx::cdiv(npxl, 256),
+                                                c->mD),
+                           dim3(256), 0, c->stream, devdefO + (size_t)datShift * npxl, devfreQ,
+                           c->dP, phaseShift, conT, k1, k2, npxl, c->ctfD);
+        THX_LAUNCH_CHECK();
+    }
     c->tex = t;
     c->iCol = deviCol;
     c->iRow = deviRow;
@@ -458,6 +466,21 @@ extern "C" int thx_ExpectLocalM(int gpuIdx, int datShift, void* mcp, const float
     THX_DEV_SET(gpuIdx);
     const size_t off = (size_t)datShift * npxl;
     THX_HIP(hipMemcpyAsync(c->pC, &oldC, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (c->mode == 0 && c->cs) {
+        // the 2D (r, t, d) phase (kernel_logDataVSLC + kernel_UpdateWLC on the
+        // 2D projections)
+        THX_RET(thx_local_phase2d_d(c->tex->vol, c->vdim, c->pf, nullptr, c->rot2, c->mR,
+                                    c->trans, c->mT, c->mD, c->pC, c->pR, c->pT, c->pD,
+                                    devdatP + 2 * off, c->ctfD, devsigP + off, c->iCol, c->iRow,
+                                    npxl, c->idim, 1, c->wC, c->wR, c->wT, c->wD, c->base, nullptr,
+                                    c->ws, c->wsBytes, c->stream));
+        THX_HIP(hipMemcpyAsync(wC, c->wC, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipMemcpyAsync(wR, c->wR, sizeof(float) * c->mR, hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipMemcpyAsync(wT, c->wT, sizeof(float) * c->mT, hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipMemcpyAsync(wD, c->wD, sizeof(float) * c->mD, hipMemcpyDeviceToHost, c->stream));
+        THX_HIP(hipStreamSynchronize(c->stream));
+        return THX_OK;
+    }
     if (c->mode == 0) {
         // the 2D phase (kernel_logDataVSL + kernel_UpdateWL on the 2D
         // projections, cuthunder.cu:2915-3140)

@@ -39,6 +39,15 @@ extern "C" int thx_debug_quat_sink(double* dst, unsigned phaseMask)
 #endif
 
 namespace thx {
+int project2d_launch(const float* vol, int vdim, int pf, const double* rot, int rotStride, int nR,
+                     const int* iCol, const int* iRow, int nPxl, float* rotP, hipStream_t s);
+int local_phase2d_launch(const float* vol, int vdim, int pf, const int* cls, const double* rot,
+                         int rotStride, int nR, const double* trans, int nT, const double* pC,
+                         const double* pR, const double* pT, const float* dat, const float* ctf,
+                         const float* sigRcp, const int* iCol, const int* iRow, int nPxl, int idim,
+                         int nImg, float* wC, float* wR, float* wT, float* baseL, float* dvp,
+                         const int* done, hipStream_t s, int nD = 0, const double* pD = nullptr,
+                         float* wD = nullptr);
 int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
                       const float* vol, int volLayout, int vdim, int pf, const double* quat, int nR,
                       const double* trans, int nT, const double* pC, const double* pR,
@@ -311,15 +320,17 @@ THX_DEV void balance_rot(const double* Q, int m, int lane, double* w)
     for (int i = lane; i < m; i += GROUP) w[i] /= tot;
 }
 
-// Particle::setPeakFactor(PAR_R), 3D (src/Particle.cpp:1920-1925) when
-// setFactor: peak = clamp(u_(n/8) / u_max, 1e-3, 0.5) with u_(k) the k-th
+// Particle::setPeakFactor(PAR_R) (src/Particle.cpp:1920-1925) when
+// setFactor: peak = clamp(u_(n/rankDiv) / u_max, 1e-3, 0.5) -- rankDiv =
+// PEAK_FACTOR_BASE^3 = 8 in 3D, PEAK_FACTOR_BASE = 2 in 2D -- with u_(k) the k-th
 // largest (0-based); then keepHalfHeightPeak (:1964-1984) in place:
 // u <- u < hh ? 0 : u - hh, hh = u_max peak.  u >= 0, so the k-th largest is
 // found by a bisection over the ordered float bit patterns.
 __global__ void __launch_bounds__(256) k_pf_peak(int nImg, int n, float* __restrict__ u, int ldu,
                                                  double* __restrict__ peak, int setFactor,
                                                  const int* __restrict__ cls = nullptr, int ldc = 0,
-                                                 const int* __restrict__ done = nullptr)
+                                                 const int* __restrict__ done = nullptr,
+                                                 int rankDiv = 8)
 {
     const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -330,7 +341,7 @@ __global__ void __launch_bounds__(256) k_pf_peak(int nImg, int n, float* __restr
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     double pk;
     if (setFactor) {
-        const int k = n / 8;
+        const int k = n / rankDiv;
         // largest bit pattern v with count(u >= v) >= k + 1
         uint32_t lo = 0, hi = __float_as_uint(mx);
         while (lo < hi) {
@@ -611,6 +622,49 @@ __global__ void __launch_bounds__(256) k_pf_mean(int nImg, int mR, const double*
     }
 }
 
+// Translation half of Particle::perturb + balanceWeight (3D and 2D alike):
+// t_i += pf N(0, s) (src/Particle.cpp:1232-1262), reCentre beyond transM
+// (:2473-2495), pT = 1/pdf of the perturbed set normalised (balanceWeight(PAR_T),
+// :2342-2375).
+THX_DEV void perturb_trans(double* Tr, double* pTl, int mT, double s0, double s1, double pf,
+                           double transS, double transM, Philox& rng, int lane)
+{
+    double sx, sy, vx, vy;
+    for (int i = lane; i < mT; i += GROUP) {
+        const double2 g = rng.gauss2();
+        double x = Tr[2 * i] + g.x * s0 * pf, y = Tr[2 * i + 1] + g.y * s1 * pf;
+        if (sqrt(x * x + y * y) > transM) {
+            const double2 h = rng.gauss2();
+            x = h.x * transS; y = h.y * transS;
+        }
+        Tr[2 * i] = x; Tr[2 * i + 1] = y;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    sx = 0; sy = 0;
+    for (int i = lane; i < mT; i += GROUP) { sx += Tr[2 * i]; sy += Tr[2 * i + 1]; }
+    sx = group_sum(sx) / mT; sy = group_sum(sy) / mT;
+    vx = 0; vy = 0;
+    for (int i = lane; i < mT; i += GROUP) {
+        vx += (Tr[2 * i] - sx) * (Tr[2 * i] - sx);
+        vy += (Tr[2 * i + 1] - sy) * (Tr[2 * i + 1] - sy);
+    }
+    vx = group_sum(vx); vy = group_sum(vy);
+    const double b0 = fmax(1e-6, mT > 1 ? sqrt(vx / (mT - 1)) : 1.0);
+    const double b1 = fmax(1e-6, mT > 1 ? sqrt(vy / (mT - 1)) : 1.0);
+    double tot = 0.0;
+    for (int i = lane; i < mT; i += GROUP) {
+        const double u = (Tr[2 * i] - sx) / b0, v = (Tr[2 * i + 1] - sy) / b1;
+        const double p = exp(-(u * u + v * v) / 2) / (2 * M_PI * b0 * b1);
+        const double x = 1.0 / fmax(p, 1e-300);
+        pTl[i] = x;
+        tot += x;
+    }
+    tot = group_sum(tot);
+    for (int i = lane; i < mT; i += GROUP) pTl[i] /= tot;
+}
+
 // Particle::perturb + balanceWeight for one image per GROUP lanes
 // (src/Particle.cpp:1149-1289, 2309-2375), with k / s from k_pf_calvari:
 //   R: mean = inferACG(mean, _r) of the current (resampled) cloud -- the
@@ -673,43 +727,185 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     balance_rot(Q, mR, lane, pR + (size_t)l * mR);
 
-    // ---- translation
-    const double s0 = sIn[2 * l], s1 = sIn[2 * l + 1];
-    double sx, sy, vx, vy;
-    for (int i = lane; i < mT; i += GROUP) {
-        const double2 g = rng.gauss2();
-        double x = Tr[2 * i] + g.x * s0 * pf, y = Tr[2 * i + 1] + g.y * s1 * pf;
-        if (sqrt(x * x + y * y) > transM) {
-            const double2 h = rng.gauss2();
-            x = h.x * transS; y = h.y * transS;
-        }
-        Tr[2 * i] = x; Tr[2 * i + 1] = y;
+    perturb_trans(Tr, pT + (size_t)l * mT, mT, sIn[2 * l], sIn[2 * l + 1], pf, transS, transM, rng,
+                  lane);
+}
+
+// ---- MODE_2D particle statistics (von Mises rotations).  A 2D rotation is
+// the particle row (cos, sin, 0, 0) of Particle::_r (sampleVMS(dmat4&),
+// src/Geometry/DirectionalStat.cpp:320-332); composition is quaternion_mul of
+// such rows, i.e. the angle sum.
+
+// gsl_sf_bessel_I0 by its power series (the argument stays below 5 where
+// pdfVMS uses it)
+THX_DEV double bessel_i0_dev(double x)
+{
+    double s = 1.0, t = 1.0;
+    for (int k = 1; k < 64; k++) {
+        t *= (x * x * 0.25) / ((double)k * k);
+        s += t;
+        if (t < 1e-17 * s) break;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    // balanceWeight(PAR_T) on the perturbed set
-    sx = 0; sy = 0;
+    return s;
+}
+
+// the concentration of sampleVMS / pdfVMS from the dispersion k = 1 - R
+// (DirectionalStat.cpp:256, 269)
+THX_DEV double vms_kappa(double k)
+{
+    return (1.0 - k) * (1.0 + 2.0 * k - k * k) / k / (2.0 - k);
+}
+
+// inferVMS(dvec2& mu, double& k, src) (DirectionalStat.cpp:334-357): mu = the
+// normalised resultant, k = 1 - |resultant| / n
+THX_DEV void infer_vms(const double* Q, int m, int lane, double& mu0, double& mu1, double& k)
+{
+    double a = 0.0, b = 0.0;
+    for (int i = lane; i < m; i += GROUP) { a += Q[4 * i]; b += Q[4 * i + 1]; }
+    a = group_sum(a);
+    b = group_sum(b);
+    const double n = sqrt(a * a + b * b);
+    k = 1.0 - n / m;
+    mu0 = a / n;
+    mu1 = b / n;
+}
+
+// Particle::balanceWeight(PAR_R), MODE_2D (src/Particle.cpp:2317-2329):
+// w_i = 1 / pdfVMS(r_i; inferVMS(r)) (pdfVMS, DirectionalStat.cpp:252-262:
+// exp(kappa x.mu) / (2 pi I0(kappa)) for kappa < 5, else the Gaussian pdf of
+// |x - mu| with sd 1/sqrt(kappa)), normalised to sum 1.
+THX_DEV void balance_rot2d(const double* Q, int m, int lane, double* w)
+{
+    double mu0, mu1, k;
+    infer_vms(Q, m, lane, mu0, mu1, k);
+    const double kappa = vms_kappa(k);
+    const bool small = kappa < 5.0;
+    const double c = small ? 1.0 / (2.0 * M_PI * bessel_i0_dev(kappa)) : 0.0;
+    const double sd = small ? 0.0 : sqrt(1.0 / kappa);
+    double tot = 0.0;
+    for (int i = lane; i < m; i += GROUP) {
+        const double x0 = Q[4 * i], x1 = Q[4 * i + 1];
+        double p;
+        if (small) {
+            p = exp(kappa * (x0 * mu0 + x1 * mu1)) * c;
+        } else {
+            const double d0 = x0 - mu0, d1 = x1 - mu1;
+            const double r2 = d0 * d0 + d1 * d1;
+            p = exp(-r2 / (2.0 * sd * sd)) / (sqrt(2.0 * M_PI) * sd);
+        }
+        const double x = 1.0 / p;
+        w[i] = x;
+        tot += x;
+    }
+    tot = group_sum(tot);
+    for (int i = lane; i < m; i += GROUP) w[i] /= tot;
+}
+
+// sampleVMS(dmat2&, mu = (1, 0), k, n) (DirectionalStat.cpp:264-318): a
+// uniform direction when kappa < 0.1, else Best & Fisher's rejection sampler
+// for the cosine f and a fair sign for the sine.
+THX_DEV void sample_vms(double kappa, Philox& rng, double& c, double& s)
+{
+    if (!(kappa >= 1e-1)) {
+        // gsl_ran_dir_2d: a uniform angle
+        const double th = 2.0 * M_PI * rng.uniform();
+        c = cos(th);
+        s = sin(th);
+        return;
+    }
+    const double a = 1.0 + sqrt(1.0 + 4.0 * kappa * kappa);
+    const double b = (a - sqrt(2.0 * a)) / (2.0 * kappa);
+    const double r = (1.0 + b * b) / (2.0 * b);
+    double f;
+    for (int it = 0; it < 1000; it++) {
+        const double z = cos(M_PI * rng.uniform());
+        f = (1.0 + r * z) / (r + z);
+        const double cc = kappa * (r - f);
+        const double u2 = rng.uniform();
+        if (cc * (2.0 - cc) > u2) break;
+        if (log(cc / u2) + 1.0 - cc >= 0.0) break;
+    }
+    const double d = sqrt((1.0 - f) * (f + 1.0));
+    c = f;
+    s = rng.uniform() > 0.5 ? -d : d;
+}
+
+// Particle::calVari, MODE_2D (src/Particle.cpp:1013-1016, 1098-1119): k1 =
+// inferVMS's 1 - R, floored at kFloor (the reseed floor of
+// src/Optimiser.cpp:2032-2044, (1 / perturbFactor) MIN_STD_FACTOR / mS; 0 in
+// the phases), written to all three k slots; T as in 3D.
+__global__ void __launch_bounds__(256) k_pf_calvari2d(int nImg, int mR, const double* __restrict__ quat,
+                                                      int mT, const double* __restrict__ trans,
+                                                      double kFloor, double sFloor,
+                                                      double* __restrict__ kOut,
+                                                      double* __restrict__ sOut,
+                                                      const int* __restrict__ done = nullptr)
+{
+    const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
+    const int lane = threadIdx.x % GROUP;
+    if (l >= nImg || (done && done[l])) return;
+    double mu0, mu1, k;
+    infer_vms(quat + (size_t)l * mR * 4, mR, lane, mu0, mu1, k);
+    const double* Tr = trans + (size_t)l * mT * 2;
+    double sx = 0, sy = 0;
     for (int i = lane; i < mT; i += GROUP) { sx += Tr[2 * i]; sy += Tr[2 * i + 1]; }
     sx = group_sum(sx) / mT; sy = group_sum(sy) / mT;
-    vx = 0; vy = 0;
+    double vx = 0, vy = 0;
     for (int i = lane; i < mT; i += GROUP) {
         vx += (Tr[2 * i] - sx) * (Tr[2 * i] - sx);
         vy += (Tr[2 * i + 1] - sy) * (Tr[2 * i + 1] - sy);
     }
     vx = group_sum(vx); vy = group_sum(vy);
-    const double b0 = fmax(1e-6, mT > 1 ? sqrt(vx / (mT - 1)) : 1.0);
-    const double b1 = fmax(1e-6, mT > 1 ? sqrt(vy / (mT - 1)) : 1.0);
-    double tot = 0.0;
-    for (int i = lane; i < mT; i += GROUP) {
-        const double u = (Tr[2 * i] - sx) / b0, v = (Tr[2 * i + 1] - sy) / b1;
-        const double p = exp(-(u * u + v * v) / 2) / (2 * M_PI * b0 * b1);
-        const double x = 1.0 / fmax(p, 1e-300);
-        pT[(size_t)l * mT + i] = x;
-        tot += x;
+    if (lane == 0) {
+        const double k1 = fmax(kFloor, k);
+        kOut[3 * l] = k1; kOut[3 * l + 1] = k1; kOut[3 * l + 2] = k1;
+        sOut[2 * l] = fmax(sFloor, mT > 1 ? sqrt(vx / (mT - 1)) : 0.0);
+        sOut[2 * l + 1] = fmax(sFloor, mT > 1 ? sqrt(vy / (mT - 1)) : 0.0);
     }
-    tot = group_sum(tot);
-    for (int i = lane; i < mT; i += GROUP) pT[(size_t)l * mT + i] /= tot;
+}
+
+__global__ void __launch_bounds__(256) k_pf_balance_rot2d(int nImg, int mR,
+                                                          const double* __restrict__ quat,
+                                                          double* __restrict__ pR)
+{
+    const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
+    if (l >= nImg) return;
+    balance_rot2d(quat + (size_t)l * mR * 4, mR, threadIdx.x % GROUP, pR + (size_t)l * mR);
+}
+
+// Particle::perturb(pf, PAR_R), MODE_2D (src/Particle.cpp:1160-1178):
+// d_i ~ sampleVMS(mu = (1, 0), k = min(PERTURB_K_MAX = 1, k1 pf)), r_i <-
+// quaternion_mul(r_i, d_i), balanceWeight(PAR_R); then T as in 3D.
+__global__ void __launch_bounds__(256) k_pf_perturb2d(int nImg, int mR, int mT,
+                                                      double* __restrict__ quat,
+                                                      double* __restrict__ trans,
+                                                      double* __restrict__ pR,
+                                                      double* __restrict__ pT,
+                                                      const double* __restrict__ kIn,
+                                                      const double* __restrict__ sIn,
+                                                      double pf, double transS, double transM,
+                                                      uint64_t seed, uint32_t stream,
+                                                      const int* __restrict__ done)
+{
+    const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
+    const int lane = threadIdx.x % GROUP;
+    if (l >= nImg || (done && done[l])) return;
+    double* Q = quat + (size_t)l * mR * 4;
+    double* Tr = trans + (size_t)l * mT * 2;
+    Philox rng(seed, (uint32_t)l, stream, 0x2d00u | (uint32_t)lane);
+    const double kappa = vms_kappa(fmin(1.0, kIn[3 * l] * pf));
+    for (int i = lane; i < mR; i += GROUP) {
+        double d[4] = {0.0, 0.0, 0.0, 0.0}, o[4];
+        sample_vms(kappa, rng, d[0], d[1]);
+        qmul(Q + 4 * i, d, o);
+        for (int k = 0; k < 4; k++) Q[4 * i + k] = o[k];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    balance_rot2d(Q, mR, lane, pR + (size_t)l * mR);
+    perturb_trans(Tr, pT + (size_t)l * mT, mT, sIn[2 * l], sIn[2 * l + 1], pf, transS, transM, rng,
+                  lane);
 }
 
 // Reseed of the class for K > 1 (src/Optimiser.cpp:1933-1965), one thread
@@ -774,13 +970,14 @@ __global__ void k_pf_converge(int nImg, int phase, int minPhase, int lastPhase,
                               double* __restrict__ bestR, double* __restrict__ bestT,
                               int* __restrict__ done, int* __restrict__ nP,
                               const double* __restrict__ sdD = nullptr,
-                              double* __restrict__ bestD = nullptr)
+                              double* __restrict__ bestD = nullptr, int twoD = 0)
 {
     const int l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= nImg || done[l]) return;
     bool stop = phase >= lastPhase;
     if (phase >= minPhase) {
-        const double vR = pow(kv[3 * l] * kv[3 * l + 1] * kv[3 * l + 2], 1.0 / 6);
+        // Particle::variR: k1 in MODE_2D, (k1 k2 k3)^(1/6) in 3D
+        const double vR = twoD ? kv[3 * l] : pow(kv[3 * l] * kv[3 * l + 1] * kv[3 * l + 2], 1.0 / 6);
         const double vT = sv[2 * l] * sv[2 * l + 1];
         const bool first = phase == minPhase;
         bool room = first || vR < bestR[l] * 0.95 || vT < bestT[l] * 0.95;
@@ -906,15 +1103,25 @@ __global__ void __launch_bounds__(256) k_pf_defocus(int nImg, int mD, int op, do
 // Gaussian: uniform on S^3), translations from a bivariate Gaussian of width
 // transS (PARTICLE_TRANS_INIT_GAUSSIAN), pR = 1/nR, pT = balanceWeight(PAR_T)
 // (:2342-2375: 1 / N2(t - m; s0, s1, rho = 0) with the sample mean and
-// gsl_stats_sd_m, normalised).  Counter RNG; one workgroup does T.
+// gsl_stats_sd_m, normalised).  Counter RNG; one workgroup does T.  twoD:
+// MODE_2D rotations (:101-103), uniform angles as rows (cos, sin, 0, 0).
 __global__ void __launch_bounds__(256) k_sample_set(int nR, int nT, double transS, uint64_t seed,
                                                     double* __restrict__ quat,
                                                     double* __restrict__ trans,
                                                     double* __restrict__ pR,
-                                                    double* __restrict__ pT)
+                                                    double* __restrict__ pT, int twoD)
 {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < nR) {
+    if (i < nR && twoD) {
+        // MODE_2D: sampleVMS(_r, (1, 0, 0, 0), k = 1) -- kappa 0, gsl_ran_dir_2d
+        Philox rng(seed, (uint32_t)i, 0x5a3u, 2u);
+        const double th = 2.0 * M_PI * rng.uniform();
+        quat[4 * (size_t)i] = cos(th);
+        quat[4 * (size_t)i + 1] = sin(th);
+        quat[4 * (size_t)i + 2] = 0.0;
+        quat[4 * (size_t)i + 3] = 0.0;
+        pR[i] = 1.0 / nR;
+    } else if (i < nR) {
         Philox rng(seed, (uint32_t)i, 0x5a3u, 0u);
         const double2 g0 = rng.gauss2(), g1 = rng.gauss2();
         const double n = sqrt(g0.x * g0.x + g0.y * g0.y + g1.x * g1.x + g1.y * g1.y);
@@ -991,7 +1198,8 @@ struct Plan {
 };
 
 // mLD > 0: the workspace of a CTF search over mLD defocus samples
-Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, int mLD = 0)
+Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, int mLD = 0,
+          bool twoD = false)
 {
     thx::Carver k(base, ~size_t(0));
     Plan p;
@@ -1002,7 +1210,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     if (mLD > nMax) nMax = mLD;
     const bool scan = c.searchType == 0;
     p.rotP = k.take<float>(scan ? (size_t)2 * c.nR * nPxl : 0);
-    p.gMat = k.take<double>(scan ? (size_t)9 * c.nR : 0);
+    p.gMat = k.take<double>(scan && !twoD ? (size_t)9 * c.nR : 0);
     p.traP = k.take<float>(scan ? (size_t)2 * c.nT * nPxl : 0);
     p.gWC = k.take<float>((size_t)nImg * nK);
     p.gWR = k.take<float>(scan ? (size_t)nImg * nK * c.nR : 0);
@@ -1035,7 +1243,9 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.nAct = k.take<int>(1);
     p.bestR = k.take<double>(nImg);
     p.bestT = k.take<double>(nImg);
-    p.localWsBytes = thx_local_phase_workspace(nImg, c.mLR, c.mLT * (mLD > 0 ? mLD : 1), nVisit);
+    p.localWsBytes = twoD ? thx_local_phase2d_d_workspace(nImg, c.mLR, c.mLT, mLD)
+                          : thx_local_phase_workspace(nImg, c.mLR, c.mLT * (mLD > 0 ? mLD : 1),
+                                                      nVisit);
     p.localWs = k.take<char>(p.localWsBytes);
     const size_t nd = mLD > 0 ? (size_t)mLD : 0, on = mLD > 0 ? 1 : 0;
     p.freq = k.take<float>(on * nPxl);
@@ -1057,7 +1267,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
 #define THX_BRICKS 0
 #endif
     p.brickStride = thx_volume_bricks_bytes(c.vdim) / sizeof(float);
-    p.bricks = THX_BRICKS && !c.volCells ? k.take<float>(p.brickStride * nK) : nullptr;
+    p.bricks = THX_BRICKS && !c.volCells && !twoD ? k.take<float>(p.brickStride * nK) : nullptr;
     p.bytes = k.off + 256;
     return p;
 }
@@ -1138,7 +1348,61 @@ extern "C" int thx_global_sample_set(int nR, int nT, double transS, unsigned lon
                   "thx_global_sample_set: bad arguments");
     hipLaunchKernelGGL(k_sample_set, dim3(thx::cdiv(nR, 256)), dim3(256), 0,
                        thx::as_stream(stream), nR, nT, transS, (uint64_t)seed, quat, trans, pR,
-                       pT);
+                       pT, 0);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" int thx_global_sample_set2d(int nR, int nT, double transS, unsigned long long seed,
+                                       double* rot, double* trans, double* pR, double* pT,
+                                       thx_stream_t stream)
+{
+    THX_CHECK_ARG(nR > 0 && nT > 1 && transS > 0.0 && rot && trans && pR && pT,
+                  "thx_global_sample_set2d: bad arguments");
+    hipLaunchKernelGGL(k_sample_set, dim3(thx::cdiv(nR, 256)), dim3(256), 0,
+                       thx::as_stream(stream), nR, nT, transS, (uint64_t)seed, rot, trans, pR,
+                       pT, 1);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" int thx_pf_calvari2d(int nImg, int mR, const double* rot, int mT, const double* trans,
+                                double kFloor, double sFloor, double* k, double* sd,
+                                thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && mR > 0 && mT > 0, "thx_pf_calvari2d: bad sizes");
+    THX_CHECK_ARG(nImg == 0 || (rot && trans && k && sd), "thx_pf_calvari2d: null argument");
+    if (nImg == 0) return THX_OK;
+    hipLaunchKernelGGL(k_pf_calvari2d, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0,
+                       thx::as_stream(stream), nImg, mR, rot, mT, trans, kFloor, sFloor, k, sd);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" int thx_pf_balance_rot2d(int nImg, int mR, const double* rot, double* pR,
+                                    thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && mR > 0, "thx_pf_balance_rot2d: bad sizes");
+    THX_CHECK_ARG(nImg == 0 || (rot && pR), "thx_pf_balance_rot2d: null argument");
+    if (nImg == 0) return THX_OK;
+    hipLaunchKernelGGL(k_pf_balance_rot2d, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0,
+                       thx::as_stream(stream), nImg, mR, rot, pR);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" int thx_pf_perturb2d(int nImg, int mR, int mT, double* rot, double* trans, double* pR,
+                                double* pT, const double* k, const double* sd, double pf,
+                                double transS, double transM, unsigned long long seed,
+                                unsigned stream_id, thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && mR > 0 && mT > 0 && pf > 0.0, "thx_pf_perturb2d: bad arguments");
+    THX_CHECK_ARG(nImg == 0 || (rot && trans && pR && pT && k && sd),
+                  "thx_pf_perturb2d: null argument");
+    if (nImg == 0) return THX_OK;
+    hipLaunchKernelGGL(k_pf_perturb2d, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0,
+                       thx::as_stream(stream), nImg, mR, mT, rot, trans, pR, pT, k, sd, pf, transS,
+                       transM, (uint64_t)seed, (uint32_t)stream_id, nullptr);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
@@ -1232,12 +1496,13 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                             const int* iRow, const int* pxOrder, int nOrd, int nPxl, int nImg,
                             double* quat, double* trans, double* pR, double* pT, float* score,
                             int* cls, int* nPhaseOut, void* workspace, size_t wsBytes,
-                            thx_stream_t stream)
+                            thx_stream_t stream, bool twoD = false)
 {
     THX_CHECK_ARG(cfg && vol && dat && (ctf || cs) && sigRcp && iCol && iRow && quat && trans &&
                       pR && pT,
                   "thx_expectation: null argument");
     const thx_expect_cfg& c = *cfg;
+    THX_CHECK_ARG(!twoD || !c.volCells, "thx_expectation2d: no cell projectee in MODE_2D");
     const bool global = c.searchType == 0;
     if (cs) {
         THX_CHECK_ARG(c.searchType == 2, "thx_expectation_ctf: searchType must be 2 (SEARCH_TYPE_CTF)");
@@ -1267,14 +1532,16 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     if (nImg == 0) return THX_OK;
     THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % 16 == 0),
                   "thx_expectation: nOrd must be a positive multiple of 16");
-    const Plan p = plan(workspace, c, nImg, nPxl, pxOrder ? nOrd : nPxl, mLD);
+    const Plan p = plan(workspace, c, nImg, nPxl, pxOrder ? nOrd : nPxl, mLD, twoD);
     THX_CHECK_ARG(workspace && p.bytes <= wsBytes, "thx_expectation: workspace too small");
     hipStream_t s = thx::as_stream(stream);
     const unsigned gImg = thx::cdiv(nImg, 4);
     const unsigned gPf = thx::cdiv(nImg * GROUP, 256);
     const unsigned gOne = thx::cdiv(nImg, 256);
     const int nK = c.nK;
-    const size_t dimSize = (size_t)(c.vdim / 2 + 1) * c.vdim * c.vdim;
+    // one class's projectee: a half-complex volume, or a half-complex image in 2D
+    const size_t dimSize = (size_t)(c.vdim / 2 + 1) * c.vdim * (twoD ? 1 : c.vdim);
+    const int rankDiv = twoD ? 2 : 8;      // setPeakFactor(PAR_R): PEAK_FACTOR_BASE (^3 in 3D)
     int* clsD = cls ? cls : p.cls;
     int* nPD = nPhaseOut ? nPhaseOut : p.nP;
     const int* clsSel = nK > 1 ? clsD : nullptr;    // rows / volumes picked per image
@@ -1286,11 +1553,15 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     if (global) {
         // ---- global scan of every class (ExpectRotran + ExpectProject + ExpectGlobal3D
         // with kIdx = class, src/Optimiser.cpp:1815-1847)
-        THX_RET(thx_rotmat(gQuat, c.nR, p.gMat, stream));
+        if (!twoD) THX_RET(thx_rotmat(gQuat, c.nR, p.gMat, stream));
         THX_RET(thx_trans_table(gTrans, c.nT, iCol, iRow, nPxl, c.idim, p.traP, stream));
         for (int k = 0; k < nK; k++) {
-            THX_RET(thx_project3d(vol + 2 * dimSize * k, c.vdim, c.pf, p.gMat, c.nR, iCol, iRow,
-                                  nPxl, p.rotP, stream));
+            if (twoD)   // ExpectGlobal2D: the class image at the (cos, sin) rows of gQuat
+                THX_RET(thx::project2d_launch(vol + 2 * dimSize * k, c.vdim, c.pf, gQuat, 4, c.nR,
+                                              iCol, iRow, nPxl, p.rotP, s));
+            else
+                THX_RET(thx_project3d(vol + 2 * dimSize * k, c.vdim, c.pf, p.gMat, c.nR, iCol,
+                                      iRow, nPxl, p.rotP, stream));
             THX_RET(thx_global_scan(p.rotP, c.nR, p.traP, c.nT, dat, ctf, sigRcp, nImg, nPxl, gPR,
                                     gPT, k, nK, p.gWC, p.gWR, p.gWT, p.gBase, c.algo, p.scanWs,
                                     p.scanWsBytes, stream));
@@ -1306,7 +1577,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             THX_HIP(hipMemsetAsync(clsD, 0, sizeof(int) * nImg, s));
         }
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.nR, p.gWR, nK * c.nR,
-                           p.peakR, 1, clsSel, c.nR, nullptr);
+                           p.peakR, 1, clsSel, c.nR, nullptr, rankDiv);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.nR, c.shuffle), s,
                            nImg, c.nR, c.mLR, gPR, 0,
@@ -1327,15 +1598,15 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, gTrans, 0L, c.nT,
                            p.anc, trans, nullptr);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT, trans,
-                           c.kMin, c.sMin, p.kv, p.sv, nullptr);
+        hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg,
+                           c.mLR, quat, c.mLT, trans, c.kMin, c.sMin, p.kv, p.sv, nullptr);
         THX_LAUNCH_CHECK();
     } else {
         // ---- local search from the caller's particle state: its spreads
         // (calVari on the given cloud) and, for the top-particle mean, calRank1st
         if (nK == 1 && !cls) THX_HIP(hipMemsetAsync(clsD, 0, sizeof(int) * nImg, s));
-        hipLaunchKernelGGL(k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT, trans,
-                           0.0, 0.0, p.kv, p.sv, nullptr);
+        hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg,
+                           c.mLR, quat, c.mLT, trans, 0.0, 0.0, p.kv, p.sv, nullptr);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_top_by_weight, dim3(gOne), dim3(256), 0, s, nImg, c.mLR, quat, pR, p.topQ);
         THX_LAUNCH_CHECK();
@@ -1374,16 +1645,25 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     }
     for (int phase = phase0; phase < phase0 + nPh; phase++) {
         const bool large = phase == phase0 && (!global || c.largeFirst);
-        if (c.perturbMean == 1) {
+        if (twoD) {
+            // MODE_2D perturb (von Mises, no mean) + balanceWeight (R, T)
+            hipLaunchKernelGGL(k_pf_perturb2d, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
+                               trans, pR, pT, p.kv, p.sv,
+                               large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
+                               c.seed, (uint32_t)(2000 + phase), done);
+            THX_LAUNCH_CHECK();
+        } else if (c.perturbMean == 1) {
             hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat,
                                c.acgIters, done, p.meanQ, nullptr);
             THX_LAUNCH_CHECK();
         }
-        hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
-                           trans, pR, pT, p.topQ, p.kv, p.sv,
-                           large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
-                           c.seed, (uint32_t)(2000 + phase), c.perturbMean, p.meanQ, done);
-        THX_LAUNCH_CHECK();
+        if (!twoD) {
+            hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
+                               trans, pR, pT, p.topQ, p.kv, p.sv,
+                               large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
+                               c.seed, (uint32_t)(2000 + phase), c.perturbMean, p.meanQ, done);
+            THX_LAUNCH_CHECK();
+        }
         if (cs) {
             // phase 0: initD(mLD, ctfRefineS); later: perturb(perturbFactorSCTF,
             // PAR_D) (src/Optimiser.cpp:1194-1195, 1208-1209); then the phase's
@@ -1407,6 +1687,15 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
 #endif
         // phases past the caller's event pairs run untimed
         hipEvent_t* ev = pi < c.nPhaseEvents ? static_cast<hipEvent_t*>(c.phaseEvents) : nullptr;
+        if (twoD) {
+            if (ev) THX_HIP(hipEventRecord(ev[2 * pi], s));
+            THX_RET(thx::local_phase2d_launch(vol, c.vdim, c.pf, clsSel, quat, 4, c.mLR, trans,
+                                              c.mLT, p.pC, pR, pT, dat, cs ? p.ctfD : ctf, sigRcp,
+                                              iCol, iRow, nPxl, c.idim, nImg, p.wC, p.wR, p.wT,
+                                              p.base, static_cast<float*>(p.localWs), done, s,
+                                              mLD, cs ? cs->pD : nullptr, p.wD));
+            if (ev) THX_HIP(hipEventRecord(ev[2 * pi + 1], s));
+        } else
         THX_RET(thx::local_phase_timed(&sel, ev ? ev[2 * pi] : nullptr, ev ? ev[2 * pi + 1] : nullptr,
                                        phaseVol, phaseLayout, c.vdim,
                                        c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT,
@@ -1414,10 +1703,10 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                        nPxl, c.idim, nImg, p.wC, p.wR, p.wT, p.base, p.localWs,
                                        p.localWsBytes, stream, mLD, cs ? cs->pD : nullptr, p.wD));
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
-                           p.peakR, 0, nullptr, 0, done);
+                           p.peakR, 0, nullptr, 0, done, rankDiv);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat, c.mLT,
-                           trans, 0.0, 0.0, p.kv, p.sv, done);
+        hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg,
+                           c.mLR, quat, c.mLT, trans, 0.0, 0.0, p.kv, p.sv, done);
         THX_LAUNCH_CHECK();
         // resample R and T by the phase marginals; ancestors gathered in place
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.mLR, c.shuffle), s,
@@ -1465,7 +1754,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         if (c.converge) {
             hipLaunchKernelGGL(k_pf_converge, dim3(gOne), dim3(256), 0, s, nImg, phase, c.minPhase,
                                phase0 + nPh - 1, p.kv, p.sv, p.bestR, p.bestT, p.done, nPD,
-                               cs ? p.sdD : nullptr, cs ? p.bestD : nullptr);
+                               cs ? p.sdD : nullptr, cs ? p.bestD : nullptr, (int)twoD);
             THX_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
             THX_LAUNCH_CHECK();
@@ -1504,6 +1793,48 @@ extern "C" int thx_expectation(const thx_expect_cfg* cfg, const float* vol,
     return expectation_impl(cfg, nullptr, vol, gQuat, gTrans, gPR, gPT, dat, ctf, sigRcp, iCol,
                             iRow, pxOrder, nOrd, nPxl, nImg, quat, trans, pR, pT, score, cls,
                             nPhaseOut, workspace, wsBytes, stream);
+}
+
+// MODE_2D (src/Optimiser.cpp's _para.mode == MODE_2D branches of
+// expectationG): vol holds nK half-complex class images, rotations are the
+// particle rows (cos, sin, 0, 0).
+extern "C" size_t thx_expectation2d_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl)
+{
+    if (!cfg) return 0;
+    return plan(nullptr, *cfg, nImg, nPxl, nPxl, 0, true).bytes;
+}
+
+extern "C" int thx_expectation2d(const thx_expect_cfg* cfg, const float* vol, const double* gRot,
+                                 const double* gTrans, const double* gPR, const double* gPT,
+                                 const float* dat, const float* ctf, const float* sigRcp,
+                                 const int* iCol, const int* iRow, int nPxl, int nImg, double* rot,
+                                 double* trans, double* pR, double* pT, float* score, int* cls,
+                                 int* nPhaseOut, void* workspace, size_t wsBytes,
+                                 thx_stream_t stream)
+{
+    return expectation_impl(cfg, nullptr, vol, gRot, gTrans, gPR, gPT, dat, ctf, sigRcp, iCol,
+                            iRow, nullptr, 0, nPxl, nImg, rot, trans, pR, pT, score, cls,
+                            nPhaseOut, workspace, wsBytes, stream, true);
+}
+
+extern "C" size_t thx_expectation2d_ctf_workspace(const thx_expect_cfg* cfg,
+                                                  const thx_ctf_search_cfg* cs, int nImg, int nPxl)
+{
+    if (!cfg || !cs || cs->mLD <= 0) return 0;
+    return plan(nullptr, *cfg, nImg, nPxl, nPxl, cs->mLD, true).bytes;
+}
+
+extern "C" int thx_expectation2d_ctf(const thx_expect_cfg* cfg, const thx_ctf_search_cfg* cs,
+                                     const float* vol, const float* dat, const float* sigRcp,
+                                     const int* iCol, const int* iRow, int nPxl, int nImg,
+                                     double* rot, double* trans, double* pR, double* pT,
+                                     float* score, int* cls, int* nPhaseOut, void* workspace,
+                                     size_t wsBytes, thx_stream_t stream)
+{
+    THX_CHECK_ARG(cs, "thx_expectation2d_ctf: null CTF-search configuration");
+    return expectation_impl(cfg, cs, vol, nullptr, nullptr, nullptr, nullptr, dat, nullptr,
+                            sigRcp, iCol, iRow, nullptr, 0, nPxl, nImg, rot, trans, pR, pT, score,
+                            cls, nPhaseOut, workspace, wsBytes, stream, true);
 }
 
 extern "C" int thx_expectation_ctf(const thx_expect_cfg* cfg, const thx_ctf_search_cfg* cs,

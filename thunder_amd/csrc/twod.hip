@@ -30,6 +30,9 @@ namespace thx {
 int launch_local_weights(const float* dvp, int nR, int nT, const double* pC, const double* pR,
                          const double* pT, float* wC, float* wR, float* wT, float* baseL, int nImg,
                          hipStream_t s);
+int launch_local_weights_d(const float* dvp, int nR, int nT, int nD, const double* pC,
+                           const double* pR, const double* pT, const double* pD, float* wC,
+                           float* wR, float* wT, float* wD, float* baseL, int nImg, hipStream_t s);
 }
 
 namespace {
@@ -67,13 +70,13 @@ THX_DEV void rot2(const double* cs, int ic, int ir, int pf, float& x, float& y)
 }
 
 __global__ void __launch_bounds__(256) k_project2d(const float2* __restrict__ vol, int vdim, int pf,
-                                                   const double* __restrict__ rot,
+                                                   const double* __restrict__ rot, int rotStride,
                                                    const int* __restrict__ iCol,
                                                    const int* __restrict__ iRow, int nPxl,
                                                    float2* __restrict__ rotP)
 {
     const int r = blockIdx.y;
-    const double cs[2] = {rot[2 * r], rot[2 * r + 1]};
+    const double cs[2] = {rot[(size_t)rotStride * r], rot[(size_t)rotStride * r + 1]};
     for (int i = blockIdx.x * 256 + threadIdx.x; i < nPxl; i += gridDim.x * 256) {
         float x, y;
         rot2(cs, iCol[i], iRow[i], pf, x, y);
@@ -83,27 +86,34 @@ __global__ void __launch_bounds__(256) k_project2d(const float2* __restrict__ vo
 
 // One workgroup per image: the class image in LDS (when it fits), per rotation
 // the projection at this thread's pixels and the direct likelihood against
-// every translation, accumulated per thread and reduced per (r, t).
+// every column, accumulated per thread and reduced per (r, column).  Columns
+// are the translations, or with CTF search (nD > 1) the (t, d) pairs of
+// kernel_logDataVSLC (column t nD + d) with the CTF of defocus sample d from
+// ctf = ctfD[nImg][nD][nPxl].
 constexpr int L2D_THREADS = 256;
-constexpr int L2D_TMAX = 16;                // translations per pass
+constexpr int L2D_TMAX = 16;                // columns per pass
 constexpr int L2D_LDS_VOX = 18432;          // 144 KiB of dynamic LDS: a projectee up to vdim 190
 
 __global__ void __launch_bounds__(L2D_THREADS) k_local2d(const float2* __restrict__ vol, int vdim,
                                                          int pf, long volStride,
                                                          const int* __restrict__ cls,
-                                                         const double* __restrict__ rot, int nR,
+                                                         const double* __restrict__ rot, int rotStride,
+                                                         int nR,
                                                          const double* __restrict__ trans, int nT,
                                                          const float2* __restrict__ dat,
                                                          const float* __restrict__ ctf,
                                                          const float* __restrict__ sig,
                                                          const int* __restrict__ iCol,
                                                          const int* __restrict__ iRow, int nPxl,
-                                                         int idim, float* __restrict__ dvp)
+                                                         int idim, float* __restrict__ dvp,
+                                                         const int* __restrict__ done, int nD)
 {
     extern __shared__ __attribute__((aligned(16))) float2 sImg[];   // the class image when staged
     __shared__ float sRed[L2D_THREADS / 64][L2D_TMAX];
     __shared__ float sTr[L2D_TMAX][2];
+    __shared__ int sCRow[L2D_TMAX];
     const int l = blockIdx.x;
+    if (done && done[l]) return;     // stopped by the driver's vari-decrease rule
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const float2* img = vol + (cls ? (size_t)cls[l] * volStride : 0);
     const long nVox = (long)(vdim / 2 + 1) * vdim;
@@ -113,16 +123,20 @@ __global__ void __launch_bounds__(L2D_THREADS) k_local2d(const float2* __restric
         __syncthreads();
     }
     const float2* src = staged ? sImg : img;
+    const int nCol = nT * nD;
     const float2* D = dat + (size_t)l * nPxl;
-    const float* C = ctf + (size_t)l * nPxl;
+    const float* C = ctf + (size_t)l * nD * nPxl;
     const float* S = sig + (size_t)l * nPxl;
     for (int r = 0; r < nR; r++) {
-        const double cs[2] = {rot[((size_t)l * nR + r) * 2], rot[((size_t)l * nR + r) * 2 + 1]};
-        for (int t0 = 0; t0 < nT; t0 += L2D_TMAX) {
-            const int nt = min(L2D_TMAX, nT - t0);
+        const size_t rq = ((size_t)l * nR + r) * rotStride;
+        const double cs[2] = {rot[rq], rot[rq + 1]};
+        for (int t0 = 0; t0 < nCol; t0 += L2D_TMAX) {
+            const int nt = min(L2D_TMAX, nCol - t0);
             if (tid < nt) {
-                sTr[tid][0] = (float)trans[((size_t)l * nT + t0 + tid) * 2] / idim;
-                sTr[tid][1] = (float)trans[((size_t)l * nT + t0 + tid) * 2 + 1] / idim;
+                const int t = (t0 + tid) / nD;
+                sTr[tid][0] = (float)trans[((size_t)l * nT + t) * 2] / idim;
+                sTr[tid][1] = (float)trans[((size_t)l * nT + t) * 2 + 1] / idim;
+                sCRow[tid] = ((t0 + tid) % nD) * nPxl;
             }
             __syncthreads();
             float acc[L2D_TMAX];
@@ -134,11 +148,12 @@ __global__ void __launch_bounds__(L2D_THREADS) k_local2d(const float2* __restric
                 rot2(cs, ic, ir, pf, x, y);
                 const float2 P = interp2(src, vdim, x, y);
                 const float2 d = D[i];
-                const float c = C[i], s = S[i];
+                const float c0 = C[i], s = S[i];
 #pragma unroll
                 for (int t = 0; t < L2D_TMAX; t++) {
                     if (t < nt) {
                         // priAllP = traP * priRotP, then logDataVSPrior_m_huabin
+                        const float c = nD == 1 ? c0 : C[sCRow[t] + i];
                         const float2 Tt = phase_shift(ic, ir, sTr[t][0], sTr[t][1]);
                         const float2 p = cmul(Tt, P);
                         const float er = d.x - c * p.x, ei = d.y - c * p.y;
@@ -155,7 +170,7 @@ __global__ void __launch_bounds__(L2D_THREADS) k_local2d(const float2* __restric
             if (tid < nt) {
                 float v = 0.f;
                 for (int w = 0; w < L2D_THREADS / 64; w++) v += sRed[w][tid];
-                dvp[((size_t)l * nR + r) * nT + t0 + tid] = v;
+                dvp[((size_t)l * nR + r) * nCol + t0 + tid] = v;
             }
             __syncthreads();
         }
@@ -238,20 +253,57 @@ __global__ void __launch_bounds__(256) k_insert2d(float2* __restrict__ F, float*
 
 }  // namespace
 
-extern "C" int thx_project2d(const float* vol, int vdim, int pf, const double* rot, int nR,
-                             const int* iCol, const int* iRow, int nPxl, float* rotP,
-                             thx_stream_t stream)
+namespace thx {
+// The 2D projection / phase with the rotations at a stride (2: (cos, sin)
+// pairs of the adapters; 4: the particle layout _r of Particle, whose columns
+// 0, 1 hold (cos, sin) in MODE_2D) -- the launchers of the C-ABI entry points
+// below and of the MODE_2D driver (csrc/optimiser.hip).
+int project2d_launch(const float* vol, int vdim, int pf, const double* rot, int rotStride, int nR,
+                     const int* iCol, const int* iRow, int nPxl, float* rotP, hipStream_t s)
 {
-    THX_CHECK_ARG(vdim > 0 && vdim % 2 == 0 && pf > 0 && nR >= 0 && nR <= 65535 && nPxl >= 0,
+    THX_CHECK_ARG(vdim > 0 && vdim % 2 == 0 && pf > 0 && nR >= 0 && nR <= 65535 && nPxl >= 0 &&
+                      rotStride >= 2,
                   "thx_project2d: bad sizes");
     if (nR == 0 || nPxl == 0) return THX_OK;
     THX_CHECK_ARG(vol && rot && iCol && iRow && rotP, "thx_project2d: null argument");
     const unsigned gx = thx::cdiv(nPxl, 256) > 32 ? 32 : thx::cdiv(nPxl, 256);
-    hipLaunchKernelGGL(k_project2d, dim3(gx, nR), dim3(256), 0, thx::as_stream(stream),
-                       reinterpret_cast<const float2*>(vol), vdim, pf, rot, iCol, iRow, nPxl,
-                       reinterpret_cast<float2*>(rotP));
+    hipLaunchKernelGGL(k_project2d, dim3(gx, nR), dim3(256), 0, s,
+                       reinterpret_cast<const float2*>(vol), vdim, pf, rot, rotStride, iCol, iRow,
+                       nPxl, reinterpret_cast<float2*>(rotP));
     THX_LAUNCH_CHECK();
     return THX_OK;
+}
+
+// dvp: nImg x nR x nT (x nD) scratch; done (may be NULL): images to skip.
+// nD >= 1 with pD / wD: CTF search, ctf = ctfD[nImg][nD][nPxl].
+int local_phase2d_launch(const float* vol, int vdim, int pf, const int* cls, const double* rot,
+                         int rotStride, int nR, const double* trans, int nT, const double* pC,
+                         const double* pR, const double* pT, const float* dat, const float* ctf,
+                         const float* sigRcp, const int* iCol, const int* iRow, int nPxl, int idim,
+                         int nImg, float* wC, float* wR, float* wT, float* baseL, float* dvp,
+                         const int* done, hipStream_t s, int nD = 0, const double* pD = nullptr,
+                         float* wD = nullptr)
+{
+    const long nVox = (long)(vdim / 2 + 1) * vdim;
+    const size_t lds = nVox <= L2D_LDS_VOX ? (size_t)nVox * sizeof(float2) : 0;
+    hipLaunchKernelGGL(k_local2d, dim3(nImg), dim3(L2D_THREADS), lds, s,
+                       reinterpret_cast<const float2*>(vol), vdim, pf, nVox, cls, rot, rotStride,
+                       nR, trans, nT, reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow,
+                       nPxl, idim, dvp, done, nD > 0 ? nD : 1);
+    THX_LAUNCH_CHECK();
+    if (nD > 0)
+        return launch_local_weights_d(dvp, nR, nT, nD, pC, pR, pT, pD, wC, wR, wT, wD, baseL, nImg,
+                                      s);
+    return launch_local_weights(dvp, nR, nT, pC, pR, pT, wC, wR, wT, baseL, nImg, s);
+}
+}  // namespace thx
+
+extern "C" int thx_project2d(const float* vol, int vdim, int pf, const double* rot, int nR,
+                             const int* iCol, const int* iRow, int nPxl, float* rotP,
+                             thx_stream_t stream)
+{
+    return thx::project2d_launch(vol, vdim, pf, rot, 2, nR, iCol, iRow, nPxl, rotP,
+                                 thx::as_stream(stream));
 }
 
 extern "C" size_t thx_local_phase2d_workspace(int nImg, int nR, int nT)
@@ -280,16 +332,43 @@ extern "C" int thx_local_phase2d(const float* vol, int vdim, int pf, const int* 
                       "thx_local_phase2d: workspace too small");
         d = static_cast<float*>(workspace);
     }
-    hipStream_t s = thx::as_stream(stream);
-    const long stride = (long)(vdim / 2 + 1) * vdim;
-    const long nVox = (long)(vdim / 2 + 1) * vdim;
-    const size_t lds = nVox <= L2D_LDS_VOX ? (size_t)nVox * sizeof(float2) : 0;
-    hipLaunchKernelGGL(k_local2d, dim3(nImg), dim3(L2D_THREADS), lds, s,
-                       reinterpret_cast<const float2*>(vol), vdim, pf, stride, cls, rot, nR, trans,
-                       nT, reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, nPxl,
-                       idim, d);
-    THX_LAUNCH_CHECK();
-    return thx::launch_local_weights(d, nR, nT, pC, pR, pT, wC, wR, wT, baseL, nImg, s);
+    return thx::local_phase2d_launch(vol, vdim, pf, cls, rot, 2, nR, trans, nT, pC, pR, pT, dat,
+                                     ctf, sigRcp, iCol, iRow, nPxl, idim, nImg, wC, wR, wT, baseL,
+                                     d, nullptr, thx::as_stream(stream));
+}
+
+extern "C" size_t thx_local_phase2d_d_workspace(int nImg, int nR, int nT, int nD)
+{
+    return (size_t)nImg * nR * nT * (nD > 0 ? nD : 1) * sizeof(float) + 256;
+}
+
+// MODE_2D CTF search phase: columns (t, d), ctfD[nImg][nD][nPxl] (thx_ctf_search),
+// priors pD / marginal wD [nImg][nD]; dvp (optional) [nImg][nR][nT][nD]
+extern "C" int thx_local_phase2d_d(const float* vol, int vdim, int pf, const int* cls,
+                                   const double* rot, int nR, const double* trans, int nT, int nD,
+                                   const double* pC, const double* pR, const double* pT,
+                                   const double* pD, const float* dat, const float* ctfD,
+                                   const float* sigRcp, const int* iCol, const int* iRow, int nPxl,
+                                   int idim, int nImg, float* wC, float* wR, float* wT, float* wD,
+                                   float* baseL, float* dvp, void* workspace, size_t wsBytes,
+                                   thx_stream_t stream)
+{
+    THX_CHECK_ARG(vdim > 0 && vdim % 2 == 0 && pf > 0 && nR > 0 && nT > 0 && nD > 0 && nPxl > 0 &&
+                      nImg >= 0 && (long)nT * nD <= 1024,
+                  "thx_local_phase2d_d: bad sizes");
+    if (nImg == 0) return THX_OK;
+    THX_CHECK_ARG(vol && rot && trans && pC && pR && pT && pD && dat && ctfD && sigRcp && iCol &&
+                      iRow && wC && wR && wT && wD && baseL,
+                  "thx_local_phase2d_d: null argument");
+    float* d = dvp;
+    if (!d) {
+        THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase2d_d_workspace(nImg, nR, nT, nD),
+                      "thx_local_phase2d_d: workspace too small");
+        d = static_cast<float*>(workspace);
+    }
+    return thx::local_phase2d_launch(vol, vdim, pf, cls, rot, 2, nR, trans, nT, pC, pR, pT, dat,
+                                     ctfD, sigRcp, iCol, iRow, nPxl, idim, nImg, wC, wR, wT, baseL,
+                                     d, nullptr, thx::as_stream(stream), nD, pD, wD);
 }
 
 static int insert2d_impl(float* F, float* T, double* O, int* counter, int vdim, int pf,

@@ -73,17 +73,25 @@ class Expectation:
     cells: ops.volume_cells(vol) (K = 1): the phases gather one 64-B cell per
            sample (thx_expect_cfg.volCells); "auto" (default) builds it for
            large boxes at full resolution (ring radius >= 300 voxels), None: off.
+    mode: "3d" (MODE_3D) or "2d" (MODE_2D, thx_expectation2d): vol holds
+          half-complex class images [vdim, vdim/2+1] or [nK, vdim, vdim/2+1],
+          rotations are rows (cos, sin, 0, 0) (gset from
+          ops.global_sample_set2d), von Mises particle statistics.
     """
 
     def __init__(self, vol, px, gset=None, mLR=125, mLT=9, n_phase=10, perturb=0.5,
                  trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7, shuffle=True,
                  search="global", converge=False, perturb_mean="acg", acg_iters=100,
                  perturb_large=2.0, large_first=False, min_phase=None, max_phase=None,
-                 mLD=9, ctf_refine_s=0.01, perturb_ctf=0.5, cells="auto"):
+                 mLD=9, ctf_refine_s=0.01, perturb_ctf=0.5, cells="auto", mode="3d"):
         dev = vol.device
         self.vol, self.px, self.dev = vol, px, dev
-        nK = vol.shape[0] if vol.dim() == 4 else 1
-        vdim = vol.shape[-3]
+        if mode not in ("3d", "2d"):
+            raise ValueError("mode: '3d' or '2d'")
+        self.two_d = mode == "2d"
+        dims = 2 if self.two_d else 3
+        nK = vol.shape[0] if vol.dim() == dims + 1 else 1
+        vdim = vol.shape[-dims]
         self.search = SEARCH[search]
         if self.search == 0:
             q, t, pR, pT = gset
@@ -95,12 +103,14 @@ class Expectation:
         else:
             self.gQuat = self.gTrans = self.gPR = self.gPT = None
             nR, nT = 0, 0
-        scan_min_std_r = nR ** (-1.0 / 3) if nR else 0.0     # src/Optimiser.cpp:765-771
+        # src/Optimiser.cpp:1748-1762: 1 / mS in 2D (nR = mS), mS^(-1/3) in 3D
+        scan_min_std_r = (1.0 / nR if self.two_d else nR ** (-1.0 / 3)) if nR else 0.0
         scan_min_std_t = 1.0 / synth.CHI2_QINV_HALF_2DOF / math.sqrt(trans_search_factor * math.pi)
         trans_m = trans_s * (-2.0 * math.log(0.05))           # reCentre, TRANS_Q = 0.05
         # reseed floors with OPTIMISER_SCAN_SET_MIN_STD_WITH_PERTURB (include/Config.h:224,
         # src/Optimiser.cpp:1033-1079); MIN_STD_FACTOR = 1
-        k_floor = (scan_min_std_r / perturb) ** 2
+        # (squared in 3D, :2045-2063; k1 itself in 2D, :2032-2044)
+        k_floor = scan_min_std_r / perturb if self.two_d else (scan_min_std_r / perturb) ** 2
         s_floor = scan_min_std_t / perturb
         if min_phase is None:
             min_phase = INCLUDE_OPTIMISER_H["MIN_N_PHASE_PER_ITER_GLOBAL" if self.search == 0
@@ -112,6 +122,8 @@ class Expectation:
                              nK, self.search, int(bool(converge)), min_phase, max_phase,
                              {"top": 0, "acg": 1}[perturb_mean], acg_iters, perturb_large,
                              int(bool(large_first)), None, None, 0)
+        if self.two_d:
+            cells = None
         if isinstance(cells, str):
             if cells != "auto":
                 raise ValueError("cells: a thx_volume_cells tensor, None or 'auto'")
@@ -130,6 +142,11 @@ class Expectation:
         self.cs = CtfSearchCfg(mLD, ctf_refine_s, perturb_ctf, None, None, None)
 
     def workspace_bytes(self, nImg):
+        if self.two_d and self.search == 2:
+            return lib().thx_expectation2d_ctf_workspace(ctypes.byref(self.cfg), ctypes.byref(self.cs),
+                                                         nImg, self.px.n)
+        if self.two_d:
+            return lib().thx_expectation2d_workspace(ctypes.byref(self.cfg), nImg, self.px.n)
         if self.search == 2:
             return lib().thx_expectation_ctf_workspace(ctypes.byref(self.cfg), ctypes.byref(self.cs),
                                                        nImg, self.px.n, len(self.px.order))
@@ -162,6 +179,13 @@ class Expectation:
         self.cs.attr, self.cs.d, self.cs.pD = attr.data_ptr(), d.data_ptr(), pD.data_ptr()
         ws = ops.workspace(self.workspace_bytes(nImg), dev)
         P = ops._ptr
+        if self.two_d:
+            check(lib().thx_expectation2d_ctf(ctypes.byref(self.cfg), ctypes.byref(self.cs),
+                                              P(self.vol), P(dat), P(sig), P(self.px.d_iCol),
+                                              P(self.px.d_iRow), nPxl, nImg, P(quat), P(trans),
+                                              P(pR), P(pT), P(score), P(cls), P(nph), P(ws),
+                                              ws.numel(), ops._stream(dev)), "thx_expectation2d_ctf")
+            return quat, trans, pR, pT, score, cls, nph, d, pD
         check(lib().thx_expectation_ctf(ctypes.byref(self.cfg), ctypes.byref(self.cs), P(self.vol),
                                         P(dat), P(sig), P(self.px.d_iCol), P(self.px.d_iRow),
                                         P(self.px.d_order), len(self.px.order), nPxl, nImg,
@@ -204,6 +228,13 @@ class Expectation:
         quat, trans, pR, pT, score, cls, nph = out
         ws = ops.workspace(self.workspace_bytes(nImg), dev)
         P = ops._ptr
+        if self.two_d:
+            check(lib().thx_expectation2d(ctypes.byref(self.cfg), P(self.vol), P(self.gQuat),
+                                          P(self.gTrans), P(self.gPR), P(self.gPT), P(dat), P(ctf),
+                                          P(sig), P(self.px.d_iCol), P(self.px.d_iRow), nPxl, nImg,
+                                          P(quat), P(trans), P(pR), P(pT), P(score), P(cls), P(nph),
+                                          P(ws), ws.numel(), ops._stream(dev)), "thx_expectation2d")
+            return out
         check(lib().thx_expectation(ctypes.byref(self.cfg), P(self.vol), P(self.gQuat),
                                     P(self.gTrans), P(self.gPR), P(self.gPT), P(dat), P(ctf),
                                     P(sig), P(self.px.d_iCol), P(self.px.d_iRow),

@@ -170,6 +170,19 @@ def global_sample_set(nR, nT, trans_s, seed, device):
     return quat, trans, pR, pT
 
 
+def global_sample_set2d(nR, nT, trans_s, seed, device):
+    """Particle::reset's MODE_2D global set on device: (rot [nR,4] rows
+    (cos, sin, 0, 0), trans [nT,2], pR, pT)."""
+    rot = torch.empty(nR, 4, dtype=torch.float64, device=device)
+    trans = torch.empty(nT, 2, dtype=torch.float64, device=device)
+    pR = torch.empty(nR, dtype=torch.float64, device=device)
+    pT = torch.empty(nT, dtype=torch.float64, device=device)
+    check(lib().thx_global_sample_set2d(nR, nT, float(trans_s), seed, _ptr(rot), _ptr(trans),
+                                        _ptr(pR), _ptr(pT), _stream(rot.device)),
+          "thx_global_sample_set2d")
+    return rot, trans, pR, pT
+
+
 # ------------------------------------------------------------------- a4
 def trans_table(trans, px):
     nT = trans.shape[0]
