@@ -681,6 +681,12 @@ int thx_expectation2d_ctf(const thx_expect_cfg* cfg, const thx_ctf_search_cfg* c
                           const int* iCol, const int* iRow, int nPxl, int nImg, double* rot,
                           double* trans, double* pR, double* pT, float* score, int* cls,
                           int* nPhaseOut, void* workspace, size_t wsBytes, thx_stream_t stream);
+/* The perturbation mean of PARTICLE_ROT_MEAN_USING_STAT_PERTURB (inferACG's
+ * principal axis, src/Geometry/DirectionalStat.cpp:93-145, 224-251; at most
+ * acgIters fixed-point iterations): meanQ nImg x 4, iters (may be NULL) the
+ * iterations each image took. */
+int thx_pf_acg_mean(int nImg, int mR, const double* quat, int acgIters, double* meanQ,
+                    int* iters, thx_stream_t stream);
 /* MODE_2D particle statistics one image at a time (rows (cos, sin, 0, 0)):
  * thx_global_sample_set2d -- Particle::reset's 2D rotations (sampleVMS with
  *   k = 1: uniform angles, src/Particle.cpp:101-103), translations / priors as

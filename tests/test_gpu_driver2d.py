@@ -65,7 +65,8 @@ def test_calvari2d_floor():
     tr = np.zeros((2, 4, 2))
     k = torch.empty(2, 3, dtype=torch.float64, device=DEV)
     sd = torch.empty(2, 2, dtype=torch.float64, device=DEV)
-    check(lib().thx_pf_calvari2d(2, 16, ops._ptr(T(R)), 4, ops._ptr(T(tr)), 0.02, 0.5,
+    dR, dT = T(R), T(tr)        # held: a temporary's memory would be reused at once
+    check(lib().thx_pf_calvari2d(2, 16, ops._ptr(dR), 4, ops._ptr(dT), 0.02, 0.5,
                                  ops._ptr(k), ops._ptr(sd), None), "thx_pf_calvari2d")
     assert np.allclose(k.cpu().numpy(), 0.02) and np.allclose(sd.cpu().numpy(), 0.5)
 
@@ -140,7 +141,8 @@ def _classes(nK, seed):
 @pytest.fixture(scope="module")
 def c1():
     """C1's shape: box 64, 8 classes, 2D global sampling mS 100 -> nR 100, nT
-    151; the scan ring rU 16 for a usable signal."""
+    151; the scan ring rU 16 for a usable signal; images of known classes at
+    grid poses, SNR 10."""
     cl = _classes(K1, 81)
     px = ops.PixelSet(N1, PF1, 16, 1, device=DEV)
     mS, nR, nT = ops.global_sample_sizes(100, mode=0)
@@ -148,8 +150,13 @@ def c1():
     n = 192
     rng = np.random.default_rng(82)
     cls = rng.integers(0, K1, n)
-    th = rng.uniform(0, 2 * np.pi, n)
-    tt = rng.standard_normal((n, 2)) * 2.0
+    # grid poses of the global set (the class is decided by the scan's class
+    # marginal, so off-grid images at nR 100 may land in a neighbour class);
+    # translations among the 40 samples nearest the centre
+    q, t = gset[0], gset[1]
+    th = np.arctan2(q[:, 1], q[:, 0])[rng.integers(0, len(q), n)]
+    near = np.argsort(np.linalg.norm(t, axis=1))[:40]
+    tt = t[near[rng.integers(0, len(near), n)]]
     ctf = ops.ctf(T(synth.ctf_attrs(n, seed=84)), px)
     P = torch.empty(n, px.n, dtype=torch.complex64, device=DEV)
     for l in range(n):

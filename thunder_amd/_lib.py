@@ -54,6 +54,7 @@ SIGNATURES = {
     "thx_pf_balance_rot": (_c_int, [_c_int, _c_int, _p, _p, _p]),
     "thx_global_sample_set2d": (_c_int, [_c_int, _c_int, _c_double, ctypes.c_ulonglong, _p, _p, _p,
                                          _p, _p]),
+    "thx_pf_acg_mean": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _p, _p]),
     "thx_pf_calvari2d": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _c_double, _c_double, _p, _p, _p]),
     "thx_pf_balance_rot2d": (_c_int, [_c_int, _c_int, _p, _p, _p]),
     "thx_pf_perturb2d": (_c_int, [_c_int, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _c_double,

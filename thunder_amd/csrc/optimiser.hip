@@ -1311,6 +1311,20 @@ extern "C" int thx_pf_calvari(int nImg, int mR, const double* quat, int mT, cons
     return THX_OK;
 }
 
+// the perturbation mean of k_pf_mean (inferACG's principal axis, capped at
+// acgIters fixed-point iterations) with the iterations each image took
+extern "C" int thx_pf_acg_mean(int nImg, int mR, const double* quat, int acgIters, double* meanQ,
+                               int* iters, thx_stream_t stream)
+{
+    THX_CHECK_ARG(nImg >= 0 && mR > 0 && acgIters > 0, "thx_pf_acg_mean: bad sizes");
+    THX_CHECK_ARG(nImg == 0 || (quat && meanQ), "thx_pf_acg_mean: null argument");
+    if (nImg == 0) return THX_OK;
+    hipLaunchKernelGGL(k_pf_mean, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0,
+                       thx::as_stream(stream), nImg, mR, quat, acgIters, nullptr, meanQ, iters);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 extern "C" int thx_pf_balance_rot(int nImg, int mR, const double* quat, double* pR,
                                   thx_stream_t stream)
 {
