@@ -525,6 +525,15 @@ int thx_reconstruct(const float* F, float* T, int N, int pf, float a, float alph
                     int joinHalf, float* dst, float* dstFT, int* nIter, float* diffOut,
                     void* workspace, size_t wsBytes, thx_stream_t stream);
 
+/* FFT::fw / FFT::bw (src/FFT.cpp) of one volume of box vdim, unnormalised:
+ * inverse 0: rl [vdim^3] real -> C [vdim][vdim][vdim/2+1] complex; inverse 1:
+ * C -> rl (C overwritten).  method 0: the reconstruction's own choice, 1:
+ * hipFFT's 3D plans, 2: LDS column passes along y / z + hipFFT's batched 1D
+ * transform along x (power-of-two vdim <= 1024).  Host-synchronous. */
+size_t thx_fft3d_workspace(int vdim);
+int thx_fft3d(float* C, float* rl, int vdim, int inverse, int method, void* workspace,
+              size_t wsBytes, thx_stream_t stream);
+
 /* ----------------------------------------------------------------- a14 ---
  * Fourier shell correlation FSC(vec&, const Volume& A, const Volume& B)
  * (src/Functions/Spectrum.cpp:302-337) of two half-complex volumes of real

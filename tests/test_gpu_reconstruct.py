@@ -93,3 +93,36 @@ def test_halfmap_fsc_end_to_end(orc):
     # relative to the FSC value, on the shells the half-maps cover
     rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-3)
     assert np.max(rel[1:]) < 1e-4, rel
+
+
+@pytest.mark.parametrize("vdim", [64, 128, 512])
+def test_fft3d_column_passes_match_numpy_and_hipfft(vdim):
+    """thx_fft3d: the LDS column passes (method 2) against numpy's rfftn /
+    irfftn (float64) and against hipFFT's 3D plans (method 1) on the same
+    input, both directions (FFT::fw / FFT::bw conventions: unnormalised)."""
+    import ctypes
+    from thunder_amd._lib import check, lib
+    rng = np.random.default_rng(vdim)
+    x = rng.standard_normal((vdim, vdim, vdim)).astype(np.float32)
+    X = np.fft.rfftn(x.astype(np.float64)) if vdim <= 128 else None
+    ws = ops.workspace(lib().thx_fft3d_workspace(vdim), DEV)
+    out = {}
+    for method in (1, 2):
+        rl = torch.as_tensor(x, device=DEV).contiguous()
+        C = torch.empty(vdim, vdim, vdim // 2 + 1, dtype=torch.complex64, device=DEV)
+        check(lib().thx_fft3d(ops._ptr(C), ops._ptr(rl), vdim, 0, method, ops._ptr(ws), ws.numel(),
+                              None), "thx_fft3d")
+        out[(method, "fw")] = C.cpu().numpy()
+        back = torch.empty_like(rl)
+        check(lib().thx_fft3d(ops._ptr(C), ops._ptr(back), vdim, 1, method, ops._ptr(ws), ws.numel(),
+                              None), "thx_fft3d")
+        out[(method, "bw")] = back.cpu().numpy()
+    scale = np.abs(out[(1, "fw")]).max()
+    assert np.max(np.abs(out[(2, "fw")] - out[(1, "fw")])) <= 2e-6 * scale
+    if X is not None:
+        assert np.max(np.abs(out[(2, "fw")] - X)) <= 2e-6 * np.abs(X).max()
+    # bw(fw(x)) = vdim^3 x
+    n3 = float(vdim) ** 3
+    for m in (1, 2):
+        assert np.max(np.abs(out[(m, "bw")] / n3 - x)) <= 2e-5 * np.abs(x).max()
+    assert np.max(np.abs(out[(2, "bw")] - out[(1, "bw")])) <= 2e-6 * np.abs(out[(1, "bw")]).max()

@@ -24,6 +24,9 @@
 // (Philox4x32-10), so a run is reproducible for a given seed, where the
 // reference draws from an urandom-seeded GSL mt19937.
 #include <cmath>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "common.h"
 
@@ -1479,6 +1482,40 @@ extern "C" int thx_pf_resample(int nImg, int nIn, int nOut, const double* w, int
     return THX_OK;
 }
 
+// calVari of a phase reads the pre-resample cloud and is only needed by the
+// next perturbation and the stopping rule, so it runs on a side stream
+// beside the resampling, the gathers and the next phase's inferACG mean --
+// two latency-bound, low-occupancy kernels side by side.  One side stream
+// and a fork / join event pair per (device, caller stream), made once; the
+// side stream only ever waits on events recorded on the caller's stream, so
+// the whole sequence stays capturable into a HIP graph.
+namespace {
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    std::mutex mu;      // calls on one caller stream are ordered anyway
+};
+
+int side_stream(hipStream_t main, SideStream** out)
+{
+    static std::mutex mu;
+    static auto* tab = new std::map<std::pair<int, hipStream_t>, SideStream*>;
+    int dev = 0;
+    THX_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(mu);
+    SideStream*& e = (*tab)[std::make_pair(dev, main)];
+    if (!e) {
+        SideStream* n = new SideStream;
+        THX_HIP(hipStreamCreateWithFlags(&n->s, hipStreamNonBlocking));
+        THX_HIP(hipEventCreateWithFlags(&n->fork, hipEventDisableTiming));
+        THX_HIP(hipEventCreateWithFlags(&n->join, hipEventDisableTiming));
+        e = n;
+    }
+    *out = e;
+    return THX_OK;
+}
+}  // namespace
+
 extern "C" size_t thx_expectation_workspace(const thx_expect_cfg* cfg, int nImg, int nPxl,
                                             int nOrd)
 {
@@ -1549,6 +1586,25 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     const Plan p = plan(workspace, c, nImg, nPxl, pxOrder ? nOrd : nPxl, mLD, twoD);
     THX_CHECK_ARG(workspace && p.bytes <= wsBytes, "thx_expectation: workspace too small");
     hipStream_t s = thx::as_stream(stream);
+    SideStream* side = nullptr;
+    THX_RET(side_stream(s, &side));
+    std::lock_guard<std::mutex> sideLock(side->mu);
+    bool sidePending = false;      // a calVari on the side stream not yet joined
+    auto fork = [&]() -> int {
+        THX_HIP(hipEventRecord(side->fork, s));
+        THX_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
+        return THX_OK;
+    };
+    auto join_rec = [&]() -> int {
+        THX_HIP(hipEventRecord(side->join, side->s));
+        sidePending = true;
+        return THX_OK;
+    };
+    auto join = [&]() -> int {
+        if (sidePending) THX_HIP(hipStreamWaitEvent(s, side->join, 0));
+        sidePending = false;
+        return THX_OK;
+    };
     const unsigned gImg = thx::cdiv(nImg, 4);
     const unsigned gPf = thx::cdiv(nImg * GROUP, 256);
     const unsigned gOne = thx::cdiv(nImg, 256);
@@ -1612,9 +1668,13 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, gTrans, 0L, c.nT,
                            p.anc, trans, nullptr);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg,
-                           c.mLR, quat, c.mLT, trans, c.kMin, c.sMin, p.kv, p.sv, nullptr);
+        // calVari with the scan floors, beside phase 1's inferACG mean (both only
+        // read the reseeded cloud)
+        THX_RET(fork());
+        hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, side->s,
+                           nImg, c.mLR, quat, c.mLT, trans, c.kMin, c.sMin, p.kv, p.sv, nullptr);
         THX_LAUNCH_CHECK();
+        THX_RET(join_rec());
     } else {
         // ---- local search from the caller's particle state: its spreads
         // (calVari on the given cloud) and, for the top-particle mean, calRank1st
@@ -1661,6 +1721,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         const bool large = phase == phase0 && (!global || c.largeFirst);
         if (twoD) {
             // MODE_2D perturb (von Mises, no mean) + balanceWeight (R, T)
+            THX_RET(join());
             hipLaunchKernelGGL(k_pf_perturb2d, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
                                trans, pR, pT, p.kv, p.sv,
                                large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
@@ -1672,6 +1733,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             THX_LAUNCH_CHECK();
         }
         if (!twoD) {
+            THX_RET(join());     // the spreads of the previous calVari
             hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
                                trans, pR, pT, p.topQ, p.kv, p.sv,
                                large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
@@ -1719,9 +1781,18 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
                            p.peakR, 0, nullptr, 0, done, rankDiv);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg,
-                           c.mLR, quat, c.mLT, trans, 0.0, 0.0, p.kv, p.sv, done);
+        // the pre-resample cloud, kept for calVari and the gathers
+        THX_HIP(hipMemcpyAsync(p.tmpQ, quat, sizeof(double) * nImg * c.mLR * 4,
+                               hipMemcpyDeviceToDevice, s));
+        THX_HIP(hipMemcpyAsync(p.tmpT, trans, sizeof(double) * nImg * c.mLT * 2,
+                               hipMemcpyDeviceToDevice, s));
+        // calVari of the pre-resample cloud on the side stream (needed by the next
+        // perturbation and the stopping rule only)
+        THX_RET(fork());
+        hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, side->s,
+                           nImg, c.mLR, p.tmpQ, c.mLT, p.tmpT, 0.0, 0.0, p.kv, p.sv, done);
         THX_LAUNCH_CHECK();
+        THX_RET(join_rec());
         // resample R and T by the phase marginals; ancestors gathered in place
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.mLR, c.shuffle), s,
                            nImg, c.mLR, c.mLR, pR,
@@ -1729,8 +1800,6 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                            p.topR, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
                            0, done);
         THX_LAUNCH_CHECK();
-        THX_HIP(hipMemcpyAsync(p.tmpQ, quat, sizeof(double) * nImg * c.mLR * 4,
-                               hipMemcpyDeviceToDevice, s));
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, p.tmpQ,
                            (long)c.mLR * 4, c.mLR, p.anc, quat, done);
         THX_LAUNCH_CHECK();
@@ -1743,8 +1812,6 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                            p.topT, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
                            0, done);
         THX_LAUNCH_CHECK();
-        THX_HIP(hipMemcpyAsync(p.tmpT, trans, sizeof(double) * nImg * c.mLT * 2,
-                               hipMemcpyDeviceToDevice, s));
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, p.tmpT,
                            (long)c.mLT * 2, c.mLT, p.anc, trans, done);
         THX_LAUNCH_CHECK();
@@ -1766,6 +1833,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             THX_LAUNCH_CHECK();
         }
         if (c.converge) {
+            THX_RET(join());
             hipLaunchKernelGGL(k_pf_converge, dim3(gOne), dim3(256), 0, s, nImg, phase, c.minPhase,
                                phase0 + nPh - 1, p.kv, p.sv, p.bestR, p.bestT, p.done, nPD,
                                cs ? p.sdD : nullptr, cs ? p.bestD : nullptr, (int)twoD);
@@ -1780,6 +1848,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             }
         }
     }
+    THX_RET(join());     // nothing of this call stays on the side stream
     if (!c.converge) {
         hipLaunchKernelGGL(k_fill_int, dim3(64), dim3(256), 0, s, nPD, (long)nImg,
                            phase0 + c.nPhase - 1);

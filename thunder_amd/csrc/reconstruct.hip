@@ -31,9 +31,12 @@
 #include <cmath>
 #include <vector>
 
+#include <atomic>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <tuple>
 
 #include "common.h"
@@ -46,6 +49,12 @@
                              #call, (int)r_);                                  \
             return THX_ERR_HIP;                                                \
         }                                                                      \
+    } while (0)
+
+#define THX_RET(call)                  \
+    do {                               \
+        int st_ = (call);              \
+        if (st_ != THX_OK) return st_; \
     } while (0)
 
 namespace {
@@ -249,6 +258,65 @@ __global__ void k_extract(float* __restrict__ dst, const float* __restrict__ src
     }
 }
 
+
+// ------------------------------------------------ strided passes of the 3D FFT
+// hipFFT's 3D plans run the two strided axes (y, z) of a 512^3 transform at
+// ~0.9 TB/s (1.25 ms per pass).  Here a workgroup takes CF_TX consecutive
+// x columns (one 128-B row piece per point) of one line along y or z into
+// LDS, bit-reversed, runs the radix-2 Cooley-Tukey stages there, and writes
+// the columns back in place: every HBM access is a coalesced row piece.  The
+// contiguous x axis stays on hipFFT (1D batched R2C / C2R), so a 3D transform
+// is two of these passes and one batched 1D pass -- the decomposition of
+// FFTW's / hipFFT's multi-dimensional real transforms (complex transforms
+// along the full axes, the real one along the halved axis), unnormalised.
+constexpr int CF_TX = 16;                // columns per tile
+constexpr int CF_PITCH = CF_TX + 1;      // LDS row pitch (float2): spreads a stage's rows over banks
+constexpr int CF_THREADS = 256;
+
+template <bool INV>
+__global__ void __launch_bounds__(CF_THREADS) k_col_fft(float2* __restrict__ a, int n, int logn,
+                                                        long sAxis, long sOuter, int nxh,
+                                                        const float2* __restrict__ tw)
+{
+    extern __shared__ float2 sm[];       // [n][CF_PITCH] data, then n / 2 twiddles
+    float2* sTw = sm + n * CF_PITCH;
+    const int x0 = blockIdx.x * CF_TX;
+    const int ncol = min(CF_TX, nxh - x0);
+    float2* col = a + (long)blockIdx.y * sOuter + x0;
+    for (int k = threadIdx.x; k < (n >> 1); k += CF_THREADS) {
+        float2 w = tw[k];                   // exp(-2 pi i k / n)
+        if (INV) w.y = -w.y;
+        sTw[k] = w;
+    }
+    // CF_THREADS / CF_TX rows per sweep; eight sweeps in flight
+#pragma unroll 8
+    for (int q = threadIdx.x; q < n * CF_TX; q += CF_THREADS) {
+        const int p = q / CF_TX, c = q % CF_TX;
+        const float2 v = c < ncol ? col[(long)p * sAxis + c] : make_float2(0.f, 0.f);
+        sm[(int)(__brev((unsigned)p) >> (32 - logn)) * CF_PITCH + c] = v;
+    }
+    __syncthreads();
+    for (int half = 1, st = n >> 1; half < n; half <<= 1, st >>= 1) {
+#pragma unroll 4
+        for (int q = threadIdx.x; q < (n >> 1) * CF_TX; q += CF_THREADS) {
+            const int j = q / CF_TX, c = q % CF_TX;
+            const int k = j & (half - 1);
+            const int i0 = ((j - k) << 1) + k, i1 = i0 + half;
+            const float2 w = sTw[k * st];
+            const float2 u = sm[i0 * CF_PITCH + c], v = sm[i1 * CF_PITCH + c];
+            const float2 t = make_float2(w.x * v.x - w.y * v.y, w.x * v.y + w.y * v.x);
+            sm[i0 * CF_PITCH + c] = make_float2(u.x + t.x, u.y + t.y);
+            sm[i1 * CF_PITCH + c] = make_float2(u.x - t.x, u.y - t.y);
+        }
+        __syncthreads();
+    }
+#pragma unroll 8
+    for (int q = threadIdx.x; q < n * CF_TX; q += CF_THREADS) {
+        const int p = q / CF_TX, c = q % CF_TX;
+        if (c < ncol) col[(long)p * sAxis + c] = sm[p * CF_PITCH + c];
+    }
+}
+
 // ---------------------------------------------------------- MKB kernel table
 // MKB_RL_R2 (src/Functions/Functions.cpp, FUNCTIONS_MKB_ORDER_0):
 // (2 pi)^1.5 a^3 / I0(alpha) * I_{3/2}(v) / v^1.5 (u^2 <= alpha^2) or
@@ -290,8 +358,18 @@ double mkb_rl_r2(double r2, double a, double alpha)
 
 struct Plans {
     hipfftHandle c2r = 0, r2c = 0, r2cN = 0;
+    hipfftHandle c2rX = 0, r2cX = 0;     // 1D batched along x (the column-pass transforms)
+    float2* tw = nullptr;                // vdim / 2 twiddles exp(-2 pi i k / vdim)
+    bool cols = false;                   // the column-pass transforms are available
     size_t work = 0;
 };
+
+// The column-pass 3D transforms: power-of-two vdim whose LDS tile fits
+bool col_fft_ok(int vdim)
+{
+    return vdim >= 16 && (vdim & (vdim - 1)) == 0 &&
+           (size_t)vdim * (CF_PITCH + 1) * sizeof(float2) <= 160 * 1024;
+}
 
 int make_plans(Plans& p, int vdim, int N)
 {
@@ -306,7 +384,92 @@ int make_plans(Plans& p, int vdim, int N)
     THX_FFT(hipfftSetAutoAllocation(p.r2cN, 0));
     THX_FFT(hipfftMakePlan3d(p.r2cN, N, N, N, HIPFFT_R2C, &w3));
     p.work = std::max(w1, std::max(w2, w3));
+    p.cols = col_fft_ok(vdim);
+    if (p.cols) {
+        size_t w4 = 0, w5 = 0;
+        int n[1] = {vdim}, nh[1] = {vdim / 2 + 1};
+        const int batch = vdim * vdim;
+        THX_FFT(hipfftCreate(&p.c2rX));
+        THX_FFT(hipfftSetAutoAllocation(p.c2rX, 0));
+        THX_FFT(hipfftMakePlanMany(p.c2rX, 1, n, nh, 1, vdim / 2 + 1, n, 1, vdim, HIPFFT_C2R, batch,
+                                   &w4));
+        THX_FFT(hipfftCreate(&p.r2cX));
+        THX_FFT(hipfftSetAutoAllocation(p.r2cX, 0));
+        THX_FFT(hipfftMakePlanMany(p.r2cX, 1, n, n, 1, vdim, nh, 1, vdim / 2 + 1, HIPFFT_R2C, batch,
+                                   &w5));
+        p.work = std::max(p.work, std::max(w4, w5));
+        std::vector<float2> h(vdim / 2);
+        for (int k = 0; k < vdim / 2; k++) {
+            const double t = -2.0 * M_PI * k / vdim;
+            h[k] = make_float2((float)std::cos(t), (float)std::sin(t));
+        }
+        THX_HIP(hipMalloc(reinterpret_cast<void**>(&p.tw), sizeof(float2) * h.size()));
+        THX_HIP(hipMemcpy(p.tw, h.data(), sizeof(float2) * h.size(), hipMemcpyHostToDevice));
+    }
     return THX_OK;
+}
+
+// The 3D C2R / R2C of the balancing loop and the final pad: hipFFT's 3D
+// plans, or (p.cols) two column passes + hipFFT's batched 1D transform along
+// x.  C is overwritten either way (hipFFT's out-of-place C2R may too).
+// THX_RECON_FFT=hipfft forces the 3D plans (A/B timing).
+bool use_cols(const Plans& p, int method = 0)
+{
+    if (method == 1) return false;
+    if (method == 2) return p.cols;
+    static const bool off = [] {
+        const char* e = std::getenv("THX_RECON_FFT");
+        return e && std::string(e) == "hipfft";
+    }();
+    return p.cols && !off;
+}
+
+int col_pass(const Plans& p, float2* C, int vdim, bool inv, bool zAxis, hipStream_t s)
+{
+    const int nxh = vdim / 2 + 1;
+    int logn = 0;
+    while ((1 << logn) < vdim) logn++;
+    const dim3 g((nxh + CF_TX - 1) / CF_TX, vdim);
+    const long sAxis = zAxis ? (long)vdim * nxh : nxh;
+    const long sOuter = zAxis ? nxh : (long)vdim * nxh;
+    const size_t lds = ((size_t)vdim * CF_PITCH + vdim / 2) * sizeof(float2);
+    static std::atomic<unsigned> ldsSet[2];
+    THX_RET(thx::set_max_lds(inv ? reinterpret_cast<const void*>(k_col_fft<true>)
+                                 : reinterpret_cast<const void*>(k_col_fft<false>),
+                             160 * 1024, ldsSet[inv ? 1 : 0]));
+    if (inv)
+        hipLaunchKernelGGL(k_col_fft<true>, g, dim3(CF_THREADS), lds, s, C, vdim, logn, sAxis, sOuter,
+                           nxh, p.tw);
+    else
+        hipLaunchKernelGGL(k_col_fft<false>, g, dim3(CF_THREADS), lds, s, C, vdim, logn, sAxis, sOuter,
+                           nxh, p.tw);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+int c2r3d(const Plans& p, float2* C, float* rl, int vdim, hipStream_t s, int method = 0)
+{
+    if (!use_cols(p, method)) {
+        THX_FFT(hipfftExecC2R(p.c2r, reinterpret_cast<hipfftComplex*>(C), rl));
+        return THX_OK;
+    }
+    int st = col_pass(p, C, vdim, true, true, s);
+    if (st == THX_OK) st = col_pass(p, C, vdim, true, false, s);
+    if (st != THX_OK) return st;
+    THX_FFT(hipfftExecC2R(p.c2rX, reinterpret_cast<hipfftComplex*>(C), rl));
+    return THX_OK;
+}
+
+int r2c3d(const Plans& p, float* rl, float2* C, int vdim, hipStream_t s, int method = 0)
+{
+    if (!use_cols(p, method)) {
+        THX_FFT(hipfftExecR2C(p.r2c, rl, reinterpret_cast<hipfftComplex*>(C)));
+        return THX_OK;
+    }
+    THX_FFT(hipfftExecR2C(p.r2cX, rl, reinterpret_cast<hipfftComplex*>(C)));
+    int st = col_pass(p, C, vdim, false, false, s);
+    if (st == THX_OK) st = col_pass(p, C, vdim, false, true, s);
+    return st;
 }
 
 // Plans per (device, vdim, N, stream), made once: creating a 512^3 hipFFT
@@ -432,6 +595,12 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
     THX_FFT(hipfftSetWorkArea(pl.r2c, fftWork));
     THX_FFT(hipfftSetStream(pl.c2r, s));
     THX_FFT(hipfftSetStream(pl.r2c, s));
+    if (pl.cols) {
+        THX_FFT(hipfftSetWorkArea(pl.c2rX, fftWork));
+        THX_FFT(hipfftSetWorkArea(pl.r2cX, fftWork));
+        THX_FFT(hipfftSetStream(pl.c2rX, s));
+        THX_FFT(hipfftSetStream(pl.r2cX, s));
+    }
     if (dstFT) {
         THX_FFT(hipfftSetWorkArea(pl.r2cN, fftWork));
         THX_FFT(hipfftSetStream(pl.r2cN, s));
@@ -466,10 +635,10 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
         unsigned* bits = nullptr;
         THX_HIP(hipHostMalloc(reinterpret_cast<void**>(&bits), sizeof(unsigned), 0));
         for (m = 0; m < 30; m++) {                                // MAX_N_ITER_BALANCE
-            THX_FFT(hipfftExecC2R(pl.c2r, reinterpret_cast<hipfftComplex*>(C), rl));
+            THX_RET(c2r3d(pl, C, rl, vdim, s));
             hipLaunchKernelGGL(k_kernel_mul, gSlab, bSlab, 0, s, rl, vdim, oct, mVdim);
             THX_LAUNCH_CHECK();
-            THX_FFT(hipfftExecR2C(pl.r2c, rl, reinterpret_cast<hipfftComplex*>(C)));
+            THX_RET(r2c3d(pl, rl, C, vdim, s));
             THX_HIP(hipMemsetAsync(diff, 0, sizeof(unsigned), s));
             // W update + the next iteration's C in one pass
             hipLaunchKernelGGL(k_update_w, gSlab, bSlab, 0, s, W, C, T, vdim, r2, mNc, diff);
@@ -495,7 +664,7 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
     // F W -> real space -> central box, kernel-corrected
     hipLaunchKernelGGL(k_pad, g, b, 0, s, C, reinterpret_cast<const float2*>(F), W, vdim, r2);
     THX_LAUNCH_CHECK();
-    THX_FFT(hipfftExecC2R(pl.c2r, reinterpret_cast<hipfftComplex*>(C), rl));
+    THX_RET(c2r3d(pl, C, rl, vdim, s));
     hipLaunchKernelGGL(k_extract, g, b, 0, s, dst, rl, N, vdim, scaleBw);
     THX_LAUNCH_CHECK();
     if (dstFT) {
@@ -504,5 +673,43 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
     }
     // the plans are shared: finish before another call rebinds their stream
     THX_HIP(hipStreamSynchronize(s));
+    return THX_OK;
+}
+
+// FFT::fw / FFT::bw of a volume (src/FFT.cpp, unnormalised r2c / c2r of
+// box vdim): rl [vdim^3] real, C [vdim][vdim][vdim/2+1] complex; inverse 1
+// overwrites C.  method 0: the reconstruction's choice, 1: hipFFT's 3D plans,
+// 2: the column passes (error if vdim is not a power of two with an LDS tile).
+extern "C" size_t thx_fft3d_workspace(int vdim)
+{
+    if (vdim <= 0 || vdim % 2) return 0;
+    std::unique_lock<std::mutex> lk;
+    PlanEntry* e = nullptr;
+    if (cached_plans(vdim, vdim / 2, nullptr, &e, lk) != THX_OK) return 0;
+    return e->p.work + 256;
+}
+
+extern "C" int thx_fft3d(float* C, float* rl, int vdim, int inverse, int method, void* workspace,
+                         size_t wsBytes, thx_stream_t stream)
+{
+    THX_CHECK_ARG(C && rl && vdim > 0 && vdim % 2 == 0 && method >= 0 && method <= 2,
+                  "thx_fft3d: bad arguments");
+    hipStream_t s = thx::as_stream(stream);
+    std::unique_lock<std::mutex> lk;
+    PlanEntry* pe = nullptr;
+    THX_RET(cached_plans(vdim, vdim / 2, s, &pe, lk));
+    Plans& pl = pe->p;
+    THX_CHECK_ARG(method != 2 || pl.cols, "thx_fft3d: no column passes for this vdim");
+    THX_CHECK_ARG(workspace && wsBytes >= pl.work, "thx_fft3d: workspace too small");
+    for (hipfftHandle h : {pl.c2r, pl.r2c, pl.c2rX, pl.r2cX}) {
+        if (!h) continue;
+        THX_FFT(hipfftSetWorkArea(h, workspace));
+        THX_FFT(hipfftSetStream(h, s));
+    }
+    if (inverse)
+        THX_RET(c2r3d(pl, reinterpret_cast<float2*>(C), rl, vdim, s, method));
+    else
+        THX_RET(r2c3d(pl, rl, reinterpret_cast<float2*>(C), vdim, s, method));
+    THX_HIP(hipStreamSynchronize(s));      // the plans are shared across calls on this stream
     return THX_OK;
 }
