@@ -410,18 +410,20 @@ int make_plans(Plans& p, int vdim, int N)
 }
 
 // The 3D C2R / R2C of the balancing loop and the final pad: hipFFT's 3D
-// plans, or (p.cols) two column passes + hipFFT's batched 1D transform along
-// x.  C is overwritten either way (hipFFT's out-of-place C2R may too).
-// THX_RECON_FFT=hipfft forces the 3D plans (A/B timing).
+// plans (default), or (p.cols) two column passes + hipFFT's batched 1D
+// transform along x.  Measured at 512^3 (profiles/r03_fft_ab.jsonl): hipFFT
+// 1.48-1.49 ms per transform, the radix-2 column passes 1.64-1.81 ms, so the
+// 3D plans stay; THX_RECON_FFT=columns selects the column passes (A/B).
+// C is overwritten either way (hipFFT's out-of-place C2R may too).
 bool use_cols(const Plans& p, int method = 0)
 {
     if (method == 1) return false;
     if (method == 2) return p.cols;
-    static const bool off = [] {
+    static const bool on = [] {
         const char* e = std::getenv("THX_RECON_FFT");
-        return e && std::string(e) == "hipfft";
+        return e && std::string(e) == "columns";
     }();
-    return p.cols && !off;
+    return p.cols && on;
 }
 
 int col_pass(const Plans& p, float2* C, int vdim, bool inv, bool zAxis, hipStream_t s)
