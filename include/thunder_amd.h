@@ -260,6 +260,10 @@ int thx_volume_cells(const float* vol, int vdim, float* cells,
  * brick when y0, z0 are even, so a sample touches ~2.8 cache lines instead
  * of ~4.25 (thx_local_phase volLayout 2; thx_expectation builds one per
  * class in its workspace).  bricks: thx_volume_bricks_bytes(vdim) bytes. */
+/* The y-pair copy of a half-complex projectee (thx_local_phase volLayout 3):
+ * element (x, y, z) = (v(x, y, z), v(x, y + 1, z)), rows wrapped, 16 B; a
+ * trilinear cell is two 32-B pieces.  ypair: 4 dimSize floats. */
+int thx_volume_ypair(const float* vol, int vdim, float* ypair, thx_stream_t stream);
 size_t thx_volume_bricks_bytes(int vdim);
 int thx_volume_bricks(const float* vol, int vdim, float* bricks, thx_stream_t stream);
 

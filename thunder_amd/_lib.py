@@ -54,6 +54,7 @@ SIGNATURES = {
     "thx_pf_balance_rot": (_c_int, [_c_int, _c_int, _p, _p, _p]),
     "thx_global_sample_set2d": (_c_int, [_c_int, _c_int, _c_double, ctypes.c_ulonglong, _p, _p, _p,
                                          _p, _p]),
+    "thx_volume_ypair": (_c_int, [_p, _c_int, _p, _p]),
     "thx_fft3d_workspace": (_c_size, [_c_int]),
     "thx_fft3d": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _p, _c_size, _p]),
     "thx_pf_acg_mean": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _p, _p]),

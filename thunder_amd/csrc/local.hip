@@ -116,6 +116,31 @@ THX_DEV float2 interp_cell_piece(const float4* __restrict__ cells, int vdim, flo
     return make_float2(re, conj ? -im : im);
 }
 
+// y-pair projectee (thx_volume_ypair): element (x, y, z) holds v(x, y, z) and
+// v(x, y + 1, z) (rows wrapped), 16 B, x fastest as the half-complex rows, so
+// a trilinear cell is two 32-B pieces -- elements x0, x0 + 1 at z0 and at
+// z0 + 1 -- instead of four 16-B row pieces, at twice the footprint (the
+// low-resolution ball of the phases: 3.9 MB at box 256).  Quad-cooperative
+// like the cells: lane j reads element x0 + (j & 1) of slice z0 + (j >> 1);
+// the quad's two lanes per slice share one 32-B segment.
+THX_DEV float2 interp_ypair_piece(const float4* __restrict__ yp, int vdim, float x, float y,
+                                  float z, int j)
+{
+    const bool conj = !(x >= 0.f);
+    if (conj) { x = -x; y = -y; z = -z; }
+    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+    const float dx = x - fx, dy = y - fy, dz = z - fz;
+    const int nColFT = vdim / 2 + 1;
+    const size_t e = ((size_t)wrap_idx(z0 + (j >> 1), vdim) * vdim + wrap_idx(y0, vdim)) * nColFT +
+                     x0 + (j & 1);
+    const float4 q = yp[e];
+    const float wxz = ((j & 1) ? dx : 1.f - dx) * ((j >> 1) ? dz : 1.f - dz);
+    const float w0 = wxz * (1.f - dy), w1 = wxz * dy;
+    const float re = q.x * w0 + q.z * w1, im = q.y * w0 + q.w * w1;
+    return make_float2(re, conj ? -im : im);
+}
+
 // sum over the lanes of each quad (DPP quad permutations), every lane gets it
 THX_DEV float quad_sum(float v)
 {
@@ -132,7 +157,9 @@ THX_DEV float quad_sum(float v)
 // (1 + 1/16) 2 2 = 4.25, at the same footprint (the L2-resident working set
 // of a phase stays L2-resident).  Rows / slices wrapped like iFTHalf; bricks
 // past the half-plane edge (x >= nColFT) hold zeros.
-enum { LAYOUT_FT = 0, LAYOUT_CELLS = 1, LAYOUT_BRICKS = 2 };
+enum { LAYOUT_FT = 0, LAYOUT_CELLS = 1, LAYOUT_BRICKS = 2, LAYOUT_YPAIR = 3 };
+// layouts gathered quad-cooperatively (no LDS boxes, no patch records)
+constexpr bool coop_layout(int l) { return l == LAYOUT_CELLS || l == LAYOUT_YPAIR; }
 
 THX_DEV int bricks_nx(int vdim) { return (vdim / 2 + 1 + 3) / 4; }
 
@@ -553,7 +580,7 @@ template <int LAYOUT, int NI = NIT, int CAP = BOX_CAP>
 THX_DEV void fetch_box(f32x4 (&pre)[NI][2], int (&dst)[NI], const Rec& b,
                        const float2* __restrict__ vol, int vdim, int tid)
 {
-    if (LAYOUT == LAYOUT_CELLS || !(b.v[10] <= CAP)) return;   // cells: never staged
+    if (coop_layout(LAYOUT) || !(b.v[10] <= CAP)) return;   // cells / y-pairs: never staged
     const int nColFT = vdim / 2 + 1;
     const int nq = b.v[6] >> 2, ny = b.v[8];
 #pragma unroll
@@ -673,7 +700,7 @@ template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false, bool ST
 // no LDS box (cell layout, or STAGE = false): no box prefetch registers, so
 // 6 waves per SIMD (three workgroups per CU) for the L2 gathers
 __global__ void __launch_bounds__(THREADS)
-__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : (LAYOUT == LAYOUT_CELLS || !STAGE) ? THX_NOBOX_WAVES : 4)))
+__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : (coop_layout(LAYOUT) || !STAGE) ? THX_NOBOX_WAVES : 4)))
 k_local_fused(const float2* __restrict__ vol,
                                                             int vdim, int pf,
                                                             const double* __restrict__ quat,
@@ -717,7 +744,7 @@ k_local_fused(const float2* __restrict__ vol,
     // the cell layout gathers every sample quad-cooperatively: no LDS box, no
     // patch records (padding entries sample pixel (0, 0)), so a CU holds as
     // many workgroups as the VGPRs allow
-    constexpr bool COOP = LAYOUT == LAYOUT_CELLS;
+    constexpr bool COOP = coop_layout(LAYOUT);
     // STAGE = false: every patch gathered from L2 (no box, no records)
     constexpr bool NOBOX = COOP || !STAGE;
     auto staged = [](const Rec& r) { return !NOBOX && r.v[10] <= BOXC; };
@@ -729,7 +756,7 @@ k_local_fused(const float2* __restrict__ vol,
 #ifndef THX_NOBOX_PP
 #define THX_NOBOX_PP 2
 #endif
-    constexpr int PP = (LAYOUT == LAYOUT_CELLS || !STAGE) && !CS ? THX_NOBOX_PP : 1;
+    constexpr int PP = (coop_layout(LAYOUT) || !STAGE) && !CS ? THX_NOBOX_PP : 1;
     constexpr int PKC = PP * KC;                        // pixels per iteration
     constexpr int NE = (PKC * TT + THREADS - 1) / THREADS;   // image-tile elements per thread
     const int r0 = blockIdx.y * RT, t0 = blockIdx.z * NC;
@@ -936,7 +963,9 @@ k_local_fused(const float2* __restrict__ vol,
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
                 const float z = (float)(m[2] * xy.x + m[5] * xy.y);
-                const float2 v = interp_cell_piece(reinterpret_cast<const float4*>(vol), vdim, x, y, z, j);
+                const float2 v = LAYOUT == LAYOUT_YPAIR
+                                     ? interp_ypair_piece(reinterpret_cast<const float4*>(vol), vdim, x, y, z, j)
+                                     : interp_cell_piece(reinterpret_cast<const float4*>(vol), vdim, x, y, z, j);
                 P[p] = make_float2(quad_sum(v.x), quad_sum(v.y));
             }
             if (!CS)
@@ -1296,6 +1325,24 @@ __global__ void __launch_bounds__(256) k_volume_cells(const float2* __restrict__
     }
 }
 
+// One thread per element of the y-pair copy: (v(x, y, z), v(x, y + 1, z)),
+// rows wrapped like iFTHalf.
+__global__ void __launch_bounds__(256) k_volume_ypair(const float2* __restrict__ vol, int vdim,
+                                                      float4* __restrict__ yp)
+{
+    const int nColFT = vdim / 2 + 1;
+    const long n = (long)nColFT * vdim * vdim;
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
+         q += (long)gridDim.x * blockDim.x) {
+        const int i = (int)(q % nColFT);
+        const long jk = q / nColFT;
+        const int j = (int)(jk % vdim), k = (int)(jk / vdim);
+        const int j1 = j + 1 == vdim ? 0 : j + 1;
+        const float2 a = vol[q], b = vol[((size_t)k * vdim + j1) * nColFT + i];
+        yp[q] = make_float4(a.x, a.y, b.x, b.y);
+    }
+}
+
 // One thread per 8-B voxel of the bricked copy (its own write coalesced).
 __global__ void __launch_bounds__(256) k_volume_bricks(const float2* __restrict__ vol,
                                                        int vdim, float2* __restrict__ out)
@@ -1371,6 +1418,15 @@ extern "C" int thx_volume_cells(const float* vol, int vdim, float* cells,
     return THX_OK;
 }
 
+extern "C" int thx_volume_ypair(const float* vol, int vdim, float* ypair, thx_stream_t stream)
+{
+    THX_CHECK_ARG(vol && ypair && vdim > 0 && vdim % 2 == 0, "thx_volume_ypair: bad arguments");
+    hipLaunchKernelGGL(k_volume_ypair, dim3(4096), dim3(256), 0, thx::as_stream(stream),
+                       reinterpret_cast<const float2*>(vol), vdim, reinterpret_cast<float4*>(ypair));
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 extern "C" size_t thx_volume_bricks_bytes(int vdim)
 {
     if (vdim <= 0 || vdim % 2) return 0;
@@ -1432,7 +1488,8 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     THX_CHECK_ARG(!nD || (pD && wD && (long)nT * nD <= LOCAL_D_MAXCOL),
                   "thx_local_phase_d: needs pD, wD and nT * nD <= 1024");
     const int nCol = nD ? nT * nD : nT;
-    THX_CHECK_ARG(volLayout >= 0 && volLayout <= 2, "thx_local_phase: volLayout must be 0, 1 or 2");
+    THX_CHECK_ARG(volLayout >= 0 && volLayout <= 3, "thx_local_phase: volLayout must be 0 .. 3");
+    THX_CHECK_ARG(volLayout != LAYOUT_YPAIR || !nD, "thx_local_phase_d: no y-pair layout with CTF search");
     THX_CHECK_ARG((long)nImg * ((nR + RT - 1) / RT) <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 &&
                       (nCol + TT - 1) / TT <= 65535,
                   "thx_local_phase: grid too large");
@@ -1475,7 +1532,7 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * nRT), dim3(64 * PB_WAVES), 0, s, quat,
                            nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct, route, 2);
         THX_LAUNCH_CHECK();
-    } else if (volLayout != LAYOUT_CELLS) {   // the cell layout's quad gathers use no patch boxes
+    } else if (!coop_layout(volLayout)) {   // the quad gathers use no patch boxes
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * nRT), dim3(64 * PB_WAVES), 0, s, quat,
                            nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct, nullptr, 0);
         THX_LAUNCH_CHECK();
@@ -1516,7 +1573,8 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         return THX_OK;
     }
     auto kern =
-        volLayout == LAYOUT_CELLS
+        volLayout == LAYOUT_YPAIR ? k_local_fused<LAYOUT_YPAIR>
+        : volLayout == LAYOUT_CELLS
             ? (big ? k_local_fused<LAYOUT_CELLS, false, 1, true> : k_local_fused<LAYOUT_CELLS>)
         : volLayout == LAYOUT_BRICKS
             ? (big ? k_local_fused<LAYOUT_BRICKS, false, 1, true> : k_local_fused<LAYOUT_BRICKS>)

@@ -26,6 +26,8 @@
 #include <cmath>
 #include <map>
 #include <mutex>
+#include <cstdlib>
+#include <string>
 #include <utility>
 
 #include "common.h"
@@ -1179,6 +1181,68 @@ __global__ void __launch_bounds__(256) k_sample_set(int nR, int nT, double trans
     for (int t = threadIdx.x; t < nT; t += 256) pT[t] /= tt;
 }
 
+// Phase launch order by slice orientation (THX_XCD_ORDER=1, A/B): workgroup
+// b of a phase launch runs on XCD b % 8, so act[b] deals the images sorted by
+// the normal of their cloud's first rotation (the slice plane's normal R e_z,
+// sign-folded to the upper hemisphere, Morton key of its (x, y) on a 64 x 64
+// grid) in eight contiguous runs, one per XCD: an XCD then gathers from the
+// planes of nearby orientations only -- about half of the projectee's ball --
+// which is what lets a larger layout (the y-pair copy) stay in its 4 MB L2.
+// One workgroup: counting sort over the 4096 keys, then the deal.
+constexpr int XO_BINS = 4096;
+__global__ void __launch_bounds__(1024) k_xcd_order(int nImg, int mR, const double* __restrict__ quat,
+                                                    int* __restrict__ key, int* __restrict__ act,
+                                                    int* __restrict__ nAct)
+{
+    __shared__ int sCnt[XO_BINS];
+    __shared__ int sW[16];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int b = tid; b < XO_BINS; b += 1024) sCnt[b] = 0;
+    __syncthreads();
+    for (int l = tid; l < nImg; l += 1024) {
+        const double* q = quat + (size_t)l * mR * 4;
+        const double w = q[0], x = q[1], y = q[2], z = q[3];
+        double nx = 2.0 * (x * z + w * y), ny = 2.0 * (y * z - w * x);
+        const double nz = 1.0 - 2.0 * (x * x + y * y);
+        if (nz < 0.0) { nx = -nx; ny = -ny; }
+        const unsigned ix = (unsigned)fmin(63.0, fmax(0.0, (nx + 1.0) * 32.0));
+        const unsigned iy = (unsigned)fmin(63.0, fmax(0.0, (ny + 1.0) * 32.0));
+        unsigned k = 0;
+        for (int bit = 0; bit < 6; bit++) k |= (((ix >> bit) & 1u) << (2 * bit)) | (((iy >> bit) & 1u) << (2 * bit + 1));
+        key[l] = (int)k;
+        atomicAdd(&sCnt[k], 1);
+    }
+    __syncthreads();
+    // exclusive prefix over the bins (4 per thread, then a block scan)
+    int loc[4], run = 0;
+    for (int u = 0; u < 4; u++) { loc[u] = run; run += sCnt[4 * tid + u]; }
+    int inc = run;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += v;
+    }
+    if (lane == 63) sW[wv] = inc;
+    __syncthreads();
+    int base = inc - run;
+    for (int w2 = 0; w2 < wv; w2++) base += sW[w2];
+    __syncthreads();
+    for (int u = 0; u < 4; u++) sCnt[4 * tid + u] = base + loc[u];
+    __syncthreads();
+    // scatter: sorted position of image l, then the deal to (XCD x, slot j)
+    for (int l = tid; l < nImg; l += 1024) {
+        const int pos = atomicAdd(&sCnt[key[l]], 1);
+        // sorted position pos -> launch slot b with XCD x = the run holding pos
+        int x = 0, start = 0;
+        for (; x < 8; x++) {
+            const int cnt = (nImg - x + 7) / 8;
+            if (pos < start + cnt) break;
+            start += cnt;
+        }
+        act[(pos - start) * 8 + x] = l;
+    }
+    if (tid == 0) *nAct = nImg;
+}
+
 struct Plan {
     // carve of the driver workspace
     float* rotP; double* gMat; float* traP;
@@ -1192,13 +1256,33 @@ struct Plan {
     float* wC; float* wR; float* wT; float* base; double* pC;
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
     double* bestR; double* bestT;                        // convergence: smallest variR / variT
+    int* xoKey; int* xoAct; int* xoN;                    // THX_XCD_ORDER: keys, launch order
     void* localWs; size_t localWsBytes;
     float* bricks; size_t brickStride;   // bricked projectees (thx_volume_bricks), per class
+    float* ypair;                        // y-pair projectees (thx_volume_ypair), per class
     // CTF search: defocus precalculation, per-phase CTF table, D statistics
     float* freq; float* dfo; float* K1; float* K2; float* ctfD; float* wD;
     double* sdD; double* bestD; double* tmpD; int* topD;
     size_t bytes;
 };
+
+bool xcd_order()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("THX_XCD_ORDER");
+        return e && std::string(e) == "1";
+    }();
+    return on;
+}
+
+bool ypair_phases()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("THX_PHASE_LAYOUT");
+        return e && std::string(e) == "ypair";
+    }();
+    return on;
+}
 
 // mLD > 0: the workspace of a CTF search over mLD defocus samples
 Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, int mLD = 0,
@@ -1246,6 +1330,9 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.nAct = k.take<int>(1);
     p.bestR = k.take<double>(nImg);
     p.bestT = k.take<double>(nImg);
+    p.xoKey = k.take<int>(nImg);
+    p.xoAct = k.take<int>(nImg);
+    p.xoN = k.take<int>(1);
     p.localWsBytes = twoD ? thx_local_phase2d_d_workspace(nImg, c.mLR, c.mLT, mLD)
                           : thx_local_phase_workspace(nImg, c.mLR, c.mLT * (mLD > 0 ? mLD : 1),
                                                       nVisit);
@@ -1271,6 +1358,10 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
 #endif
     p.brickStride = thx_volume_bricks_bytes(c.vdim) / sizeof(float);
     p.bricks = THX_BRICKS && !c.volCells && !twoD ? k.take<float>(p.brickStride * nK) : nullptr;
+    // THX_PHASE_LAYOUT=ypair (A/B): the phases gather from y-pair copies
+    p.ypair = ypair_phases() && !p.bricks && !c.volCells && !twoD && mLD == 0
+                  ? k.take<float>((size_t)4 * (c.vdim / 2 + 1) * c.vdim * c.vdim * nK)
+                  : nullptr;
     p.bytes = k.off + 256;
     return p;
 }
@@ -1615,6 +1706,10 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     int* clsD = cls ? cls : p.cls;
     int* nPD = nPhaseOut ? nPhaseOut : p.nP;
     const int* clsSel = nK > 1 ? clsD : nullptr;    // rows / volumes picked per image
+    if (p.ypair)
+        for (int k = 0; k < nK; k++)
+            THX_RET(thx_volume_ypair(vol + 2 * dimSize * k, c.vdim,
+                                     p.ypair + 4 * dimSize * k, stream));
     if (p.bricks)
         for (int k = 0; k < nK; k++)
             THX_RET(thx_volume_bricks(vol + 2 * dimSize * k, c.vdim, p.bricks + p.brickStride * k,
@@ -1705,10 +1800,10 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     const int nPh = c.converge ? c.maxPhase - phase0 : c.nPhase;
     const int* done = nullptr;
     // the phases' volume: the caller's cell copy, the bricked copies, or vol
-    const float* phaseVol = c.volCells ? c.volCells : p.bricks ? p.bricks : vol;
-    const int phaseLayout = c.volCells ? 1 : p.bricks ? 2 : 0;
+    const float* phaseVol = c.volCells ? c.volCells : p.bricks ? p.bricks : p.ypair ? p.ypair : vol;
+    const int phaseLayout = c.volCells ? 1 : p.bricks ? 2 : p.ypair ? 3 : 0;
     thx_local_sel sel{nullptr, nullptr, clsSel,
-                      (long long)(p.bricks ? p.brickStride / 2 : dimSize)};
+                      (long long)(p.bricks ? p.brickStride / 2 : p.ypair ? 2 * dimSize : dimSize)};
     if (c.converge) {
         THX_HIP(hipMemsetAsync(p.done, 0, sizeof(int) * nImg, s));
         hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
@@ -1763,6 +1858,13 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
 #endif
         // phases past the caller's event pairs run untimed
         hipEvent_t* ev = pi < c.nPhaseEvents ? static_cast<hipEvent_t*>(c.phaseEvents) : nullptr;
+        if (xcd_order() && !c.converge && !twoD) {
+            hipLaunchKernelGGL(k_xcd_order, dim3(1), dim3(1024), 0, s, nImg, c.mLR, quat, p.xoKey,
+                               p.xoAct, p.xoN);
+            THX_LAUNCH_CHECK();
+            sel.active = p.xoAct;
+            sel.nActive = p.xoN;
+        }
         if (twoD) {
             if (ev) THX_HIP(hipEventRecord(ev[2 * pi], s));
             THX_RET(thx::local_phase2d_launch(vol, c.vdim, c.pf, clsSel, quat, 4, c.mLR, trans,

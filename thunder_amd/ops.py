@@ -288,10 +288,13 @@ def volume_cells(vol):
     return out
 
 
-def _layout(vol, cells, bricks):
+def _layout(vol, cells, bricks, ypair=None):
     """(volLayout, volume argument) of thx_local_phase for the given copies."""
-    if cells is not None and bricks is not None:
-        raise ValueError("cells and bricks are alternatives")
+    if sum(x is not None for x in (cells, bricks, ypair)) > 1:
+        raise ValueError("cells, bricks and ypair are alternatives")
+    if ypair is not None:
+        _req(ypair, torch.complex64, tuple(vol.shape) + (2,), "ypair")
+        return 3, ypair
     if cells is not None:
         _req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
         return 1, cells
@@ -300,6 +303,16 @@ def _layout(vol, cells, bricks):
         _req(bricks, torch.complex64, (lib().thx_volume_bricks_bytes(vdim) // 8,), "bricks")
         return 2, bricks
     return 0, vol
+
+
+def volume_ypair(vol):
+    """y-pair copy [vdim, vdim, vdim/2+1, 2]: element (x, y, z) = (v(x, y, z),
+    v(x, y+1, z)), so a trilinear cell is two 32-B pieces (thx_volume_ypair)."""
+    vdim = _vol_dim(vol)
+    out = torch.empty(tuple(vol.shape) + (2,), dtype=torch.complex64, device=vol.device)
+    check(lib().thx_volume_ypair(_ptr(vol), vdim, _ptr(out), _stream(vol.device)),
+          "thx_volume_ypair")
+    return out
 
 
 def volume_bricks(vol):
@@ -314,12 +327,12 @@ def volume_bricks(vol):
 
 
 def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False, cells=None,
-                tiled=True, bricks=None):
+                tiled=True, bricks=None, ypair=None):
     """cells / bricks: optional thx_volume_cells / thx_volume_bricks copy of
     vol (used for the gathers and the staged boxes).
     tiled: visit pixels in px.order (LDS-staged neighbourhoods) instead of set order."""
     vdim = _vol_dim(vol)
-    layout, src = _layout(vol, cells, bricks)
+    layout, src = _layout(vol, cells, bricks, ypair)
     nImg, nPxl = _images(dat, ctf_, sig)
     if nPxl != px.n:
         raise ValueError("pixel set / image size mismatch")
