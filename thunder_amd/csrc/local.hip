@@ -39,6 +39,9 @@
 
 #include <cmath>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 #include "patch.h"
 
@@ -328,9 +331,26 @@ THX_DEV int store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __res
 #endif
 constexpr int ROUTE_SAMPLE = 16;   // every 16th image's records are counted
 
+// Third route (round 3): when the driver supplies a y-pair copy (route[7] =
+// 1) and fewer than THX_YPAIR_MAX_PCT per cent of the sampled patches have a
+// box of at most 8 BOX_CAP voxels -- the wide clouds of the first phases --
+// the quad-cooperative y-pair kernel runs: two 32-B pieces per sample cost
+// fewer 128-B L2 -> L1 lines than four row pieces when L1 reuse is low
+// (measured on the bench's phases: 13.0 vs 16.4 ms in phase 1, equal at the
+// 20 % point (phase 5), slower after; profiles/r03_ypair_ab.jsonl,
+// r03_route_stats.txt).
+#ifndef THX_YPAIR_MAX_PCT
+#define THX_YPAIR_MAX_PCT 20
+#endif
+constexpr int ROUTE_STAGED = 0, ROUTE_NOBOX = 1, ROUTE_YPAIR = 2;
 THX_DEV bool route_nostage(const int* __restrict__ route)
 {
     return (long)route[0] * 100 < (long)THX_STAGE_MIN_PCT * route[1];
+}
+THX_DEV int route_pick(const int* __restrict__ route)
+{
+    if (route[7] == 1 && (long)route[4] * 100 < (long)THX_YPAIR_MAX_PCT * route[1]) return ROUTE_YPAIR;
+    return route_nostage(route) ? ROUTE_NOBOX : ROUTE_STAGED;
 }
 
 #ifndef THX_SKIP_PAD
@@ -436,7 +456,7 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
     __shared__ int sPerm[RT];
     // routeMode 1: count the records of every ROUTE_SAMPLE-th image into
     // route; 2: build all records unless the count chose the box-less kernel
-    if (routeMode == 2 && route_nostage(route)) return;
+    if (routeMode == 2 && route_pick(route) != ROUTE_STAGED) return;
     const int nC = (nVisit + KC - 1) / KC, nRT = (nR + RT - 1) / RT;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ry = blockIdx.x % nRT;
@@ -445,7 +465,7 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
         if (l >= *nAct) return;
         l = act[l];
     }
-    int nFit = 0, nAll = 0;
+    int nFit = 0, nAll = 0, nF2 = 0, nF4 = 0, nF8 = 0, nF16 = 0;
     const int nRl = min(RT, nR - ry * RT);
     const double* Q = quat + ((size_t)l * nR + ry * RT) * 4;
     rotation_slots(Q, nRl, threadIdx.x, sKey, sPerm);
@@ -539,15 +559,27 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
             const int nv = store_rec(e, ic0, ir0, vdim, rec + (((size_t)l * nRT + ry) * nC + c) * REC);
             nFit += nv <= BOX_CAP;
             nAll += 1;
+            nF2 += nv <= 2 * BOX_CAP;     // the spread of the clouds (y-pair route)
+            nF4 += nv <= 4 * BOX_CAP;
+            nF8 += nv <= 8 * BOX_CAP;
+            nF16 += nv <= 16 * BOX_CAP;
         }
         __syncthreads();
     }
     if (routeMode == 1 && wv == 0) {
         nFit = wave_sum(nFit);
         nAll = wave_sum(nAll);
+        nF2 = wave_sum(nF2);
+        nF4 = wave_sum(nF4);
+        nF8 = wave_sum(nF8);
+        nF16 = wave_sum(nF16);
         if (lane == 0) {
             atomicAdd(&route[0], nFit);
             atomicAdd(&route[1], nAll);
+            atomicAdd(&route[2], nF2);
+            atomicAdd(&route[3], nF4);
+            atomicAdd(&route[4], nF8);
+            atomicAdd(&route[5], nF16);
         }
     }
 }
@@ -730,7 +762,8 @@ k_local_fused(const float2* __restrict__ vol,
                                                             const int* __restrict__ route = nullptr)
 {
     // routed phases launch the staged and the box-less kernel; one exits
-    if (route && route_nostage(route) == STAGE) return;
+    if (route && route_pick(route) != (LAYOUT == LAYOUT_YPAIR ? ROUTE_YPAIR
+                                       : STAGE ? ROUTE_STAGED : ROUTE_NOBOX)) return;
     int l = blockIdx.x;
     if (act) {
         if (l >= *nAct) return;
@@ -1481,7 +1514,8 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
                             const int* pxOrder, int nOrd, int nPxl, int idim, int nImg, float* wC,
                             float* wR, float* wT, float* baseL, float* dvp, void* workspace,
                             size_t wsBytes, thx_stream_t stream, int nD = 0,
-                            const double* pD = nullptr, float* wD = nullptr)
+                            const double* pD = nullptr, float* wD = nullptr,
+                            const float* ypair = nullptr)
 {
     THX_CHECK_ARG(nR > 0 && nT > 0 && nPxl > 0 && nImg >= 0 && vdim > 0 && pf > 0 && nD >= 0,
                   "thx_local_phase: bad sizes");
@@ -1524,7 +1558,8 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     const bool routed = THX_ROUTE && volLayout == LAYOUT_FT && !nD && !big;
     const unsigned nRT = thx::cdiv(nR, RT);
     if (routed) {
-        THX_HIP(hipMemsetAsync(route, 0, 2 * sizeof(int), s));
+        THX_HIP(hipMemsetAsync(route, 0, 8 * sizeof(int), s));
+        if (ypair) THX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(route + 7), 1, 1, s));
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)thx::cdiv(nImg, ROUTE_SAMPLE) * nRT),
                            dim3(64 * PB_WAVES), 0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim,
                            rec, act, nAct, route, 1);
@@ -1593,6 +1628,23 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     if (routed) {
         launch(k_local_fused<LAYOUT_FT, false, 1, false, true>, route);
         launch(k_local_fused<LAYOUT_FT, false, 1, false, false>, route);
+        if (ypair) {
+            hipLaunchKernelGGL(k_local_fused<LAYOUT_YPAIR>, grid, dim3(THREADS), 0, s,
+                               reinterpret_cast<const float2*>(ypair), vdim, pf, quat, nR, trans, nT,
+                               reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
+                               nVisit, nPxl, idim, rec, fuse ? dvp : d, act, nAct, cls,
+                               cls ? 2 * vs : 0L, 1, pC, pR, pT, fuse ? wC : nullptr,
+                               fuse ? wR : nullptr, fuse ? wT : nullptr, fuse ? baseL : nullptr,
+                               route);
+        }
+        static const bool dbg = std::getenv("THX_ROUTE_DEBUG") != nullptr;
+        if (dbg) {      // diagnostic: the route sample's box-size counts (synchronises)
+            int h[6];
+            THX_HIP(hipMemcpyAsync(h, route, sizeof(h), hipMemcpyDeviceToHost, s));
+            THX_HIP(hipStreamSynchronize(s));
+            std::fprintf(stderr, "[route] all %d fit %d x2 %d x4 %d x8 %d x16 %d\n", h[1], h[0], h[2],
+                         h[3], h[4], h[5]);
+        }
     } else {
         launch(kern, nullptr);
     }
@@ -1663,10 +1715,19 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
                       int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
                       void* workspace, size_t wsBytes, thx_stream_t stream, int nD,
-                      const double* pD, float* wD)
+                      const double* pD, float* wD, const float* ypair)
 {
     return local_phase_impl(sel, evBeg, evEnd, vol, volLayout, vdim, pf, quat, nR, trans, nT, pC,
                             pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg,
-                            wC, wR, wT, baseL, nullptr, workspace, wsBytes, stream, nD, pD, wD);
+                            wC, wR, wT, baseL, nullptr, workspace, wsBytes, stream, nD, pD, wD,
+                            ypair);
+}
+
+// whether local_phase_impl routes a phase on the device (half-complex layout,
+// no CTF search, 64 KiB boxes) -- the phases that can use a y-pair copy
+bool phase_routed(int volLayout, int pf, int nPxl, int nD)
+{
+    return THX_ROUTE && volLayout == LAYOUT_FT && !nD &&
+           !(pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R);
 }
 }  // namespace thx

@@ -60,7 +60,9 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
                       int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
                       void* workspace, size_t wsBytes, thx_stream_t stream, int nD = 0,
-                      const double* pD = nullptr, float* wD = nullptr);
+                      const double* pD = nullptr, float* wD = nullptr,
+                      const float* ypair = nullptr);
+bool phase_routed(int volLayout, int pf, int nPxl, int nD);
 }
 
 namespace {
@@ -1260,6 +1262,7 @@ struct Plan {
     void* localWs; size_t localWsBytes;
     float* bricks; size_t brickStride;   // bricked projectees (thx_volume_bricks), per class
     float* ypair;                        // y-pair projectees (thx_volume_ypair), per class
+    bool ypairAll;                       // every phase on the y-pair copy (A/B)
     // CTF search: defocus precalculation, per-phase CTF table, D statistics
     float* freq; float* dfo; float* K1; float* K2; float* ctfD; float* wD;
     double* sdD; double* bestD; double* tmpD; int* topD;
@@ -1275,14 +1278,20 @@ bool xcd_order()
     return on;
 }
 
-bool ypair_phases()
+// THX_PHASE_LAYOUT (A/B): unset = the device route with the y-pair copy for
+// wide clouds; "ft" = the route without it; "ypair" = every phase on the
+// y-pair copy
+int phase_layout_mode()
 {
-    static const bool on = [] {
+    static const int m = [] {
         const char* e = std::getenv("THX_PHASE_LAYOUT");
-        return e && std::string(e) == "ypair";
+        if (!e) return 0;
+        const std::string v(e);
+        return v == "ft" ? 1 : v == "ypair" ? 2 : 0;
     }();
-    return on;
+    return m;
 }
+bool ypair_phases() { return phase_layout_mode() == 2; }
 
 // mLD > 0: the workspace of a CTF search over mLD defocus samples
 Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, int mLD = 0,
@@ -1359,9 +1368,12 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.brickStride = thx_volume_bricks_bytes(c.vdim) / sizeof(float);
     p.bricks = THX_BRICKS && !c.volCells && !twoD ? k.take<float>(p.brickStride * nK) : nullptr;
     // THX_PHASE_LAYOUT=ypair (A/B): the phases gather from y-pair copies
-    p.ypair = ypair_phases() && !p.bricks && !c.volCells && !twoD && mLD == 0
-                  ? k.take<float>((size_t)4 * (c.vdim / 2 + 1) * c.vdim * c.vdim * nK)
-                  : nullptr;
+    // the y-pair copy: every phase on it (THX_PHASE_LAYOUT=ypair), or the
+    // device route's third kernel for wide clouds (default)
+    p.ypairAll = ypair_phases();
+    const bool yp = !p.bricks && !c.volCells && !twoD && mLD == 0 &&
+                    (p.ypairAll || (phase_layout_mode() == 0 && thx::phase_routed(0, c.pf, nPxl, 0)));
+    p.ypair = yp ? k.take<float>((size_t)4 * (c.vdim / 2 + 1) * c.vdim * c.vdim * nK) : nullptr;
     p.bytes = k.off + 256;
     return p;
 }
@@ -1800,10 +1812,13 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     const int nPh = c.converge ? c.maxPhase - phase0 : c.nPhase;
     const int* done = nullptr;
     // the phases' volume: the caller's cell copy, the bricked copies, or vol
-    const float* phaseVol = c.volCells ? c.volCells : p.bricks ? p.bricks : p.ypair ? p.ypair : vol;
-    const int phaseLayout = c.volCells ? 1 : p.bricks ? 2 : p.ypair ? 3 : 0;
+    const bool ypAll = p.ypair && p.ypairAll;
+    const float* phaseVol = c.volCells ? c.volCells : p.bricks ? p.bricks : ypAll ? p.ypair : vol;
+    const int phaseLayout = c.volCells ? 1 : p.bricks ? 2 : ypAll ? 3 : 0;
+    // the route's y-pair kernel (phaseLayout 0 only)
+    const float* ypRoute = p.ypair && !ypAll ? p.ypair : nullptr;
     thx_local_sel sel{nullptr, nullptr, clsSel,
-                      (long long)(p.bricks ? p.brickStride / 2 : p.ypair ? 2 * dimSize : dimSize)};
+                      (long long)(p.bricks ? p.brickStride / 2 : ypAll ? 2 * dimSize : dimSize)};
     if (c.converge) {
         THX_HIP(hipMemsetAsync(p.done, 0, sizeof(int) * nImg, s));
         hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
@@ -1879,7 +1894,8 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                        c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT,
                                        dat, cs ? p.ctfD : ctf, sigRcp, iCol, iRow, pxOrder, nOrd,
                                        nPxl, c.idim, nImg, p.wC, p.wR, p.wT, p.base, p.localWs,
-                                       p.localWsBytes, stream, mLD, cs ? cs->pD : nullptr, p.wD));
+                                       p.localWsBytes, stream, mLD, cs ? cs->pD : nullptr, p.wD,
+                                       ypRoute));
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
                            p.peakR, 0, nullptr, 0, done, rankDiv);
         THX_LAUNCH_CHECK();
