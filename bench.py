@@ -200,18 +200,19 @@ def local_roofline(vol, N, pf, device, n_img=512, reps=3, spreads=(1.5, 3.0, 0.0
     pR = torch.full((n_img, mR), 1.0 / mR, dtype=torch.float64, device=device)
     pT = torch.full((n_img, mT), 1.0 / mT, dtype=torch.float64, device=device)
     cells = ops.volume_cells(vol)
+    ypair = ops.volume_ypair(vol)
     out = {"clouds": []}
     for sp in spreads:
         q = (synth.clustered_quaternions(n_img, mR, sp, rng) if sp > 0
              else synth.uniform_quaternions(n_img * mR, rng).reshape(n_img, mR, 4))
         q = torch.as_tensor(np.ascontiguousarray(q), device=device)
         row = {"spread_deg": sp if sp > 0 else "uniform"}
-        for name, cl in (("halfcomplex", None), ("cells", cells)):
+        for name, kw in (("halfcomplex", {}), ("cells", {"cells": cells}), ("ypair", {"ypair": ypair})):
             row[name + "_ms"] = timed_events(lambda: ops.local_phase(vol, q, trans, pC, pR, pT, dat,
-                                                                     ctf, sig, px, cells=cl),
+                                                                     ctf, sig, px, **kw),
                                              reps, st) * 1e3
         out["clouds"].append(row)
-    del cells
+    del cells, ypair
     out["algo_bytes"] = n_img * (64.0 * mR * px.n + 16.0 * px.n)
     out["nPxl"] = px.n
     out["n_img"] = n_img
@@ -472,7 +473,7 @@ def main():
         t = traffic.get(key) if ok else None
         return (t["traffic_bytes"], f"{traffic_src}: {key}") if t else (None, None)
 
-    # ---- dominant kernel of the timed step: k_local_fused<0> (half-complex layout)
+    # ---- dominant kernel of the timed step: k_local_fused (routed per phase)
     if local_ms:
         nL = chunks[0][1] - chunks[0][0]
         per_img = 56.0 * mR * px.n + 15.0 * mR * mT * px.n        # SURVEY §8(d), per image-phase
@@ -505,8 +506,9 @@ def main():
             "frac": tap_bytes / t_launch / 1e12 / roof, "traffic": tr,
             "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
             "peak_source": roof_src or "MI355X_MICROARCH.md L2", **line_fields,
-            "kernel": f"k_local_fused<0> (particle-filter phase, nPxl={px.n}, {mR}x{mT}, "
-                      f"{nL} images per launch)",
+            "kernel": f"k_local_fused (particle-filter phase, nPxl={px.n}, {mR}x{mT}, {nL} images "
+                      "per launch), routed on the device per phase: the y-pair kernel <3> for wide "
+                      "clouds, the half-complex kernels <0> (staged / box-less) after",
             "launch_ms": t_launch * 1e3, "launches_timed": len(local_ms),
             "launch_ms_by_phase": [round(float(np.mean(local_ms[k::a.phases])), 3)
                                    for k in range(a.phases)] if len(local_ms) == a.phases * a.steps else None,
@@ -515,7 +517,8 @@ def main():
             "fp32_TFLOPs": achieved, "fp32_frac": achieved / PEAK_FP32_TFLOPS,
             "tap_bytes_per_launch": tap_bytes,
             "note": "HIP events recorded by the driver on its launch stream around every "
-                    "k_local_fused launch of the timed steps; achieved = 64 B of taps per "
+                    "phase's routed k_local_fused launches of the timed steps (three dispatches, "
+                    "two exit at entry; rocprof lists them per variant); achieved = 64 B of taps per "
                     "rotation-pixel (SURVEY 8(d)) per launch / launch time, peak = the L2 -> L1 "
                     "line bandwidth for random 16-B row pieces (tools/probes/l2_roof.hip, = the "
                     "guide's L2 figure); each tap row piece costs a 128-B line unless L1 or the "
@@ -561,13 +564,14 @@ def main():
         lbytes = lr["algo_bytes"]
         frac = lambda ms: lbytes / (ms / 1e3) / 1e9 / PEAK_HBM_GBS
         clouds = []
+        lays = ("halfcomplex", "cells", "ypair")
         for row in lr["clouds"]:
-            best = min(("halfcomplex", "cells"), key=lambda k: row[k + "_ms"])
+            best = min(lays, key=lambda k: row[k + "_ms"])
             clouds.append({**{k: (round(v, 3) if isinstance(v, float) else v) for k, v in row.items()},
-                           "frac_halfcomplex": round(frac(row["halfcomplex_ms"]), 3),
-                           "frac_cells": round(frac(row["cells_ms"]), 3), "best": best})
+                           **{"frac_" + k: round(frac(row[k + "_ms"]), 3) for k in lays},
+                           "best": best})
         head = clouds[0]
-        lsec = min(head["halfcomplex_ms"], head["cells_ms"]) / 1e3
+        lsec = min(head[k + "_ms"] for k in lays) / 1e3
         extras["roofline_local"] = {
             "bound": "hbm", "achieved": lbytes / lsec / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": lbytes / lsec / 1e9 / PEAK_HBM_GBS, "traffic": tr,

@@ -28,28 +28,25 @@ def main():
                     if "k_local_fused" not in name or int(r["Grid_Size"]) != 12500 * 512:
                         continue
                     d = rows.setdefault(int(r["Dispatch_Id"]),
-                                        {"_nostage": re.search(r"false, false>", name) is not None})
+                                        {"_nostage": re.search(r"false, false>", name) is not None,
+                                         "_staged": re.search(r"<0, false, 1, false, true>", name)
+                                         is not None})
                     d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    # a routed phase is two dispatches (the staged kernel, then the box-less
-    # one; the one not chosen exits at entry): sum consecutive dispatches into
-    # phases, a phase closing on the box-less variant (STAGE = false) or when
-    # the next dispatch is a staged one
+    # a routed phase is two or three dispatches (the staged kernel, the
+    # box-less one, the y-pair one; those not chosen exit at entry): a staged
+    # dispatch opens a phase, the others add to it
     phases, cur = [], None
     for k in sorted(rows):
         d = rows[k]
-        nostage = d.pop("_nostage")
-        if cur is None:
-            cur = dict(d)
-        else:
-            if not nostage:                 # a staged dispatch opens a new phase
+        d.pop("_nostage")
+        staged = d.pop("_staged")
+        if staged or cur is None:
+            if cur is not None:
                 phases.append(cur)
-                cur = dict(d)
-                continue
-            for c, v in d.items():
-                cur[c] = cur.get(c, 0.0) + v
-        if nostage:
-            phases.append(cur)
-            cur = None
+            cur = dict(d)
+            continue
+        for c, v in d.items():
+            cur[c] = cur.get(c, 0.0) + v
     if cur is not None:
         phases.append(cur)
     if not phases:

@@ -91,6 +91,21 @@ def single(rd, wr, name, grid, factor, shape, per=1):
                   shape)
 
 
+def routed_phase(rd, wr, grid, factor, shape):
+    """Bytes per routed bench phase: its two k_local_fused<0> dispatches
+    (staged / box-less variant) plus its k_local_fused<3> (y-pair) dispatch;
+    the kernels not chosen exit at entry."""
+    r0 = [v for n, g, v in rd if "k_local_fused<0," in n and g == grid]
+    w0 = [v for n, g, v in wr if "k_local_fused<0," in n and g == grid]
+    r3 = [v for n, g, v in rd if "k_local_fused<3," in n and g == grid]
+    w3 = [v for n, g, v in wr if "k_local_fused<3," in n and g == grid]
+    if not r0 or not w0:
+        return None
+    nph = len(r0) // 2
+    return _entry((sum(r0) + sum(r3)) / nph, (sum(w0) + sum(w3)) / nph, factor, nph,
+                  ["k_local_fused<0,", "k_local_fused<3,"], shape)
+
+
 def sliced(rd, wr, name, grid, k, per, factor, shape, pair=1):
     """Average bytes per launch of the k-th run of `per` consecutive launches
     of one kernel at one grid (bench.local_roofline: 1 + reps launches per
@@ -142,8 +157,8 @@ def main():
                                                   "64-B cell gathers"),
         # the bench step's dominant kernel: one k_local_fused<0> launch per
         # phase over the whole 12 500-image batch (grid 12500 x 1 x 1 of 512)
-        "local_bench": single(rd, wr, "k_local_fused<0,", 12500 * 512, 2,
-                              "staged box rows (128-B requests) + 16-B row taps", per=2),
+        "local_bench": routed_phase(rd, wr, 12500 * 512, 2,
+                                    "16-B row taps / 32-B y-pair pieces"),
     }
     ex = exact_split(tag, "k_local_fused<0,", 12500 * 512)
     if ex and res["local_bench"]:
