@@ -349,7 +349,7 @@ THX_DEV bool route_nostage(const int* __restrict__ route)
 }
 THX_DEV int route_pick(const int* __restrict__ route)
 {
-    if (route[7] == 1 && (long)route[4] * 100 < (long)THX_YPAIR_MAX_PCT * route[1]) return ROUTE_YPAIR;
+    if (route[7] == 1 && (long)route[4] * 100 < (long)route[6] * route[1]) return ROUTE_YPAIR;
     return route_nostage(route) ? ROUTE_NOBOX : ROUTE_STAGED;
 }
 
@@ -1559,7 +1559,16 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     const unsigned nRT = thx::cdiv(nR, RT);
     if (routed) {
         THX_HIP(hipMemsetAsync(route, 0, 8 * sizeof(int), s));
-        if (ypair) THX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(route + 7), 1, 1, s));
+        if (ypair) {
+            // route[6]: the y-pair threshold (THX_YPAIR_MAX_PCT overrides it, A/B),
+            // route[7]: a y-pair copy exists
+            static const int pct = [] {
+                const char* e = std::getenv("THX_YPAIR_MAX_PCT");
+                return e ? std::atoi(e) : THX_YPAIR_MAX_PCT;
+            }();
+            THX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(route + 6), pct, 1, s));
+            THX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(route + 7), 1, 1, s));
+        }
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)thx::cdiv(nImg, ROUTE_SAMPLE) * nRT),
                            dim3(64 * PB_WAVES), 0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim,
                            rec, act, nAct, route, 1);
