@@ -144,6 +144,66 @@ THX_DEV float2 interp_ypair_piece(const float4* __restrict__ yp, int vdim, float
     return make_float2(re, conj ? -im : im);
 }
 
+// The quad pieces from a sample's precomputed cell (folded base x0, y0, z0,
+// fractions, conj): the quad's lanes compute the coordinates of four
+// different samples once and share them (coop_step), instead of each lane
+// repeating all four samples' FP64 rotation -- the same values either way.
+struct Cell {
+    int x0, y0, z0;
+    float dx, dy, dz;
+    bool conj;
+};
+THX_DEV Cell cell_of(float x, float y, float z)
+{
+    Cell c;
+    c.conj = !(x >= 0.f);
+    if (c.conj) { x = -x; y = -y; z = -z; }
+    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+    c.x0 = (int)fx; c.y0 = (int)fy; c.z0 = (int)fz;
+    c.dx = x - fx; c.dy = y - fy; c.dz = z - fz;
+    return c;
+}
+THX_DEV float2 ypair_piece(const float4* __restrict__ yp, int vdim, const Cell& c, int j)
+{
+    const int nColFT = vdim / 2 + 1;
+    const size_t e = ((size_t)wrap_idx(c.z0 + (j >> 1), vdim) * vdim + wrap_idx(c.y0, vdim)) * nColFT +
+                     c.x0 + (j & 1);
+    const float4 q = yp[e];
+    const float wxz = ((j & 1) ? c.dx : 1.f - c.dx) * ((j >> 1) ? c.dz : 1.f - c.dz);
+    const float w0 = wxz * (1.f - c.dy), w1 = wxz * c.dy;
+    const float re = q.x * w0 + q.z * w1, im = q.y * w0 + q.w * w1;
+    return make_float2(re, c.conj ? -im : im);
+}
+THX_DEV float2 cell_piece(const float4* __restrict__ cells, int vdim, const Cell& c, int j)
+{
+    const int nColFT = vdim / 2 + 1;
+    const size_t e = (((size_t)wrap_idx(c.z0, vdim) * vdim + wrap_idx(c.y0, vdim)) * nColFT + c.x0) * 4 + j;
+    const float4 q = cells[e];
+    const float wy = (j & 1) ? c.dy : 1.f - c.dy, wz = (j >> 1) ? c.dz : 1.f - c.dz;
+    const float w0 = (1.f - c.dx) * wy * wz, w1 = c.dx * wy * wz;
+    const float re = q.x * w0 + q.z * w1, im = q.y * w0 + q.w * w1;
+    return make_float2(re, c.conj ? -im : im);
+}
+// lane p's value of a quad, to all four lanes (DPP quad_perm [p, p, p, p])
+template <int P>
+THX_DEV int quad_bcast(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, P | (P << 2) | (P << 4) | (P << 6), 0xf, 0xf, false);
+}
+template <int P>
+THX_DEV Cell quad_bcast_cell(const Cell& c)
+{
+    Cell o;
+    o.x0 = quad_bcast<P>(c.x0);
+    o.y0 = quad_bcast<P>(c.y0);
+    o.z0 = quad_bcast<P>(c.z0);
+    o.dx = __int_as_float(quad_bcast<P>(__float_as_int(c.dx)));
+    o.dy = __int_as_float(quad_bcast<P>(__float_as_int(c.dy)));
+    o.dz = __int_as_float(quad_bcast<P>(__float_as_int(c.dz)));
+    o.conj = quad_bcast<P>((int)c.conj) != 0;
+    return o;
+}
+
 // sum over the lanes of each quad (DPP quad permutations), every lane gets it
 THX_DEV float quad_sum(float v)
 {
@@ -989,16 +1049,22 @@ k_local_fused(const float2* __restrict__ vol,
         // lane 4 r + k of the quad layout
         auto coop_step = [&](int s) {
             const int j = lane & 3;
+            // lane j of the quad rotates pixel 4s + j; the four cells are then
+            // shared across the quad (quad_bcast_cell)
+            Cell mine;
+            {
+                const double2 xy = sXY[4 * s + j];
+                mine = cell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
+                               (float)(m[2] * xy.x + m[5] * xy.y));
+            }
             float2 P[4];
 #pragma unroll
             for (int p = 0; p < 4; p++) {
-                const double2 xy = sXY[4 * s + p];
-                const float x = (float)(m[0] * xy.x + m[3] * xy.y);
-                const float y = (float)(m[1] * xy.x + m[4] * xy.y);
-                const float z = (float)(m[2] * xy.x + m[5] * xy.y);
+                const Cell c = p == 0 ? quad_bcast_cell<0>(mine) : p == 1 ? quad_bcast_cell<1>(mine)
+                             : p == 2 ? quad_bcast_cell<2>(mine) : quad_bcast_cell<3>(mine);
                 const float2 v = LAYOUT == LAYOUT_YPAIR
-                                     ? interp_ypair_piece(reinterpret_cast<const float4*>(vol), vdim, x, y, z, j)
-                                     : interp_cell_piece(reinterpret_cast<const float4*>(vol), vdim, x, y, z, j);
+                                     ? ypair_piece(reinterpret_cast<const float4*>(vol), vdim, c, j)
+                                     : cell_piece(reinterpret_cast<const float4*>(vol), vdim, c, j);
                 P[p] = make_float2(quad_sum(v.x), quad_sum(v.y));
             }
             if (!CS)
