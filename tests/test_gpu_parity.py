@@ -258,8 +258,10 @@ def test_local_phase_staged_patches(orc, stack64, spread, lo, hi):
     # route (interp_ft's unfused sum) where the bricked one stages (packed FMA)
     assert np.max(np.abs(e[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
     # the y-pair copy (two 32-B pieces per cell, quad-cooperative)
-    y = ops.local_phase(vol, *args, want_dvp=True, ypair=ops.volume_ypair(vol))
-    assert np.max(np.abs(y[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
+    yp = ops.volume_ypair(vol)
+    for pair in (False, True):       # quad / pair forms of the y-pair gather
+        y = ops.local_phase(vol, *args, want_dvp=True, ypair=yp, pair=pair)
+        assert np.max(np.abs(y[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
     da, db = a[4].cpu().numpy(), b[4].cpu().numpy()
     assert np.max(np.abs(da - db) / np.abs(db)) < 2e-6      # pixel summation order only
     for l in range(nImg):

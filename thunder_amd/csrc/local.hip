@@ -204,6 +204,49 @@ THX_DEV Cell quad_bcast_cell(const Cell& c)
     return o;
 }
 
+// Pair form of the y-pair gather (LAYOUT_YPAIR2): lane j of a pair reads
+// element x0 + j of slices z0 and z0 + 1 (two 16-B loads); the pair's two
+// lanes meet on the same 32-B pieces, so a sample costs two accesses with
+// half the lanes of the quad form.  Returns this lane's weighted part.
+THX_DEV float2 ypair_pair_part(const float4* __restrict__ yp, int vdim, const Cell& c, int j)
+{
+    const int nColFT = vdim / 2 + 1;
+    const size_t e0 = ((size_t)wrap_idx(c.z0, vdim) * vdim + wrap_idx(c.y0, vdim)) * nColFT + c.x0 + j;
+    const size_t e1 = ((size_t)wrap_idx(c.z0 + 1, vdim) * vdim + wrap_idx(c.y0, vdim)) * nColFT + c.x0 + j;
+    const float4 q0 = yp[e0], q1 = yp[e1];
+    const float wx = j ? c.dx : 1.f - c.dx;
+    const float wa = wx * (1.f - c.dz), wb = wx * c.dz;
+    const float w00 = wa * (1.f - c.dy), w01 = wa * c.dy, w10 = wb * (1.f - c.dy), w11 = wb * c.dy;
+    const float re = q0.x * w00 + q0.z * w01 + q1.x * w10 + q1.z * w11;
+    const float im = q0.y * w00 + q0.w * w01 + q1.y * w10 + q1.w * w11;
+    return make_float2(re, c.conj ? -im : im);
+}
+// the pair's other lane's value (DPP quad_perm [1, 0, 3, 2])
+THX_DEV float pair_swap(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));
+}
+// lane IT of each pair, to both lanes (quad_perm [IT, IT, 2 + IT, 2 + IT])
+template <int IT>
+THX_DEV int pair_bcast(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, IT | (IT << 2) | ((2 + IT) << 4) | ((2 + IT) << 6), 0xf,
+                                       0xf, false);
+}
+template <int IT>
+THX_DEV Cell pair_bcast_cell(const Cell& c)
+{
+    Cell o;
+    o.x0 = pair_bcast<IT>(c.x0);
+    o.y0 = pair_bcast<IT>(c.y0);
+    o.z0 = pair_bcast<IT>(c.z0);
+    o.dx = __int_as_float(pair_bcast<IT>(__float_as_int(c.dx)));
+    o.dy = __int_as_float(pair_bcast<IT>(__float_as_int(c.dy)));
+    o.dz = __int_as_float(pair_bcast<IT>(__float_as_int(c.dz)));
+    o.conj = pair_bcast<IT>((int)c.conj) != 0;
+    return o;
+}
+
 // sum over the lanes of each quad (DPP quad permutations), every lane gets it
 THX_DEV float quad_sum(float v)
 {
@@ -220,7 +263,7 @@ THX_DEV float quad_sum(float v)
 // (1 + 1/16) 2 2 = 4.25, at the same footprint (the L2-resident working set
 // of a phase stays L2-resident).  Rows / slices wrapped like iFTHalf; bricks
 // past the half-plane edge (x >= nColFT) hold zeros.
-enum { LAYOUT_FT = 0, LAYOUT_CELLS = 1, LAYOUT_BRICKS = 2, LAYOUT_YPAIR = 3 };
+enum { LAYOUT_FT = 0, LAYOUT_CELLS = 1, LAYOUT_BRICKS = 2, LAYOUT_YPAIR = 3, LAYOUT_YPAIR2 = 4 };
 // layouts gathered quad-cooperatively (no LDS boxes, no patch records)
 constexpr bool coop_layout(int l) { return l == LAYOUT_CELLS || l == LAYOUT_YPAIR; }
 
@@ -392,15 +435,17 @@ THX_DEV int store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __res
 constexpr int ROUTE_SAMPLE = 16;   // every 16th image's records are counted
 
 // Third route (round 3): when the driver supplies a y-pair copy (route[7] =
-// 1) and fewer than THX_YPAIR_MAX_PCT per cent of the sampled patches have a
-// box of at most 8 BOX_CAP voxels -- the wide clouds of the first phases --
-// the quad-cooperative y-pair kernel runs: two 32-B pieces per sample cost
-// fewer 128-B L2 -> L1 lines than four row pieces when L1 reuse is low
-// (measured on the bench's phases: 13.0 vs 16.4 ms in phase 1, equal at the
-// 20 % point (phase 5), slower after; profiles/r03_ypair_ab.jsonl,
-// r03_route_stats.txt).
+// 1), every phase whose boxes do not pay gathers from it instead of the
+// box-less half-complex kernel.  The pair form (LAYOUT_YPAIR2: two lanes per
+// sample, the 32-B pieces of slices z0 and z0 + 1) reads two accesses per
+// sample where the half-complex rows take four; on the bench's phases it is
+// faster in all ten (phase 1 11.3-12.4 vs 16.4-16.9 ms, phase 10 7.8-8.2 vs
+// 8.1-8.5; 85-86k vs 81-82k with the quad form, 75-76k without y-pairs;
+// profiles/r03_pair_ab.jsonl, r03_ypair_ab.jsonl, r03_yroute_ab.jsonl).
+// route[6] (THX_YPAIR_MAX_PCT below 100, A/B) restricts it to clouds with
+// fewer than that per cent of 8x boxes (r03_route_stats.txt).
 #ifndef THX_YPAIR_MAX_PCT
-#define THX_YPAIR_MAX_PCT 20
+#define THX_YPAIR_MAX_PCT 100
 #endif
 constexpr int ROUTE_STAGED = 0, ROUTE_NOBOX = 1, ROUTE_YPAIR = 2;
 THX_DEV bool route_nostage(const int* __restrict__ route)
@@ -409,7 +454,14 @@ THX_DEV bool route_nostage(const int* __restrict__ route)
 }
 THX_DEV int route_pick(const int* __restrict__ route)
 {
-    if (route[7] == 1 && (long)route[4] * 100 < (long)route[6] * route[1]) return ROUTE_YPAIR;
+    // with a y-pair copy (route[7]): the staged kernel where the boxes pay, the
+    // y-pair kernel everywhere else (the pair form beats the box-less
+    // half-complex kernel in every phase of the bench, profiles/r03_pair_ab.jsonl);
+    // route[6] < 100 keeps the box-less kernel for clouds with at least that
+    // per cent of 8x boxes (the quad form's rule, A/B)
+    if (route[7] == 1 && !route_nostage(route)) return ROUTE_STAGED;
+    if (route[7] == 1 && (route[6] >= 100 || (long)route[4] * 100 < (long)route[6] * route[1]))
+        return ROUTE_YPAIR;
     return route_nostage(route) ? ROUTE_NOBOX : ROUTE_STAGED;
 }
 
@@ -792,7 +844,7 @@ template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false, bool ST
 // no LDS box (cell layout, or STAGE = false): no box prefetch registers, so
 // 6 waves per SIMD (three workgroups per CU) for the L2 gathers
 __global__ void __launch_bounds__(THREADS)
-__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : (coop_layout(LAYOUT) || !STAGE) ? THX_NOBOX_WAVES : 4)))
+__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : (coop_layout(LAYOUT) || LAYOUT == LAYOUT_YPAIR2 || !STAGE) ? THX_NOBOX_WAVES : 4)))
 k_local_fused(const float2* __restrict__ vol,
                                                             int vdim, int pf,
                                                             const double* __restrict__ quat,
@@ -822,7 +874,7 @@ k_local_fused(const float2* __restrict__ vol,
                                                             const int* __restrict__ route = nullptr)
 {
     // routed phases launch the staged and the box-less kernel; one exits
-    if (route && route_pick(route) != (LAYOUT == LAYOUT_YPAIR ? ROUTE_YPAIR
+    if (route && route_pick(route) != (LAYOUT == LAYOUT_YPAIR || LAYOUT == LAYOUT_YPAIR2 ? ROUTE_YPAIR
                                        : STAGE ? ROUTE_STAGED : ROUTE_NOBOX)) return;
     int l = blockIdx.x;
     if (act) {
@@ -839,7 +891,9 @@ k_local_fused(const float2* __restrict__ vol,
     // many workgroups as the VGPRs allow
     constexpr bool COOP = coop_layout(LAYOUT);
     // STAGE = false: every patch gathered from L2 (no box, no records)
-    constexpr bool NOBOX = COOP || !STAGE;
+    // the pair form of the y-pair gather (two lanes per sample)
+    constexpr bool PAIR = LAYOUT == LAYOUT_YPAIR2;
+    constexpr bool NOBOX = COOP || PAIR || !STAGE;
     auto staged = [](const Rec& r) { return !NOBOX && r.v[10] <= BOXC; };
     constexpr int NC = NCT * TT;   // columns per workgroup
     // box-less kernels stage PP patches' image tiles per barrier pair (fewer
@@ -849,7 +903,7 @@ k_local_fused(const float2* __restrict__ vol,
 #ifndef THX_NOBOX_PP
 #define THX_NOBOX_PP 2
 #endif
-    constexpr int PP = (coop_layout(LAYOUT) || !STAGE) && !CS ? THX_NOBOX_PP : 1;
+    constexpr int PP = (coop_layout(LAYOUT) || PAIR || !STAGE) && !CS ? THX_NOBOX_PP : 1;
     constexpr int PKC = PP * KC;                        // pixels per iteration
     constexpr int NE = (PKC * TT + THREADS - 1) / THREADS;   // image-tile elements per thread
     const int r0 = blockIdx.y * RT, t0 = blockIdx.z * NC;
@@ -873,7 +927,9 @@ k_local_fused(const float2* __restrict__ vol,
     double m[6];
     {
         // COOP: lane 4 r + j works on rotation slot 16 wv + r (its quad's sample)
-        const int r = r0 + slot_rotation(sPerm, COOP ? wv * 16 + (lane >> 2) : rl, nRl);
+        // PAIR: lane 2 k + j works on rotation slot 16 wv + (k & 15)
+        const int r = r0 + slot_rotation(sPerm, COOP ? wv * 16 + (lane >> 2)
+                                                : PAIR ? wv * 16 + ((lane >> 1) & 15) : rl, nRl);
         double q[4], mm[9];
         for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
         quat_to_mat(q, mm);
@@ -1100,7 +1156,55 @@ k_local_fused(const float2* __restrict__ vol,
                 }
             }
         };
-        if (COOP) {
+        // PAIR step: pair (r, h) = lanes 2 (16 h + r) + j evaluates rotation 16 wv +
+        // r at pixels 4s + h (it 0) and 4s + h + 2 (it 1); lane j rotates the
+        // it = j sample and the pair shares the cells.  MFMA A rows: (pixels
+        // 4s, 4s + 2) from the h = 0 pairs, (4s + 1, 4s + 3) from the h = 1 pairs.
+        auto pair_step = [&](int s) {
+            const int j = lane & 1, h = (lane >> 5) & 1;
+            Cell mine;
+            {
+                const double2 xy = sXY[4 * s + h + 2 * j];
+                mine = cell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
+                               (float)(m[2] * xy.x + m[5] * xy.y));
+            }
+            float2 P[2];
+#pragma unroll
+            for (int it = 0; it < 2; it++) {
+                const Cell c = it == 0 ? pair_bcast_cell<0>(mine) : pair_bcast_cell<1>(mine);
+                const float2 v = ypair_pair_part(reinterpret_cast<const float4*>(vol), vdim, c, j);
+                P[it] = make_float2(v.x + pair_swap(v.x), v.y + pair_swap(v.y));
+            }
+            if (!CS)
+#pragma unroll
+                for (int it = 0; it < 2; it++)
+                    bias += sBq[4 * s + h + 2 * it] * (P[it].x * P[it].x + P[it].y * P[it].y);
+            // A[r][kk]: kk < 2 -> component kk of it 0, kk >= 2 -> component kk - 2 of it 1,
+            // from lane 2 r + (kk & 1) (a1: h = 0 pairs) or 32 + 2 r + (kk & 1) (a2: h = 1)
+            const float c0 = j ? P[0].y : P[0].x, c1 = j ? P[1].y : P[1].x;
+            const int sa = (2 * (lane & 15) + (kk & 1)) * 4;
+            const float t10 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(c0)));
+            const float t11 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(c1)));
+            const float t20 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa + 128, __float_as_int(c0)));
+            const float t21 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa + 128, __float_as_int(c1)));
+            const float a1 = kk < 2 ? t10 : t11, a2 = kk < 2 ? t20 : t21;
+            const int q0 = 4 * s + (kk < 2 ? 0 : 2), q1 = q0 + 1;
+#pragma unroll
+            for (int ct = 0; ct < NCT; ct++) {
+                const float b0 = sB[(q0 * 2 + (kk & 1)) * NC + ct * TT + tc];
+                const float b1 = sB[(q1 * 2 + (kk & 1)) * NC + ct * TT + tc];
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[ct], 0, 0, 0);
+                acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2, b1, acc[ct], 0, 0, 0);
+            }
+        };
+        if (PAIR) {
+#pragma unroll 4
+            for (int s = 0; s < 4 * PP; s++) {
+                if (pad_step(s)) { MCOUNT(3); continue; }
+                MCOUNT(2);
+                pair_step(s);
+            }
+        } else if (COOP) {
 // all four steps unrolled: 16 cell reads in flight per wave (C5 +3-4 %,
 // full-res 1.5-3 deg 2-5 % over 2; profiles/r03_coop_unroll_ab.jsonl)
 #ifndef THX_COOP_UNROLL
@@ -1163,7 +1267,10 @@ k_local_fused(const float2* __restrict__ vol,
     if (lane == 0) sRed[wv] = aConst;
     // B_r: the four pixel slots of a rotation are lanes l, l + 16, l + 32, l + 48
     // (COOP: every lane of quad r holds rotation r's whole sum)
-    if (COOP) {
+    if (PAIR) {
+        // rotation r's pixels are split over the pairs (r, h = 0) and (r, h = 1)
+        bias = __shfl(bias, 2 * (lane & 15), 64) + __shfl(bias, 32 + 2 * (lane & 15), 64);
+    } else if (COOP) {
         bias = __shfl(bias, 4 * (lane & 15), 64);
     } else {
         bias += __shfl_xor(bias, 16, 64);
@@ -1588,8 +1695,8 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     THX_CHECK_ARG(!nD || (pD && wD && (long)nT * nD <= LOCAL_D_MAXCOL),
                   "thx_local_phase_d: needs pD, wD and nT * nD <= 1024");
     const int nCol = nD ? nT * nD : nT;
-    THX_CHECK_ARG(volLayout >= 0 && volLayout <= 3, "thx_local_phase: volLayout must be 0 .. 3");
-    THX_CHECK_ARG(volLayout != LAYOUT_YPAIR || !nD, "thx_local_phase_d: no y-pair layout with CTF search");
+    THX_CHECK_ARG(volLayout >= 0 && volLayout <= 4, "thx_local_phase: volLayout must be 0 .. 4");
+    THX_CHECK_ARG(volLayout < LAYOUT_YPAIR || !nD, "thx_local_phase_d: no y-pair layout with CTF search");
     THX_CHECK_ARG((long)nImg * ((nR + RT - 1) / RT) <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 &&
                       (nCol + TT - 1) / TT <= 65535,
                   "thx_local_phase: grid too large");
@@ -1642,7 +1749,7 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * nRT), dim3(64 * PB_WAVES), 0, s, quat,
                            nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct, route, 2);
         THX_LAUNCH_CHECK();
-    } else if (!coop_layout(volLayout)) {   // the quad gathers use no patch boxes
+    } else if (!coop_layout(volLayout) && volLayout != LAYOUT_YPAIR2) {   // no boxes for these
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * nRT), dim3(64 * PB_WAVES), 0, s, quat,
                            nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct, nullptr, 0);
         THX_LAUNCH_CHECK();
@@ -1684,6 +1791,7 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     }
     auto kern =
         volLayout == LAYOUT_YPAIR ? k_local_fused<LAYOUT_YPAIR>
+        : volLayout == LAYOUT_YPAIR2 ? k_local_fused<LAYOUT_YPAIR2>
         : volLayout == LAYOUT_CELLS
             ? (big ? k_local_fused<LAYOUT_CELLS, false, 1, true> : k_local_fused<LAYOUT_CELLS>)
         : volLayout == LAYOUT_BRICKS
@@ -1703,8 +1811,14 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     if (routed) {
         launch(k_local_fused<LAYOUT_FT, false, 1, false, true>, route);
         launch(k_local_fused<LAYOUT_FT, false, 1, false, false>, route);
+        // the pair form of the y-pair gather; THX_YPAIR_KERNEL=1 (A/B): the quad form
+        static const bool ypQuad = [] {
+            const char* e = std::getenv("THX_YPAIR_KERNEL");
+            return e && e[0] == '1';
+        }();
         if (ypair) {
-            hipLaunchKernelGGL(k_local_fused<LAYOUT_YPAIR>, grid, dim3(THREADS), 0, s,
+            auto kyp = ypQuad ? k_local_fused<LAYOUT_YPAIR> : k_local_fused<LAYOUT_YPAIR2>;
+            hipLaunchKernelGGL(kyp, grid, dim3(THREADS), 0, s,
                                reinterpret_cast<const float2*>(ypair), vdim, pf, quat, nR, trans, nT,
                                reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
                                nVisit, nPxl, idim, rec, fuse ? dvp : d, act, nAct, cls,

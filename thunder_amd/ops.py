@@ -288,13 +288,14 @@ def volume_cells(vol):
     return out
 
 
-def _layout(vol, cells, bricks, ypair=None):
-    """(volLayout, volume argument) of thx_local_phase for the given copies."""
+def _layout(vol, cells, bricks, ypair=None, pair=False):
+    """(volLayout, volume argument) of thx_local_phase for the given copies
+    (ypair with pair=True: the two-lanes-per-sample form, volLayout 4)."""
     if sum(x is not None for x in (cells, bricks, ypair)) > 1:
         raise ValueError("cells, bricks and ypair are alternatives")
     if ypair is not None:
         _req(ypair, torch.complex64, tuple(vol.shape) + (2,), "ypair")
-        return 3, ypair
+        return (4 if pair else 3), ypair
     if cells is not None:
         _req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
         return 1, cells
@@ -327,12 +328,12 @@ def volume_bricks(vol):
 
 
 def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False, cells=None,
-                tiled=True, bricks=None, ypair=None):
+                tiled=True, bricks=None, ypair=None, pair=False):
     """cells / bricks: optional thx_volume_cells / thx_volume_bricks copy of
     vol (used for the gathers and the staged boxes).
     tiled: visit pixels in px.order (LDS-staged neighbourhoods) instead of set order."""
     vdim = _vol_dim(vol)
-    layout, src = _layout(vol, cells, bricks, ypair)
+    layout, src = _layout(vol, cells, bricks, ypair, pair)
     nImg, nPxl = _images(dat, ctf_, sig)
     if nPxl != px.n:
         raise ValueError("pixel set / image size mismatch")
