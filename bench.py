@@ -507,8 +507,8 @@ def main():
             "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
             "peak_source": roof_src or "MI355X_MICROARCH.md L2", **line_fields,
             "kernel": f"k_local_fused (particle-filter phase, nPxl={px.n}, {mR}x{mT}, {nL} images "
-                      "per launch), routed on the device per phase: the y-pair kernel <3> for wide "
-                      "clouds, the half-complex kernels <0> (staged / box-less) after",
+                      "per launch), routed on the device per phase: the staged half-complex kernel "
+                      "<0> where the LDS boxes pay, else the pair-form y-pair kernel <4>",
             "launch_ms": t_launch * 1e3, "launches_timed": len(local_ms),
             "launch_ms_by_phase": [round(float(np.mean(local_ms[k::a.phases])), 3)
                                    for k in range(a.phases)] if len(local_ms) == a.phases * a.steps else None,
