@@ -189,7 +189,7 @@ def local_roofline(vol, N, pf, device, n_img=512, reps=3, spreads=(1.5, 3.0, 0.0
     rotations, every tap a gather), each in the half-complex layout (taps of
     compact patches staged in LDS boxes, the rest gathered row by row) and
     in the cell-expanded layout (every sample one quad-cooperative 64-B cell
-    read)."""
+    read) and the y-pair copy (pair form: two 32-B pieces per sample)."""
     rU = N // 2 - 2
     px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, 1, n_img, device, seed=17, vol=vol)
     rng = np.random.default_rng(3)
@@ -207,7 +207,8 @@ def local_roofline(vol, N, pf, device, n_img=512, reps=3, spreads=(1.5, 3.0, 0.0
              else synth.uniform_quaternions(n_img * mR, rng).reshape(n_img, mR, 4))
         q = torch.as_tensor(np.ascontiguousarray(q), device=device)
         row = {"spread_deg": sp if sp > 0 else "uniform"}
-        for name, kw in (("halfcomplex", {}), ("cells", {"cells": cells}), ("ypair", {"ypair": ypair})):
+        for name, kw in (("halfcomplex", {}), ("cells", {"cells": cells}),
+                         ("ypair", {"ypair": ypair, "pair": True})):
             row[name + "_ms"] = timed_events(lambda: ops.local_phase(vol, q, trans, pC, pR, pT, dat,
                                                                      ctf, sig, px, **kw),
                                              reps, st) * 1e3
