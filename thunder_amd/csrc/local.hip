@@ -703,6 +703,9 @@ struct Pix {
     float c, s;
 };
 
+#ifndef THX_IMG_NT
+#define THX_IMG_NT 0
+#endif
 THX_DEV Pix load_pix(int p, const int* __restrict__ iCol, const int* __restrict__ iRow,
                      const float2* __restrict__ D, const float* __restrict__ C,
                      const float* __restrict__ S)
@@ -711,9 +714,17 @@ THX_DEV Pix load_pix(int p, const int* __restrict__ iCol, const int* __restrict_
     if (p >= 0) {
         x.ic = iCol[p];
         x.ir = iRow[p];
+#if THX_IMG_NT
+        // read-once image data past L2 (A/B: keep the y-pair ball resident)
+        x.d.x = __builtin_nontemporal_load(reinterpret_cast<const float*>(D + p));
+        x.d.y = __builtin_nontemporal_load(reinterpret_cast<const float*>(D + p) + 1);
+        x.c = __builtin_nontemporal_load(C + p);
+        x.s = __builtin_nontemporal_load(S + p);
+#else
         x.d = D[p];
         x.c = C[p];
         x.s = S[p];
+#endif
     }
     return x;
 }
