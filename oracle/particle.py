@@ -25,13 +25,16 @@ def conj(q):
     return q * np.array([1.0, -1.0, -1.0, -1.0])
 
 
-def infer_acg(Q):
+def infer_acg(Q, max_it=None):
     """inferACG(dmat44&, const dmat4&), src/Geometry/DirectionalStat.cpp:93-145:
     Tyler's fixed point B = 4/nf sum q q^T / (q^T A^-1 q), from B = I, while
     sum|A - B| > 1e-3; returns the last A.  A NaN criterion (a singular A on a
-    degenerate cloud) ends the loop like the reference's `while`."""
+    degenerate cloud) ends the loop like the reference's `while`.  max_it caps
+    the iterations as the driver's perturbation mean does (acgIters)."""
     B = np.eye(4)
-    while True:
+    it = 0
+    while max_it is None or it < max_it:
+        it += 1
         A = B
         with np.errstate(all="ignore"):
             Ai = np.linalg.inv(A) if np.all(np.isfinite(A)) and abs(np.linalg.det(A)) > 0 else \
@@ -43,6 +46,7 @@ def infer_acg(Q):
         crit = np.abs(A - B).sum()
         if not crit > 1e-3:
             return A
+    return A
 
 
 def principal_axis(A):

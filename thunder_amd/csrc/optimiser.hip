@@ -156,8 +156,14 @@ THX_DEV double group_sum(double v)
 // last A.  Particle q_i is read as pre q_i (pre = conj(mean) de-means).
 // Clouds of up to GROUP * QREG particles keep this lane's (de-meaned)
 // particles in registers across the iterations -- the loop is a serial
-// chain, and re-reading them from L2 every iteration was its latency; the
-// arithmetic and its order are the same either way.
+// chain, and re-reading them from L2 every iteration was its latency.  Each
+// lane then holds a block of QREG consecutive particles as runs of equal
+// ones: a resampled cloud stores an ancestor's copies next to each other, so
+// the term of a run is taken once with its multiplicity.  The degenerate
+// clouds that run the fixed point to its cap are the ones with a few
+// ancestors, so their iterations cost one or two terms per lane instead of
+// QREG.  The sum is the reference's up to rounding (multiplicity x term for
+// repeated additions, block for strided order).
 constexpr int QREG = 128 / GROUP;
 
 template <bool REG>
@@ -165,13 +171,32 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
                            int maxIt)
 {
     double qr[REG ? QREG : 1][4];
+    int nd = 0, nIn = 0;                          // runs, particles this lane holds
+    unsigned runs = 0;                            // bit p: block particle p starts a run
     if (REG) {
+        const int i0 = lane * QREG;
+        nIn = max(0, min(QREG, m - i0));
+        unsigned starts = 0;
+        double prev[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int p = 0; p < QREG; p++) {
-            const int i = lane + p * GROUP;
-            if (i < m) {
-                if (pre) qmul(pre, Q + 4 * i, qr[p]);
-                else for (int k = 0; k < 4; k++) qr[p][k] = Q[4 * i + k];
+            if (p < nIn) {
+                const double* c = Q + 4 * (i0 + p);
+                const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+                if (p == 0 || c0 != prev[0] || c1 != prev[1] || c2 != prev[2] || c3 != prev[3])
+                    starts |= 1u << p;
+                prev[0] = c0; prev[1] = c1; prev[2] = c2; prev[3] = c3;
+            }
+        }
+        runs = starts;
+        nd = __builtin_popcount(starts);
+#pragma unroll
+        for (int p = 0; p < QREG; p++) {
+            if (starts) {
+                const double* c = Q + 4 * (i0 + __builtin_ctz(starts));
+                starts &= starts - 1;
+                if (pre) qmul(pre, c, qr[p]);
+                else for (int k = 0; k < 4; k++) qr[p][k] = c[k];
             }
         }
     }
@@ -183,8 +208,8 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
         inv4(A, Ai);
         pack10(Ai, Mp);
         double b[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nf = 0.0;
-        auto term = [&](const double* q) {
-            const double r = 1.0 / quad10(Mp, q);
+        auto term = [&](const double* q, double w) {
+            const double r = w / quad10(Mp, q);
             int t = 0;
             for (int j = 0; j < 4; j++) {
                 const double qj = q[j] * r;
@@ -193,15 +218,21 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
             nf += r;
         };
         if (REG) {
+            unsigned rs = runs;
 #pragma unroll
-            for (int p = 0; p < QREG; p++)
-                if (lane + p * GROUP < m) term(qr[p]);
+            for (int p = 0; p < QREG; p++) {
+                if (p < nd) {
+                    const int s0 = __builtin_ctz(rs);
+                    rs &= rs - 1;
+                    term(qr[p], (double)((rs ? __builtin_ctz(rs) : nIn) - s0));
+                }
+            }
         } else {
             for (int i = lane; i < m; i += GROUP) {
                 double q[4];
                 if (pre) qmul(pre, Q + 4 * i, q);
                 else for (int k = 0; k < 4; k++) q[k] = Q[4 * i + k];
-                term(q);
+                term(q, 1.0);
             }
         }
         for (int t = 0; t < 10; t++) b[t] = group_sum(b[t]);

@@ -3,7 +3,8 @@
 particle clouds: the C3 workload (bench.make_workload) run for k = 1 .. 10
 phases; the resampled clouds after phase k are the next phase's k_pf_mean
 input.  Prints one JSON line per k: the iteration histogram and the
-k_pf_mean time."""
+k_pf_mean time, and the median number of runs of equal particles (distinct
+ancestors, as k_gather stores copies together) over all and over capped clouds."""
 import ctypes
 import json
 import os
@@ -37,6 +38,10 @@ for k in range(1, 11):
     b.record(st)
     torch.cuda.synchronize()
     h = it.cpu().numpy()
+    q = quat.cpu().numpy()
+    runs = (q[:, 1:] != q[:, :-1]).any(-1).sum(1) + 1
     print(json.dumps({"phase": k, "ms": a.elapsed_time(b), "p50": float(np.median(h)),
                       "p90": float(np.percentile(h, 90)), "p99": float(np.percentile(h, 99)),
-                      "max": int(h.max()), "capped": int((h >= 100).sum()), "n": n}), flush=True)
+                      "max": int(h.max()), "capped": int((h >= 100).sum()), "n": n,
+                      "runs_p50": float(np.median(runs)),
+                      "runs_capped_p50": float(np.median(runs[h >= 100])) if (h >= 100).any() else None}), flush=True)
