@@ -208,7 +208,7 @@ def local_roofline(vol, N, pf, device, n_img=512, reps=3, spreads=(1.5, 3.0, 0.0
         q = torch.as_tensor(np.ascontiguousarray(q), device=device)
         row = {"spread_deg": sp if sp > 0 else "uniform"}
         for name, kw in (("halfcomplex", {}), ("cells", {"cells": cells}),
-                         ("ypair", {"ypair": ypair, "pair": True})):
+                         ("ypair", {"ypair": ypair})):
             row[name + "_ms"] = timed_events(lambda: ops.local_phase(vol, q, trans, pC, pR, pT, dat,
                                                                      ctf, sig, px, **kw),
                                              reps, st) * 1e3

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define THX_ABI_VERSION 5
+#define THX_ABI_VERSION 6
 
 enum {
     THX_OK = 0,
@@ -168,9 +168,10 @@ int thx_global_scan(const float* rotP, int nR, const float* traP, int nT,
  * volLayout 0: `vol` is the half-complex projectee; 1: `vol` is its
  * cell-expanded copy from thx_volume_cells (8x the bytes, one aligned 64-B
  * segment per trilinear gather -- the layout for HBM-bound full-resolution
- * phases); 2: `vol` is its bricked copy from thx_volume_bricks (the same
- * bytes, fewer cache lines per gather -- the layout for L2-resident
- * phases).
+ * phases); 2: `vol` is its y-pair copy from thx_volume_ypair (2x the bytes,
+ * two 32-B pieces per gather, read by lane pairs -- the layout for wide
+ * clouds on an L2-resident ball).  (ABI 6 retired the bricked layout and the
+ * quad form of the y-pair gather, volLayout 2 / 3 of ABI 5.)
  * pxOrder (device, nOrd ints, may be NULL = set order, nOrd ignored): the
  * pixel visiting order from thx_pixel_tile_order (-1 entries skipped).
  * Pixels are taken 16 at a time; when the
@@ -215,6 +216,26 @@ int thx_local_phase_sel(const thx_local_sel* sel, const float* vol, int volLayou
                         float* baseL, float* dvp, void* workspace, size_t wsBytes,
                         thx_stream_t stream);
 
+/* The phase on the device route (what thx_expectation runs for half-complex
+ * phases without CTF search): a sample of every 16th image's patch records
+ * picks, on the device, the LDS-staged half-complex kernel where the patch
+ * boxes of the clouds fit (>= 50 %) and otherwise the pair-form y-pair kernel
+ * on `ypair` (thx_volume_ypair of vol), or the box-less half-complex kernel
+ * when ypair is NULL; no host round trip.  route (device int, may be NULL)
+ * receives the choice: 0 staged, 1 box-less, 2 y-pair, -1 not routed (the
+ * large-box full-resolution phases, pf sqrt(2 nPxl / pi) >= 300, run the
+ * big-box staged kernel).  pxOrder is required; the rest as
+ * thx_local_phase_sel with volLayout 0. */
+int thx_local_phase_routed(const thx_local_sel* sel, const float* vol,
+                           const float* ypair, int vdim, int pf, const double* quat,
+                           int nR, const double* trans, int nT, const double* pC,
+                           const double* pR, const double* pT, const float* dat,
+                           const float* ctf, const float* sigRcp, const int* iCol,
+                           const int* iRow, const int* pxOrder, int nOrd, int nPxl,
+                           int idim, int nImg, float* wC, float* wR, float* wT,
+                           float* baseL, float* dvp, int* route, void* workspace,
+                           size_t wsBytes, thx_stream_t stream);
+
 /* ---------------------------------------------------- CTF search (a2/a9) ---
  * SEARCH_TYPE_CTF: the local phase over nD defocus samples per image.
  * thx_defocus_pre -- allocPreCal's cSearch branch (src/Optimiser.cpp:
@@ -252,20 +273,10 @@ int thx_local_phase_d(const thx_local_sel* sel, const float* vol, int volLayout,
 int thx_volume_cells(const float* vol, int vdim, float* cells,
                      thx_stream_t stream);
 
-/* Bricked copy of a half-complex volume, the same bytes: 128-B bricks of
- * 4 x 2 x 2 (x, y, z) voxels, brick (bx, by, bz) at float2 offset
- * 16 ((bz vdim/2 + by) nxB + bx), nxB = ceil((vdim/2 + 1) / 4), voxel
- * (x & 3) + 4 (y & 1) + 8 (z & 1) inside; rows / slices wrapped like
- * iFTHalf, x >= vdim/2 + 1 zero.  The four rows of a trilinear cell share a
- * brick when y0, z0 are even, so a sample touches ~2.8 cache lines instead
- * of ~4.25 (thx_local_phase volLayout 2; thx_expectation builds one per
- * class in its workspace).  bricks: thx_volume_bricks_bytes(vdim) bytes. */
-/* The y-pair copy of a half-complex projectee (thx_local_phase volLayout 3):
+/* The y-pair copy of a half-complex projectee (thx_local_phase volLayout 2):
  * element (x, y, z) = (v(x, y, z), v(x, y + 1, z)), rows wrapped, 16 B; a
  * trilinear cell is two 32-B pieces.  ypair: 4 dimSize floats. */
 int thx_volume_ypair(const float* vol, int vdim, float* ypair, thx_stream_t stream);
-size_t thx_volume_bricks_bytes(int vdim);
-int thx_volume_bricks(const float* vol, int vdim, float* bricks, thx_stream_t stream);
 
 /* ----------------------------------------------------------------- a10 ---
  * Systematic resampling of Particle::resample (src/Particle.cpp:1291-1478)
@@ -620,6 +631,11 @@ typedef struct thx_expect_cfg {
                                  fit LDS; NULL: the half-complex projectee */
     /* ABI 5 */
     int nPhaseEvents;         /* event pairs phaseEvents holds: phases past it are not timed */
+    /* ABI 6 */
+    int* phaseRoute;          /* optional device int[nPhaseRoute]: the kernel the device route
+                                 picked in each phase (as thx_local_phase_routed's route: 0
+                                 staged, 1 box-less, 2 y-pair, -1 not routed); NULL: none */
+    int nPhaseRoute;
 } thx_expect_cfg;
 
 /* nOrd: length of pxOrder (<= 0 when pxOrder is NULL). */
@@ -734,12 +750,16 @@ int thx_event_pairs_destroy(void* events, int n);
  * device, as cuthunder deals batches round-robin over every visible GPU
  * (gpu/src/cuthunder.cu:2002-2198, 5570-5826); insert partial half-maps are
  * summed onto the first device.  The devices (also what thx_getAviDevice
- * reports to the per-image local path): every visible GPU; or the list in the
- * environment variable THX_DEVICES ("0,2,5"); THX_DEVICES=local -- device
- * (local rank % GPU count) from LOCAL_RANK / OMPI_COMM_WORLD_LOCAL_RANK /
- * MPI_LOCALRANKID / SLURM_LOCALID, one MPI process per GPU without any change
- * to the caller; THX_DEVICES=current -- the caller's current device.  This
- * returns the list (devs may be NULL when cap is 0). */
+ * reports to the per-image local path), THX_DEVICES unset: one device per
+ * process, (local rank % GPU count), when the launcher's environment says
+ * several processes share the node (LOCAL_WORLD_SIZE /
+ * OMPI_COMM_WORLD_LOCAL_SIZE / MPI_LOCALNRANKS / SLURM_NTASKS_PER_NODE > 1
+ * with LOCAL_RANK / OMPI_COMM_WORLD_LOCAL_RANK / MPI_LOCALRANKID /
+ * SLURM_LOCALID), otherwise every visible GPU; THX_DEVICES=all / local /
+ * current (the caller's current device) / a list ("0,2,5") forces one.  A
+ * hemisphere communicator passed to the insert adapters must live on the
+ * first of these devices (checked: THX_ERR_ARG otherwise).  This returns the
+ * list (devs may be NULL when cap is 0). */
 int thx_adapter_devices(int* devs, int cap, int* n);
 /* hipSetDevice for C++ callers without HIP headers (e.g. before
  * thx_rccl_comm_init, whose communicator lives on the current device). */

@@ -72,8 +72,8 @@ def phase_inputs(s, orc, nImg, nR, nT, nD, seed, spread=None):
 
 
 @pytest.mark.parametrize("nR,nT,nD,layout", [(10, 9, 3, 0), (10, 9, 3, 1), (20, 5, 9, 0),
-                                             (130, 3, 1, 0), (12, 4, 7, 1), (20, 5, 9, 2),
-                                             (130, 3, 1, 2)])
+                                             (130, 3, 1, 0), (12, 4, 7, 1), (20, 5, 9, 1),
+                                             (130, 3, 1, 1)])
 def test_local_phase_d(orc, stack, nR, nT, nD, layout):
     s = stack
     px = dev_pixels(s)
@@ -81,10 +81,9 @@ def test_local_phase_d(orc, stack, nR, nT, nD, layout):
     quat, trans, ctfD, pC, pR, pT, pD = phase_inputs(s, orc, nImg, nR, nT, nD, seed=nR + nD)
     vol = T(s["vol"])
     cells = ops.volume_cells(vol) if layout == 1 else None
-    bricks = ops.volume_bricks(vol) if layout == 2 else None
     wC, wR, wT, wD, base, d = ops.local_phase_d(vol, T(quat), T(trans), T(pC), T(pR), T(pT), T(pD),
                                                 T(s["dat"][:nImg]), T(ctfD), T(s["sig"][:nImg]),
-                                                px, want_dvp=True, cells=cells, bricks=bricks)
+                                                px, want_dvp=True, cells=cells)
     wC, wR, wT, wD, base, d = [x.cpu().numpy() for x in (wC, wR, wT, wD, base, d)]
     for l in range(nImg):
         rc, rr, rt, rdd, rb, rdv = orc.local_phase_d(s["vol"], s["vdim"], s["pf"], quat[l],

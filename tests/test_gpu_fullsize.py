@@ -58,24 +58,35 @@ def test_dvp_matches_oracle_subset(orc, c3):
     assert np.max(np.abs(d - ref) / np.abs(ref)) < 1e-5
 
 
-@pytest.mark.parametrize("cells", [False, True])
-def test_full_resolution_phase_matches_oracle(orc, c3, cells):
+@pytest.mark.parametrize("layout", ["halfcomplex", "cells", "ypair", "routed"])
+@pytest.mark.parametrize("spread", [1.5, 3.0, 0.0])
+def test_full_resolution_phase_matches_oracle(orc, c3, layout, spread):
+    """The north-star shape (box 256, nPxl 24 746, 125 x 9) on 1.5 and 3
+    degree clouds and uniformly random rotations (spread 0), in every layout
+    the bench's roofline_local prices and on the device route with a y-pair
+    copy; dvp 1e-5 relative to the oracle."""
     from bench import make_stack
     N, pf = c3["N"], c3["pf"]
     px, dat, ctf, sig, *_ = make_stack(N, pf, 126, 1, 3, DEV, seed=13, vol=c3["vol"])
     assert px.n == 24746
     nImg, mR, mT = 3, 125, 9
     rng = np.random.default_rng(4)
-    quat = synth.uniform_quaternions(nImg * mR, rng).reshape(nImg, mR, 4)
+    quat = (synth.clustered_quaternions(nImg, mR, spread, rng) if spread > 0
+            else synth.uniform_quaternions(nImg * mR, rng).reshape(nImg, mR, 4))
     trans = rng.standard_normal((nImg, mT, 2))
     ones = np.ones(nImg)
     pR = np.full((nImg, mR), 1 / mR)
     pT = np.full((nImg, mT), 1 / mT)
     T = lambda a: torch.as_tensor(a, device=DEV)
-    cl = ops.volume_cells(c3["vol"]) if cells else None
-    wC, wR, wT, base, d = ops.local_phase(c3["vol"], T(quat), T(trans), T(ones), T(pR), T(pT), dat,
-                                          ctf, sig, px, want_dvp=True, cells=cl)
-    d = d.cpu().numpy()
+    cl = ops.volume_cells(c3["vol"]) if layout == "cells" else None
+    yp = ops.volume_ypair(c3["vol"]) if layout in ("ypair", "routed") else None
+    out = ops.local_phase(c3["vol"], T(quat), T(trans), T(ones), T(pR), T(pT), dat, ctf, sig, px,
+                          want_dvp=True, cells=cl, ypair=yp, routed=layout == "routed")
+    d = out[4].cpu().numpy()
+    if layout == "routed":
+        assert out[5] in (0, 2), out[5]
+        if spread == 0.0:
+            assert out[5] == 2          # uniform rotations: no box fits
     pxh = orc.pixel_set(N, pf, 126, 1)
     vnp = c3["vol"].cpu().numpy()
     for l in range(nImg):

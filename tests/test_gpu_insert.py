@@ -124,6 +124,56 @@ def test_rccl_halfmap_allreduce_single_rank():
     comm.close()
 
 
+def test_rccl_halfmap_sendrecv_self():
+    """thx_halfmap_sendrecv (the leads' B -> A hand-over) as a self send /
+    receive in one group on a one-rank communicator: the map arrives
+    bit-identical; a receive-only and a send-only call to self pair up the
+    same way inside the group."""
+    comm = ops.RcclComm(1, ops.RcclComm.unique_id(), 0)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    src = torch.randn(3 * 1000 + 7, generator=g, device=DEV)
+    dst = torch.full_like(src, -1.0)
+    comm.sendrecv(send=src, peer_send=0, recv=dst, peer_recv=0, n_recv=src.numel())
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+    comm.close()
+
+
+def test_rccl_round_end_single_rank_group():
+    """ops.RcclComm.from_group on a one-rank torch.distributed (gloo) group
+    and hemisphere.RoundEnd's RCCL transport at world 1: the unique id goes
+    through the group's broadcast, the hemisphere reduction is the identity."""
+    import socket
+
+    import torch.distributed as dist
+
+    from thunder_amd import hemisphere
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        comm = ops.RcclComm.from_group(dist.group.WORLD, DEV)
+        assert comm.nranks == 1 and comm.rank == 0
+        hm = ops.HalfMap(32, DEV)
+        hm.F.copy_(torch.complex(torch.randn(hm.F.shape, device=DEV), torch.randn(hm.F.shape, device=DEV)))
+        hm.T.copy_(torch.rand(hm.T.shape, device=DEV))
+        hm.counter.fill_(3)
+        ref = [x.clone() for x in (hm.F, hm.T, hm.counter)]
+        comm.allreduce(hm)
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip((hm.F, hm.T, hm.counter), ref))
+        comm.close()
+        re = hemisphere.RoundEnd(1, 0, "rccl", DEV)
+        assert re.is_lead and re.hemi_comm.nranks == 1
+        re.reduce(hm)
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip((hm.F, hm.T, hm.counter), ref))
+        re.close()
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("rmax_div,mReco,nImg", [(2, 7, 3), (1, 1, 1)])
 def test_binned_insert_outside_tile_grid_and_single_sample(orc, stack, rmax_div, mReco, nImg):
     """thx_insert3d_binned with an rMax below the pixel set's radius: the
@@ -241,3 +291,29 @@ def test_binned_insert_keeps_small_t_per_voxel(orc, stack):
     assert np.max(np.abs(gT - Tm)[m] / Tm[m]) < 1e-5
     gF = hm.F.cpu().numpy().reshape(-1)
     assert np.max(np.abs(gF - F)) <= 1e-5 * np.max(np.abs(F))
+
+
+def test_adapter_devices_default_policy(monkeypatch):
+    """THX_DEVICES unset: every visible GPU for a lone process per node, one
+    device (local rank % count) when the launcher reports several processes
+    per node (ranks sharing a node must not all fan out and bind
+    their hemisphere communicators to device 0)."""
+    L = lib()
+    nDev = torch.cuda.device_count()
+    buf = (ctypes.c_int * 16)()
+    n = ctypes.c_int()
+    monkeypatch.delenv("THX_DEVICES", raising=False)
+    for v in ("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS",
+              "MV2_COMM_WORLD_LOCAL_SIZE", "SLURM_NTASKS_PER_NODE", "PMI_LOCAL_SIZE",
+              "LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID",
+              "MV2_COMM_WORLD_LOCAL_RANK", "SLURM_LOCALID", "PMI_LOCAL_RANK"):
+        monkeypatch.delenv(v, raising=False)
+    assert L.thx_adapter_devices(buf, 16, ctypes.byref(n)) == 0
+    assert list(buf[:n.value]) == list(range(nDev))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    assert L.thx_adapter_devices(buf, 16, ctypes.byref(n)) == 0
+    assert list(buf[:n.value]) == [1 % nDev]
+    monkeypatch.setenv("THX_DEVICES", "all")
+    assert L.thx_adapter_devices(buf, 16, ctypes.byref(n)) == 0
+    assert list(buf[:n.value]) == list(range(nDev))

@@ -253,15 +253,19 @@ def test_local_phase_staged_patches(orc, stack64, spread, lo, hi):
     b = ops.local_phase(vol, *args, want_dvp=True, tiled=False)
     c = ops.local_phase(vol, *args, want_dvp=True, cells=ops.volume_cells(vol))
     assert np.max(np.abs(c[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
-    e = ops.local_phase(vol, *args, want_dvp=True, bricks=ops.volume_bricks(vol))
-    # the same taps from bricks; the half-complex phase may take the box-less
-    # route (interp_ft's unfused sum) where the bricked one stages (packed FMA)
-    assert np.max(np.abs(e[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
-    # the y-pair copy (two 32-B pieces per cell, quad-cooperative)
+    # the y-pair copy (pair form: two 32-B pieces per cell, lane pairs)
     yp = ops.volume_ypair(vol)
-    for pair in (False, True):       # quad / pair forms of the y-pair gather
-        y = ops.local_phase(vol, *args, want_dvp=True, ypair=yp, pair=pair)
-        assert np.max(np.abs(y[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
+    y = ops.local_phase(vol, *args, want_dvp=True, ypair=yp)
+    assert np.max(np.abs(y[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
+    # the device route, with and without the y-pair copy: the staged kernel
+    # for compact clouds (>= half the sampled boxes fit), else the pair-form
+    # y-pair kernel, or the box-less half-complex one without a copy
+    for ypc in (yp, None):
+        r = ops.local_phase(vol, *args, want_dvp=True, ypair=ypc, routed=True)
+        want = 0 if spread < 5 else (2 if ypc is not None else 1)
+        if spread != 8.0:     # 8 degrees sits near the 50 % threshold
+            assert r[5] == want, (spread, frac, r[5])
+        assert np.max(np.abs(r[4].cpu().numpy() - a[4].cpu().numpy()) / np.abs(a[4].cpu().numpy())) < 2e-6
     da, db = a[4].cpu().numpy(), b[4].cpu().numpy()
     assert np.max(np.abs(da - db) / np.abs(db)) < 2e-6      # pixel summation order only
     for l in range(nImg):
@@ -520,21 +524,14 @@ def test_empty_batches(orc, stack):
     torch.cuda.synchronize()
 
 
-def test_volume_bricks_layout():
-    """thx_volume_bricks against the layout its header states: voxel (x, y, z)
-    at 16 ((z/2 vdim/2 + y/2) nxB + x/4) + (x & 3) + 4 (y & 1) + 8 (z & 1),
-    zeros past the half-plane edge; the bytes equal the half-complex volume's
-    rounded up to whole bricks."""
+def test_volume_ypair_layout():
+    """thx_volume_ypair against the layout its header states: element
+    (z, y, x) = (v(z, y, x), v(z, (y + 1) mod vdim, x))."""
     vdim = 24
     g = torch.Generator().manual_seed(3)
     vol = torch.complex(torch.randn(vdim, vdim, vdim // 2 + 1, generator=g),
                         torch.randn(vdim, vdim, vdim // 2 + 1, generator=g)).to(DEV)
-    b = ops.volume_bricks(vol).cpu()
-    nxB = (vdim // 2 + 1 + 3) // 4
-    assert b.numel() == nxB * 16 * (vdim // 2) ** 2
-    z, y, x = torch.meshgrid(torch.arange(vdim), torch.arange(vdim), torch.arange(nxB * 4),
-                             indexing="ij")
-    idx = 16 * (((z // 2) * (vdim // 2) + y // 2) * nxB + x // 4) + (x & 3) + 4 * (y & 1) + 8 * (z & 1)
-    got = b[idx.reshape(-1)].reshape(vdim, vdim, nxB * 4)
-    assert torch.equal(got[..., :vdim // 2 + 1], vol.cpu())
-    assert torch.count_nonzero(got[..., vdim // 2 + 1:]) == 0
+    yp = ops.volume_ypair(vol).cpu()
+    v = vol.cpu()
+    assert torch.equal(yp[..., 0], v)
+    assert torch.equal(yp[..., 1], torch.roll(v, -1, dims=1))

@@ -27,8 +27,6 @@ SIGNATURES = {
                                  _c_int, _c_int, _p, _p, _p, _p, _c_int, _p, _c_size, _p]),
     "thx_local_phase_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "thx_volume_cells": (_c_int, [_p, _c_int, _p, _p]),
-    "thx_volume_bricks": (_c_int, [_p, _c_int, _p, _p]),
-    "thx_volume_bricks_bytes": (ctypes.c_size_t, [_c_int]),
     "thx_pixel_tile_order": (_c_int, [_p, _p, _c_int, _c_int, _p, _p]),
     "thx_local_phase": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _p, _p,
                                  _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p, _p, _p, _p,
@@ -123,6 +121,9 @@ SIGNATURES = {
     "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int, _c_int]),
     "thx_expectation": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int,
                                  _p, _p, _p, _p, _p, _p, _p, _p, _c_size, _p]),
+    "thx_local_phase_routed": (_c_int, [_p, _p, _p, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
+                                        _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p,
+                                        _p, _p, _p, _p, _p, _c_size, _p]),
     "thx_local_phase_sel": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p,
                                      _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int, _p, _p, _p,
                                      _p, _p, _p, _c_size, _p]),

@@ -57,6 +57,9 @@ inline int set_max_lds(const void* fn, int bytes, std::atomic<unsigned>& done)
 // the devices the host adapters use and getAviDevice reports (interface.hip)
 int adapter_devices(std::vector<int>& devs);
 
+// the device an RCCL communicator was created on (halfmap.hip)
+int comm_device(void* comm, int* dev);
+
 // the RCCL half-map all-reduce with oDim doubles of O per class (halfmap.hip)
 int halfmap_allreduce_impl(void* comm, float* F, float* T, double* O, int oDim, int* counter,
                            long long dimSize, int nK, hipStream_t s);

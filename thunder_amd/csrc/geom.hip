@@ -86,11 +86,8 @@ extern "C" int thx_pixel_tile_order(const int* iCol, const int* iRow, int nPxl, 
     }
     // inside a square: its 2x2 quads in turn, so that every 4 consecutive
     // entries (one step of the local phase's lanes) are a compact quad
-#ifndef THX_QUAD_ORDER
-#define THX_QUAD_ORDER 1
-#endif
     std::vector<int> sub(nPxl, 0);
-    for (int i = 0; THX_QUAD_ORDER && i < nPxl; i++) {
+    for (int i = 0; i < nPxl; i++) {
         const int lc = (iCol[i] - cMin) % TILE, lr = (iRow[i] - rMin) % TILE;
         sub[i] = ((lr / 2) * 2 + lc / 2) * 4 + (lr % 2) * 2 + lc % 2;
     }

@@ -84,6 +84,13 @@ static int group_end(ncclResult_t first, const char* what)
 }
 
 namespace thx {
+int comm_device(void* comm, int* dev)
+{
+    THX_CHECK_ARG(comm && dev, "comm_device: null");
+    THX_NCCL(ncclCommCuDevice(static_cast<ncclComm_t>(comm), dev));
+    return THX_OK;
+}
+
 // oDim doubles of O per class (3 in 3D, 2 for the 2D InsertI2D's O2D)
 int halfmap_allreduce_impl(void* comm, float* F, float* T, double* O, int oDim, int* counter,
                            long long dimSize, int nK, hipStream_t s)

@@ -252,9 +252,6 @@ __global__ void __launch_bounds__(INS_THREADS) k_insert_patches(float2* __restri
                     for (int ix = 0; ix < 2; ix++) {
                         const float wt = wx[ix] * wy[jy] * wz[kz];
                         const int v = a + kz * sp + jy * nx + ix;
-#ifdef THX_INS_NOACC      // diagnostic builds only (tools/diag_insert.py)
-                        if (wt != 12345.f) continue;
-#endif
                         atomicAdd(&sF[v].x, vr * wt);
                         atomicAdd(&sF[v].y, vi * wt);
                         atomicAdd(&sT[v], tv * wt);
@@ -263,9 +260,6 @@ __global__ void __launch_bounds__(INS_THREADS) k_insert_patches(float2* __restri
         }
         __syncthreads();
         // flush: one box row per wave pass, lanes over the row's floats
-#ifdef THX_INS_NOFLUSH    // diagnostic builds only (tools/diag_insert.py)
-        continue;
-#endif
         const int rowsSide = zn * ny;
         const int rows0 = nv0 > 0 ? rowsSide : 0, rows = rows0 + (nv1 > 0 ? rowsSide : 0);
         for (int row = wv; row < rows; row += INS_WAVES) {

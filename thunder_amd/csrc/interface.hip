@@ -180,10 +180,23 @@ static int local_rank_env()
     return -1;
 }
 
+// the number of processes the launcher placed on this node (-1: unknown)
+static int local_size_env()
+{
+    for (const char* v : {"LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS",
+                          "MV2_COMM_WORLD_LOCAL_SIZE", "SLURM_NTASKS_PER_NODE", "PMI_LOCAL_SIZE"}) {
+        const char* e = std::getenv(v);
+        if (e && *e) return std::atoi(e);
+    }
+    return -1;
+}
+
 // The devices the batch adapters spread work over and getAviDevice reports
-// (see the file comment): THX_DEVICES unset -> every visible GPU; "current"
-// -> the caller's current device; "local" -> device (local rank % count), the
-// one-process-per-GPU deployment with no change to the caller; "0,3" -> a list.
+// (see the file comment): THX_DEVICES unset -> one device per process, (local
+// rank % count), when the launcher put several processes on this node, else
+// every visible GPU (the reference's one-rank-per-node layout); "current" ->
+// the caller's current device; "local" -> (local rank % count); "all" ->
+// every visible GPU; "0,3" -> a list.
 int adapter_devices(std::vector<int>& devs)
 {
     devs.clear();
@@ -196,12 +209,13 @@ int adapter_devices(std::vector<int>& devs)
         devs.push_back(cur);
         return THX_OK;
     }
-    if (env && std::strcmp(env, "local") == 0) {
+    const bool several = local_size_env() > 1 && local_rank_env() >= 0;
+    if ((env && std::strcmp(env, "local") == 0) || ((!env || !*env) && several)) {
         const int lr = local_rank_env();
         devs.push_back(lr >= 0 ? lr % n : cur);
         return THX_OK;
     }
-    if (env && *env) {
+    if (env && *env && std::strcmp(env, "all") != 0) {
         std::string s(env);
         size_t i = 0;
         while (i < s.size()) {
@@ -417,6 +431,14 @@ int reduce_maps(std::vector<DevMap>& maps, const std::vector<int>& devs, size_t 
         }
     }
     if (comm) {
+        // the communicator must live on the device the partial maps were summed
+        // onto (several ranks per node: THX_DEVICES unset or "local" gives each
+        // its own device)
+        int cdev = -1;
+        THX_RET(thx::comm_device(comm, &cdev));
+        THX_CHECK_ARG(cdev == d0,
+                      "hemisphere communicator on device %d, adapter maps on device %d "
+                      "(one device per rank: THX_DEVICES=local)", cdev, d0);
         THX_RET(thx::halfmap_allreduce_impl(comm, maps[0].F.as<float>(), maps[0].T.as<float>(),
                                             maps[0].O.as<double>(), oDim, maps[0].C.as<int>(),
                                             (long long)img, nk, nullptr));

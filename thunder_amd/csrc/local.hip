@@ -119,31 +119,6 @@ THX_DEV float2 interp_cell_piece(const float4* __restrict__ cells, int vdim, flo
     return make_float2(re, conj ? -im : im);
 }
 
-// y-pair projectee (thx_volume_ypair): element (x, y, z) holds v(x, y, z) and
-// v(x, y + 1, z) (rows wrapped), 16 B, x fastest as the half-complex rows, so
-// a trilinear cell is two 32-B pieces -- elements x0, x0 + 1 at z0 and at
-// z0 + 1 -- instead of four 16-B row pieces, at twice the footprint (the
-// low-resolution ball of the phases: 3.9 MB at box 256).  Quad-cooperative
-// like the cells: lane j reads element x0 + (j & 1) of slice z0 + (j >> 1);
-// the quad's two lanes per slice share one 32-B segment.
-THX_DEV float2 interp_ypair_piece(const float4* __restrict__ yp, int vdim, float x, float y,
-                                  float z, int j)
-{
-    const bool conj = !(x >= 0.f);
-    if (conj) { x = -x; y = -y; z = -z; }
-    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
-    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
-    const float dx = x - fx, dy = y - fy, dz = z - fz;
-    const int nColFT = vdim / 2 + 1;
-    const size_t e = ((size_t)wrap_idx(z0 + (j >> 1), vdim) * vdim + wrap_idx(y0, vdim)) * nColFT +
-                     x0 + (j & 1);
-    const float4 q = yp[e];
-    const float wxz = ((j & 1) ? dx : 1.f - dx) * ((j >> 1) ? dz : 1.f - dz);
-    const float w0 = wxz * (1.f - dy), w1 = wxz * dy;
-    const float re = q.x * w0 + q.z * w1, im = q.y * w0 + q.w * w1;
-    return make_float2(re, conj ? -im : im);
-}
-
 // The quad pieces from a sample's precomputed cell (folded base x0, y0, z0,
 // fractions, conj): the quad's lanes compute the coordinates of four
 // different samples once and share them (coop_step), instead of each lane
@@ -162,17 +137,6 @@ THX_DEV Cell cell_of(float x, float y, float z)
     c.x0 = (int)fx; c.y0 = (int)fy; c.z0 = (int)fz;
     c.dx = x - fx; c.dy = y - fy; c.dz = z - fz;
     return c;
-}
-THX_DEV float2 ypair_piece(const float4* __restrict__ yp, int vdim, const Cell& c, int j)
-{
-    const int nColFT = vdim / 2 + 1;
-    const size_t e = ((size_t)wrap_idx(c.z0 + (j >> 1), vdim) * vdim + wrap_idx(c.y0, vdim)) * nColFT +
-                     c.x0 + (j & 1);
-    const float4 q = yp[e];
-    const float wxz = ((j & 1) ? c.dx : 1.f - c.dx) * ((j >> 1) ? c.dz : 1.f - c.dz);
-    const float w0 = wxz * (1.f - c.dy), w1 = wxz * c.dy;
-    const float re = q.x * w0 + q.z * w1, im = q.y * w0 + q.w * w1;
-    return make_float2(re, c.conj ? -im : im);
 }
 THX_DEV float2 cell_piece(const float4* __restrict__ cells, int vdim, const Cell& c, int j)
 {
@@ -255,78 +219,14 @@ THX_DEV float quad_sum(float v)
     return v;
 }
 
-// Bricked projectee (thx_volume_bricks): the half-complex volume in 128-B
-// bricks of 4 x 2 x 2 (x, y, z) voxels, x fastest inside a brick row, so the
-// four rows (y0, y0 + 1) x (z0, z0 + 1) of a trilinear cell share a brick
-// whenever y0 and z0 are even.  A sample then touches (1 + 1/4)(1 + 1/2)
-// (1 + 1/2) = 2.8 128-B lines on average instead of the half-complex rows'
-// (1 + 1/16) 2 2 = 4.25, at the same footprint (the L2-resident working set
-// of a phase stays L2-resident).  Rows / slices wrapped like iFTHalf; bricks
-// past the half-plane edge (x >= nColFT) hold zeros.
-enum { LAYOUT_FT = 0, LAYOUT_CELLS = 1, LAYOUT_BRICKS = 2, LAYOUT_YPAIR = 3, LAYOUT_YPAIR2 = 4 };
+// Projectee layouts of the phase: the half-complex volume (0), its
+// cell-expanded copy (1, quad-cooperative gathers, no LDS boxes) and its
+// y-pair copy (2, thx_volume_ypair: element (x, y, z) holds v(x, y, z) and
+// v(x, y + 1, z), so a trilinear cell is two 32-B pieces, gathered by lane
+// pairs -- ypair_pair_part).
+enum { LAYOUT_FT = 0, LAYOUT_CELLS = 1, LAYOUT_YPAIR2 = 2 };
 // layouts gathered quad-cooperatively (no LDS boxes, no patch records)
-constexpr bool coop_layout(int l) { return l == LAYOUT_CELLS || l == LAYOUT_YPAIR; }
-
-THX_DEV int bricks_nx(int vdim) { return (vdim / 2 + 1 + 3) / 4; }
-
-// float2 index of voxel 0 of the brick row holding wrapped row (yw, zw)
-THX_DEV size_t brick_row(int yw, int zw, int vdim, int nxB)
-{
-    return (((size_t)(zw >> 1) * (vdim >> 1) + (yw >> 1)) * nxB << 4) + ((((zw & 1) << 1) | (yw & 1)) << 2);
-}
-
-THX_DEV int brick_x(int x) { return ((x >> 2) << 4) + (x & 3); }
-
-// interp_ft's taps, weights and summation order from the bricked layout
-THX_DEV float2 interp_bricks(const float2* __restrict__ vol, int vdim, float x, float y, float z)
-{
-    const bool conj = !(x >= 0.f);
-    if (conj) { x = -x; y = -y; z = -z; }
-    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
-    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
-    const float dx = x - fx, dy = y - fy, dz = z - fz;
-    const float vx[2] = {1.f - dx, dx};
-    const float vy[2] = {1.f - dy, dy};
-    const float vz[2] = {1.f - dz, dz};
-    const int nxB = bricks_nx(vdim);
-    const int ya = wrap_idx(y0, vdim), yb = wrap_idx(y0 + 1, vdim);
-    const int za = wrap_idx(z0, vdim), zb = wrap_idx(z0 + 1, vdim);
-    const int o0 = brick_x(x0), o1 = brick_x(x0 + 1);
-    const size_t r00 = brick_row(ya, za, vdim, nxB), r01 = brick_row(yb, za, vdim, nxB);
-    const size_t r10 = brick_row(ya, zb, vdim, nxB), r11 = brick_row(yb, zb, vdim, nxB);
-#ifdef THX_BRICK_PAIR
-    // the x pair is one 16-B piece unless x0 ends a brick row (1 in 4):
-    // then the upper half is re-read from the next brick
-    const bool split = (x0 & 3) == 3;
-    auto pair = [&](size_t r, float2& lo, float2& hi) {
-        const f32x4u v = *reinterpret_cast<const f32x4u*>(vol + r + o0);
-        lo = make_float2(v.x, v.y);
-        hi = make_float2(v.z, v.w);
-        if (split) hi = vol[r + o1];
-    };
-    float2 a0, a1, b0, b1, c0, c1, d0, d1;
-    pair(r00, a0, a1);
-    pair(r01, b0, b1);
-    pair(r10, c0, c1);
-    pair(r11, d0, d1);
-#else
-    const float2 a0 = vol[r00 + o0], a1 = vol[r00 + o1];
-    const float2 b0 = vol[r01 + o0], b1 = vol[r01 + o1];
-    const float2 c0 = vol[r10 + o0], c1 = vol[r10 + o1];
-    const float2 d0 = vol[r11 + o0], d1 = vol[r11 + o1];
-#endif
-    float re = 0.f, im = 0.f;
-    float w;
-    w = vx[0] * vy[0] * vz[0]; re += a0.x * w; im += a0.y * w;
-    w = vx[1] * vy[0] * vz[0]; re += a1.x * w; im += a1.y * w;
-    w = vx[0] * vy[1] * vz[0]; re += b0.x * w; im += b0.y * w;
-    w = vx[1] * vy[1] * vz[0]; re += b1.x * w; im += b1.y * w;
-    w = vx[0] * vy[0] * vz[1]; re += c0.x * w; im += c0.y * w;
-    w = vx[1] * vy[0] * vz[1]; re += c1.x * w; im += c1.y * w;
-    w = vx[0] * vy[1] * vz[1]; re += d0.x * w; im += d0.y * w;
-    w = vx[1] * vy[1] * vz[1]; re += d1.x * w; im += d1.y * w;
-    return make_float2(re, conj ? -im : im);
-}
+constexpr bool coop_layout(int l) { return l == LAYOUT_CELLS; }
 
 // Patch record (k_patch_boxes -> k_local_fused): layout in patch.h.
 struct Rec {
@@ -434,19 +334,15 @@ THX_DEV int store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __res
 #endif
 constexpr int ROUTE_SAMPLE = 16;   // every 16th image's records are counted
 
-// Third route (round 3): when the driver supplies a y-pair copy (route[7] =
-// 1), every phase whose boxes do not pay gathers from it instead of the
-// box-less half-complex kernel.  The pair form (LAYOUT_YPAIR2: two lanes per
-// sample, the 32-B pieces of slices z0 and z0 + 1) reads two accesses per
-// sample where the half-complex rows take four; on the bench's phases it is
-// faster in all ten (phase 1 11.3-12.4 vs 16.4-16.9 ms, phase 10 7.8-8.2 vs
-// 8.1-8.5; 85-86k vs 81-82k with the quad form, 75-76k without y-pairs;
-// profiles/r03_pair_ab.jsonl, r03_ypair_ab.jsonl, r03_yroute_ab.jsonl).
-// route[6] (THX_YPAIR_MAX_PCT below 100, A/B) restricts it to clouds with
-// fewer than that per cent of 8x boxes (r03_route_stats.txt).
-#ifndef THX_YPAIR_MAX_PCT
-#define THX_YPAIR_MAX_PCT 100
-#endif
+// Third route (round 3): when the caller supplies a y-pair copy (route[2] =
+// 1), every phase whose boxes do not pay gathers from it with the pair form
+// (LAYOUT_YPAIR2: two lanes per sample, the 32-B pieces of slices z0 and
+// z0 + 1), two accesses per sample where the half-complex rows take four;
+// faster than the box-less half-complex kernel in all ten bench phases
+// (profiles/r03_pair_ab.jsonl), so with a y-pair copy the box-less
+// half-complex kernel is not launched at all.
+// route[0]: sampled patches whose box fits, route[1]: sampled patches,
+// route[2]: a y-pair copy exists.
 constexpr int ROUTE_STAGED = 0, ROUTE_NOBOX = 1, ROUTE_YPAIR = 2;
 THX_DEV bool route_nostage(const int* __restrict__ route)
 {
@@ -454,15 +350,14 @@ THX_DEV bool route_nostage(const int* __restrict__ route)
 }
 THX_DEV int route_pick(const int* __restrict__ route)
 {
-    // with a y-pair copy (route[7]): the staged kernel where the boxes pay, the
-    // y-pair kernel everywhere else (the pair form beats the box-less
-    // half-complex kernel in every phase of the bench, profiles/r03_pair_ab.jsonl);
-    // route[6] < 100 keeps the box-less kernel for clouds with at least that
-    // per cent of 8x boxes (the quad form's rule, A/B)
-    if (route[7] == 1 && !route_nostage(route)) return ROUTE_STAGED;
-    if (route[7] == 1 && (route[6] >= 100 || (long)route[4] * 100 < (long)route[6] * route[1]))
-        return ROUTE_YPAIR;
-    return route_nostage(route) ? ROUTE_NOBOX : ROUTE_STAGED;
+    if (!route_nostage(route)) return ROUTE_STAGED;
+    return route[2] == 1 ? ROUTE_YPAIR : ROUTE_NOBOX;
+}
+// the route's choice to the caller (thx_local_phase_routed, the driver's
+// phaseRoute)
+__global__ void k_route_out(const int* __restrict__ route, int* __restrict__ out)
+{
+    if (threadIdx.x == 0) *out = route_pick(route);
 }
 
 #ifndef THX_SKIP_PAD
@@ -577,7 +472,7 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
         if (l >= *nAct) return;
         l = act[l];
     }
-    int nFit = 0, nAll = 0, nF2 = 0, nF4 = 0, nF8 = 0, nF16 = 0;
+    int nFit = 0, nAll = 0;
     const int nRl = min(RT, nR - ry * RT);
     const double* Q = quat + ((size_t)l * nR + ry * RT) * 4;
     rotation_slots(Q, nRl, threadIdx.x, sKey, sPerm);
@@ -671,27 +566,15 @@ __global__ void __launch_bounds__(64 * PB_WAVES) k_patch_boxes(const double* __r
             const int nv = store_rec(e, ic0, ir0, vdim, rec + (((size_t)l * nRT + ry) * nC + c) * REC);
             nFit += nv <= BOX_CAP;
             nAll += 1;
-            nF2 += nv <= 2 * BOX_CAP;     // the spread of the clouds (y-pair route)
-            nF4 += nv <= 4 * BOX_CAP;
-            nF8 += nv <= 8 * BOX_CAP;
-            nF16 += nv <= 16 * BOX_CAP;
         }
         __syncthreads();
     }
     if (routeMode == 1 && wv == 0) {
         nFit = wave_sum(nFit);
         nAll = wave_sum(nAll);
-        nF2 = wave_sum(nF2);
-        nF4 = wave_sum(nF4);
-        nF8 = wave_sum(nF8);
-        nF16 = wave_sum(nF16);
         if (lane == 0) {
             atomicAdd(&route[0], nFit);
             atomicAdd(&route[1], nAll);
-            atomicAdd(&route[2], nF2);
-            atomicAdd(&route[3], nF4);
-            atomicAdd(&route[4], nF8);
-            atomicAdd(&route[5], nF16);
         }
     }
 }
@@ -703,9 +586,6 @@ struct Pix {
     float c, s;
 };
 
-#ifndef THX_IMG_NT
-#define THX_IMG_NT 0
-#endif
 THX_DEV Pix load_pix(int p, const int* __restrict__ iCol, const int* __restrict__ iRow,
                      const float2* __restrict__ D, const float* __restrict__ C,
                      const float* __restrict__ S)
@@ -714,17 +594,9 @@ THX_DEV Pix load_pix(int p, const int* __restrict__ iCol, const int* __restrict_
     if (p >= 0) {
         x.ic = iCol[p];
         x.ir = iRow[p];
-#if THX_IMG_NT
-        // read-once image data past L2 (A/B: keep the y-pair ball resident)
-        x.d.x = __builtin_nontemporal_load(reinterpret_cast<const float*>(D + p));
-        x.d.y = __builtin_nontemporal_load(reinterpret_cast<const float*>(D + p) + 1);
-        x.c = __builtin_nontemporal_load(C + p);
-        x.s = __builtin_nontemporal_load(S + p);
-#else
         x.d = D[p];
         x.c = C[p];
         x.s = S[p];
-#endif
     }
     return x;
 }
@@ -752,13 +624,6 @@ THX_DEV void fetch_box(f32x4 (&pre)[NI][2], int (&dst)[NI], const Rec& b,
             const int gx = (s1 ? b.v[3] : b.v[0]) + 4 * xq;
             const int gy = wrap_idx((s1 ? b.v[4] : b.v[1]) + y, vdim);
             const int gz = wrap_idx((s1 ? b.v[5] : b.v[2]) + z, vdim);
-            if (LAYOUT == LAYOUT_BRICKS) {   // gx % 4 == 0: one 32-B brick row piece
-                const f32x4* p = reinterpret_cast<const f32x4*>(
-                    vol + brick_row(gy, gz, vdim, bricks_nx(vdim)) + brick_x(gx));
-                pre[j][0] = p[0];
-                pre[j][1] = p[1];
-                continue;
-            }
             const unsigned g = ((unsigned)gz * vdim + gy) * nColFT + gx;
             if (LAYOUT == LAYOUT_FT && gx + 3 < nColFT) {
                 const f32x4u* p = reinterpret_cast<const f32x4u*>(vol + g);
@@ -824,19 +689,6 @@ THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int sp, int of
 }
 
 
-#ifdef THX_LOCAL_STAMPS
-// diagnostic: per-iteration phase cycles of staged patches, waves 0 and 7
-__device__ unsigned long long g_local_stamps[12];
-#endif
-#ifdef THX_STEP_COUNT
-// diagnostic: wave-steps gathered from the shared box, straight from vol,
-// and skipped (padding); slot 1 unused
-__device__ unsigned long long g_step_counts[4];
-#define MCOUNT(k) (mc[k] += 1)
-#else
-#define MCOUNT(k) ((void)0)
-#endif
-
 // CS (CTF search, SEARCH_TYPE_CTF): the columns are the nT x nD (t, d) pairs
 // of kernel_logDataVSLC (gpu/src/Kernel.cu:889-939), column j = t nD + d; the
 // image tile takes its CTF from ctfD[l][d] (thx_ctf_search) per column, and
@@ -848,6 +700,9 @@ __device__ unsigned long long g_step_counts[4];
 #ifndef THX_NOBOX_WAVES
 #define THX_NOBOX_WAVES 6
 #endif
+#ifndef THX_PAIR_WAVES
+#define THX_PAIR_WAVES THX_NOBOX_WAVES
+#endif
 template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false, bool STAGE = true>
 // non-CS: two workgroups per CU (LDS-bound), 4 waves per SIMD, 128 VGPRs;
 // CS: the NCT accumulators and CTF prefetches need the 256-VGPR budget;
@@ -855,7 +710,7 @@ template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false, bool ST
 // no LDS box (cell layout, or STAGE = false): no box prefetch registers, so
 // 6 waves per SIMD (three workgroups per CU) for the L2 gathers
 __global__ void __launch_bounds__(THREADS)
-__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : (coop_layout(LAYOUT) || LAYOUT == LAYOUT_YPAIR2 || !STAGE) ? THX_NOBOX_WAVES : 4)))
+__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : LAYOUT == LAYOUT_YPAIR2 ? THX_PAIR_WAVES : (coop_layout(LAYOUT) || !STAGE) ? THX_NOBOX_WAVES : 4)))
 k_local_fused(const float2* __restrict__ vol,
                                                             int vdim, int pf,
                                                             const double* __restrict__ quat,
@@ -885,7 +740,7 @@ k_local_fused(const float2* __restrict__ vol,
                                                             const int* __restrict__ route = nullptr)
 {
     // routed phases launch the staged and the box-less kernel; one exits
-    if (route && route_pick(route) != (LAYOUT == LAYOUT_YPAIR || LAYOUT == LAYOUT_YPAIR2 ? ROUTE_YPAIR
+    if (route && route_pick(route) != (LAYOUT == LAYOUT_YPAIR2 ? ROUTE_YPAIR
                                        : STAGE ? ROUTE_STAGED : ROUTE_NOBOX)) return;
     int l = blockIdx.x;
     if (act) {
@@ -1004,15 +859,6 @@ k_local_fused(const float2* __restrict__ vol,
     if (!NOBOX) fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rc, vol, vdim, tid);
 
     __syncthreads();
-#ifdef THX_STEP_COUNT
-    unsigned long long mc[4] = {0, 0, 0, 0};
-#endif
-#ifdef THX_LOCAL_STAMPS
-    unsigned long long st[6] = {0, 0, 0, 0, 0, 0}, tp = __builtin_amdgcn_s_memtime(), tq;
-#define STAMP(k) do { tq = __builtin_amdgcn_s_memtime(); if (staged(rc)) st[k] += tq - tp; tp = tq; } while (0)
-#else
-#define STAMP(k) do {} while (0)
-#endif
     for (int c = 0; c < nC; c += PP) {
         // ---- stage patch c: box voxels, image tile B[px][U, V][t], b, (iCol, iRow) pf
         if (staged(rc)) {
@@ -1057,9 +903,7 @@ k_local_fused(const float2* __restrict__ vol,
                 sXY[q] = make_double2((double)(ic * pf), (double)(ir * pf));
             }
         }
-        STAMP(0);
         __syncthreads();
-        STAMP(1);
         // ---- prefetch patches c + PP .. (in flight during the gathers below)
         Rec r2 = rn;
         if (c + PP < nC) {
@@ -1073,7 +917,6 @@ k_local_fused(const float2* __restrict__ vol,
             if (!NOBOX) fetch_box<LAYOUT, NITC, BOXC>(pre, dst, rn, vol, vdim, tid);
             if (!NOBOX && c + 2 < nC) r2 = load_rec(R + (size_t)(c + 2) * REC);
         }
-        STAMP(2);
         // ---- projection samples: this lane's rotation x pixels 4s + g
         // one step: the sample's bias term, then (re, im) of pixels 4s, 4s+2 and
         // 4s+1, 4s+3 regrouped into two MFMA A operands against [U, V]
@@ -1129,9 +972,7 @@ k_local_fused(const float2* __restrict__ vol,
             for (int p = 0; p < 4; p++) {
                 const Cell c = p == 0 ? quad_bcast_cell<0>(mine) : p == 1 ? quad_bcast_cell<1>(mine)
                              : p == 2 ? quad_bcast_cell<2>(mine) : quad_bcast_cell<3>(mine);
-                const float2 v = LAYOUT == LAYOUT_YPAIR
-                                     ? ypair_piece(reinterpret_cast<const float4*>(vol), vdim, c, j)
-                                     : cell_piece(reinterpret_cast<const float4*>(vol), vdim, c, j);
+                const float2 v = cell_piece(reinterpret_cast<const float4*>(vol), vdim, c, j);
                 P[p] = make_float2(quad_sum(v.x), quad_sum(v.y));
             }
             if (!CS)
@@ -1209,12 +1050,14 @@ k_local_fused(const float2* __restrict__ vol,
             }
         };
         if (PAIR) {
-#pragma unroll 4
-            for (int s = 0; s < 4 * PP; s++) {
-                if (pad_step(s)) { MCOUNT(3); continue; }
-                MCOUNT(2);
-                pair_step(s);
-            }
+            // every step of the iteration, no padding branch (a padding step
+            // adds exactly zero: U = V = b = 0), fully unrolled so that the
+            // loads of later steps can be issued before earlier steps reduce:
+            // 90.1k vs 87.5k images/s with the per-step branch
+            // (profiles/r04_pair_pipe_ab.jsonl; an explicit two-step software
+            // pipeline needs 112 VGPRs, 4 waves per SIMD: 83k)
+#pragma unroll
+            for (int s = 0; s < 4 * PP; s++) pair_step(s);
         } else if (COOP) {
 // all four steps unrolled: 16 cell reads in flight per wave (C5 +3-4 %,
 // full-res 1.5-3 deg 2-5 % over 2; profiles/r03_coop_unroll_ab.jsonl)
@@ -1223,16 +1066,14 @@ k_local_fused(const float2* __restrict__ vol,
 #endif
 #pragma unroll THX_COOP_UNROLL
             for (int s = 0; s < 4 * PP; s++) {
-                if (pad_step(s)) { MCOUNT(3); continue; }
-                MCOUNT(2);
+                if (pad_step(s)) continue;
                 coop_step(s);
             }
         } else if (staged(rc)) {
             const int nx = rc.v[6], sp = rc.v[7], off0 = rc.v[15], off1 = rc.v[16];
 #pragma unroll
             for (int s = 0; s < 4 * PP; s++) {
-                if (pad_step(s)) { MCOUNT(3); continue; }
-                MCOUNT(0);
+                if (pad_step(s)) continue;
                 const double2 xy = sXY[4 * s + g];
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
@@ -1242,37 +1083,18 @@ k_local_fused(const float2* __restrict__ vol,
         } else {
 #pragma unroll 2
             for (int s = 0; s < 4 * PP; s++) {
-                if (pad_step(s)) { MCOUNT(3); continue; }
-                MCOUNT(2);
+                if (pad_step(s)) continue;
                 const double2 xy = sXY[4 * s + g];
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
                 const float z = (float)(m[2] * xy.x + m[5] * xy.y);
-                reduce_step(s, LAYOUT == LAYOUT_BRICKS ? interp_bricks(vol, vdim, x, y, z)
-                                                       : interp_ft(vol, vdim, x, y, z));
+                reduce_step(s, interp_ft(vol, vdim, x, y, z));
             }
         }
-        STAMP(3);
-#ifdef THX_LOCAL_STAMPS
-        const bool stg = staged(rc);
-#endif
         rc = rn;
         rn = r2;
         __syncthreads();
-#ifdef THX_LOCAL_STAMPS
-        tq = __builtin_amdgcn_s_memtime();
-        if (stg) { st[4] += tq - tp; st[5] += 1; }
-        tp = tq;
-#endif
     }
-#ifdef THX_STEP_COUNT
-    if (lane == 0)
-        for (int k = 0; k < 4; k++) atomicAdd(&g_step_counts[k], mc[k]);
-#endif
-#ifdef THX_LOCAL_STAMPS
-    if (lane == 0 && (wv == 0 || wv == 7))
-        for (int k = 0; k < 6; k++) atomicAdd(&g_local_stamps[(wv == 7) * 6 + k], st[k]);
-#endif
     // A_l = sum_i s |d|^2 (staging threads with bt == 0 accumulated it)
     aConst = wave_sum(aConst);
     if (lane == 0) sRed[wv] = aConst;
@@ -1560,24 +1382,6 @@ __global__ void __launch_bounds__(256) k_volume_ypair(const float2* __restrict__
     }
 }
 
-// One thread per 8-B voxel of the bricked copy (its own write coalesced).
-__global__ void __launch_bounds__(256) k_volume_bricks(const float2* __restrict__ vol,
-                                                       int vdim, float2* __restrict__ out)
-{
-    const int nColFT = vdim / 2 + 1, nxB = (nColFT + 3) / 4;
-    const long n = (long)nxB * 16 * (vdim / 2) * (vdim / 2);
-    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
-         q += (long)gridDim.x * blockDim.x) {
-        const int in = (int)(q & 15);
-        const long b = q >> 4;
-        const int bx = (int)(b % nxB);
-        const long yz = b / nxB;
-        const int by = (int)(yz % (vdim / 2)), bz = (int)(yz / (vdim / 2));
-        const int x = 4 * bx + (in & 3), y = 2 * by + ((in >> 2) & 1), z = 2 * bz + (in >> 3);
-        out[q] = x < nColFT ? vol[((size_t)z * vdim + y) * nColFT + x] : make_float2(0.f, 0.f);
-    }
-}
-
 size_t dvp_bytes(int nImg, int nR, int nT) { return (size_t)nImg * nR * nT * sizeof(float); }
 
 size_t rec_bytes(int nImg, int nR, int nVisit)
@@ -1594,20 +1398,21 @@ size_t patch_rec_bytes(int nImg, int nR, int nVisit) { return rec_bytes(nImg, nR
 // the per-image normalisation of a materialised dvp (also the 2D phase's)
 int launch_local_weights(const float* dvp, int nR, int nT, const double* pC, const double* pR,
                          const double* pT, float* wC, float* wR, float* wT, float* baseL, int nImg,
-                         hipStream_t s)
+                         hipStream_t s, const int* act, const int* nAct)
 {
     hipLaunchKernelGGL(k_local_weights, dim3(nImg), dim3(256), 0, s, dvp, nR, nT, pC, pR, pT, wC,
-                       wR, wT, baseL, nullptr, nullptr);
+                       wR, wT, baseL, act, nAct);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
 
 int launch_local_weights_d(const float* dvp, int nR, int nT, int nD, const double* pC,
                            const double* pR, const double* pT, const double* pD, float* wC,
-                           float* wR, float* wT, float* wD, float* baseL, int nImg, hipStream_t s)
+                           float* wR, float* wT, float* wD, float* baseL, int nImg, hipStream_t s,
+                           const int* act, const int* nAct)
 {
     hipLaunchKernelGGL(k_local_weights_d, dim3(nImg), dim3(256), 0, s, dvp, nR, nT, nD, pC, pR,
-                       pT, pD, wC, wR, wT, wD, baseL, nullptr, nullptr);
+                       pT, pD, wC, wR, wT, wD, baseL, act, nAct);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
@@ -1644,45 +1449,6 @@ extern "C" int thx_volume_ypair(const float* vol, int vdim, float* ypair, thx_st
     return THX_OK;
 }
 
-extern "C" size_t thx_volume_bricks_bytes(int vdim)
-{
-    if (vdim <= 0 || vdim % 2) return 0;
-    return (size_t)((vdim / 2 + 1 + 3) / 4) * 16 * (vdim / 2) * (vdim / 2) * 2 * sizeof(float);
-}
-
-extern "C" int thx_volume_bricks(const float* vol, int vdim, float* bricks, thx_stream_t stream)
-{
-    THX_CHECK_ARG(vol && bricks && vdim > 0 && vdim % 2 == 0, "thx_volume_bricks: bad arguments");
-    hipLaunchKernelGGL(k_volume_bricks, dim3(8192), dim3(256), 0, thx::as_stream(stream),
-                       reinterpret_cast<const float2*>(vol), vdim, reinterpret_cast<float2*>(bricks));
-    THX_LAUNCH_CHECK();
-    return THX_OK;
-}
-
-#ifdef THX_LOCAL_STAMPS
-extern "C" int thx_debug_local_stamps(unsigned long long* out, int reset)
-{
-    THX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_local_stamps), sizeof(unsigned long long) * 12));
-    if (reset) {
-        const unsigned long long z[12] = {0};
-        THX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_local_stamps), z, sizeof(z)));
-    }
-    return THX_OK;
-}
-#endif
-
-#ifdef THX_STEP_COUNT
-extern "C" int thx_debug_step_counts(unsigned long long* out, int reset)
-{
-    THX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_step_counts), sizeof(unsigned long long) * 4));
-    if (reset) {
-        const unsigned long long z[4] = {0};
-        THX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_step_counts), z, sizeof(z)));
-    }
-    return THX_OK;
-}
-#endif
-
 extern "C" size_t thx_local_phase_workspace(int nImg, int nR, int nT, int nVisit)
 {
     return dvp_bytes(nImg, nR, nT) + rec_bytes(nImg, nR, nVisit) + 256 + 768;
@@ -1699,15 +1465,15 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
                             float* wR, float* wT, float* baseL, float* dvp, void* workspace,
                             size_t wsBytes, thx_stream_t stream, int nD = 0,
                             const double* pD = nullptr, float* wD = nullptr,
-                            const float* ypair = nullptr)
+                            const float* ypair = nullptr, int* routeOut = nullptr)
 {
     THX_CHECK_ARG(nR > 0 && nT > 0 && nPxl > 0 && nImg >= 0 && vdim > 0 && pf > 0 && nD >= 0,
                   "thx_local_phase: bad sizes");
     THX_CHECK_ARG(!nD || (pD && wD && (long)nT * nD <= LOCAL_D_MAXCOL),
                   "thx_local_phase_d: needs pD, wD and nT * nD <= 1024");
     const int nCol = nD ? nT * nD : nT;
-    THX_CHECK_ARG(volLayout >= 0 && volLayout <= 4, "thx_local_phase: volLayout must be 0 .. 4");
-    THX_CHECK_ARG(volLayout < LAYOUT_YPAIR || !nD, "thx_local_phase_d: no y-pair layout with CTF search");
+    THX_CHECK_ARG(volLayout >= 0 && volLayout <= 2, "thx_local_phase: volLayout must be 0 .. 2");
+    THX_CHECK_ARG(volLayout != LAYOUT_YPAIR2 || !nD, "thx_local_phase_d: no y-pair layout with CTF search");
     THX_CHECK_ARG((long)nImg * ((nR + RT - 1) / RT) <= 0x7fffffff && (nR + RT - 1) / RT <= 65535 &&
                       (nCol + TT - 1) / TT <= 65535,
                   "thx_local_phase: grid too large");
@@ -1719,6 +1485,8 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     THX_CHECK_ARG(!act == !nAct, "thx_local_phase_sel: active and nActive go together");
     THX_CHECK_ARG(!cls || (sel->volStride > 0), "thx_local_phase_sel: cls needs a volStride");
     if (nImg == 0) return THX_OK;
+    THX_CHECK_ARG(!ypair || (volLayout == LAYOUT_FT && pxOrder && !nD),
+                  "thx_local_phase_routed: a y-pair copy goes with the half-complex layout and pxOrder");
     const int nVisit = pxOrder ? nOrd : nPxl;
     THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase_workspace(nImg, nR, nCol, nVisit),
                   "thx_local_phase: workspace too small");
@@ -1733,34 +1501,26 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
 #define THX_BIGBOX_MIN_R 300
 #endif
     const bool big = pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R;
-    // the staged / box-less route of a half-complex phase, chosen on the device
-    // from a sample of the patch records (route_nostage); THX_ROUTE = 0 keeps the
-    // staged kernel (A/B builds)
-#ifndef THX_ROUTE
-#define THX_ROUTE 1
-#endif
-    const bool routed = THX_ROUTE && volLayout == LAYOUT_FT && !nD && !big;
+    // the staged / box-less (or y-pair) route of a half-complex phase, chosen
+    // on the device from a sample of the patch records (route_pick)
+    const bool routed = volLayout == LAYOUT_FT && !nD && !big;
     const unsigned nRT = thx::cdiv(nR, RT);
     if (routed) {
-        THX_HIP(hipMemsetAsync(route, 0, 8 * sizeof(int), s));
-        if (ypair) {
-            // route[6]: the y-pair threshold (THX_YPAIR_MAX_PCT overrides it, A/B),
-            // route[7]: a y-pair copy exists
-            static const int pct = [] {
-                const char* e = std::getenv("THX_YPAIR_MAX_PCT");
-                return e ? std::atoi(e) : THX_YPAIR_MAX_PCT;
-            }();
-            THX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(route + 6), pct, 1, s));
-            THX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(route + 7), 1, 1, s));
-        }
+        THX_HIP(hipMemsetAsync(route, 0, 2 * sizeof(int), s));
+        THX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(route + 2), ypair ? 1 : 0, 1, s));
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)thx::cdiv(nImg, ROUTE_SAMPLE) * nRT),
                            dim3(64 * PB_WAVES), 0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim,
                            rec, act, nAct, route, 1);
         THX_LAUNCH_CHECK();
+        if (routeOut) {
+            hipLaunchKernelGGL(k_route_out, dim3(1), dim3(64), 0, s, route, routeOut);
+            THX_LAUNCH_CHECK();
+        }
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * nRT), dim3(64 * PB_WAVES), 0, s, quat,
                            nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct, route, 2);
         THX_LAUNCH_CHECK();
     } else if (!coop_layout(volLayout) && volLayout != LAYOUT_YPAIR2) {   // no boxes for these
+        if (routeOut) THX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(routeOut), -1, 1, s));
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)nImg * nRT), dim3(64 * PB_WAVES), 0, s, quat,
                            nR, iCol, iRow, pxOrder, nVisit, pf, vdim, rec, act, nAct, nullptr, 0);
         THX_LAUNCH_CHECK();
@@ -1782,9 +1542,6 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         auto kern = volLayout == LAYOUT_CELLS
                         ? pick(k_local_fused<LAYOUT_CELLS, true, 1>, k_local_fused<LAYOUT_CELLS, true, 2>,
                                k_local_fused<LAYOUT_CELLS, true, 4>, k_local_fused<LAYOUT_CELLS, true, 6>)
-                    : volLayout == LAYOUT_BRICKS
-                        ? pick(k_local_fused<LAYOUT_BRICKS, true, 1>, k_local_fused<LAYOUT_BRICKS, true, 2>,
-                               k_local_fused<LAYOUT_BRICKS, true, 4>, k_local_fused<LAYOUT_BRICKS, true, 6>)
                         : pick(k_local_fused<LAYOUT_FT, true, 1>, k_local_fused<LAYOUT_FT, true, 2>,
                                k_local_fused<LAYOUT_FT, true, 4>, k_local_fused<LAYOUT_FT, true, 6>);
         grid.z = thx::cdiv(nCol, TT * nct);
@@ -1801,12 +1558,9 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
         return THX_OK;
     }
     auto kern =
-        volLayout == LAYOUT_YPAIR ? k_local_fused<LAYOUT_YPAIR>
-        : volLayout == LAYOUT_YPAIR2 ? k_local_fused<LAYOUT_YPAIR2>
+        volLayout == LAYOUT_YPAIR2 ? k_local_fused<LAYOUT_YPAIR2>
         : volLayout == LAYOUT_CELLS
             ? (big ? k_local_fused<LAYOUT_CELLS, false, 1, true> : k_local_fused<LAYOUT_CELLS>)
-        : volLayout == LAYOUT_BRICKS
-            ? (big ? k_local_fused<LAYOUT_BRICKS, false, 1, true> : k_local_fused<LAYOUT_BRICKS>)
             : (big ? k_local_fused<LAYOUT_FT, false, 1, true> : k_local_fused<LAYOUT_FT>);
     // one workgroup per image (nR <= 128, nT <= 16, the phases' 125 x 9):
     // the normalisation runs in the kernel's epilogue and dvp is only written
@@ -1820,30 +1574,20 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
                            fuse ? wT : nullptr, fuse ? baseL : nullptr, rt);
     };
     if (routed) {
+        // two launches, the staged kernel and (with a y-pair copy) the pair-form
+        // y-pair kernel or (without) the box-less half-complex one; the kernel
+        // the route did not pick exits at entry
         launch(k_local_fused<LAYOUT_FT, false, 1, false, true>, route);
-        launch(k_local_fused<LAYOUT_FT, false, 1, false, false>, route);
-        // the pair form of the y-pair gather; THX_YPAIR_KERNEL=1 (A/B): the quad form
-        static const bool ypQuad = [] {
-            const char* e = std::getenv("THX_YPAIR_KERNEL");
-            return e && e[0] == '1';
-        }();
         if (ypair) {
-            auto kyp = ypQuad ? k_local_fused<LAYOUT_YPAIR> : k_local_fused<LAYOUT_YPAIR2>;
-            hipLaunchKernelGGL(kyp, grid, dim3(THREADS), 0, s,
+            hipLaunchKernelGGL(k_local_fused<LAYOUT_YPAIR2>, grid, dim3(THREADS), 0, s,
                                reinterpret_cast<const float2*>(ypair), vdim, pf, quat, nR, trans, nT,
                                reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
                                nVisit, nPxl, idim, rec, fuse ? dvp : d, act, nAct, cls,
                                cls ? 2 * vs : 0L, 1, pC, pR, pT, fuse ? wC : nullptr,
                                fuse ? wR : nullptr, fuse ? wT : nullptr, fuse ? baseL : nullptr,
                                route);
-        }
-        static const bool dbg = std::getenv("THX_ROUTE_DEBUG") != nullptr;
-        if (dbg) {      // diagnostic: the route sample's box-size counts (synchronises)
-            int h[6];
-            THX_HIP(hipMemcpyAsync(h, route, sizeof(h), hipMemcpyDeviceToHost, s));
-            THX_HIP(hipStreamSynchronize(s));
-            std::fprintf(stderr, "[route] all %d fit %d x2 %d x4 %d x8 %d x16 %d\n", h[1], h[0], h[2],
-                         h[3], h[4], h[5]);
+        } else {
+            launch(k_local_fused<LAYOUT_FT, false, 1, false, false>, route);
         }
     } else {
         launch(kern, nullptr);
@@ -1906,6 +1650,23 @@ extern "C" int thx_local_phase_d(const thx_local_sel* sel, const float* vol, int
                             nImg, wC, wR, wT, baseL, dvp, workspace, wsBytes, stream, nD, pD, wD);
 }
 
+extern "C" int thx_local_phase_routed(const thx_local_sel* sel, const float* vol,
+                                      const float* ypair, int vdim, int pf, const double* quat,
+                                      int nR, const double* trans, int nT, const double* pC,
+                                      const double* pR, const double* pT, const float* dat,
+                                      const float* ctf, const float* sigRcp, const int* iCol,
+                                      const int* iRow, const int* pxOrder, int nOrd, int nPxl,
+                                      int idim, int nImg, float* wC, float* wR, float* wT,
+                                      float* baseL, float* dvp, int* route, void* workspace,
+                                      size_t wsBytes, thx_stream_t stream)
+{
+    THX_CHECK_ARG(pxOrder, "thx_local_phase_routed: needs pxOrder (thx_pixel_tile_order)");
+    return local_phase_impl(sel, nullptr, nullptr, vol, LAYOUT_FT, vdim, pf, quat, nR, trans, nT,
+                            pC, pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim,
+                            nImg, wC, wR, wT, baseL, dvp, workspace, wsBytes, stream, 0, nullptr,
+                            nullptr, ypair, route);
+}
+
 namespace thx {
 // the driver's phase launch, with optional events around k_local_fused
 int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
@@ -1915,19 +1676,19 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
                       int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
                       void* workspace, size_t wsBytes, thx_stream_t stream, int nD,
-                      const double* pD, float* wD, const float* ypair)
+                      const double* pD, float* wD, const float* ypair, int* routeOut)
 {
     return local_phase_impl(sel, evBeg, evEnd, vol, volLayout, vdim, pf, quat, nR, trans, nT, pC,
                             pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg,
                             wC, wR, wT, baseL, nullptr, workspace, wsBytes, stream, nD, pD, wD,
-                            ypair);
+                            ypair, routeOut);
 }
 
 // whether local_phase_impl routes a phase on the device (half-complex layout,
 // no CTF search, 64 KiB boxes) -- the phases that can use a y-pair copy
 bool phase_routed(int volLayout, int pf, int nPxl, int nD)
 {
-    return THX_ROUTE && volLayout == LAYOUT_FT && !nD &&
+    return volLayout == LAYOUT_FT && !nD &&
            !(pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R);
 }
 }  // namespace thx

@@ -32,16 +32,6 @@
 
 #include "common.h"
 
-#ifdef THX_DUMP_QUAT
-static double* g_quat_sink = nullptr;   // [popcount(mask)][nImg][mLR][4], device
-static unsigned g_quat_mask = 0;
-extern "C" int thx_debug_quat_sink(double* dst, unsigned phaseMask)
-{
-    g_quat_sink = dst;
-    g_quat_mask = phaseMask;
-    return 0;
-}
-#endif
 
 namespace thx {
 int project2d_launch(const float* vol, int vdim, int pf, const double* rot, int rotStride, int nR,
@@ -52,7 +42,7 @@ int local_phase2d_launch(const float* vol, int vdim, int pf, const int* cls, con
                          const float* sigRcp, const int* iCol, const int* iRow, int nPxl, int idim,
                          int nImg, float* wC, float* wR, float* wT, float* baseL, float* dvp,
                          const int* done, hipStream_t s, int nD = 0, const double* pD = nullptr,
-                         float* wD = nullptr);
+                         float* wD = nullptr, const int* act = nullptr, const int* nAct = nullptr);
 int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
                       const float* vol, int volLayout, int vdim, int pf, const double* quat, int nR,
                       const double* trans, int nT, const double* pC, const double* pR,
@@ -61,7 +51,7 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
                       void* workspace, size_t wsBytes, thx_stream_t stream, int nD = 0,
                       const double* pD = nullptr, float* wD = nullptr,
-                      const float* ypair = nullptr);
+                      const float* ypair = nullptr, int* routeOut = nullptr);
 bool phase_routed(int volLayout, int pf, int nPxl, int nD);
 }
 
@@ -138,10 +128,7 @@ THX_DEV double quad10(const double* Mp, const double* q)
 // register-resident particles give the fixed point's quadratic forms ILP.
 // Measured on 12 500 x 125 (tools/pf_bench.py, profiles/r02_pf_group_ab.jsonl):
 // calVari 0.145 / 0.105 ms at GROUP 16 / 8 on 3-degree clouds, 32 and 64 slower.
-#ifndef THX_PF_GROUP
-#define THX_PF_GROUP 8
-#endif
-constexpr int GROUP = THX_PF_GROUP;
+constexpr int GROUP = 8;
 
 // v from another lane of the row by DPP (both 32-bit halves)
 template <int CTRL>
@@ -1234,67 +1221,6 @@ __global__ void __launch_bounds__(256) k_sample_set(int nR, int nT, double trans
     for (int t = threadIdx.x; t < nT; t += 256) pT[t] /= tt;
 }
 
-// Phase launch order by slice orientation (THX_XCD_ORDER=1, A/B): workgroup
-// b of a phase launch runs on XCD b % 8, so act[b] deals the images sorted by
-// the normal of their cloud's first rotation (the slice plane's normal R e_z,
-// sign-folded to the upper hemisphere, Morton key of its (x, y) on a 64 x 64
-// grid) in eight contiguous runs, one per XCD: an XCD then gathers from the
-// planes of nearby orientations only -- about half of the projectee's ball --
-// which is what lets a larger layout (the y-pair copy) stay in its 4 MB L2.
-// One workgroup: counting sort over the 4096 keys, then the deal.
-constexpr int XO_BINS = 4096;
-__global__ void __launch_bounds__(1024) k_xcd_order(int nImg, int mR, const double* __restrict__ quat,
-                                                    int* __restrict__ key, int* __restrict__ act,
-                                                    int* __restrict__ nAct)
-{
-    __shared__ int sCnt[XO_BINS];
-    __shared__ int sW[16];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (int b = tid; b < XO_BINS; b += 1024) sCnt[b] = 0;
-    __syncthreads();
-    for (int l = tid; l < nImg; l += 1024) {
-        const double* q = quat + (size_t)l * mR * 4;
-        const double w = q[0], x = q[1], y = q[2], z = q[3];
-        double nx = 2.0 * (x * z + w * y), ny = 2.0 * (y * z - w * x);
-        const double nz = 1.0 - 2.0 * (x * x + y * y);
-        if (nz < 0.0) { nx = -nx; ny = -ny; }
-        const unsigned ix = (unsigned)fmin(63.0, fmax(0.0, (nx + 1.0) * 32.0));
-        const unsigned iy = (unsigned)fmin(63.0, fmax(0.0, (ny + 1.0) * 32.0));
-        unsigned k = 0;
-        for (int bit = 0; bit < 6; bit++) k |= (((ix >> bit) & 1u) << (2 * bit)) | (((iy >> bit) & 1u) << (2 * bit + 1));
-        key[l] = (int)k;
-        atomicAdd(&sCnt[k], 1);
-    }
-    __syncthreads();
-    // exclusive prefix over the bins (4 per thread, then a block scan)
-    int loc[4], run = 0;
-    for (int u = 0; u < 4; u++) { loc[u] = run; run += sCnt[4 * tid + u]; }
-    int inc = run;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += v;
-    }
-    if (lane == 63) sW[wv] = inc;
-    __syncthreads();
-    int base = inc - run;
-    for (int w2 = 0; w2 < wv; w2++) base += sW[w2];
-    __syncthreads();
-    for (int u = 0; u < 4; u++) sCnt[4 * tid + u] = base + loc[u];
-    __syncthreads();
-    // scatter: sorted position of image l, then the deal to (XCD x, slot j)
-    for (int l = tid; l < nImg; l += 1024) {
-        const int pos = atomicAdd(&sCnt[key[l]], 1);
-        // sorted position pos -> launch slot b with XCD x = the run holding pos
-        int x = 0, start = 0;
-        for (; x < 8; x++) {
-            const int cnt = (nImg - x + 7) / 8;
-            if (pos < start + cnt) break;
-            start += cnt;
-        }
-        act[(pos - start) * 8 + x] = l;
-    }
-    if (tid == 0) *nAct = nImg;
-}
 
 struct Plan {
     // carve of the driver workspace
@@ -1309,40 +1235,14 @@ struct Plan {
     float* wC; float* wR; float* wT; float* base; double* pC;
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
     double* bestR; double* bestT;                        // convergence: smallest variR / variT
-    int* xoKey; int* xoAct; int* xoN;                    // THX_XCD_ORDER: keys, launch order
     void* localWs; size_t localWsBytes;
-    float* bricks; size_t brickStride;   // bricked projectees (thx_volume_bricks), per class
     float* ypair;                        // y-pair projectees (thx_volume_ypair), per class
-    bool ypairAll;                       // every phase on the y-pair copy (A/B)
     // CTF search: defocus precalculation, per-phase CTF table, D statistics
     float* freq; float* dfo; float* K1; float* K2; float* ctfD; float* wD;
     double* sdD; double* bestD; double* tmpD; int* topD;
     size_t bytes;
 };
 
-bool xcd_order()
-{
-    static const bool on = [] {
-        const char* e = std::getenv("THX_XCD_ORDER");
-        return e && std::string(e) == "1";
-    }();
-    return on;
-}
-
-// THX_PHASE_LAYOUT (A/B): unset = the device route with the y-pair copy for
-// wide clouds; "ft" = the route without it; "ypair" = every phase on the
-// y-pair copy
-int phase_layout_mode()
-{
-    static const int m = [] {
-        const char* e = std::getenv("THX_PHASE_LAYOUT");
-        if (!e) return 0;
-        const std::string v(e);
-        return v == "ft" ? 1 : v == "ypair" ? 2 : 0;
-    }();
-    return m;
-}
-bool ypair_phases() { return phase_layout_mode() == 2; }
 
 // mLD > 0: the workspace of a CTF search over mLD defocus samples
 Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, int mLD = 0,
@@ -1390,9 +1290,6 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.nAct = k.take<int>(1);
     p.bestR = k.take<double>(nImg);
     p.bestT = k.take<double>(nImg);
-    p.xoKey = k.take<int>(nImg);
-    p.xoAct = k.take<int>(nImg);
-    p.xoN = k.take<int>(1);
     p.localWsBytes = twoD ? thx_local_phase2d_d_workspace(nImg, c.mLR, c.mLT, mLD)
                           : thx_local_phase_workspace(nImg, c.mLR, c.mLT * (mLD > 0 ? mLD : 1),
                                                       nVisit);
@@ -1408,22 +1305,9 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.bestD = k.take<double>(on * nImg);
     p.tmpD = k.take<double>(nd * nImg);
     p.topD = k.take<int>(on * nImg);
-    // THX_BRICKS=1 (A/B builds): the phases gather from a bricked copy of
-    // every class's projectee (thx_volume_bricks, 1x the bytes) unless the
-    // caller gave volCells.  Off by default: 9 % faster on the first,
-    // uniform-like phase but 15 % slower on the later ones, where the
-    // half-complex rows' L1 reuse wins
-#ifndef THX_BRICKS
-#define THX_BRICKS 0
-#endif
-    p.brickStride = thx_volume_bricks_bytes(c.vdim) / sizeof(float);
-    p.bricks = THX_BRICKS && !c.volCells && !twoD ? k.take<float>(p.brickStride * nK) : nullptr;
-    // THX_PHASE_LAYOUT=ypair (A/B): the phases gather from y-pair copies
-    // the y-pair copy: every phase on it (THX_PHASE_LAYOUT=ypair), or the
-    // device route's third kernel for wide clouds (default)
-    p.ypairAll = ypair_phases();
-    const bool yp = !p.bricks && !c.volCells && !twoD && mLD == 0 &&
-                    (p.ypairAll || (phase_layout_mode() == 0 && thx::phase_routed(0, c.pf, nPxl, 0)));
+    // the y-pair copy of every class's projectee for the device route's
+    // pair-form kernel (phases whose LDS boxes do not pay)
+    const bool yp = !c.volCells && !twoD && mLD == 0 && thx::phase_routed(0, c.pf, nPxl, 0);
     p.ypair = yp ? k.take<float>((size_t)4 * (c.vdim / 2 + 1) * c.vdim * c.vdim * nK) : nullptr;
     p.bytes = k.off + 256;
     return p;
@@ -1744,7 +1628,22 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     THX_RET(side_stream(s, &side));
     std::lock_guard<std::mutex> sideLock(side->mu);
     bool sidePending = false;      // a calVari on the side stream not yet joined
+    // every exit, error paths included, leaves no side-stream work behind the
+    // caller's stream: the caller may free or reuse the workspace right after
+    struct SideGuard {
+        SideStream* side;
+        hipStream_t s;
+        bool open = false;         // forked and not yet joined into s
+        ~SideGuard()
+        {
+            if (!open) return;
+            (void)hipEventRecord(side->join, side->s);
+            (void)hipStreamWaitEvent(s, side->join, 0);
+            (void)hipStreamSynchronize(side->s);
+        }
+    } sideGuard{side, s};
     auto fork = [&]() -> int {
+        sideGuard.open = true;
         THX_HIP(hipEventRecord(side->fork, s));
         THX_HIP(hipStreamWaitEvent(side->s, side->fork, 0));
         return THX_OK;
@@ -1757,6 +1656,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     auto join = [&]() -> int {
         if (sidePending) THX_HIP(hipStreamWaitEvent(s, side->join, 0));
         sidePending = false;
+        sideGuard.open = false;
         return THX_OK;
     };
     const unsigned gImg = thx::cdiv(nImg, 4);
@@ -1773,10 +1673,6 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         for (int k = 0; k < nK; k++)
             THX_RET(thx_volume_ypair(vol + 2 * dimSize * k, c.vdim,
                                      p.ypair + 4 * dimSize * k, stream));
-    if (p.bricks)
-        for (int k = 0; k < nK; k++)
-            THX_RET(thx_volume_bricks(vol + 2 * dimSize * k, c.vdim, p.bricks + p.brickStride * k,
-                                      stream));
 
     if (global) {
         // ---- global scan of every class (ExpectRotran + ExpectProject + ExpectGlobal3D
@@ -1862,14 +1758,11 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     const int phase0 = global ? 1 : 0;
     const int nPh = c.converge ? c.maxPhase - phase0 : c.nPhase;
     const int* done = nullptr;
-    // the phases' volume: the caller's cell copy, the bricked copies, or vol
-    const bool ypAll = p.ypair && p.ypairAll;
-    const float* phaseVol = c.volCells ? c.volCells : p.bricks ? p.bricks : ypAll ? p.ypair : vol;
-    const int phaseLayout = c.volCells ? 1 : p.bricks ? 2 : ypAll ? 3 : 0;
-    // the route's y-pair kernel (phaseLayout 0 only)
-    const float* ypRoute = p.ypair && !ypAll ? p.ypair : nullptr;
-    thx_local_sel sel{nullptr, nullptr, clsSel,
-                      (long long)(p.bricks ? p.brickStride / 2 : ypAll ? 2 * dimSize : dimSize)};
+    // the phases' volume: the caller's cell copy or vol (with the y-pair copy
+    // for the device route)
+    const float* phaseVol = c.volCells ? c.volCells : vol;
+    const int phaseLayout = c.volCells ? 1 : 0;
+    thx_local_sel sel{nullptr, nullptr, clsSel, (long long)dimSize};
     if (c.converge) {
         THX_HIP(hipMemsetAsync(p.done, 0, sizeof(int) * nImg, s));
         hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
@@ -1914,30 +1807,16 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                    p.ctfD, stream));
         }
         const int pi = phase - phase0;
-#ifdef THX_DUMP_QUAT
-        // diagnostic build: the clouds the local phase evaluates (after perturb)
-        if (g_quat_sink && pi < 32 && ((g_quat_mask >> pi) & 1u)) {
-            const int slot = __builtin_popcount(g_quat_mask & ((1u << pi) - 1u));
-            THX_HIP(hipMemcpyAsync(g_quat_sink + (size_t)slot * nImg * c.mLR * 4, quat,
-                                   sizeof(double) * nImg * c.mLR * 4, hipMemcpyDeviceToDevice, s));
-        }
-#endif
         // phases past the caller's event pairs run untimed
         hipEvent_t* ev = pi < c.nPhaseEvents ? static_cast<hipEvent_t*>(c.phaseEvents) : nullptr;
-        if (xcd_order() && !c.converge && !twoD) {
-            hipLaunchKernelGGL(k_xcd_order, dim3(1), dim3(1024), 0, s, nImg, c.mLR, quat, p.xoKey,
-                               p.xoAct, p.xoN);
-            THX_LAUNCH_CHECK();
-            sel.active = p.xoAct;
-            sel.nActive = p.xoN;
-        }
         if (twoD) {
             if (ev) THX_HIP(hipEventRecord(ev[2 * pi], s));
             THX_RET(thx::local_phase2d_launch(vol, c.vdim, c.pf, clsSel, quat, 4, c.mLR, trans,
                                               c.mLT, p.pC, pR, pT, dat, cs ? p.ctfD : ctf, sigRcp,
                                               iCol, iRow, nPxl, c.idim, nImg, p.wC, p.wR, p.wT,
                                               p.base, static_cast<float*>(p.localWs), done, s,
-                                              mLD, cs ? cs->pD : nullptr, p.wD));
+                                              mLD, cs ? cs->pD : nullptr, p.wD, sel.active,
+                                              sel.nActive));
             if (ev) THX_HIP(hipEventRecord(ev[2 * pi + 1], s));
         } else
         THX_RET(thx::local_phase_timed(&sel, ev ? ev[2 * pi] : nullptr, ev ? ev[2 * pi + 1] : nullptr,
@@ -1946,7 +1825,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                        dat, cs ? p.ctfD : ctf, sigRcp, iCol, iRow, pxOrder, nOrd,
                                        nPxl, c.idim, nImg, p.wC, p.wR, p.wT, p.base, p.localWs,
                                        p.localWsBytes, stream, mLD, cs ? cs->pD : nullptr, p.wD,
-                                       ypRoute));
+                                       p.ypair, pi < c.nPhaseRoute ? c.phaseRoute + pi : nullptr));
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
                            p.peakR, 0, nullptr, 0, done, rankDiv);
         THX_LAUNCH_CHECK();

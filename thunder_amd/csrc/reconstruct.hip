@@ -413,17 +413,11 @@ int make_plans(Plans& p, int vdim, int N)
 // plans (default), or (p.cols) two column passes + hipFFT's batched 1D
 // transform along x.  Measured at 512^3 (profiles/r03_fft_ab.jsonl): hipFFT
 // 1.48-1.49 ms per transform, the radix-2 column passes 1.64-1.81 ms, so the
-// 3D plans stay; THX_RECON_FFT=columns selects the column passes (A/B).
+// 3D plans stay (thx_fft3d's method 2 runs the column passes).
 // C is overwritten either way (hipFFT's out-of-place C2R may too).
 bool use_cols(const Plans& p, int method = 0)
 {
-    if (method == 1) return false;
-    if (method == 2) return p.cols;
-    static const bool on = [] {
-        const char* e = std::getenv("THX_RECON_FFT");
-        return e && std::string(e) == "columns";
-    }();
-    return p.cols && on;
+    return method == 2 && p.cols;
 }
 
 int col_pass(const Plans& p, float2* C, int vdim, bool inv, bool zAxis, hipStream_t s)
@@ -484,6 +478,7 @@ struct PlanEntry {
     std::mutex mu;
     Plans p;
     bool made = false;
+    unsigned* bits = nullptr;   // pinned host word: the balancing loop's read-back
 };
 
 struct PlanCache {
@@ -515,6 +510,7 @@ int cached_plans(int vdim, int N, hipStream_t s, PlanEntry** out,
     if (!e->made) {
         const int st = make_plans(e->p, vdim, N);
         if (st != THX_OK) return st;
+        THX_HIP(hipHostMalloc(reinterpret_cast<void**>(&e->bits), sizeof(unsigned), 0));
         e->made = true;
     }
     *out = e;
@@ -634,8 +630,7 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_kernel_octant, g, b, 0, s, oct, vdim, tab, nf, scaleBw);
         THX_LAUNCH_CHECK();
-        unsigned* bits = nullptr;
-        THX_HIP(hipHostMalloc(reinterpret_cast<void**>(&bits), sizeof(unsigned), 0));
+        unsigned* bits = pe->bits;   // the entry's pinned word (no allocation per solve)
         for (m = 0; m < 30; m++) {                                // MAX_N_ITER_BALANCE
             THX_RET(c2r3d(pl, C, rl, vdim, s));
             hipLaunchKernelGGL(k_kernel_mul, gSlab, bSlab, 0, s, rl, vdim, oct, mVdim);
@@ -657,7 +652,6 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
                 break;
             }
         }
-        (void)hipHostFree(bits);
     } else {
         hipLaunchKernelGGL(k_w_from_t, g, b, 0, s, W, T, vdim, r2);
         THX_LAUNCH_CHECK();

@@ -494,19 +494,6 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
     }
 
     // ------------------------------------------------------------ epilogue
-#ifdef THX_SCAN_NOEPI      // diagnostic: main loop only
-    {
-        float t = 0.f;
-#pragma unroll
-        for (int a = 0; a < 2; a++)
-#pragma unroll
-            for (int f = 0; f < NF; f++)
-#pragma unroll
-                for (int j = 0; j < 16; j++) t += acc[a][f][j];
-        pM[(size_t)rb * nImgPad + l0 + lane] = t;
-        return;
-    }
-#endif
     float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][64]  A_l + B[l][r]
     float* sInv = sBias + ROT_TILE * 64;               // [64]           2^-e_l
     float* sMax = sInv + ROT_TILE * 64;                // [8 waves][64 rows]

@@ -29,10 +29,11 @@
 namespace thx {
 int launch_local_weights(const float* dvp, int nR, int nT, const double* pC, const double* pR,
                          const double* pT, float* wC, float* wR, float* wT, float* baseL, int nImg,
-                         hipStream_t s);
+                         hipStream_t s, const int* act = nullptr, const int* nAct = nullptr);
 int launch_local_weights_d(const float* dvp, int nR, int nT, int nD, const double* pC,
                            const double* pR, const double* pT, const double* pD, float* wC,
-                           float* wR, float* wT, float* wD, float* baseL, int nImg, hipStream_t s);
+                           float* wR, float* wT, float* wD, float* baseL, int nImg, hipStream_t s,
+                           const int* act = nullptr, const int* nAct = nullptr);
 }
 
 namespace {
@@ -282,8 +283,10 @@ int local_phase2d_launch(const float* vol, int vdim, int pf, const int* cls, con
                          const float* sigRcp, const int* iCol, const int* iRow, int nPxl, int idim,
                          int nImg, float* wC, float* wR, float* wT, float* baseL, float* dvp,
                          const int* done, hipStream_t s, int nD = 0, const double* pD = nullptr,
-                         float* wD = nullptr)
+                         float* wD = nullptr, const int* act = nullptr, const int* nAct = nullptr)
 {
+    // act / nAct (the driver's active list, with done): the weights of the
+    // images still running only, as the 3D phase
     const long nVox = (long)(vdim / 2 + 1) * vdim;
     const size_t lds = nVox <= L2D_LDS_VOX ? (size_t)nVox * sizeof(float2) : 0;
     hipLaunchKernelGGL(k_local2d, dim3(nImg), dim3(L2D_THREADS), lds, s,
@@ -293,8 +296,8 @@ int local_phase2d_launch(const float* vol, int vdim, int pf, const int* cls, con
     THX_LAUNCH_CHECK();
     if (nD > 0)
         return launch_local_weights_d(dvp, nR, nT, nD, pC, pR, pT, pD, wC, wR, wT, wD, baseL, nImg,
-                                      s);
-    return launch_local_weights(dvp, nR, nT, pC, pR, pT, wC, wR, wT, baseL, nImg, s);
+                                      s, act, nAct);
+    return launch_local_weights(dvp, nR, nT, pC, pR, pT, wC, wR, wT, baseL, nImg, s, act, nAct);
 }
 }  // namespace thx
 

@@ -43,7 +43,9 @@ class ExpectCfg(ctypes.Structure):
                 # ABI 4
                 ("volCells", ctypes.c_void_p),
                 # ABI 5
-                ("nPhaseEvents", ctypes.c_int)]
+                ("nPhaseEvents", ctypes.c_int),
+                # ABI 6
+                ("phaseRoute", ctypes.c_void_p), ("nPhaseRoute", ctypes.c_int)]
 
 
 class CtfSearchCfg(ctypes.Structure):
@@ -121,7 +123,7 @@ class Expectation:
                              k_floor, s_floor, trans_s, trans_m, seed, int(bool(shuffle)),
                              nK, self.search, int(bool(converge)), min_phase, max_phase,
                              {"top": 0, "acg": 1}[perturb_mean], acg_iters, perturb_large,
-                             int(bool(large_first)), None, None, 0)
+                             int(bool(large_first)), None, None, 0, None, 0)
         if self.two_d:
             cells = None
         if isinstance(cells, str):
@@ -140,6 +142,15 @@ class Expectation:
             self.cfg.volCells = cells.data_ptr()
         self.mLR, self.mLT, self.nK = mLR, mLT, nK
         self.cs = CtfSearchCfg(mLD, ctf_refine_s, perturb_ctf, None, None, None)
+
+    def track_routes(self, n_phase):
+        """Record the device route's kernel choice for the next runs' first
+        n_phase phases (thx_expect_cfg.phaseRoute): returns the device int32
+        tensor (0 staged, 1 box-less, 2 y-pair, -1 not routed, -2 not run)."""
+        self.routes = torch.full((n_phase,), -2, dtype=torch.int32, device=self.dev)
+        self.cfg.phaseRoute = self.routes.data_ptr()
+        self.cfg.nPhaseRoute = n_phase
+        return self.routes
 
     def workspace_bytes(self, nImg):
         if self.two_d and self.search == 2:

@@ -45,7 +45,9 @@ class RoundEnd:
             raise ValueError("transport: 'rccl' or 'torch'")
         self.world, self.rank, self.transport = world, rank, transport
         self.device = device
-        self.hemi_groups = [dist.new_group([r for r in range(world) if r % 2 == h]) for h in (0, 1)]
+        # (world 1: hemisphere B has no rank, and no group)
+        self.hemi_groups = [dist.new_group([r for r in range(world) if r % 2 == h])
+                            if h < world else None for h in (0, 1)]
         self.lead_group = dist.new_group(list(leads(world))) if world > 1 else None
         self.hemi_comm = self.lead_comm = None
         if transport == "rccl":

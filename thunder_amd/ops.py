@@ -288,21 +288,17 @@ def volume_cells(vol):
     return out
 
 
-def _layout(vol, cells, bricks, ypair=None, pair=False):
-    """(volLayout, volume argument) of thx_local_phase for the given copies
-    (ypair with pair=True: the two-lanes-per-sample form, volLayout 4)."""
-    if sum(x is not None for x in (cells, bricks, ypair)) > 1:
-        raise ValueError("cells, bricks and ypair are alternatives")
+def _layout(vol, cells, ypair=None):
+    """(volLayout, volume argument) of thx_local_phase for the given copy:
+    0 half-complex, 1 cells, 2 y-pair (pair form)."""
+    if cells is not None and ypair is not None:
+        raise ValueError("cells and ypair are alternatives")
     if ypair is not None:
         _req(ypair, torch.complex64, tuple(vol.shape) + (2,), "ypair")
-        return (4 if pair else 3), ypair
+        return 2, ypair
     if cells is not None:
         _req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
         return 1, cells
-    if bricks is not None:
-        vdim = _vol_dim(vol)
-        _req(bricks, torch.complex64, (lib().thx_volume_bricks_bytes(vdim) // 8,), "bricks")
-        return 2, bricks
     return 0, vol
 
 
@@ -316,24 +312,17 @@ def volume_ypair(vol):
     return out
 
 
-def volume_bricks(vol):
-    """Bricked copy (4 x 2 x 2 voxels per 128-B brick, the same bytes as vol):
-    the trilinear rows of a sample share cache lines (thx_volume_bricks)."""
-    vdim = _vol_dim(vol)
-    out = torch.empty(lib().thx_volume_bricks_bytes(vdim) // 8, dtype=torch.complex64,
-                      device=vol.device)
-    check(lib().thx_volume_bricks(_ptr(vol), vdim, _ptr(out), _stream(vol.device)),
-          "thx_volume_bricks")
-    return out
-
-
 def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False, cells=None,
-                tiled=True, bricks=None, ypair=None, pair=False):
-    """cells / bricks: optional thx_volume_cells / thx_volume_bricks copy of
-    vol (used for the gathers and the staged boxes).
-    tiled: visit pixels in px.order (LDS-staged neighbourhoods) instead of set order."""
+                tiled=True, ypair=None, routed=False):
+    """cells / ypair: optional thx_volume_cells / thx_volume_ypair copy of vol.
+    tiled: visit pixels in px.order (LDS-staged neighbourhoods) instead of set order.
+    routed: the device route of thx_local_phase_routed (vol half-complex, ypair
+    optional, pxOrder), which then also returns the kernel it picked (0 staged,
+    1 box-less, 2 y-pair, -1 not routed) as a sixth value."""
     vdim = _vol_dim(vol)
-    layout, src = _layout(vol, cells, bricks, ypair, pair)
+    layout, src = (0, vol) if routed else _layout(vol, cells, ypair)
+    if routed and (cells is not None or not tiled):
+        raise ValueError("the routed phase takes the half-complex volume and the tile order")
     nImg, nPxl = _images(dat, ctf_, sig)
     if nPxl != px.n:
         raise ValueError("pixel set / image size mismatch")
@@ -344,15 +333,30 @@ def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False
     _req(pC, torch.float64, (nImg,), "pC")
     _req(pR, torch.float64, (nImg, nR), "pR")
     _req(pT, torch.float64, (nImg, nT), "pT")
+    if routed and ypair is not None:
+        _req(ypair, torch.complex64, tuple(vol.shape) + (2,), "ypair")
     wC = torch.empty(nImg, dtype=torch.float32, device=dev)
     wR = torch.empty(nImg, nR, dtype=torch.float32, device=dev)
     wT = torch.empty(nImg, nT, dtype=torch.float32, device=dev)
     base = torch.empty(nImg, dtype=torch.float32, device=dev)
     d = torch.empty(nImg, nR, nT, dtype=torch.float32, device=dev) if want_dvp else None
+    route = torch.full((1,), -2, dtype=torch.int32, device=dev)
     ws = workspace(lib().thx_local_phase_workspace(min(nImg, 65535), nR, nT,
                                                    len(px.order) if tiled else nPxl), dev)
     for l0 in range(0, nImg, 65535):
         nb = min(65535, nImg - l0)
+        if routed:
+            check(lib().thx_local_phase_routed(None, _ptr(vol), _ptr(ypair) if ypair is not None else None,
+                                               vdim, px.pf, _ptr(quat[l0:]), nR, _ptr(trans[l0:]), nT,
+                                               _ptr(pC[l0:]), _ptr(pR[l0:]), _ptr(pT[l0:]),
+                                               _ptr(dat[l0:]), _ptr(ctf_[l0:]), _ptr(sig[l0:]),
+                                               _ptr(px.d_iCol), _ptr(px.d_iRow), _ptr(px.d_order),
+                                               len(px.order), nPxl, px.idim, nb, _ptr(wC[l0:]),
+                                               _ptr(wR[l0:]), _ptr(wT[l0:]), _ptr(base[l0:]),
+                                               _ptr(d[l0:]) if d is not None else None, _ptr(route),
+                                               _ptr(ws), ws.numel(), _stream(dev)),
+                  "thx_local_phase_routed")
+            continue
         check(lib().thx_local_phase(_ptr(src), layout, vdim, px.pf, _ptr(quat[l0:]), nR,
                                     _ptr(trans[l0:]),
                                     nT, _ptr(pC[l0:]), _ptr(pR[l0:]), _ptr(pT[l0:]), _ptr(dat[l0:]),
@@ -362,15 +366,17 @@ def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False
                                     _ptr(wR[l0:]), _ptr(wT[l0:]), _ptr(base[l0:]),
                                     _ptr(d[l0:]) if d is not None else None, _ptr(ws),
                                     ws.numel(), _stream(dev)), "thx_local_phase")
+    if routed:
+        return wC, wR, wT, base, d, int(route.item())
     return wC, wR, wT, base, d
 
 
 def local_phase_d(vol, quat, trans, pC, pR, pT, pD, dat, ctfD, sig, px, want_dvp=False,
-                  cells=None, tiled=True, bricks=None):
+                  cells=None, tiled=True):
     """CTF-search phase (thx_local_phase_d): ctfD [nImg, nD, nPxl], pD [nImg, nD];
     returns wC, wR, wT, wD, baseL, dvp [nImg, nR, nT, nD] (or None)."""
     vdim = _vol_dim(vol)
-    layout, src = _layout(vol, cells, bricks)
+    layout, src = _layout(vol, cells)
     nImg, nPxl = dat.shape
     nR, nT, nD = quat.shape[1], trans.shape[1], pD.shape[1]
     dev = dat.device

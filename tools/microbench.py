@@ -53,7 +53,7 @@ def main():
     p.add_argument("--ru", type=int, default=24)
     p.add_argument("--images", type=int, default=4096)
     p.add_argument("--cells", type=int, default=0)
-    p.add_argument("--bricks", type=int, default=0, help="local: gather from ops.volume_bricks(vol)")
+    p.add_argument("--ypair", type=int, default=0, help="local: gather from ops.volume_ypair(vol)")
     p.add_argument("--algo", type=int, default=2)
     p.add_argument("--nr", type=int, default=2000)
     p.add_argument("--mreco", type=int, default=100)
@@ -67,10 +67,8 @@ def main():
     p.add_argument("--spread", type=float, default=3.0,
                    help="local: rotation spread (deg) of each image's cloud, 0 = uniform")
     p.add_argument("--clouds", default="",
-                   help="local: npz of bench clouds (tools/dump_clouds.py) instead of synthetic ones")
+                   help="local: npz of quaternion clouds (quat_k<k>: [images, 125, 4]) instead of synthetic ones")
     p.add_argument("--k", type=int, default=0, help="local: phase of --clouds (quat_k<k>)")
-    p.add_argument("--counts", type=int, default=0,
-                   help="local: wave-step counts of a THX_STEP_COUNT build (thx_debug_step_counts)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     N, pf = a.box, 2
@@ -96,36 +94,25 @@ def main():
         pR = torch.full((a.images, mR), 1.0 / mR, dtype=torch.float64, device=dev)
         pT = torch.full((a.images, mT), 1.0 / mT, dtype=torch.float64, device=dev)
         cells = ops.volume_cells(vol) if a.cells else None
-        bricks = ops.volume_bricks(vol) if a.bricks else None
-        out.update(cells=a.cells, bricks=a.bricks)
+        ypair = ops.volume_ypair(vol) if a.ypair else None
+        out.update(cells=a.cells, ypair=a.ypair)
         if a.nd > 0:
             dD = torch.as_tensor(1 + rng.standard_normal((a.images, a.nd)) * 0.01, device=dev)
             ctfD = (ctf[:, None, :] * (1 + 0.01 * torch.arange(a.nd, device=dev)[None, :, None]))
             ctfD = ctfD.float().contiguous()
             pD = torch.full((a.images, a.nd), 1.0 / a.nd, dtype=torch.float64, device=dev)
             sec = timed_events(lambda: ops.local_phase_d(vol, quat, trans, pC, pR, pT, pD, dat, ctfD,
-                                                         sig, px, cells=cells, bricks=bricks),
+                                                         sig, px, cells=cells),
                                a.reps, st)
             out["nd"] = a.nd
             del dD
         else:
             sec = timed_events(lambda: ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig,
                                                        px, cells=cells, tiled=bool(a.tiled),
-                                                       bricks=bricks),
+                                                       ypair=ypair),
                                a.reps, st)
         if a.stats:
             out.update(box_stats(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px))
-        if a.counts:
-            import ctypes
-            from thunder_amd._lib import lib
-            c = (ctypes.c_ulonglong * 4)()
-            lib().thx_debug_step_counts(c, 1)
-            ops.local_phase(vol, quat, trans, pC, pR, pT, dat, ctf, sig, px, cells=cells,
-                            bricks=bricks)
-            torch.cuda.synchronize()
-            lib().thx_debug_step_counts(c, 1)
-            tot = max(1, sum(c))
-            out["wave_steps"] = dict(zip(("shared", "unused", "direct", "pad"), [x / tot for x in c]))
         out.update(ms=sec * 1e3, us_per_image_phase=sec / a.images * 1e6,
                    algo_GBps=a.images * (64.0 * mR * px.n + 16.0 * px.n) / sec / 1e9)
     elif a.what == "scan":
