@@ -549,6 +549,37 @@ size_t thx_fft3d_workspace(int vdim);
 int thx_fft3d(float* C, float* rl, int vdim, int inverse, int method, void* workspace,
               size_t wsBytes, thx_stream_t stream);
 
+/* ------------------------------------------------- f1 / a3 / a10: symmetry ---
+ * thx_symmetry (host) -- the non-identity elements of a point group, as
+ *   Symmetry(const char*) builds them (src/Geometry/Symmetry.cpp:104-278,
+ *   SymmetryFunctions.cpp:13-152): "C<n>", "D<n>", "T", "O", "I1".."I4";
+ *   R[cap][3][3] row-major, quat[cap][4] (quaternion(dvec4&, dmat33&)); cap 0
+ *   only counts.  *nSymElem = group order - 1 (C1: 0).
+ * thx_symmetrize_ft -- SYMMETRIZE_FT (include/Geometry/Transformation.h:
+ *   170-194) of a half-complex volume (complex: F, 2 floats per voxel; real: T):
+ *   dst(v) = src(v) + sum_i [|R_i v|^2 < r^2] trilinear(src, R_i v); R
+ *   (device) nSymElem x 9 row-major; dst != src.
+ * thx_prepare_tf -- Reconstructor::prepareTF's device part (src/Reconstructor.cpp:
+ *   1056-1091, 2455-2479, 2676-2690; GPU PrepareTF, gpu/src/cuthunder.cu:6176):
+ *   F, T *= 1 / T[0], then both symmetrized with r = maxRadius pf + 1;
+ *   nSymElem 0 normalises only.  workspace >= thx_prepare_tf_workspace(vdim).
+ * thx_pf_symmetrise -- Particle::symmetrise (src/Particle.cpp:2445-2471) of
+ *   nImg clouds quat[nImg][mR][4] in place: each particle -> the symmetry
+ *   counterpart closest to the anchor (symmetryCounterpart, Symmetry.cpp:
+ *   309-335); anchorMode 0: (1, 0, 0, 0) (Particle::reset, the global sample
+ *   set); 1: anchor[nImg][4] (the perturbation mean); 2: a particle of the
+ *   cloud drawn with the counter RNG (seed, streamId) (calVari).  symQuat
+ *   (device) nSymElem x 4. */
+int thx_symmetry(const char* sym, int cap, double* R, double* quat, int* nSymElem);
+int thx_symmetrize_ft(const float* src, float* dst, int isComplex, int vdim, const double* R,
+                      int nSymElem, double r, thx_stream_t stream);
+size_t thx_prepare_tf_workspace(int vdim);
+int thx_prepare_tf(float* F, float* T, int vdim, const double* R, int nSymElem, int maxRadius,
+                   int pf, void* workspace, size_t wsBytes, thx_stream_t stream);
+int thx_pf_symmetrise(int nImg, int mR, double* quat, int anchorMode, const double* anchor,
+                      const double* symQuat, int nSymElem, unsigned long long seed,
+                      unsigned streamId, thx_stream_t stream);
+
 /* ----------------------------------------------------------------- a14 ---
  * Fourier shell correlation FSC(vec&, const Volume& A, const Volume& B)
  * (src/Functions/Spectrum.cpp:302-337) of two half-complex volumes of real
@@ -636,6 +667,11 @@ typedef struct thx_expect_cfg {
                                  picked in each phase (as thx_local_phase_routed's route: 0
                                  staged, 1 box-less, 2 y-pair, -1 not routed); NULL: none */
     int nPhaseRoute;
+    const double* symQuat;    /* device nSymElem x 4 (thx_symmetry), 3D: Particle::symmetrise
+                                 after every perturbation (anchor: the perturbation mean) and
+                                 before every calVari (anchor: a drawn particle), as the
+                                 reference does for non-C1 groups; NULL / 0: C1 */
+    int nSymElem;
 } thx_expect_cfg;
 
 /* nOrd: length of pxOrder (<= 0 when pxOrder is NULL). */

@@ -66,7 +66,7 @@ def _phase_vs_oracle(orc, vol, px, pxh, N, pf, quat, trans, dat, ctf, sig, cells
     out = ops.local_phase(vol, T(quat), T(trans), T(np.ones(nImg)), T(pR), T(pT), dat, ctf, sig, px,
                           want_dvp=True, cells=cells, ypair=ypair, routed=routed)
     wC, wR, wT, base, d = out[:5]
-    d, wR, base = d.cpu().numpy(), wR.cpu().numpy(), base.cpu().numpy()
+    d, wR, wT, base = d.cpu().numpy(), wR.cpu().numpy(), wT.cpu().numpy(), base.cpu().numpy()
     vnp = vol.cpu().numpy()
     for l in range(nImg):
         rC, rR, rT, rb, rd = orc.local_phase(vnp, pf * N, pf, quat[l], trans[l], 1.0, pR[l], pT[l],

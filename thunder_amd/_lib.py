@@ -116,6 +116,12 @@ SIGNATURES = {
     "thx_reconstruct_workspace": (_c_size, [_c_int, _c_int]),
     "thx_reconstruct": (_c_int, [_p, _p, _c_int, _c_int, _c_float, _c_float, _c_int, _c_int, _c_int, _p,
                                  _c_int, _c_int, _p, _p, _p, _p, _p, _c_size, _p]),
+    "thx_symmetry": (_c_int, [ctypes.c_char_p, _c_int, _p, _p, _p]),
+    "thx_symmetrize_ft": (_c_int, [_p, _p, _c_int, _c_int, _p, _c_int, ctypes.c_double, _p]),
+    "thx_prepare_tf_workspace": (_c_size, [_c_int]),
+    "thx_prepare_tf": (_c_int, [_p, _p, _c_int, _p, _c_int, _c_int, _c_int, _p, _c_size, _p]),
+    "thx_pf_symmetrise": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _p, _c_int, ctypes.c_ulonglong,
+                                   ctypes.c_uint, _p]),
     "thx_fsc_workspace": (_c_size, [_c_int]),
     "thx_fsc": (_c_int, [_p, _p, _c_int, _c_int, _p, _p, _c_size, _p]),
     "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int, _c_int]),

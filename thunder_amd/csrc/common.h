@@ -40,6 +40,13 @@ void set_error(const char* fmt, ...);
 
 #define THX_LAUNCH_CHECK() THX_HIP(hipGetLastError())
 
+// propagate a THX_* status
+#define THX_RET(call)                  \
+    do {                               \
+        int st_ = (call);              \
+        if (st_ != THX_OK) return st_; \
+    } while (0)
+
 // Raise a kernel's dynamic-LDS limit once per device (the attribute is per
 // device; a host may drive several GPUs from one process).  `done` is the
 // kernel's own device bit mask.

@@ -61,12 +61,6 @@ struct DBuf {
         }                                                                      \
     } while (0)
 
-#define THX_RET(call)                  \
-    do {                               \
-        int st_ = (call);              \
-        if (st_ != THX_OK) return st_; \
-    } while (0)
-
 // Runs fn(slot, device, l0, l1) for a contiguous image block per device, one
 // host thread per device (each with its device current); the first failure's
 // status and message come back to the caller's thread.

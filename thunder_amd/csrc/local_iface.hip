@@ -65,12 +65,6 @@ int dalloc(T** p, size_t n)
     return THX_OK;
 }
 
-#define THX_RET(call)                  \
-    do {                               \
-        int st_ = (call);              \
-        if (st_ != THX_OK) return st_; \
-    } while (0)
-
 __global__ void k_rot2_from_quat(const double* __restrict__ quat, int n, double* __restrict__ rot2)
 {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;

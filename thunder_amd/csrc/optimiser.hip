@@ -31,6 +31,7 @@
 #include <utility>
 
 #include "common.h"
+#include "symmetry.h"
 
 
 namespace thx {
@@ -53,6 +54,9 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       const double* pD = nullptr, float* wD = nullptr,
                       const float* ypair = nullptr, int* routeOut = nullptr);
 bool phase_routed(int volLayout, int pf, int nPxl, int nD);
+int pf_symmetrise_launch(int nImg, int mR, double* quat, int anchorMode, const double* anchor,
+                         const double* symQ, int nSym, uint64_t seed, uint32_t stream,
+                         const int* done, hipStream_t s);
 }
 
 namespace {
@@ -738,7 +742,9 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
                                                     uint64_t seed, uint32_t stream,
                                                     int meanMode,
                                                     const double* __restrict__ meanQ,
-                                                    const int* __restrict__ done)
+                                                    const int* __restrict__ done,
+                                                    const double* __restrict__ symQ = nullptr,
+                                                    int nSym = 0)
 {
     const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
     const int lane = threadIdx.x % GROUP;
@@ -765,7 +771,10 @@ __global__ void __launch_bounds__(256) k_pf_perturb(int nImg, int mR, int mT,
         qmul(d, a, b);                 // pert * .
         qmul(mean, b, c);              // mean * .
         const double cn = sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2] + c[3] * c[3]);
-        for (int k = 0; k < 4; k++) Q[4 * i + k] = c[k] / cn;
+        for (int k = 0; k < 4; k++) c[k] /= cn;
+        // symmetrise(&mean) (src/Particle.cpp:1234): the counterpart nearest the mean
+        if (nSym) thx::sym_counterpart(c, mean, symQ, nSym);
+        for (int k = 0; k < 4; k++) Q[4 * i + k] = c[k];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -1569,12 +1578,6 @@ extern "C" size_t thx_expectation_ctf_workspace(const thx_expect_cfg* cfg,
     return plan(nullptr, *cfg, nImg, nPxl, nOrd > 0 ? nOrd : nPxl, cs->mLD).bytes;
 }
 
-#define THX_RET(call)                  \
-    do {                               \
-        int st_ = (call);              \
-        if (st_ != THX_OK) return st_; \
-    } while (0)
-
 // cs != NULL: SEARCH_TYPE_CTF (searchType 2) -- a local search whose phases
 // also sample nD = cs->mLD defocus factors per image (src/Optimiser.cpp:
 // 1183-1616 with the _searchType == SEARCH_TYPE_CTF branches).
@@ -1621,6 +1624,8 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     if (nImg == 0) return THX_OK;
     THX_CHECK_ARG(!pxOrder || (nOrd > 0 && nOrd % 16 == 0),
                   "thx_expectation: nOrd must be a positive multiple of 16");
+    THX_CHECK_ARG(c.nSymElem >= 0 && c.nSymElem <= thx::SYM_MAX && (c.nSymElem == 0 || c.symQuat),
+                  "thx_expectation: nSymElem 0 .. 64 with symQuat");
     const Plan p = plan(workspace, c, nImg, nPxl, pxOrder ? nOrd : nPxl, mLD, twoD);
     THX_CHECK_ARG(workspace && p.bytes <= wsBytes, "thx_expectation: workspace too small");
     hipStream_t s = thx::as_stream(stream);
@@ -1663,6 +1668,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     const unsigned gPf = thx::cdiv(nImg * GROUP, 256);
     const unsigned gOne = thx::cdiv(nImg, 256);
     const int nK = c.nK;
+    const int nSym = twoD ? 0 : c.nSymElem;     // point-group symmetry: MODE_3D only
     // one class's projectee: a half-complex volume, or a half-complex image in 2D
     const size_t dimSize = (size_t)(c.vdim / 2 + 1) * c.vdim * (twoD ? 1 : c.vdim);
     const int rankDiv = twoD ? 2 : 8;      // setPeakFactor(PAR_R): PEAK_FACTOR_BASE (^3 in 3D)
@@ -1723,7 +1729,11 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                            p.anc, trans, nullptr);
         THX_LAUNCH_CHECK();
         // calVari with the scan floors, beside phase 1's inferACG mean (both only
-        // read the reseeded cloud)
+        // read the reseeded cloud); its symmetrise (src/Particle.cpp:1028-1036)
+        // first, on the stream both read from
+        if (!twoD)
+            THX_RET(thx::pf_symmetrise_launch(nImg, c.mLR, quat, 2, nullptr, c.symQuat, nSym, c.seed,
+                                              1002u, nullptr, s));
         THX_RET(fork());
         hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, side->s,
                            nImg, c.mLR, quat, c.mLT, trans, c.kMin, c.sMin, p.kv, p.sv, nullptr);
@@ -1733,6 +1743,9 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         // ---- local search from the caller's particle state: its spreads
         // (calVari on the given cloud) and, for the top-particle mean, calRank1st
         if (nK == 1 && !cls) THX_HIP(hipMemsetAsync(clsD, 0, sizeof(int) * nImg, s));
+        if (!twoD)
+            THX_RET(thx::pf_symmetrise_launch(nImg, c.mLR, quat, 2, nullptr, c.symQuat, nSym, c.seed,
+                                              1002u, nullptr, s));
         hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg,
                            c.mLR, quat, c.mLT, trans, 0.0, 0.0, p.kv, p.sv, nullptr);
         THX_LAUNCH_CHECK();
@@ -1791,7 +1804,8 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
                                trans, pR, pT, p.topQ, p.kv, p.sv,
                                large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
-                               c.seed, (uint32_t)(2000 + phase), c.perturbMean, p.meanQ, done);
+                               c.seed, (uint32_t)(2000 + phase), c.perturbMean, p.meanQ, done,
+                               c.symQuat, nSym);
             THX_LAUNCH_CHECK();
         }
         if (cs) {
@@ -1829,7 +1843,12 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
                            p.peakR, 0, nullptr, 0, done, rankDiv);
         THX_LAUNCH_CHECK();
-        // the pre-resample cloud, kept for calVari and the gathers
+        // calVari's symmetrise (a drawn particle as the anchor) on the cloud the
+        // resampling gathers from, then the pre-resample cloud, kept for calVari
+        // and the gathers
+        if (!twoD)
+            THX_RET(thx::pf_symmetrise_launch(nImg, c.mLR, quat, 2, nullptr, c.symQuat, nSym, c.seed,
+                                              (uint32_t)(5000 + phase), done, s));
         THX_HIP(hipMemcpyAsync(p.tmpQ, quat, sizeof(double) * nImg * c.mLR * 4,
                                hipMemcpyDeviceToDevice, s));
         THX_HIP(hipMemcpyAsync(p.tmpT, trans, sizeof(double) * nImg * c.mLT * 2,

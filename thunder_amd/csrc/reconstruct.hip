@@ -51,12 +51,6 @@
         }                                                                      \
     } while (0)
 
-#define THX_RET(call)                  \
-    do {                               \
-        int st_ = (call);              \
-        if (st_ != THX_OK) return st_; \
-    } while (0)
-
 namespace {
 
 constexpr int TAB_N = 100000;   // _kernelRL.init(MKB_RL_R2, 0, 1, 1e5) (src/Reconstructor.cpp:77-88)

@@ -45,7 +45,8 @@ class ExpectCfg(ctypes.Structure):
                 # ABI 5
                 ("nPhaseEvents", ctypes.c_int),
                 # ABI 6
-                ("phaseRoute", ctypes.c_void_p), ("nPhaseRoute", ctypes.c_int)]
+                ("phaseRoute", ctypes.c_void_p), ("nPhaseRoute", ctypes.c_int),
+                ("symQuat", ctypes.c_void_p), ("nSymElem", ctypes.c_int)]
 
 
 class CtfSearchCfg(ctypes.Structure):
@@ -75,6 +76,8 @@ class Expectation:
     cells: ops.volume_cells(vol) (K = 1): the phases gather one 64-B cell per
            sample (thx_expect_cfg.volCells); "auto" (default) builds it for
            large boxes at full resolution (ring radius >= 300 voxels), None: off.
+    sym: point group ("C4", "D2", ... ; MODE_3D): Particle::symmetrise in the
+         particle filter (thx_expect_cfg.symQuat / nSymElem).
     mode: "3d" (MODE_3D) or "2d" (MODE_2D, thx_expectation2d): vol holds
           half-complex class images [vdim, vdim/2+1] or [nK, vdim, vdim/2+1],
           rotations are rows (cos, sin, 0, 0) (gset from
@@ -85,7 +88,7 @@ class Expectation:
                  trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7, shuffle=True,
                  search="global", converge=False, perturb_mean="acg", acg_iters=100,
                  perturb_large=2.0, large_first=False, min_phase=None, max_phase=None,
-                 mLD=9, ctf_refine_s=0.01, perturb_ctf=0.5, cells="auto", mode="3d"):
+                 mLD=9, ctf_refine_s=0.01, perturb_ctf=0.5, cells="auto", mode="3d", sym=None):
         dev = vol.device
         self.vol, self.px, self.dev = vol, px, dev
         if mode not in ("3d", "2d"):
@@ -123,7 +126,7 @@ class Expectation:
                              k_floor, s_floor, trans_s, trans_m, seed, int(bool(shuffle)),
                              nK, self.search, int(bool(converge)), min_phase, max_phase,
                              {"top": 0, "acg": 1}[perturb_mean], acg_iters, perturb_large,
-                             int(bool(large_first)), None, None, 0, None, 0)
+                             int(bool(large_first)), None, None, 0, None, 0, None, 0)
         if self.two_d:
             cells = None
         if isinstance(cells, str):
@@ -140,6 +143,16 @@ class Expectation:
                 raise ValueError("cells: single-class projectee only")
             ops._req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
             self.cfg.volCells = cells.data_ptr()
+        # point-group symmetry (MODE_3D): the particle clouds are symmetrised
+        # like Particle's (thx_expect_cfg.symQuat); the sample set gset should
+        # come from ops.global_sample_set(..., sym=sym)
+        self.symQ = None
+        if sym is not None and not self.two_d:
+            _, q = ops.symmetry(sym)
+            if len(q):
+                self.symQ = torch.as_tensor(q, device=dev).contiguous()
+                self.cfg.symQuat = self.symQ.data_ptr()
+                self.cfg.nSymElem = len(q)
         self.mLR, self.mLT, self.nK = mLR, mLT, nK
         self.cs = CtfSearchCfg(mLD, ctf_refine_s, perturb_ctf, None, None, None)
 

@@ -158,8 +158,12 @@ def global_sample_sizes(mS, trans_s=10.0, trans_search_factor=0.25, n_sym_elem=0
     return tuple(o.value for o in out)
 
 
-def global_sample_set(nR, nT, trans_s, seed, device):
-    """Particle::reset's global set on device: (quat [nR,4], trans [nT,2], pR, pT)."""
+def global_sample_set(nR, nT, trans_s, seed, device, sym=None):
+    """Particle::reset's global set on device: (quat [nR,4], trans [nT,2], pR, pT);
+    sym (a point-group name, non-C1): the rotations symmetrised towards the
+    identity (Particle::reset's symmetrise(), src/Particle.cpp:168), the
+    asymmetric unit the scan then covers (nR from global_sample_sizes with
+    the group's n_sym_elem)."""
     quat = torch.empty(nR, 4, dtype=torch.float64, device=device)
     trans = torch.empty(nT, 2, dtype=torch.float64, device=device)
     pR = torch.empty(nR, dtype=torch.float64, device=device)
@@ -167,6 +171,10 @@ def global_sample_set(nR, nT, trans_s, seed, device):
     check(lib().thx_global_sample_set(nR, nT, float(trans_s), seed, _ptr(quat), _ptr(trans),
                                       _ptr(pR), _ptr(pT), _stream(quat.device)),
           "thx_global_sample_set")
+    if sym is not None:
+        _, symQ = symmetry(sym)
+        if len(symQ):
+            pf_symmetrise(quat.view(1, nR, 4), symQ)
     return quat, trans, pR, pT
 
 
@@ -684,6 +692,60 @@ def insert2d(hm, dat, ctf_, rot, trans, offS, w, px, nc=None):
 
 
 # ------------------------------------------------------------------- f1
+# --------------------------------------------------------- point groups
+def symmetry(name):
+    """thx_symmetry: (R [n, 3, 3] row-major, quat [n, 4]) float64 numpy of the
+    non-identity elements of point group `name` ("C4", "D2", "T", "O", "I1"..)."""
+    n = ctypes.c_int(0)
+    check(lib().thx_symmetry(name.encode(), 0, None, None, ctypes.byref(n)), "thx_symmetry")
+    R = np.zeros((max(n.value, 1), 3, 3))
+    Q = np.zeros((max(n.value, 1), 4))
+    check(lib().thx_symmetry(name.encode(), max(n.value, 1), R.ctypes.data_as(ctypes.c_void_p),
+                             Q.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n)), "thx_symmetry")
+    return R[:n.value], Q[:n.value]
+
+
+def symmetrize_ft(vol, R, r):
+    """thx_symmetrize_ft of a half-complex volume (complex64 F or float32 T)
+    with the symmetry matrices R (device or numpy [n, 3, 3]); returns a new tensor."""
+    if vol.dim() != 3 or vol.shape[-1] != vol.shape[0] // 2 + 1 or vol.shape[1] != vol.shape[0]:
+        raise ValueError("half-complex volume [vdim, vdim, vdim/2+1] expected")
+    cplx = vol.dtype == torch.complex64
+    if not cplx:
+        _req(vol, torch.float32, None, "vol")
+    Rd = torch.as_tensor(np.ascontiguousarray(R, np.float64).reshape(-1, 9) if not torch.is_tensor(R)
+                         else R.reshape(-1, 9), dtype=torch.float64, device=vol.device).contiguous()
+    out = torch.empty_like(vol)
+    check(lib().thx_symmetrize_ft(_ptr(vol), _ptr(out), int(cplx), vol.shape[0], _ptr(Rd),
+                                  Rd.shape[0], float(r), _stream(vol.device)), "thx_symmetrize_ft")
+    return out
+
+
+def prepare_tf(hm, R, max_radius, pf):
+    """thx_prepare_tf on half-map hm in place: F, T /= T[0], then symmetrized
+    (Reconstructor::prepareTF); R: [n, 3, 3] (n = 0: normalise only)."""
+    dev = hm.F.device
+    R = np.asarray(R, np.float64).reshape(-1, 9)
+    Rd = torch.as_tensor(np.ascontiguousarray(R), device=dev) if len(R) else None
+    ws = workspace(lib().thx_prepare_tf_workspace(hm.vdim), dev)
+    check(lib().thx_prepare_tf(_ptr(hm.F), _ptr(hm.T), hm.vdim, _ptr(Rd), len(R), int(max_radius),
+                               int(pf), _ptr(ws), ws.numel(), _stream(dev)), "thx_prepare_tf")
+    return hm
+
+
+def pf_symmetrise(quat, symQ, anchor_mode=0, anchor=None, seed=0, stream_id=0):
+    """thx_pf_symmetrise of clouds quat [nImg, mR, 4] (device float64) in place."""
+    nImg, mR = quat.shape[:2]
+    _req(quat, torch.float64, (nImg, mR, 4), "quat")
+    Q = torch.as_tensor(np.ascontiguousarray(symQ, np.float64), device=quat.device).reshape(-1, 4)
+    if anchor is not None:
+        _req(anchor, torch.float64, (nImg, 4), "anchor")
+    check(lib().thx_pf_symmetrise(nImg, mR, _ptr(quat), int(anchor_mode), _ptr(anchor), _ptr(Q),
+                                  Q.shape[0], int(seed), int(stream_id), _stream(quat.device)),
+          "thx_pf_symmetrise")
+    return quat
+
+
 def reconstruct(hm, N, pf=2, a=1.9, alpha=15.0, grid_corr=True, max_radius=0, fsc=None,
                 join_half=False, want_ft=True):
     """thx_reconstruct: the reconstruction solve of half-map hm (F, T at box

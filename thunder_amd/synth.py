@@ -22,14 +22,22 @@ def n_trans_global(trans_s=10.0, trans_search_factor=0.25):
     return max(30, int(round(math.pi * (trans_s * CHI2_QINV_HALF_2DOF) ** 2 * trans_search_factor)))
 
 
-def blob_volume(N, n_blobs=40, seed=1, device="cpu"):
-    """Real-space N^3 float32 volume of Gaussian blobs inside radius 0.35 N."""
+def blob_volume(N, n_blobs=40, seed=1, device="cpu", sym_R=None):
+    """Real-space N^3 float32 volume of Gaussian blobs inside radius 0.35 N;
+    sym_R ([n, 3, 3], the non-identity elements of a point group, e.g.
+    ops.symmetry("C4")[0]): every blob is repeated at R c for every element,
+    so V(R x) = V(x) about the box centre (x, y, z = column, row, slice)."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     centers = (torch.rand(n_blobs, 3, generator=g, dtype=torch.float64) * 2 - 1)
     centers = centers / centers.norm(dim=1, keepdim=True).clamp(min=1) * 0.35 * N * torch.rand(
         n_blobs, 1, generator=g, dtype=torch.float64)
     widths = 1.0 + torch.rand(n_blobs, generator=g, dtype=torch.float64) * (N / 32.0)
     amps = 0.5 + torch.rand(n_blobs, generator=g, dtype=torch.float64)
+    if sym_R is not None and len(sym_R):
+        Rs = torch.as_tensor(np.asarray(sym_R, np.float64))
+        centers = torch.cat([centers] + [centers @ R.T for R in Rs])
+        widths = widths.repeat(len(Rs) + 1)
+        amps = amps.repeat(len(Rs) + 1)
     ax = torch.arange(N, dtype=torch.float32, device=device) - N // 2
     vol = torch.zeros(N, N, N, dtype=torch.float32, device=device)
     zz, yy, xx = ax.view(N, 1, 1), ax.view(1, N, 1), ax.view(1, 1, N)

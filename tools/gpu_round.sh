@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 for s in $steps; do
   case $s in
     tests)
-      (cd $R && timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 \
+      (cd $R && timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail 15 --timeout 120 \
           --timeout-method thread > $O/tests.log 2>&1) ;;
     bench)
       (cd $R && timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err) ;;
