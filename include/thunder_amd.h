@@ -540,6 +540,23 @@ int thx_reconstruct(const float* F, float* T, int N, int pf, float a, float alph
                     int joinHalf, float* dst, float* dstFT, int* nIter, float* diffOut,
                     void* workspace, size_t wsBytes, thx_stream_t stream);
 
+/* MODE_2D: the 2D branches of Reconstructor::reconstruct (src/Reconstructor.cpp:
+ * 1136-1589, 1669-1818; GPU ExposePT2D / ExposeWT2D / ExposePF2D /
+ * ExposeCorrF2D) for nK class images at once, each with its own balancing
+ * iterations and stopping rule (OPTIMISER_2D_GRID_CORR, include/Config.h:206):
+ *   F [nK][vdim][vdim/2+1] Complex (read), T [nK][vdim][vdim/2+1] float
+ *   (modified in place), vdim = pf N; fsc (device, may be NULL: no MAP)
+ *   [nK][nFsc]; dst [nK][N][N] real space, origin at [0][0], negatives
+ *   wrapped; nIter (host, may be NULL) [nK].  Host-synchronous.
+ * thx_prepare_tf2d -- prepareTF's MODE_2D part: F_k, T_k *= 1 / T_k[0] per class
+ *   (RECONSTRUCTOR_NORMALISE_T_F, src/Reconstructor.cpp:2459-2466). */
+int thx_prepare_tf2d(float* F, float* T, int vdim, int nK, thx_stream_t stream);
+size_t thx_reconstruct2d_workspace(int N, int pf, int nK);
+int thx_reconstruct2d(const float* F, float* T, int nK, int N, int pf, float a, float alpha,
+                      int gridCorr, int maxRadius, const double* fsc, int nFsc, int joinHalf,
+                      float* dst, int* nIter, void* workspace, size_t wsBytes,
+                      thx_stream_t stream);
+
 /* FFT::fw / FFT::bw (src/FFT.cpp) of one volume of box vdim, unnormalised:
  * inverse 0: rl [vdim^3] real -> C [vdim][vdim][vdim/2+1] complex; inverse 1:
  * C -> rl (C overwritten).  method 0: the reconstruction's own choice, 1:

@@ -11,6 +11,8 @@ src/FFT.cpp: forward unnormalised, backward scaled by 1/size):
   balancing :1356-1552 (convoluteC :2595-2675, checkC :2522-2593, constants
   include/Reconstructor.h:61-75), no-grid-correction W :1553-1587, F W ->
   real space -> VOL_EXTRACT_RL -> / TIK_RL :1669-1818.
+reconstruct2d: the MODE_2D branches of the same function (rings instead of
+shells, IMG_EXTRACT_RL), one class image.
 The MKB real-space kernel is tabulated like TabFunction (src/TabFunction.cpp:
 TabFunction::init / operator(): 1e5 + 1 samples on [0, 1], nearest entry) with
 closed forms of the half-integer Bessel functions (MKB_RL_R2,
@@ -124,6 +126,74 @@ def reconstruct(F, T, N, pf=2, a=1.9, alpha=15.0, grid_corr=True, max_radius=0, 
     c = np.fft.fftfreq(N, 1.0 / N).astype(np.int64)
     box = rl[np.ix_(c % vdim, c % vdim, c % vdim)]
     r = np.sqrt(_rl_quad(N).astype(np.float64)) / vdim
+    x = np.pi * r
+    j0 = np.where(x == 0, 1.0, np.sin(x) / np.where(x == 0, 1.0, x))
+    return box / (j0 * j0), m, diffs
+
+
+def _ft_quad2(vdim):
+    i = np.arange(vdim // 2 + 1)
+    j = np.fft.fftfreq(vdim, 1.0 / vdim).astype(np.int64)
+    return j[:, None] ** 2 + i[None, :] ** 2                  # [j][i]
+
+
+def _rl_quad2(n):
+    c = np.fft.fftfreq(n, 1.0 / n).astype(np.int64)
+    return c[:, None] ** 2 + c[None, :] ** 2
+
+
+def reconstruct2d(F, T, N, pf=2, a=1.9, alpha=15.0, grid_corr=True, max_radius=0, fsc=None,
+                  join_half=False):
+    """F: [vdim, vdim/2+1] complex, T: same shape real (one class).  Returns
+    (image [N, N] real space, origin at index 0; iterations; diffs)."""
+    vdim = pf * N
+    F = np.asarray(F, np.complex128)
+    T = np.array(T, np.float64)
+    maxR = max_radius if max_radius > 0 else N // 2 - int(math.ceil(a))
+    quad = _ft_quad2(vdim)
+    inside = quad < (maxR * pf) ** 2
+    if fsc is not None:
+        lo, hi = (5 * pf) ** 2, (maxR * pf) ** 2
+        m = (quad >= lo) & (quad < hi)
+        u = np.rint(np.sqrt(quad[m].astype(np.float64))).astype(np.int64)
+        idx = u // pf
+        f = np.where(idx >= len(fsc), 0.0, np.asarray(fsc)[np.minimum(idx, len(fsc) - 1)])
+        f = np.clip(f, 1e-3, 1 - 1e-3)
+        if join_half:
+            f = np.sqrt(2 * f / (1 + f))
+        T[m] = T[m] / f
+    W = inside.astype(np.float64)
+    T = np.maximum(T, 1e-25)
+    diffs = []
+    m = 0
+    if grid_corr:
+        tab = mkb_rl_r2(np.arange(TAB_N + 1) * 1e-5, a, alpha).astype(np.float32).astype(np.float64)
+        nf = float(mkb_rl_r2(np.array([0.0]), a, alpha)[0])
+        kern = tab[np.minimum(np.rint((_rl_quad2(vdim) / float(vdim * vdim)) / 1e-5).astype(np.int64),
+                              TAB_N)] / nf
+        diff_prev = diff = np.finfo(np.float32).max
+        n_no = 0
+        for m in range(30):
+            C = T * W
+            c = np.fft.irfftn(C, s=(vdim, vdim)) * kern
+            C = np.fft.rfftn(c)
+            a_ = np.abs(C)
+            W = np.where(inside, W / np.maximum(a_, 1e-6), W)
+            diff_prev, diff = diff, float(np.max(np.abs(a_[inside] - 1)))
+            diffs.append(diff)
+            n_no = n_no + 1 if diff > diff_prev * 0.95 else 0
+            if diff < 1e-2 or (m >= 10 and n_no == 2):
+                m += 1
+                break
+        else:
+            m = 30
+    else:
+        W = np.where(inside, 1.0 / np.maximum(np.abs(T), 1e-6), W)
+    pad = np.where(inside, F * W, 0)
+    rl = np.fft.irfftn(pad, s=(vdim, vdim))
+    c = np.fft.fftfreq(N, 1.0 / N).astype(np.int64)
+    box = rl[np.ix_(c % vdim, c % vdim)]
+    r = np.sqrt(_rl_quad2(N).astype(np.float64)) / vdim
     x = np.pi * r
     j0 = np.where(x == 0, 1.0, np.sin(x) / np.where(x == 0, 1.0, x))
     return box / (j0 * j0), m, diffs

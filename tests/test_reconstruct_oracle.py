@@ -51,3 +51,33 @@ def test_grid_correction_balances_C():
     _, it, diffs = rc.reconstruct(F, T, N, pf, grid_corr=True)
     assert 1 <= it <= 30 and len(diffs) == it
     assert diffs[-1] < diffs[0]
+
+
+def test_2d_no_grid_correction_inverts_T():
+    """MODE_2D restatement: without grid correction the class image is the
+    inverse FFT of F / T in the disc, IMG_EXTRACT_RL'd and kernel-corrected."""
+    N, pf = 32, 2
+    vdim = N * pf
+    rng = np.random.default_rng(5)
+    X = np.fft.rfftn(rng.standard_normal((vdim, vdim)))
+    T = rng.uniform(0.5, 2.0, X.shape)
+    got, it, _ = rc.reconstruct2d(X * T, T, N, pf, grid_corr=False)
+    quad = rc._ft_quad2(vdim)
+    maxR = N // 2 - 2
+    ref_rl = np.fft.irfftn(np.where(quad < (maxR * pf) ** 2, X, 0), s=(vdim, vdim))
+    c = np.fft.fftfreq(N, 1.0 / N).astype(int)
+    box = ref_rl[np.ix_(c % vdim, c % vdim)]
+    r = np.sqrt(rc._rl_quad2(N).astype(float)) / vdim
+    j0 = np.where(r == 0, 1.0, np.sin(np.pi * r) / np.where(r == 0, 1, np.pi * r))
+    assert it == 0
+    assert np.allclose(got, box / j0 ** 2, atol=1e-10)
+
+
+def test_2d_grid_correction_balances_C():
+    N, pf = 32, 2
+    vdim = N * pf
+    rng = np.random.default_rng(6)
+    T = rng.uniform(0.5, 2.0, (vdim, vdim // 2 + 1))
+    _, it, diffs = rc.reconstruct2d(np.zeros_like(T, dtype=complex), T, N, pf, grid_corr=True)
+    assert 1 <= it <= 30 and len(diffs) == it
+    assert diffs[-1] < diffs[0]

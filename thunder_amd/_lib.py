@@ -122,6 +122,10 @@ SIGNATURES = {
     "thx_prepare_tf": (_c_int, [_p, _p, _c_int, _p, _c_int, _c_int, _c_int, _p, _c_size, _p]),
     "thx_pf_symmetrise": (_c_int, [_c_int, _c_int, _p, _c_int, _p, _p, _c_int, ctypes.c_ulonglong,
                                    ctypes.c_uint, _p]),
+    "thx_prepare_tf2d": (_c_int, [_p, _p, _c_int, _c_int, _p]),
+    "thx_reconstruct2d_workspace": (_c_size, [_c_int, _c_int, _c_int]),
+    "thx_reconstruct2d": (_c_int, [_p, _p, _c_int, _c_int, _c_int, _c_float, _c_float, _c_int, _c_int,
+                                   _p, _c_int, _c_int, _p, _p, _p, _c_size, _p]),
     "thx_fsc_workspace": (_c_size, [_c_int]),
     "thx_fsc": (_c_int, [_p, _p, _c_int, _c_int, _p, _p, _c_size, _p]),
     "thx_expectation_workspace": (_c_size, [_p, _c_int, _c_int, _c_int]),

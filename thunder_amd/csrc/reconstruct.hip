@@ -703,3 +703,327 @@ extern "C" int thx_fft3d(float* C, float* rl, int vdim, int inverse, int method,
     THX_HIP(hipStreamSynchronize(s));      // the plans are shared across calls on this stream
     return THX_OK;
 }
+
+// ------------------------------------------------------------------ MODE_2D
+// The 2D branches of Reconstructor::reconstruct (src/Reconstructor.cpp:
+// 1136-1589, 1669-1818; GPU twin reconstructG's ExposePT2D / ExposeWT2D /
+// ExposePF2D / ExposeCorrF2D) for nK class images at once: the same MAP
+// factor on rings, W = 1 in the disc |k| < maxR pf, T = max(T, 1e-25), the
+// MKB balancing (convoluteC's 2D branch: kernelRL(QUAD(i, j) / (N pf)^2) /
+// nf, checkC's max, the same stopping rule per class -- OPTIMISER_2D_GRID_CORR
+// is on in include/Config.h:206), or W = 1 / max(|T|, 1e-6); pad = F W ->
+// FFT::bw (1 / vdim^2) -> the central N^2 (IMG_EXTRACT_RL) / TIK_RL(|r| /
+// (pf N)).  Layouts: F / T [nK][vdim][vdim/2+1] (Image FT, i fastest, rows
+// wrapped); dst [nK][N][N] real space, origin at [0][0], negatives wrapped.
+namespace {
+
+THX_DEV void ft2_coord(long q, int vdim, int& k, int& i, int& j)
+{
+    const int nc = vdim / 2 + 1;
+    const long per = (long)nc * vdim;
+    k = (int)(q / per);
+    const long r = q - (long)k * per;
+    i = (int)(r % nc);
+    j = (int)(r / nc);
+    if (j >= vdim / 2) j -= vdim;
+}
+
+__global__ void k2_prep(float* __restrict__ T, float* __restrict__ W, int vdim, int nK, long r2,
+                        int map, int pf, int maxR, const double* __restrict__ fsc, int nFsc,
+                        int joinHalf)
+{
+    const long n = (long)nK * (vdim / 2 + 1) * vdim;
+    const long lo = (long)5 * pf * 5 * pf;                 // WIENER_FACTOR_MIN_R
+    GRID_STRIDE(q, n)
+    {
+        int k, i, j;
+        ft2_coord(q, vdim, k, i, j);
+        const long quad = (long)i * i + (long)j * j;
+        float t = T[q];
+        if (map && quad >= lo && quad < r2) {
+            const int u = (int)rintf(sqrtf((float)quad));   // AROUND(NORM(i, j))
+            float f = (u / pf >= nFsc) ? 0.f : (float)fsc[(size_t)k * nFsc + u / pf];
+            f = fmaxf(1e-3f, fminf(1.f - 1e-3f, f));        // FSC_BASE_L / _H
+            if (joinHalf) f = sqrtf(2.f * f / (1.f + f));
+            t = t / f;
+        }
+        t = fmaxf(t, 1e-25f);
+        T[q] = t;
+        W[q] = quad < r2 ? 1.f : 0.f;
+    }
+}
+
+__global__ void k2_w_from_t(float* __restrict__ W, const float* __restrict__ T, int vdim, int nK,
+                            long r2)
+{
+    const long n = (long)nK * (vdim / 2 + 1) * vdim;
+    GRID_STRIDE(q, n)
+    {
+        int k, i, j;
+        ft2_coord(q, vdim, k, i, j);
+        if ((long)i * i + (long)j * j < r2) W[q] = 1.f / fmaxf(fabsf(T[q]), 1e-6f);
+    }
+}
+
+__global__ void k2_c_from_tw(float2* __restrict__ C, const float* __restrict__ T,
+                             const float* __restrict__ W, long n)
+{
+    GRID_STRIDE(q, n) C[q] = make_float2(T[q] * W[q], 0.f);
+}
+
+// real space [nK][vdim][vdim]: c *= kernelRL(QUAD(i, j) / vdim^2) / nf / vdim^2
+__global__ void k2_kernel_mul(float* __restrict__ c, int vdim, int nK, const float* __restrict__ tab,
+                              float nf, float scale)
+{
+    const long n = (long)nK * vdim * vdim;
+    const float inv = 1.f / ((float)vdim * (float)vdim);
+    GRID_STRIDE(q, n)
+    {
+        const long r = q % ((long)vdim * vdim);
+        int i = (int)(r % vdim), j = (int)(r / vdim);
+        if (i > vdim / 2) i -= vdim;
+        if (j > vdim / 2) j -= vdim;
+        const float x = (float)(i * i + j * j) * inv;
+        const int t = min(TAB_N, (int)rintf(x / 1e-5f));
+        c[q] *= scale * tab[t] / nf;
+    }
+}
+
+// W /= max(|C|, 1e-6) inside the disc for the classes still balancing; their
+// max | |C| - 1 |; the next C = T W
+__global__ void k2_update_w(float* __restrict__ W, float2* __restrict__ C, const float* __restrict__ T,
+                            int vdim, int nK, long r2, const int* __restrict__ active,
+                            unsigned* __restrict__ diffBits)
+{
+    const int k = blockIdx.y;
+    if (!active[k]) return;
+    const int nc = vdim / 2 + 1;
+    const long per = (long)nc * vdim;
+    float dmax = 0.f;
+    for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < per; r += (long)gridDim.x * blockDim.x) {
+        const long e = (long)k * per + r;
+        const int i = (int)(r % nc);
+        int j = (int)(r / nc);
+        if (j >= vdim / 2) j -= vdim;
+        float w = W[e];
+        if ((long)i * i + (long)j * j < r2) {
+            const float2 cv = C[e];
+            const float a = sqrtf(cv.x * cv.x + cv.y * cv.y);
+            w = w / fmaxf(a, 1e-6f);
+            W[e] = w;
+            dmax = fmaxf(dmax, fabsf(a - 1.f));
+        }
+        C[e] = make_float2(T[e] * w, 0.f);
+    }
+    dmax = wave_max(dmax);
+    __shared__ float sm[4];
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = dmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float m = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+        if (m > 0.f) atomicMax(diffBits + k, __float_as_uint(m));
+    }
+}
+
+__global__ void k2_pad(float2* __restrict__ P, const float2* __restrict__ F, const float* __restrict__ W,
+                       int vdim, int nK, long r2)
+{
+    const long n = (long)nK * (vdim / 2 + 1) * vdim;
+    GRID_STRIDE(q, n)
+    {
+        int k, i, j;
+        ft2_coord(q, vdim, k, i, j);
+        const float2 f = F[q];
+        const float w = W[q];
+        P[q] = ((long)i * i + (long)j * j < r2) ? make_float2(f.x * w, f.y * w) : make_float2(0.f, 0.f);
+    }
+}
+
+__global__ void k2_extract(float* __restrict__ dst, const float* __restrict__ src, int N, int vdim,
+                           int nK, float scale)
+{
+    const long n = (long)nK * N * N;
+    GRID_STRIDE(q, n)
+    {
+        const int k = (int)(q / ((long)N * N));
+        const long r = q - (long)k * N * N;
+        int i = (int)(r % N), j = (int)(r / N);
+        if (i >= N / 2) i -= N;
+        if (j >= N / 2) j -= N;
+        const long s = (long)k * vdim * vdim + (long)wrap_idx(j, vdim) * vdim + wrap_idx(i, vdim);
+        const float x = (float)M_PI * sqrtf((float)(i * i + j * j)) / (float)vdim;
+        const float j0 = x == 0.f ? 1.f : sinf(x) / x;
+        dst[q] = src[s] * scale / (j0 * j0);              // / TIK_RL
+    }
+}
+
+// per-class normalisation 1 / T_k[0] (RECONSTRUCTOR_NORMALISE_T_F, MODE_2D)
+__global__ void k2_normalise(float* __restrict__ F, float* __restrict__ T, int vdim, int nK)
+{
+    const long per = (long)(vdim / 2 + 1) * vdim;
+    const int k = blockIdx.y;
+    const float sf = 1.f / T[(size_t)k * per];   // element 0 is scaled last (k2_normalise_first)
+    for (long r = blockIdx.x * (long)blockDim.x + threadIdx.x; r < per; r += (long)gridDim.x * blockDim.x) {
+        const size_t e = (size_t)k * per + r;
+        if (r == 0) continue;
+        T[e] *= sf;
+        float2* f = reinterpret_cast<float2*>(F) + e;
+        *f = make_float2(f->x * sf, f->y * sf);
+    }
+}
+
+__global__ void k2_normalise_first(float* __restrict__ F, float* __restrict__ T, int vdim, int nK)
+{
+    const long per = (long)(vdim / 2 + 1) * vdim;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nK) return;
+    const size_t e = (size_t)k * per;
+    const float sf = 1.f / T[e];
+    T[e] *= sf;
+    float2* f = reinterpret_cast<float2*>(F) + e;
+    *f = make_float2(f->x * sf, f->y * sf);
+}
+
+struct Plans2 {
+    hipfftHandle c2r = 0, r2c = 0;
+};
+
+int plans2d(int vdim, int nK, hipStream_t s, Plans2** out, std::unique_lock<std::mutex>& lock)
+{
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int, hipStream_t>, std::unique_ptr<std::pair<std::mutex, Plans2>>>*
+        cache = new std::map<std::tuple<int, int, int, hipStream_t>,
+                             std::unique_ptr<std::pair<std::mutex, Plans2>>>;
+    int dev = 0;
+    THX_HIP(hipGetDevice(&dev));
+    std::pair<std::mutex, Plans2>* e = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto& slot = (*cache)[std::make_tuple(dev, vdim, nK, s)];
+        if (!slot) slot.reset(new std::pair<std::mutex, Plans2>());
+        e = slot.get();
+    }
+    lock = std::unique_lock<std::mutex>(e->first);
+    Plans2& p = e->second;
+    if (!p.c2r) {
+        int n[2] = {vdim, vdim};
+        THX_FFT(hipfftPlanMany(&p.c2r, 2, n, nullptr, 1, 0, nullptr, 1, 0, HIPFFT_C2R, nK));
+        THX_FFT(hipfftPlanMany(&p.r2c, 2, n, nullptr, 1, 0, nullptr, 1, 0, HIPFFT_R2C, nK));
+    }
+    THX_FFT(hipfftSetStream(p.c2r, s));
+    THX_FFT(hipfftSetStream(p.r2c, s));
+    *out = &p;
+    return THX_OK;
+}
+
+}  // namespace
+
+extern "C" int thx_prepare_tf2d(float* F, float* T, int vdim, int nK, thx_stream_t stream)
+{
+    THX_CHECK_ARG(F && T && vdim > 0 && vdim % 2 == 0 && nK > 0, "thx_prepare_tf2d: bad arguments");
+    hipStream_t s = thx::as_stream(stream);
+    const long per = (long)(vdim / 2 + 1) * vdim;
+    hipLaunchKernelGGL(k2_normalise, dim3((unsigned)std::min<long>(thx::cdiv(per, 256), 1024), nK),
+                       dim3(256), 0, s, F, T, vdim, nK);
+    THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k2_normalise_first, dim3(thx::cdiv(nK, 64)), dim3(64), 0, s, F, T, vdim, nK);
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" size_t thx_reconstruct2d_workspace(int N, int pf, int nK)
+{
+    if (N <= 0 || pf <= 0 || nK <= 0) return 0;
+    const int vdim = N * pf;
+    const size_t img = (size_t)(vdim / 2 + 1) * vdim * nK;
+    thx::Carver k(nullptr, ~size_t(0));
+    k.take<float>(img);                              // W
+    k.take<float2>(img);                             // C / pad
+    k.take<float>((size_t)vdim * vdim * nK);         // real space
+    k.take<float>(TAB_N + 1);                        // kernel table
+    k.take<unsigned>(nK);                            // diffs
+    k.take<int>(nK);                                 // active classes
+    return k.off + 256;
+}
+
+extern "C" int thx_reconstruct2d(const float* F, float* T, int nK, int N, int pf, float a,
+                                 float alpha, int gridCorr, int maxRadius, const double* fsc,
+                                 int nFsc, int joinHalf, float* dst, int* nIter, void* workspace,
+                                 size_t wsBytes, thx_stream_t stream)
+{
+    THX_CHECK_ARG(F && T && dst && nK > 0 && N > 0 && N % 2 == 0 && pf > 0 && a > 0 && alpha > 0,
+                  "thx_reconstruct2d: bad arguments");
+    THX_CHECK_ARG(!fsc || nFsc > 0, "thx_reconstruct2d: fsc needs nFsc");
+    const int vdim = N * pf;
+    const int maxR = maxRadius > 0 ? maxRadius : N / 2 - (int)std::ceil(a);
+    THX_CHECK_ARG(maxR > 0 && maxR <= N / 2, "thx_reconstruct2d: bad maxRadius");
+    THX_CHECK_ARG(workspace && wsBytes >= thx_reconstruct2d_workspace(N, pf, nK),
+                  "thx_reconstruct2d: workspace too small");
+    hipStream_t s = thx::as_stream(stream);
+    const size_t img = (size_t)(vdim / 2 + 1) * vdim * nK;
+    thx::Carver k(workspace, wsBytes);
+    float* W = k.take<float>(img);
+    float2* C = k.take<float2>(img);
+    float* rl = k.take<float>((size_t)vdim * vdim * nK);
+    float* tab = k.take<float>(TAB_N + 1);
+    unsigned* diff = k.take<unsigned>(nK);
+    int* active = k.take<int>(nK);
+    std::unique_lock<std::mutex> lk;
+    Plans2* pl = nullptr;
+    THX_RET(plans2d(vdim, nK, s, &pl, lk));
+    const long r2 = (long)maxR * pf * maxR * pf;
+    const float scaleBw = 1.f / ((float)vdim * vdim);
+    const dim3 g(1024), b(256);
+    hipLaunchKernelGGL(k2_prep, g, b, 0, s, T, W, vdim, nK, r2, fsc ? 1 : 0, pf, maxR, fsc, nFsc,
+                       joinHalf);
+    THX_LAUNCH_CHECK();
+    std::vector<int> iters(nK, 0);
+    if (gridCorr) {
+        const std::vector<float>& htab = kernel_table(a, alpha);
+        const float nf = (float)mkb_rl_r2(0.0, a, alpha);
+        THX_HIP(hipMemcpyAsync(tab, htab.data(), sizeof(float) * (TAB_N + 1), hipMemcpyHostToDevice, s));
+        std::vector<int> act(nK, 1), nNoDec(nK, 0);
+        std::vector<float> diffC(nK, 3.4e38f), prev(nK, 3.4e38f);
+        std::vector<unsigned> bits(nK);
+        THX_HIP(hipMemcpyAsync(active, act.data(), sizeof(int) * nK, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k2_c_from_tw, g, b, 0, s, C, T, W, (long)img);
+        THX_LAUNCH_CHECK();
+        for (int m = 0; m < 30; m++) {                                  // MAX_N_ITER_BALANCE
+            THX_FFT(hipfftExecC2R(pl->c2r, reinterpret_cast<hipfftComplex*>(C), rl));
+            hipLaunchKernelGGL(k2_kernel_mul, g, b, 0, s, rl, vdim, nK, tab, nf, scaleBw);
+            THX_LAUNCH_CHECK();
+            THX_FFT(hipfftExecR2C(pl->r2c, rl, reinterpret_cast<hipfftComplex*>(C)));
+            THX_HIP(hipMemsetAsync(diff, 0, sizeof(unsigned) * nK, s));
+            hipLaunchKernelGGL(k2_update_w, dim3(16, nK), dim3(256), 0, s, W, C, T, vdim, nK, r2,
+                               active, diff);
+            THX_LAUNCH_CHECK();
+            THX_HIP(hipMemcpyAsync(bits.data(), diff, sizeof(unsigned) * nK, hipMemcpyDeviceToHost, s));
+            THX_HIP(hipStreamSynchronize(s));
+            bool any = false;
+            for (int c = 0; c < nK; c++) {
+                if (!act[c]) continue;
+                prev[c] = diffC[c];
+                diffC[c] = __builtin_bit_cast(float, bits[c]);
+                iters[c] = m + 1;
+                if (diffC[c] > prev[c] * 0.95f) nNoDec[c] += 1;        // DIFF_C_DECREASE_THRES
+                else nNoDec[c] = 0;
+                if (diffC[c] < 1e-2f || (m >= 10 && nNoDec[c] == 2)) act[c] = 0;
+                any = any || act[c];
+            }
+            if (!any) break;
+            THX_HIP(hipMemcpyAsync(active, act.data(), sizeof(int) * nK, hipMemcpyHostToDevice, s));
+        }
+    } else {
+        hipLaunchKernelGGL(k2_w_from_t, g, b, 0, s, W, T, vdim, nK, r2);
+        THX_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(k2_pad, g, b, 0, s, C, reinterpret_cast<const float2*>(F), W, vdim, nK, r2);
+    THX_LAUNCH_CHECK();
+    THX_FFT(hipfftExecC2R(pl->c2r, reinterpret_cast<hipfftComplex*>(C), rl));
+    hipLaunchKernelGGL(k2_extract, g, b, 0, s, dst, rl, N, vdim, nK, scaleBw);
+    THX_LAUNCH_CHECK();
+    if (nIter)
+        for (int c = 0; c < nK; c++) nIter[c] = iters[c];
+    THX_HIP(hipStreamSynchronize(s));      // the plans are shared across calls on this stream
+    return THX_OK;
+}

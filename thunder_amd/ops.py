@@ -692,6 +692,40 @@ def insert2d(hm, dat, ctf_, rot, trans, offS, w, px, nc=None):
 
 
 # ------------------------------------------------------------------- f1
+def prepare_tf2d(hm):
+    """thx_prepare_tf2d on a HalfMap2D in place: F_k, T_k /= T_k[0]."""
+    check(lib().thx_prepare_tf2d(_ptr(hm.F), _ptr(hm.T), hm.vdim, hm.nK, _stream(hm.F.device)),
+          "thx_prepare_tf2d")
+    return hm
+
+
+def reconstruct2d(hm, N, pf=2, a=1.9, alpha=15.0, grid_corr=True, max_radius=0, fsc=None,
+                  join_half=False):
+    """thx_reconstruct2d: the nK class images of HalfMap2D hm (T modified in
+    place); returns (images [nK, N, N] real space, origin at [0, 0],
+    iterations per class)."""
+    vdim = pf * N
+    if hm.vdim != vdim:
+        raise ValueError("half-map box != pf N")
+    dev = hm.F.device
+    nK = hm.nK
+    dst = torch.empty(nK, N, N, dtype=torch.float32, device=dev)
+    it = (ctypes.c_int * nK)()
+    fs = None
+    if fsc is not None:
+        fs = torch.as_tensor(np.ascontiguousarray(np.atleast_2d(fsc)), dtype=torch.float64,
+                             device=dev)
+        if fs.shape[0] != nK:
+            raise ValueError("fsc: one row per class")
+    ws = workspace(lib().thx_reconstruct2d_workspace(N, pf, nK), dev)
+    check(lib().thx_reconstruct2d(_ptr(hm.F), _ptr(hm.T), nK, N, pf, float(a), float(alpha),
+                                  int(bool(grid_corr)), int(max_radius), _ptr(fs),
+                                  fs.shape[1] if fs is not None else 0, int(bool(join_half)),
+                                  _ptr(dst), it, _ptr(ws), ws.numel(), _stream(dev)),
+          "thx_reconstruct2d")
+    return dst, list(it)
+
+
 # --------------------------------------------------------- point groups
 def symmetry(name):
     """thx_symmetry: (R [n, 3, 3] row-major, quat [n, 4]) float64 numpy of the
