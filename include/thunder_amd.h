@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define THX_ABI_VERSION 6
+#define THX_ABI_VERSION 7
 
 enum {
     THX_OK = 0,
@@ -969,6 +969,115 @@ int thx_InsertFTComm(float* F3D, float* T3D, double* O3D, int* counter,
                      const float* w, const double* nR, const double* nT, const int* nC,
                      const int* iCol, const int* iRow, int opf, int npxl,
                      int mReco, int idim, int vdim, int imgNum, void* comm);
+
+/* ------------------------------------------ reconstruction host adapters ---
+ * gpu/interface/Interface.h:320-528 (ABI 7): the reconstruction and
+ * preprocessing entry points Reconstructor::reconstructG / prepareTFG
+ * (src/Reconstructor.cpp:1021-1052, 1835-2346) and Optimiser (src/
+ * Optimiser.cpp:5059, 6185, 7402-7425) call, host pointers in and out as the
+ * cuthunder bodies take them (gpu/src/cuthunder.cu:6176-9819), Complex as
+ * float[2], RFLOAT as float.  Half-complex arrays [k][j][i], (dim/2+1) x dim
+ * (x dim); real-space arrays dim x dim (x dim), origin at index 0.  gpuIdx:
+ * the device the call runs on.  Device-resident equivalents: thx_prepare_tf,
+ * thx_reconstruct, thx_reconstruct2d.  All return THX_OK or an error code. */
+
+/* PrepareTF (:320): F and T scaled by 1 / T[0], then symmetrised with
+ * r = maxRadius pf + 1 (SYMMETRIZE_FT); T = max(T, 1e-25).  T3D: the real
+ * parts of T (the forward converts the complex Volume).  symMat: nSymElem 3x3
+ * matrices as prepareTFG packs them (Eigen column-major). */
+int thx_PrepareTF(int gpuIdx, float* F3D, float* T3D, const double* symMat, int nSymElem,
+                  int maxRadius, int pf, int dim);
+
+/* ExposePT / ExposePT2D (:328-344): the MAP step, T /= FSC' on wienerF pf <=
+ * |k| < maxRadius pf (kernel_CalculateFSC), then T = max(T, 1e-25); fsc:
+ * nFsc values of the FSC per shell (the RFLOAT vec _FSC). */
+int thx_ExposePT(int gpuIdx, float* T3D, int maxRadius, int pf, int dim, const float* fsc,
+                 int nFsc, int joinHalf, int wienerF);
+int thx_ExposePT2D(int gpuIdx, float* T2D, int maxRadius, int pf, int dim, const float* fsc,
+                   int nFsc, int joinHalf, int wienerF);
+
+/* ExposeWT / ExposeWT2D with the kernel table (:346-356, 438-448): the
+ * grid-correction balancing loop, W = 1 inside |k| < maxRadius pf, then
+ * C = T W -> C2R -> / size x tab(|r|^2 / (pf size)^2) / nf -> R2C -> W /=
+ * max(|C|, 1e-6) until max | |C| - 1 | < 1e-2 or (m >= minIter and two
+ * iterations in a row not below 0.95 of the previous) or maxIter.  tab:
+ * tabSize entries at spacing step (TabFunction::getData / getStep); the
+ * index is clamped into the table.  nIter (may be NULL): iterations run. */
+int thx_ExposeWT(int gpuIdx, const float* T3D, float* W3D, const float* tab, float step,
+                 int tabSize, float nf, int maxRadius, int pf, int dim, int maxIter, int minIter,
+                 int size, int* nIter);
+int thx_ExposeWT2D(int gpuIdx, const float* T2D, float* W2D, const float* tab, float step,
+                   int tabSize, float nf, int maxRadius, int pf, int dim, int maxIter,
+                   int minIter, int size, int* nIter);
+/* ExposeWT / ExposeWT2D without grid correction (:450-462): W = 1 /
+ * max(|T|, 1e-6) inside |k| < maxRadius pf, W untouched outside. */
+int thx_ExposeWT_T(int gpuIdx, const float* T3D, float* W3D, int maxRadius, int pf, int dim);
+int thx_ExposeWT2D_T(int gpuIdx, const float* T2D, float* W2D, int maxRadius, int pf, int dim);
+
+/* The split-step 3D balancing reconstructG drives with its own host FFTs
+ * between the steps (:358-436).  thx_AllocDevicePoint: device C (room for the
+ * dim^3 real C too), W, T, table and the max cell on gpuIdx, and one HIP
+ * stream in stream[0] (stream[1..streamNum) = NULL; devDiff / devCount =
+ * NULL: RECONSTRUCTOR_CHECK_C_AVERAGE is off).  thx_HostDeviceInit: uploads
+ * T and the table, W = 1 inside the sphere.  thx_ExposeC: C3D (host,
+ * half-complex) = T W.  thx_ExposeForConvC: C3D (host, real dim^3, after the
+ * caller's scaled backward FFT) x tab(|r|^2 / (pf size)^2) / nf.
+ * thx_ExposeWC: C3D (host, after the forward FFT) -> W /= max(|C|, 1e-6)
+ * inside, *diffC = max | |C| - 1 | inside.  thx_FreeDevHostPoint: volumeW =
+ * W, then frees everything and destroys the stream. */
+int thx_AllocDevicePoint(int gpuIdx, float** dev_C, float** dev_W, float** dev_T, float** dev_tab,
+                         float** devDiff, float** devMax, int** devCount, void** stream,
+                         int streamNum, int tabSize, int dim);
+int thx_HostDeviceInit(int gpuIdx, const float* T3D, const float* tab, float* dev_W, float* dev_T,
+                       float* dev_tab, void** stream, int streamNum, int tabSize, int maxRadius,
+                       int pf, int dim);
+int thx_ExposeC(int gpuIdx, float* C3D, float* dev_C, const float* dev_T, const float* dev_W,
+                void** stream, int streamNum, int dim);
+int thx_ExposeForConvC(int gpuIdx, float* C3D, float* dev_C, const float* dev_tab, void** stream,
+                       float step, int tabSize, float nf, int streamNum, int pf, int size, int dim);
+int thx_ExposeWC(int gpuIdx, const float* C3D, float* dev_C, float* dev_W, float* devMax,
+                 void** stream, float* diffC, int streamNum, int maxRadius, int pf, int dim);
+int thx_FreeDevHostPoint(int gpuIdx, float** dev_C, float** dev_W, float** dev_T, float** dev_tab,
+                         float** devDiff, float** devMax, int** devCount, void** stream,
+                         float* volumeW, int streamNum, int dim);
+
+/* ExposePFW (:472): padDst (pdim half-complex) = F W inside |k| < maxRadius
+ * pf, zero elsewhere.  ExposePF / ExposePF2D (:464-485): the same padded
+ * array back-transformed and divided by its size into padDstR (pdim^3 /
+ * pdim^2 real). */
+int thx_ExposePFW(int gpuIdx, float* padDst, const float* F3D, const float* W3D, int maxRadius,
+                  int pf, int pdim, int fdim);
+int thx_ExposePF(int gpuIdx, float* padDstR, const float* F3D, const float* W3D, int maxRadius,
+                 int pf, int pdim, int fdim);
+int thx_ExposePF2D(int gpuIdx, float* padDstR, const float* F2D, const float* W2D, int maxRadius,
+                   int pf, int pdim, int fdim);
+
+/* ExposeCorrF (:493-502) / ExposeCorrF2D (:487): the real-space kernel
+ * correction, x / mkbRL(|i|, |j|, |k|) (x nf when nf != 0: the MKB-kernel
+ * build; reconstructG passes nf = 0 with the trilinear kernel); mkbRL:
+ * (dim/2+1)^3 (2D: ^2) values, i fastest.  thx_ExposeCorrF: dst (dim^3 real)
+ * in place.  thx_ExposeCorrFT (the two-volume overload): dstN corrected and
+ * forward-transformed into dst (half-complex).  thx_ExposeCorrF2D: imgDst
+ * (dim^2 real) corrected and forward-transformed into dst. */
+int thx_ExposeCorrF(int gpuIdx, float* dst, const float* mkbRL, float nf, int dim);
+int thx_ExposeCorrFT(int gpuIdx, const float* dstN, float* dst, const float* mkbRL, float nf,
+                     int dim);
+int thx_ExposeCorrF2D(int gpuIdx, const float* imgDst, float* dst, const float* mkbRL, float nf,
+                      int dim);
+
+/* TranslateI / TranslateI2D (:504-515): the half-complex volume / image x
+ * exp(-2 pi i (i ox + j oy + k oz) / dim) inside i^2 + j^2 + k^2 < r^2. */
+int thx_TranslateI(int gpuIdx, float* ref, double ox, double oy, double oz, int r, int dim);
+int thx_TranslateI2D(int gpuIdx, float* img, double ox, double oy, int r, int dim);
+
+/* ReMask (:517): each image's transform (img[l]: idim x (idim/2+1) Complex)
+ * back-transformed / idim^2, soft-masked at maskRadius / pixelSize with edge
+ * ew, forward-transformed, in place.  GCTFinit (:524): img[l] = (CTF, 0) of
+ * ctfAttr[l] (7 floats, CTFAttr) over the whole half-complex grid.  Images
+ * are dealt over thx_adapter_devices(). */
+int thx_ReMask(float* const* img, float maskRadius, float pixelSize, float ew, int idim,
+               int imgNum);
+int thx_GCTFinit(float* const* img, const float* ctfAttr, float pixelSize, int idim, int imgNum);
 
 #ifdef __cplusplus
 }

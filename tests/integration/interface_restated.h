@@ -1,12 +1,11 @@
-// interface_restated.h -- TEST-ONLY restatement of the hot-path prototypes of
+// interface_restated.h -- TEST-ONLY restatement of the prototypes of
 // THUNDER's GPU plugin boundary, gpu/interface/Interface.h (line numbers
 // below), over the restated types of thunder_restated.h.  The INTEGRATION.md
 // forwards are compiled with -Werror=missing-declarations after this header:
 // a forward whose signature drifts from the reference's declaration is a new
 // overload without a previous declaration and fails the build
-// (tests/test_integration.py).  Out-of-scope Interface.h entries
-// (PrepareTF, Expose*, TranslateI*, ReMask, GCTFinit, ExpectPrecal) are not
-// restated: the drop-in keeps the reference's own bodies for them.
+// (tests/test_integration.py).  Every Interface.h function src/ calls is
+// restated; ExpectPrecal (:166), which nothing in src/ calls, is not.
 #pragma once
 #include "thunder_restated.h"
 
@@ -76,3 +75,48 @@ void InsertFT(Volume& F3D, Volume& T3D, double* O3D, int* counter, MPI_Comm& hem
               double* offS, RFLOAT* w, double* nR, double* nT, double* nD, const int* iCol,
               const int* iRow, RFLOAT pixelSize, bool cSearch, int opf, int npxl, int mReco,
               int idim, int dimSize, int imgNum);                                // :294-318
+void PrepareTF(int gpuIdx, Volume& F3D, Volume& T3D, double* symMat, int nSymmetryElement,
+               int maxRadius, int pf);                                           // :320-326
+void ExposePT2D(int gpuIdx, RFLOAT* T2D, int maxRadius, int pf, int dim, vec FSC, bool joinHalf,
+                const int wienerF);                                              // :328-335
+void ExposePT(int gpuIdx, RFLOAT* T3D, int maxRadius, int pf, int dim, vec FSC, bool joinHalf,
+              const int wienerF);                                                // :337-344
+void ExposeWT2D(int gpuIdx, RFLOAT* T2D, RFLOAT* W2D, TabFunction& kernelRL, RFLOAT nf,
+                int maxRadius, int pf, int dim, int maxIter, int minIter, int size); // :346-356
+void AllocDevicePoint(int gpuIdx, Complex** dev_C, RFLOAT** dev_W, RFLOAT** dev_T,
+                      RFLOAT** dev_tab, RFLOAT** devDiff, RFLOAT** devMax, int** devCount,
+                      void** stream, int streamNum, int tabSize, int dim);      // :358-369
+void HostDeviceInit(int gpuIdx, Volume& C3D, RFLOAT* W3D, RFLOAT* T3D, RFLOAT* tab,
+                    RFLOAT* dev_W, RFLOAT* dev_T, RFLOAT* dev_tab, void** stream, int streamNum,
+                    int tabSize, int maxRadius, int pf, int dim);                // :371-384
+void ExposeC(int gpuIdx, Volume& C3D, Complex* dev_C, RFLOAT* dev_T, RFLOAT* dev_W,
+             void** stream, int streamNum, int dim);                             // :386-393
+void ExposeForConvC(int gpuIdx, Volume& C3D, Complex* dev_C, RFLOAT* dev_tab, void** stream,
+                    TabFunction& kernelRL, RFLOAT nf, int streamNum, int tabSize, int pf,
+                    int size);                                                   // :395-405
+void ExposeWC(int gpuIdx, Volume& C3D, Complex* dev_C, RFLOAT* diff, RFLOAT* cmax,
+              RFLOAT* dev_W, RFLOAT* devDiff, RFLOAT* devMax, int* devCount, int* counter,
+              void** stream, RFLOAT& diffC, int streamNum, int maxRadius, int pf); // :407-421
+void FreeDevHostPoint(int gpuIdx, Complex** dev_C, RFLOAT** dev_W, RFLOAT** dev_T,
+                      RFLOAT** dev_tab, RFLOAT** devDiff, RFLOAT** devMax, int** devCount,
+                      void** stream, Volume& C3D, RFLOAT* volumeW, RFLOAT* volumeT,
+                      int streamNum, int dim);                                   // :423-436
+void ExposeWT(int gpuIdx, RFLOAT* T3D, RFLOAT* W3D, TabFunction& kernelRL, RFLOAT nf,
+              int maxRadius, int pf, int dim, int maxIter, int minIter, int size); // :438-448
+void ExposeWT2D(int gpuIdx, RFLOAT* T2D, RFLOAT* W2D, int maxRadius, int pf, int dim); // :450-455
+void ExposeWT(int gpuIdx, RFLOAT* T3D, RFLOAT* W3D, int maxRadius, int pf, int dim); // :457-462
+void ExposePF2D(int gpuIdx, Image& padDst, Image& padDstR, Image& F2D, RFLOAT* W2D,
+                int maxRadius, int pf);                                          // :464-470
+void ExposePFW(int gpuIdx, Volume& padDst, Volume& F3D, RFLOAT* W3D, int maxRadius,
+               int pf);                                                          // :472-477
+void ExposePF(int gpuIdx, Volume& padDst, Volume& padDstR, Volume& F3D, RFLOAT* W3D,
+              int maxRadius, int pf);                                            // :479-485
+void ExposeCorrF2D(int gpuIdx, Image& imgDst, Volume& dst, RFLOAT* mkbRL, RFLOAT nf); // :487-491
+void ExposeCorrF(int gpuIdx, Volume& dst, RFLOAT* mkbRL, RFLOAT nf);            // :493-496
+void ExposeCorrF(int gpuIdx, Volume& dstN, Volume& dst, RFLOAT* mkbRL, RFLOAT nf); // :498-502
+void TranslateI2D(int gpuIdx, Image& img, double ox, double oy, int r);         // :504-508
+void TranslateI(int gpuIdx, Volume& ref, double ox, double oy, double oz, int r); // :510-515
+void ReMask(std::vector<Image>& img, RFLOAT maskRadius, RFLOAT pixelSize, RFLOAT ew, int idim,
+            int imgNum);                                                         // :517-522
+void GCTFinit(std::vector<Image>& img, std::vector<CTFAttr>& ctfAttr, RFLOAT pixelSize,
+              int idim, int imgNum);                                             // :524-528

@@ -17,6 +17,23 @@ MPI_INC = "/opt/conda/include"
 MPI_LIB = "/opt/conda/lib"
 
 
+# The Interface.h functions (gpu/interface/Interface.h:16-528) that THUNDER's
+# src/ calls, with their overload counts; ExpectPrecal (:166) is the one
+# declaration nothing in src/ calls.
+SRC_CALLED = {
+    "getAviDevice": 1, "ExpectPreidx": 1, "ExpectPrefre": 1, "ExpectLocalIn": 1,
+    "ExpectLocalV2D": 1, "ExpectLocalV3D": 1, "ExpectLocalP": 1, "ExpectLocalHostA": 1,
+    "ExpectLocalRTD": 1, "ExpectLocalPreI2D": 1, "ExpectLocalPreI3D": 1, "ExpectLocalM": 1,
+    "ExpectLocalHostF": 1, "ExpectLocalFin": 1, "ExpectFreeIdx": 1, "ExpectGlobal2D": 1,
+    "ExpectRotran": 1, "ExpectProject": 1, "ExpectGlobal3D": 1, "InsertI2D": 1, "InsertFT": 2,
+    "PrepareTF": 1, "ExposePT2D": 1, "ExposePT": 1, "ExposeWT2D": 2, "AllocDevicePoint": 1,
+    "HostDeviceInit": 1, "ExposeC": 1, "ExposeForConvC": 1, "ExposeWC": 1,
+    "FreeDevHostPoint": 1, "ExposeWT": 2, "ExposePF2D": 1, "ExposePFW": 1, "ExposePF": 1,
+    "ExposeCorrF2D": 1, "ExposeCorrF": 2, "TranslateI2D": 1, "TranslateI": 1, "ReMask": 1,
+    "GCTFinit": 1,
+}
+
+
 def blocks():
     txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     out = []
@@ -29,13 +46,9 @@ def blocks():
 
 def test_integration_blocks_present():
     iface, handles = blocks()
-    # every hot-path Interface.h entry point of SURVEY §8(b) is forwarded
-    for fn in ("getAviDevice", "ExpectRotran", "ExpectProject", "ExpectGlobal3D", "ExpectPreidx",
-               "ExpectPrefre", "ExpectLocalIn", "ExpectLocalV3D", "ExpectLocalP",
-               "ExpectLocalHostA", "ExpectLocalRTD", "ExpectLocalPreI3D", "ExpectLocalM",
-               "ExpectLocalHostF", "ExpectLocalFin", "ExpectFreeIdx", "InsertFT",
-               "ExpectGlobal2D", "ExpectLocalV2D", "ExpectLocalPreI2D", "InsertI2D"):
-        assert re.search(rf"\bvoid {fn}\(", iface), fn
+    # every Interface.h entry point src/ calls is forwarded, overloads included
+    for fn, n in SRC_CALLED.items():
+        assert len(re.findall(rf"^void {fn}\(", iface, re.M)) == n, fn
     assert "thx_tex_create" in handles and "thx_calpoint_create" in handles
 
 
@@ -62,8 +75,15 @@ def test_forwards_compile_and_link(tmp_path):
     for sig in ("ExpectLocalM(int, int, ManagedCalPoint*", "InsertFT(Volume&, Volume&, double*, int*",
                 "ManagedCalPoint::Init(int, int, int, int, int, int, int)", "getAviDevice(",
                 "InsertI2D(Complex*, float*, double*, int*, ompi_communicator_t*&",
-                "ExpectGlobal2D(Complex*, Complex*, float*"):
+                "ExpectGlobal2D(Complex*, Complex*, float*",
+                "ExposeWC(int, Volume&, Complex*, float*, float*, float*, float*, float*, int*, int*, "
+                "void**, float&", "ExposeCorrF(int, Volume&, Volume&, float*, float)",
+                "ReMask(std::vector<Image, std::allocator<Image> >&", "PrepareTF(int, Volume&, Volume&"):
         assert sig.split("ompi")[0] in nm, sig
+    # every forward is a defined, exported symbol of the drop-in library
+    defined = re.findall(r"^[0-9a-f]+ T (\w+)\(", nm, re.M)
+    for fn, n in SRC_CALLED.items():
+        assert defined.count(fn) == n, (fn, defined.count(fn))
 
 
 def test_drifted_forward_fails_to_compile(tmp_path):

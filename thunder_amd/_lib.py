@@ -174,6 +174,34 @@ SIGNATURES = {
                                _c_int, _c_int, _c_int, _c_int]),
     "thx_InsertFTComm": (_c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int,
                                   _c_int, _c_int, _c_int, _c_int, _p]),
+    # reconstruction host adapters (Interface.h:320-528)
+    "thx_PrepareTF": (_c_int, [_c_int, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
+    "thx_ExposePT": (_c_int, [_c_int, _p, _c_int, _c_int, _c_int, _p, _c_int, _c_int, _c_int]),
+    "thx_ExposePT2D": (_c_int, [_c_int, _p, _c_int, _c_int, _c_int, _p, _c_int, _c_int, _c_int]),
+    "thx_ExposeWT": (_c_int, [_c_int, _p, _p, _p, _c_float, _c_int, _c_float, _c_int, _c_int, _c_int,
+                              _c_int, _c_int, _c_int, _p]),
+    "thx_ExposeWT2D": (_c_int, [_c_int, _p, _p, _p, _c_float, _c_int, _c_float, _c_int, _c_int, _c_int,
+                                _c_int, _c_int, _c_int, _p]),
+    "thx_ExposeWT_T": (_c_int, [_c_int, _p, _p, _c_int, _c_int, _c_int]),
+    "thx_ExposeWT2D_T": (_c_int, [_c_int, _p, _p, _c_int, _c_int, _c_int]),
+    "thx_AllocDevicePoint": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int]),
+    "thx_HostDeviceInit": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int,
+                                    _c_int]),
+    "thx_ExposeC": (_c_int, [_c_int, _p, _p, _p, _p, _p, _c_int, _c_int]),
+    "thx_ExposeForConvC": (_c_int, [_c_int, _p, _p, _p, _p, _c_float, _c_int, _c_float, _c_int, _c_int,
+                                    _c_int, _c_int]),
+    "thx_ExposeWC": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
+    "thx_FreeDevHostPoint": (_c_int, [_c_int, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_int, _c_int]),
+    "thx_ExposePFW": (_c_int, [_c_int, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
+    "thx_ExposePF": (_c_int, [_c_int, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
+    "thx_ExposePF2D": (_c_int, [_c_int, _p, _p, _p, _c_int, _c_int, _c_int, _c_int]),
+    "thx_ExposeCorrF": (_c_int, [_c_int, _p, _p, _c_float, _c_int]),
+    "thx_ExposeCorrFT": (_c_int, [_c_int, _p, _p, _p, _c_float, _c_int]),
+    "thx_ExposeCorrF2D": (_c_int, [_c_int, _p, _p, _p, _c_float, _c_int]),
+    "thx_TranslateI": (_c_int, [_c_int, _p, _c_double, _c_double, _c_double, _c_int, _c_int]),
+    "thx_TranslateI2D": (_c_int, [_c_int, _p, _c_double, _c_double, _c_int, _c_int]),
+    "thx_ReMask": (_c_int, [_p, _c_float, _c_float, _c_float, _c_int, _c_int]),
+    "thx_GCTFinit": (_c_int, [_p, _p, _c_float, _c_int, _c_int]),
 }
 
 _lib = None
