@@ -181,12 +181,12 @@ def scan_roofline(vol, px, gset, dat, ctf, sig, algo, reps=3):
     return sec, issued, algorithmic, peak
 
 
-def local_roofline(vol, N, pf, device, n_img=512, reps=3, spreads=(1.5, 3.0, 0.0)):
+def local_roofline(vol, N, pf, device, n_img=512, reps=3, spreads=(1.5, 2.0, 3.0, 0.0)):
     """Full-resolution particle-filter phase (nPxl = 24746 at box 256,
     mLR = 125, mLT = 9): algorithmic bytes 64 * mLR * nPxl + 16 * nPxl per
     image-phase.  Clouds of `spreads` degrees around one pose per image (the
     narrow clouds of a C5-style local refinement; 0 = uniformly random
-    rotations, every tap a gather), each in the half-complex layout (taps of
+    rotations, every tap a gather; 2.0 = SURVEY 8(d)'s sigma), each in the half-complex layout (taps of
     compact patches staged in LDS boxes, the rest gathered row by row) and
     in the cell-expanded layout (every sample one quad-cooperative 64-B cell
     read) and the y-pair copy (pair form: two 32-B pieces per sample)."""
@@ -687,6 +687,18 @@ def main():
             extras["reconstruct_ms_per_halfmap"] = (time.perf_counter() - t1) * 1e3 / 2
             extras["reconstruct_ms_two_halfmaps_concurrent"] = (time.perf_counter() - t1) * 1e3
             extras["reconstruct_balancing_iterations"] = [o[2] for o in recs_out]
+            # one half-map's solve alone, for the concurrency ratio
+            hm1 = ops.HalfMap(recs[0].hm.vdim, dev)
+            hm1.F.copy_(recs[0].hm.F)
+            hm1.T.copy_(T0[0])
+            ops.reconstruct(hm1, N, pf)               # this stream's plans (first call)
+            hm1.T.copy_(T0[0])
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            ops.reconstruct(hm1, N, pf)
+            torch.cuda.synchronize()
+            extras["reconstruct_ms_one_halfmap_alone"] = (time.perf_counter() - t1) * 1e3
+            del hm1
             fsc = ops.fsc(recs_out[0][1], recs_out[1][1], N // 2)
             extras["reconstructed_fsc_shells_4_16_32_64"] = [round(float(fsc[k]), 4)
                                                            for k in (4, 16, 32, 64)]

@@ -185,6 +185,44 @@ THX_DEV float2 ypair_pair_part(const float4* __restrict__ yp, int vdim, const Ce
     const float im = q0.y * w00 + q0.w * w01 + q1.y * w10 + q1.w * w11;
     return make_float2(re, c.conj ? -im : im);
 }
+// A pair-form sample as its rotating lane hands it to the pair: the two
+// slices' element offsets (32-bit: the y-pair copy has < 2^31 elements up to
+// vdim 1024) and the fractions, the Hermitian fold in dx's sign bit -- five
+// DPP broadcasts and one address computation per sample instead of seven
+// broadcasts and 64-bit index arithmetic in both lanes.
+struct PCell {
+    unsigned e0, e1;
+    float dx, dy, dz;
+};
+THX_DEV PCell pcell_of(float x, float y, float z, int vdim)
+{
+    const bool conj = !(x >= 0.f);
+    if (conj) { x = -x; y = -y; z = -z; }
+    const float fx = floorf(x), fy = floorf(y), fz = floorf(z);
+    const int x0 = (int)fx, y0 = (int)fy, z0 = (int)fz;
+    const unsigned nc = (unsigned)(vdim / 2 + 1);
+    const unsigned yw = (unsigned)wrap_idx(y0, vdim);
+    PCell c;
+    c.e0 = ((unsigned)wrap_idx(z0, vdim) * (unsigned)vdim + yw) * nc + (unsigned)x0;
+    c.e1 = ((unsigned)wrap_idx(z0 + 1, vdim) * (unsigned)vdim + yw) * nc + (unsigned)x0;
+    c.dx = __uint_as_float(__float_as_uint(x - fx) | (conj ? 0x80000000u : 0u));
+    c.dy = y - fy;
+    c.dz = z - fz;
+    return c;
+}
+// lane j of the pair: element x0 + j of slices z0 and z0 + 1
+THX_DEV float2 ypair_pcell_part(const float4* __restrict__ yp, const PCell& c, int j)
+{
+    const float4 q0 = yp[c.e0 + (unsigned)j], q1 = yp[c.e1 + (unsigned)j];
+    const bool conj = (__float_as_uint(c.dx) >> 31) != 0;
+    const float dx = fabsf(c.dx);
+    const float wx = j ? dx : 1.f - dx;
+    const float wa = wx * (1.f - c.dz), wb = wx * c.dz;
+    const float w00 = wa * (1.f - c.dy), w01 = wa * c.dy, w10 = wb * (1.f - c.dy), w11 = wb * c.dy;
+    const float re = q0.x * w00 + q0.z * w01 + q1.x * w10 + q1.z * w11;
+    const float im = q0.y * w00 + q0.w * w01 + q1.y * w10 + q1.w * w11;
+    return make_float2(re, conj ? -im : im);
+}
 // the pair's other lane's value (DPP quad_perm [1, 0, 3, 2])
 THX_DEV float pair_swap(float v)
 {
@@ -196,6 +234,17 @@ THX_DEV int pair_bcast(int v)
 {
     return __builtin_amdgcn_update_dpp(0, v, IT | (IT << 2) | ((2 + IT) << 4) | ((2 + IT) << 6), 0xf,
                                        0xf, false);
+}
+template <int IT>
+THX_DEV PCell pair_bcast_pcell(const PCell& c)
+{
+    PCell o;
+    o.e0 = (unsigned)pair_bcast<IT>((int)c.e0);
+    o.e1 = (unsigned)pair_bcast<IT>((int)c.e1);
+    o.dx = __int_as_float(pair_bcast<IT>(__float_as_int(c.dx)));
+    o.dy = __int_as_float(pair_bcast<IT>(__float_as_int(c.dy)));
+    o.dz = __int_as_float(pair_bcast<IT>(__float_as_int(c.dz)));
+    return o;
 }
 template <int IT>
 THX_DEV Cell pair_bcast_cell(const Cell& c)
@@ -801,6 +850,14 @@ k_local_fused(const float2* __restrict__ vol,
         quat_to_mat(q, mm);
         for (int k = 0; k < 6; k++) m[k] = mm[k];
     }
+#ifndef THX_PAIR_F32ROT
+#define THX_PAIR_F32ROT 0
+#endif
+    // A/B: the pair path's rotation in FP32 (the reference rotates in FP64)
+    float mf[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) mf[k] = (float)m[k];
+    (void)mf;
     // columns: translations, or (t, d) pairs for CS (nT counts the columns)
     if (tid < NC) {
         const int t = CS ? (t0 + tid) / nD : t0 + tid;
@@ -1014,17 +1071,40 @@ k_local_fused(const float2* __restrict__ vol,
         // 4s, 4s + 2) from the h = 0 pairs, (4s + 1, 4s + 3) from the h = 1 pairs.
         auto pair_step = [&](int s) {
             const int j = lane & 1, h = (lane >> 5) & 1;
+#ifndef THX_PAIR_PCELL
+#define THX_PAIR_PCELL 1
+#endif
+#if THX_PAIR_PCELL
+            PCell mine;
+            {
+                const double2 xy = sXY[4 * s + h + 2 * j];
+#if THX_PAIR_F32ROT
+                const float fx = (float)xy.x, fy = (float)xy.y;
+                mine = pcell_of(fmaf(mf[0], fx, mf[3] * fy), fmaf(mf[1], fx, mf[4] * fy),
+                                fmaf(mf[2], fx, mf[5] * fy), vdim);
+#else
+                mine = pcell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
+                                (float)(m[2] * xy.x + m[5] * xy.y), vdim);
+#endif
+            }
+#else
             Cell mine;
             {
                 const double2 xy = sXY[4 * s + h + 2 * j];
                 mine = cell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                (float)(m[2] * xy.x + m[5] * xy.y));
             }
+#endif
             float2 P[2];
 #pragma unroll
             for (int it = 0; it < 2; it++) {
+#if THX_PAIR_PCELL
+                const PCell c = it == 0 ? pair_bcast_pcell<0>(mine) : pair_bcast_pcell<1>(mine);
+                const float2 v = ypair_pcell_part(reinterpret_cast<const float4*>(vol), c, j);
+#else
                 const Cell c = it == 0 ? pair_bcast_cell<0>(mine) : pair_bcast_cell<1>(mine);
                 const float2 v = ypair_pair_part(reinterpret_cast<const float4*>(vol), vdim, c, j);
+#endif
                 P[it] = make_float2(v.x + pair_swap(v.x), v.y + pair_swap(v.y));
             }
             if (!CS)
@@ -1056,7 +1136,10 @@ k_local_fused(const float2* __restrict__ vol,
             // 90.1k vs 87.5k images/s with the per-step branch
             // (profiles/r04_pair_pipe_ab.jsonl; an explicit two-step software
             // pipeline needs 112 VGPRs, 4 waves per SIMD: 83k)
-#pragma unroll
+#ifndef THX_PAIR_UNROLL
+#define THX_PAIR_UNROLL 2
+#endif
+#pragma unroll THX_PAIR_UNROLL
             for (int s = 0; s < 4 * PP; s++) pair_step(s);
         } else if (COOP) {
 // all four steps unrolled: 16 cell reads in flight per wave (C5 +3-4 %,

@@ -40,6 +40,7 @@
 #include <tuple>
 
 #include "common.h"
+#include "fft_lds.h"
 
 #define THX_FFT(call)                                                          \
     do {                                                                       \
@@ -311,6 +312,229 @@ __global__ void __launch_bounds__(CF_THREADS) k_col_fft(float2* __restrict__ a, 
     }
 }
 
+// ------------------------------------------ balancing on the even half-grid
+// Inside the balancing loop C = T W is real, and real + Hermitian makes it
+// point-even, C(-k) = C(k); so is c = IFFT(C), c times the (even) kernel,
+// and the forward transform of that.  A real point-even array is determined
+// by half of it, and both transforms of the iteration run on half grids
+// (N = vdim, H = N / 2 + 1):
+//   frequency side: C / W / T on the half-complex grid [kz][ky][kx < H];
+//   space side:     c on [nz < H][ny][nx];
+//   between:        G [nz < H][ky or ny][kx < H] complex (H N H, half of a
+//                   full half-complex volume).
+// One iteration is four passes over G (each column / row transformed in
+// LDS by one wave, wave_fft in fft_lds.h):
+//   x rows   (nz, ny): Hermitian in kx -> C2R (+) -> c * kernel / N^3 -> R2C (-)
+//   y columns (nz, kx): C2C (-);
+//   z columns (ky, kx): Hermitian in nz (G(-nz) = conj G(nz)) -> C2R (-) =
+//             the balanced C of this iteration -> W /= max(|C|, 1e-6) inside,
+//             max | |C| - 1 | -> next C = T W -> R2C (+) along z;
+//   y columns (nz, kx): C2C (+);
+// against two full 3D transforms and two element passes over N^3 arrays.
+// The kx = 0 and kx = N / 2 planes of T are replaced by their Hermitian
+// average first: a C2R reads only that average of those planes (FFTW,
+// hipFFT and numpy's irfftn alike), so the balanced W is unchanged.
+#ifndef EVEN_BALANCE
+#define EVEN_BALANCE 1             // 0: the hipFFT loop everywhere (A/B builds)
+#endif
+constexpr int EV_CT = 16;          // columns per tile of the column passes
+constexpr int EV_WAVES = 4;
+
+bool even_ok(int vdim) { return vdim == 64 || vdim == 128 || vdim == 256 || vdim == 512; }
+
+template <int N>
+constexpr size_t even_col_lds() { return (size_t)(EV_CT * N + EV_WAVES * N) * sizeof(float2); }
+
+template <int N>
+constexpr size_t even_row_lds() { return (size_t)EV_WAVES * 2 * N * sizeof(float2); }
+
+// T on the kx = 0 and kx = N / 2 planes := (T(k) + T(-k)) / 2
+__global__ void k_sym_planes(float* __restrict__ T, int vdim)
+{
+    const int nc = vdim / 2 + 1;
+    const long n = 2L * vdim * vdim;
+    GRID_STRIDE(q, n)
+    {
+        const int x = q < (long)vdim * vdim ? 0 : vdim / 2;
+        const long jk = q % ((long)vdim * vdim);
+        const int j = (int)(jk % vdim), k = (int)(jk / vdim);
+        const int pj = (vdim - j) % vdim, pk = (vdim - k) % vdim;
+        const long a = ((long)k * vdim + j) * nc + x, b = ((long)pk * vdim + pj) * nc + x;
+        if (a < b) {
+            const float m = 0.5f * (T[a] + T[b]);
+            T[a] = m;
+            T[b] = m;
+        }
+    }
+}
+
+// z columns.  INIT: C = T W (W as k_init_w left it) -> R2C (+) along z.
+// Otherwise first the C2R (-) along z of G's Hermitian nz-half: the balanced
+// C, whose |C| updates W inside the sphere (and the max | |C| - 1 |), then the
+// same as INIT.  Grid (ceil(H / EV_CT), N): a tile of EV_CT kx columns at one ky.
+template <int N, bool INIT>
+__global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G, float* __restrict__ W,
+                                                         const float* __restrict__ T, int r2,
+                                                         unsigned* __restrict__ diffBits,
+                                                         const float2* __restrict__ tw)
+{
+    extern __shared__ float2 sm[];
+    constexpr int H = N / 2 + 1, M = N - 1;
+    float2* tile = sm;                                   // [EV_CT][N], column c rotated by c
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    float2* scr = sm + EV_CT * N + wv * N;
+    const int kx0 = blockIdx.x * EV_CT, ky = blockIdx.y;
+    const int ncol = min(EV_CT, H - kx0);
+    const int c = tid % EV_CT, rr = tid / EV_CT;         // row mapping: column c, rows rr + 16 i
+    constexpr int RSTEP = 64 * EV_WAVES / EV_CT;
+    const int jy = ky < N / 2 ? ky : ky - N;
+    const int ix = kx0 + c;
+    if (!INIT) {
+        for (int nz = rr; nz < H; nz += RSTEP) {
+            const float2 v = c < ncol ? G[((size_t)nz * N + ky) * H + ix] : make_float2(0.f, 0.f);
+            tile[c * N + ((nz + c) & M)] = v;
+            if (nz > 0 && nz < N / 2) tile[c * N + ((N - nz + c) & M)] = make_float2(v.x, -v.y);
+        }
+        __syncthreads();
+        for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * N, cc, scr, tw, -1.f, lane);
+        __syncthreads();
+    }
+    float dmax = 0.f;
+    if (c < ncol) {
+        for (int kz = rr; kz < N; kz += RSTEP) {
+            const size_t e = ((size_t)kz * N + ky) * H + ix;
+            float w = W[e];
+            if (!INIT) {
+                const int jz = kz < N / 2 ? kz : kz - N;
+                if (ix * ix + jy * jy + jz * jz < r2) {
+                    const float m = fabsf(tile[c * N + ((kz + c) & M)].x);
+                    w = w / fmaxf(m, 1e-6f);
+                    W[e] = w;
+                    dmax = fmaxf(dmax, fabsf(m - 1.f));
+                }
+            }
+            tile[c * N + ((kz + c) & M)] = make_float2(T[e] * w, 0.f);
+        }
+    }
+    __syncthreads();
+    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * N, cc, scr, tw, 1.f, lane);
+    __syncthreads();
+    if (c < ncol)
+        for (int nz = rr; nz < H; nz += RSTEP) G[((size_t)nz * N + ky) * H + ix] = tile[c * N + ((nz + c) & M)];
+    if (!INIT) {
+        dmax = wave_max(dmax);
+        __shared__ float sMax[EV_WAVES];
+        if (lane == 0) sMax[wv] = dmax;
+        __syncthreads();
+        if (tid == 0) {
+            float m = sMax[0];
+            for (int k = 1; k < EV_WAVES; k++) m = fmaxf(m, sMax[k]);
+            if (m > 0.f) atomicMax(diffBits, __float_as_uint(m));
+        }
+    }
+}
+
+// y columns: C2C along y, sign S.  Grid (ceil(H / EV_CT), H): one nz per row of tiles.
+template <int N, int S>
+__global__ void __launch_bounds__(64 * EV_WAVES) k_even_y(float2* __restrict__ G, const float2* __restrict__ tw)
+{
+    extern __shared__ float2 sm[];
+    constexpr int H = N / 2 + 1, M = N - 1;
+    float2* tile = sm;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    float2* scr = sm + EV_CT * N + wv * N;
+    const int kx0 = blockIdx.x * EV_CT, nz = blockIdx.y;
+    const int ncol = min(EV_CT, H - kx0);
+    const int c = tid % EV_CT, rr = tid / EV_CT;
+    constexpr int RSTEP = 64 * EV_WAVES / EV_CT;
+    float2* base = G + (size_t)nz * N * H + kx0 + c;
+    if (c < ncol)
+        for (int y = rr; y < N; y += RSTEP) tile[c * N + ((y + c) & M)] = base[(size_t)y * H];
+    __syncthreads();
+    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * N, cc, scr, tw, (float)S, lane);
+    __syncthreads();
+    if (c < ncol)
+        for (int y = rr; y < N; y += RSTEP) base[(size_t)y * H] = tile[c * N + ((y + c) & M)];
+}
+
+// x rows (nz < H, ny): the Hermitian kx-half -> C2R (+) -> times the kernel
+// octant (1 / N^3 and 1 / nf included) -> R2C (-), in place.  One wave per row.
+template <int N>
+__global__ void __launch_bounds__(64 * EV_WAVES) k_even_x(float2* __restrict__ G, const float* __restrict__ oct,
+                                                         const float2* __restrict__ tw)
+{
+    extern __shared__ float2 sm[];
+    constexpr int H = N / 2 + 1;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const long row = (long)blockIdx.x * EV_WAVES + wv;
+    if (row >= (long)H * N) return;
+    float2* buf = sm + wv * 2 * N;
+    float2* scr = buf + N;
+    float2* g = G + row * H;
+    for (int x = lane; x < H; x += 64) {
+        const float2 v = g[x];
+        buf[x] = v;
+        if (x > 0 && x < N / 2) buf[N - x] = make_float2(v.x, -v.y);
+    }
+    thx::wave_lds_sync();
+    thx::wave_fft<N>(buf, 0, scr, tw, 1.f, lane);
+    const int nz = (int)(row / N), ny = (int)(row % N);
+    const int ay = ny <= N / 2 ? ny : N - ny;
+    const float* o = oct + ((size_t)nz * H + ay) * H;
+    for (int x = lane; x < N; x += 64) {
+        const int ax = x <= N / 2 ? x : N - x;
+        buf[x] = make_float2(buf[x].x * o[ax], 0.f);
+    }
+    thx::wave_lds_sync();
+    thx::wave_fft<N>(buf, 0, scr, tw, -1.f, lane);
+    for (int x = lane; x < H; x += 64) g[x] = buf[x];
+}
+
+template <int N>
+int even_iteration_n(float2* G, float* W, const float* T, const float* oct, int r2, unsigned* diff,
+                     const float2* tw, bool init, bool update, hipStream_t s)
+{
+    constexpr int H = N / 2 + 1;
+    const dim3 b(64 * EV_WAVES);
+    const dim3 gz((H + EV_CT - 1) / EV_CT, N), gy((H + EV_CT - 1) / EV_CT, H);
+    const dim3 gx((unsigned)(((long)H * N + EV_WAVES - 1) / EV_WAVES));
+    constexpr size_t lc = even_col_lds<N>(), lr = even_row_lds<N>();
+    static std::atomic<unsigned> set[5];
+    THX_RET(thx::set_max_lds(reinterpret_cast<const void*>(k_even_z<N, true>), (int)lc, set[0]));
+    THX_RET(thx::set_max_lds(reinterpret_cast<const void*>(k_even_z<N, false>), (int)lc, set[1]));
+    THX_RET(thx::set_max_lds(reinterpret_cast<const void*>(k_even_y<N, 1>), (int)lc, set[2]));
+    THX_RET(thx::set_max_lds(reinterpret_cast<const void*>(k_even_y<N, -1>), (int)lc, set[3]));
+    THX_RET(thx::set_max_lds(reinterpret_cast<const void*>(k_even_x<N>), (int)lr, set[4]));
+    if (init) {
+        hipLaunchKernelGGL((k_even_z<N, true>), gz, b, lc, s, G, W, T, r2, diff, tw);
+        THX_LAUNCH_CHECK();
+    }
+    if (update) {
+        hipLaunchKernelGGL((k_even_y<N, 1>), gy, b, lc, s, G, tw);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL((k_even_x<N>), gx, b, lr, s, G, oct, tw);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL((k_even_y<N, -1>), gy, b, lc, s, G, tw);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL((k_even_z<N, false>), gz, b, lc, s, G, W, T, r2, diff, tw);
+        THX_LAUNCH_CHECK();
+    }
+    return THX_OK;
+}
+
+// init: G = R2C_z(T W); update: one balancing iteration (W, diff updated, G = the next C's z-transform)
+int even_iteration(int vdim, float2* G, float* W, const float* T, const float* oct, long r2,
+                   unsigned* diff, const float2* tw, bool init, bool update, hipStream_t s)
+{
+    switch (vdim) {
+        case 64: return even_iteration_n<64>(G, W, T, oct, (int)r2, diff, tw, init, update, s);
+        case 128: return even_iteration_n<128>(G, W, T, oct, (int)r2, diff, tw, init, update, s);
+        case 256: return even_iteration_n<256>(G, W, T, oct, (int)r2, diff, tw, init, update, s);
+        case 512: return even_iteration_n<512>(G, W, T, oct, (int)r2, diff, tw, init, update, s);
+        default: thx::set_error("even balancing: unsupported vdim %d", vdim); return THX_ERR_ARG;
+    }
+}
+
 // ---------------------------------------------------------- MKB kernel table
 // MKB_RL_R2 (src/Functions/Functions.cpp, FUNCTIONS_MKB_ORDER_0):
 // (2 pi)^1.5 a^3 / I0(alpha) * I_{3/2}(v) / v^1.5 (u^2 <= alpha^2) or
@@ -353,7 +577,7 @@ double mkb_rl_r2(double r2, double a, double alpha)
 struct Plans {
     hipfftHandle c2r = 0, r2c = 0, r2cN = 0;
     hipfftHandle c2rX = 0, r2cX = 0;     // 1D batched along x (the column-pass transforms)
-    float2* tw = nullptr;                // vdim / 2 twiddles exp(-2 pi i k / vdim)
+    float2* tw = nullptr;                // vdim twiddles exp(-2 pi i k / vdim)
     bool cols = false;                   // the column-pass transforms are available
     size_t work = 0;
 };
@@ -392,8 +616,8 @@ int make_plans(Plans& p, int vdim, int N)
         THX_FFT(hipfftMakePlanMany(p.r2cX, 1, n, n, 1, vdim, nh, 1, vdim / 2 + 1, HIPFFT_R2C, batch,
                                    &w5));
         p.work = std::max(p.work, std::max(w4, w5));
-        std::vector<float2> h(vdim / 2);
-        for (int k = 0; k < vdim / 2; k++) {
+        std::vector<float2> h(vdim);     // the column passes read k < vdim / 2, the even loop all
+        for (int k = 0; k < vdim; k++) {
             const double t = -2.0 * M_PI * k / vdim;
             h[k] = make_float2((float)std::cos(t), (float)std::sin(t));
         }
@@ -620,20 +844,34 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
         int nNoDec = 0;
         const dim3 gSlab(RB_SPLIT, vdim), bSlab(RB_THREADS);
         const unsigned mVdim = magic_u((unsigned)vdim), mNc = magic_u((unsigned)(vdim / 2 + 1));
-        hipLaunchKernelGGL(k_c_from_tw, g, b, 0, s, C, T, W, nFT);
-        THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_kernel_octant, g, b, 0, s, oct, vdim, tab, nf, scaleBw);
         THX_LAUNCH_CHECK();
+        // the even half-grid loop where its transforms exist, else two hipFFT
+        // 3D transforms per iteration
+        const bool even = EVEN_BALANCE && even_ok(vdim) && pl.tw;
+        if (even) {
+            hipLaunchKernelGGL(k_sym_planes, g, b, 0, s, T, vdim);
+            THX_LAUNCH_CHECK();
+            THX_RET(even_iteration(vdim, C, W, T, oct, r2, diff, pl.tw, true, false, s));
+        } else {
+            hipLaunchKernelGGL(k_c_from_tw, g, b, 0, s, C, T, W, nFT);
+            THX_LAUNCH_CHECK();
+        }
         unsigned* bits = pe->bits;   // the entry's pinned word (no allocation per solve)
         for (m = 0; m < 30; m++) {                                // MAX_N_ITER_BALANCE
-            THX_RET(c2r3d(pl, C, rl, vdim, s));
-            hipLaunchKernelGGL(k_kernel_mul, gSlab, bSlab, 0, s, rl, vdim, oct, mVdim);
-            THX_LAUNCH_CHECK();
-            THX_RET(r2c3d(pl, rl, C, vdim, s));
-            THX_HIP(hipMemsetAsync(diff, 0, sizeof(unsigned), s));
-            // W update + the next iteration's C in one pass
-            hipLaunchKernelGGL(k_update_w, gSlab, bSlab, 0, s, W, C, T, vdim, r2, mNc, diff);
-            THX_LAUNCH_CHECK();
+            if (even) {
+                THX_HIP(hipMemsetAsync(diff, 0, sizeof(unsigned), s));
+                THX_RET(even_iteration(vdim, C, W, T, oct, r2, diff, pl.tw, false, true, s));
+            } else {
+                THX_RET(c2r3d(pl, C, rl, vdim, s));
+                hipLaunchKernelGGL(k_kernel_mul, gSlab, bSlab, 0, s, rl, vdim, oct, mVdim);
+                THX_LAUNCH_CHECK();
+                THX_RET(r2c3d(pl, rl, C, vdim, s));
+                THX_HIP(hipMemsetAsync(diff, 0, sizeof(unsigned), s));
+                // W update + the next iteration's C in one pass
+                hipLaunchKernelGGL(k_update_w, gSlab, bSlab, 0, s, W, C, T, vdim, r2, mNc, diff);
+                THX_LAUNCH_CHECK();
+            }
             THX_HIP(hipMemcpyAsync(bits, diff, sizeof(unsigned), hipMemcpyDeviceToHost, s));
             THX_HIP(hipStreamSynchronize(s));
             diffPrev = diffC;

@@ -317,6 +317,18 @@ __global__ void __launch_bounds__(256) k_scan_bias(const float* __restrict__ Bc,
     }
 }
 
+// LDS stages of the chunk pipeline: chunk ck + STAGES - 1 is copied while
+// chunk ck is multiplied, so each copy has STAGES - 1 chunks to land
+#ifndef SCAN_STAGES
+#define SCAN_STAGES 3
+#endif
+
+template <int N>
+THX_DEV void wait_vm()
+{
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 template <int MODE, int NF>
 struct Smem {
     static constexpr int NTP = NF * 32;
@@ -339,7 +351,7 @@ struct Smem {
     static constexpr int P_OFF = (NPLANE * TQ + AQ) * 1024;
     static constexpr int STAGE_B = NQ * 1024;
     static constexpr int EPI_B = ROT_TILE * 64 * 3 * 4 + 32 * NTP * 8;
-    static constexpr int TOTAL_B = 2 * STAGE_B > EPI_B ? 2 * STAGE_B : EPI_B;
+    static constexpr int TOTAL_B = SCAN_STAGES * STAGE_B > EPI_B ? SCAN_STAGES * STAGE_B : EPI_B;
 };
 
 // 16 bytes global -> LDS without registers: lane L's piece lands at
@@ -420,14 +432,28 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
             }
         }
     };
-    auto stage_at = [&](int ck) { return lds + (ck & 1) * S::STAGE_B; };
+    auto stage_at = [&](int ck) { return lds + (ck % SCAN_STAGES) * S::STAGE_B; };
     const int nCk = nPxlPad / KC;
-    issue_chunk(0, stage_at(0));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // LDS-DMA instructions this wave issues per chunk (issue_chunk's q = u NWAVE + w)
+    constexpr int QLO = S::NQ / NWAVE, QREM = S::NQ % NWAVE;
+    const bool qHi = w < QREM;
+    // wait until at most the copies of the newest `ahead` chunks are in flight
+    auto wait_ahead = [&](int ahead) {
+        if (SCAN_STAGES == 3 && ahead == 1) {
+            if (qHi) wait_vm<QLO + 1>(); else wait_vm<QLO>();
+        } else {
+            wait_vm<0>();
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < SCAN_STAGES - 1; k++)
+        if (k < nCk) issue_chunk(k, stage_at(k));
+    wait_ahead(nCk > 1 && SCAN_STAGES == 3 ? 1 : 0);
     __syncthreads();
     for (int ck = 0; ck < nCk; ck++) {
-        const bool more = ck + 1 < nCk;
-        if (more) issue_chunk(ck + 1, stage_at(ck + 1));
+        // the stage chunk ck + STAGES - 1 lands in was last read in chunk ck - 1
+        const bool more = ck + SCAN_STAGES - 1 < nCk;
+        if (more) issue_chunk(ck + SCAN_STAGES - 1, stage_at(ck + SCAN_STAGES - 1));
         const char* stage = stage_at(ck);
         const uint16_t* sTh = reinterpret_cast<const uint16_t*>(stage);
         const uint16_t* sTl = reinterpret_cast<const uint16_t*>(stage + S::TL_OFF);
@@ -489,7 +515,8 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                 }
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // chunk ck + 1 must have landed; the newer copy may stay in flight
+        wait_ahead(more && SCAN_STAGES == 3 ? 1 : 0);
         __syncthreads();
     }
 
