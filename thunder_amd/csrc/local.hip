@@ -210,10 +210,31 @@ THX_DEV PCell pcell_of(float x, float y, float z, int vdim)
     c.dz = z - fz;
     return c;
 }
-// lane j of the pair: element x0 + j of slices z0 and z0 + 1
-THX_DEV float2 ypair_pcell_part(const float4* __restrict__ yp, const PCell& c, int j)
+// lane j of the pair: element x0 + j of slices z0 and z0 + 1.  RSRC: the
+// y-pair copy through a buffer descriptor (32-bit byte offsets, no 64-bit
+// address arithmetic; the copy must be < 4 GiB -- ypair_bytes_ok)
+#ifndef THX_PAIR_BUF
+#define THX_PAIR_BUF 0
+#endif
+struct YpSrc {
+    const float4* p;
+#if THX_PAIR_BUF
+    __amdgpu_buffer_rsrc_t r;
+#endif
+};
+THX_DEV float4 yp_load(const YpSrc& y, unsigned e)
 {
-    const float4 q0 = yp[c.e0 + (unsigned)j], q1 = yp[c.e1 + (unsigned)j];
+#if THX_PAIR_BUF
+    typedef float f32x4v_ __attribute__((ext_vector_type(4)));
+    const f32x4v_ v = __builtin_amdgcn_raw_buffer_load_b128(y.r, e * 16u, 0, 0);
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return y.p[e];
+#endif
+}
+THX_DEV float2 ypair_pcell_part(const YpSrc& yp, const PCell& c, int j)
+{
+    const float4 q0 = yp_load(yp, c.e0 + (unsigned)j), q1 = yp_load(yp, c.e1 + (unsigned)j);
     const bool conj = (__float_as_uint(c.dx) >> 31) != 0;
     const float dx = fabsf(c.dx);
     const float wx = j ? dx : 1.f - dx;
@@ -798,6 +819,16 @@ k_local_fused(const float2* __restrict__ vol,
     }
     // classification: image l projects its own class's volume
     if (cls) vol += (size_t)cls[l] * volStride;
+    YpSrc ysrc;
+    ysrc.p = reinterpret_cast<const float4*>(vol);
+#if THX_PAIR_BUF
+    if (LAYOUT == LAYOUT_YPAIR2)
+        ysrc.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(vol), (short)0,
+                                                   (int)(unsigned)min((size_t)0xFFFFFFF0u,
+                                                                      (size_t)16 * (vdim / 2 + 1) * vdim * vdim),
+                                                   0x00020000);
+#endif
+    (void)ysrc;
     static_assert(CS || NCT == 1, "column tiles per workgroup: CTF search only");
     constexpr int BOXC = BIGBOX ? BOX_CAP_BIG : BOX_CAP;
     constexpr int NITC = BOXC / 4 / THREADS;
@@ -826,7 +857,9 @@ k_local_fused(const float2* __restrict__ vol,
     const int nRl = min(RT, nR - r0);
     __shared__ __attribute__((aligned(16))) float2 sBox[NOBOX ? 8 : BOXC];
     __shared__ __attribute__((aligned(16))) float sB[PKC * 2 * NC];  // [px][U, V][t]
-    __shared__ __attribute__((aligned(16))) double2 sXY[PKC];       // (iCol pf, iRow pf)
+    // (iCol pf, iRow pf): small integers, exact in FP32 and widened exactly to
+    // FP64 by the FP64 rotations
+    __shared__ __attribute__((aligned(8))) float2 sXY[PKC];
     __shared__ float sBq[CS ? KC * NC : PKC];                        // b = s c^2 ([px][col] for CS)
     __shared__ int sValid[PKC];                                      // 0: padding entry
     __shared__ float sTr[NC][2];
@@ -957,7 +990,7 @@ k_local_fused(const float2* __restrict__ vol,
                 sValid[q] = ok;
                 // padding entries sample the patch's first pixel (inside the box)
                 const int ic = ok ? x.ic : NOBOX ? 0 : rc.v[17], ir = ok ? x.ir : NOBOX ? 0 : rc.v[18];
-                sXY[q] = make_double2((double)(ic * pf), (double)(ir * pf));
+                sXY[q] = make_float2((float)(ic * pf), (float)(ir * pf));
             }
         }
         __syncthreads();
@@ -1020,7 +1053,7 @@ k_local_fused(const float2* __restrict__ vol,
             // shared across the quad (quad_bcast_cell)
             Cell mine;
             {
-                const double2 xy = sXY[4 * s + j];
+                const double2 xy = make_double2(sXY[4 * s + j].x, sXY[4 * s + j].y);
                 mine = cell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                (float)(m[2] * xy.x + m[5] * xy.y));
             }
@@ -1077,12 +1110,13 @@ k_local_fused(const float2* __restrict__ vol,
 #if THX_PAIR_PCELL
             PCell mine;
             {
-                const double2 xy = sXY[4 * s + h + 2 * j];
+                const float2 xyf = sXY[4 * s + h + 2 * j];
 #if THX_PAIR_F32ROT
-                const float fx = (float)xy.x, fy = (float)xy.y;
+                const float fx = xyf.x, fy = xyf.y;
                 mine = pcell_of(fmaf(mf[0], fx, mf[3] * fy), fmaf(mf[1], fx, mf[4] * fy),
                                 fmaf(mf[2], fx, mf[5] * fy), vdim);
 #else
+                const double2 xy = make_double2(xyf.x, xyf.y);
                 mine = pcell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                 (float)(m[2] * xy.x + m[5] * xy.y), vdim);
 #endif
@@ -1090,7 +1124,7 @@ k_local_fused(const float2* __restrict__ vol,
 #else
             Cell mine;
             {
-                const double2 xy = sXY[4 * s + h + 2 * j];
+                const double2 xy = make_double2(sXY[4 * s + h + 2 * j].x, sXY[4 * s + h + 2 * j].y);
                 mine = cell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                (float)(m[2] * xy.x + m[5] * xy.y));
             }
@@ -1100,7 +1134,7 @@ k_local_fused(const float2* __restrict__ vol,
             for (int it = 0; it < 2; it++) {
 #if THX_PAIR_PCELL
                 const PCell c = it == 0 ? pair_bcast_pcell<0>(mine) : pair_bcast_pcell<1>(mine);
-                const float2 v = ypair_pcell_part(reinterpret_cast<const float4*>(vol), c, j);
+                const float2 v = ypair_pcell_part(ysrc, c, j);
 #else
                 const Cell c = it == 0 ? pair_bcast_cell<0>(mine) : pair_bcast_cell<1>(mine);
                 const float2 v = ypair_pair_part(reinterpret_cast<const float4*>(vol), vdim, c, j);
@@ -1157,7 +1191,7 @@ k_local_fused(const float2* __restrict__ vol,
 #pragma unroll
             for (int s = 0; s < 4 * PP; s++) {
                 if (pad_step(s)) continue;
-                const double2 xy = sXY[4 * s + g];
+                const double2 xy = make_double2(sXY[4 * s + g].x, sXY[4 * s + g].y);
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
                 const float z = (float)(m[2] * xy.x + m[5] * xy.y);
@@ -1167,7 +1201,7 @@ k_local_fused(const float2* __restrict__ vol,
 #pragma unroll 2
             for (int s = 0; s < 4 * PP; s++) {
                 if (pad_step(s)) continue;
-                const double2 xy = sXY[4 * s + g];
+                const double2 xy = make_double2(sXY[4 * s + g].x, sXY[4 * s + g].y);
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
                 const float z = (float)(m[2] * xy.x + m[5] * xy.y);
@@ -1475,6 +1509,7 @@ size_t rec_bytes(int nImg, int nR, int nVisit)
 }  // namespace
 
 namespace thx {
+bool ypair_bytes_ok(int vdim);
 
 size_t patch_rec_bytes(int nImg, int nR, int nVisit) { return rec_bytes(nImg, nR, nVisit); }
 
@@ -1570,6 +1605,9 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     if (nImg == 0) return THX_OK;
     THX_CHECK_ARG(!ypair || (volLayout == LAYOUT_FT && pxOrder && !nD),
                   "thx_local_phase_routed: a y-pair copy goes with the half-complex layout and pxOrder");
+    THX_CHECK_ARG((volLayout != LAYOUT_YPAIR2 && !ypair) || thx::ypair_bytes_ok(vdim),
+                  "thx_local_phase: the y-pair copy of vdim %d exceeds the 4 GiB its gathers address",
+                  vdim);
     const int nVisit = pxOrder ? nOrd : nPxl;
     THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase_workspace(nImg, nR, nCol, nVisit),
                   "thx_local_phase: workspace too small");
@@ -1769,6 +1807,13 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
 
 // whether local_phase_impl routes a phase on the device (half-complex layout,
 // no CTF search, 64 KiB boxes) -- the phases that can use a y-pair copy
+// the pair-form kernel addresses its y-pair copy through a buffer
+// descriptor with 32-bit byte offsets: vdim <= 812
+bool ypair_bytes_ok(int vdim)
+{
+    return (size_t)16 * (vdim / 2 + 1) * vdim * vdim <= 0xFFFFFFF0ull;
+}
+
 bool phase_routed(int volLayout, int pf, int nPxl, int nD)
 {
     return volLayout == LAYOUT_FT && !nD &&
