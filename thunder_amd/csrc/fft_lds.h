@@ -1,19 +1,34 @@
 // fft_lds.h -- one wave's complex FFT of a power-of-two length N (16 .. 512)
 // held in LDS: mixed-radix Stockham autosort stages (radix 8 while 8 divides
-// the remaining length, then one radix-4 or radix-2 stage), ping-ponging
-// between the column buffer and a scratch buffer of the wave, unnormalised,
-// sign s = -1 (forward, e^{-2 pi i k n / N}) or +1 (inverse).  Each lane takes
-// the N / R butterflies j = lane, lane + 64, ...: it reads R values a distance
-// N / R apart, applies the twiddles W_{Ns R}^{(j mod Ns) r} (the table holds
-// e^{-2 pi i q / N}, q < N), runs the R-point DFT in registers and writes the
-// outputs Ns apart from (j / Ns) Ns R + j mod Ns.
-// A column buffer may be rotated: element i of the column lives at
-// base[(i + off) & (N - 1)] (the load / store tiles of the column passes use
-// off = column index so that a row of columns spreads over the LDS banks).
+// the remaining length, then one radix-4 or radix-2 stage), unnormalised,
+// sign s = -1 (forward, e^{-2 pi i k n / N}) or +1 (inverse).  A stage has
+// N / R <= 64 butterflies: lane j reads R values N / R apart, applies the
+// twiddles W_{Ns R}^{(j mod Ns) r} (the table holds e^{-2 pi i q / N},
+// q < N), runs the R-point DFT in registers and writes the outputs Ns apart
+// from (j / Ns) Ns R + j mod Ns.  Every lane holds all its inputs in
+// registers before any lane writes (one butterfly per lane, the wave in
+// lockstep), so the stages run in place in one buffer.
+// Layout of a column: element i lives at slot q = (i + off) mod N (off: the
+// column's rotation -- the load / store tiles of the column passes rotate
+// column c by c so a row of columns spreads over the banks), stored at
+// q + q / 8: one pad slot every 8 elements, which turns the stride-8 and
+// stride-64-group writes of the first two radix-8 stages from 8-way bank
+// conflicts into the 2-way minimum of 8-byte accesses.
 #pragma once
 #include "common.h"
 
 namespace thx {
+
+// LDS slots a padded column of N elements occupies
+template <int N>
+constexpr int fft_pitch() { return N + N / 8; }
+
+template <int N>
+THX_DEV int fft_slot(int i, int off)
+{
+    const int q = (i + off) & (N - 1);
+    return q + (q >> 3);
+}
 
 THX_DEV float2 cmulf(float2 a, float2 b) { return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
 
@@ -67,53 +82,45 @@ THX_DEV void wave_lds_sync()
 }
 
 template <int N, int NS>
-THX_DEV void fft_stages(float2* a, int aOff, float2* b, int bOff, const float2* __restrict__ tw, float s,
-                        int lane, float2** out, int* outOff)
+THX_DEV void fft_stages(float2* a, int off, const float2* __restrict__ tw, float s, int lane)
 {
-    if constexpr (NS >= N) {
-        *out = a;
-        *outOff = aOff;
-    } else {
+    if constexpr (NS < N) {
         constexpr int REM = N / NS;
         constexpr int R = REM % 8 == 0 ? 8 : REM;
-        constexpr int M = N / R;            // butterflies per stage
+        constexpr int M = N / R;            // butterflies per stage (<= 64)
         constexpr int TS = N / (NS * R);    // twiddle index step
-        constexpr int MASK = N - 1;
-        for (int j = lane; j < M; j += 64) {
+        static_assert(M <= 64, "one butterfly per lane");
+        if (lane < M) {
+            const int j = lane;
             float2 v[R];
 #pragma unroll
-            for (int r = 0; r < R; r++) v[r] = a[(j + r * M + aOff) & MASK];
+            for (int r = 0; r < R; r++) v[r] = a[fft_slot<N>(j + r * M, off)];
             const int k = j % NS;
             if (NS > 1) {
 #pragma unroll
                 for (int r = 1; r < R; r++) {
-                    const float2 w = tw[(k * r * TS) & MASK];
+                    const float2 w = tw[(k * r * TS) & (N - 1)];
                     v[r] = cmulf(v[r], make_float2(w.x, -s * w.y));
                 }
             }
             dft_small<R>(v, s);
             const int d = (j / NS) * NS * R + k;
+            // every lane's reads of this stage precede its writes, in lockstep
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int r = 0; r < R; r++) b[(d + r * NS + bOff) & MASK] = v[r];
+            for (int r = 0; r < R; r++) a[fft_slot<N>(d + r * NS, off)] = v[r];
         }
         wave_lds_sync();
-        fft_stages<N, NS * R>(b, bOff, a, aOff, tw, s, lane, out, outOff);
+        fft_stages<N, NS * R>(a, off, tw, s, lane);
     }
 }
 
-// In place on the column (col, colOff): the result is copied back from the
-// scratch when the stage count is odd.  tw: e^{-2 pi i q / N}, q < N.
+// In place on the padded column (col, off); tw: e^{-2 pi i q / N}, q < N.
+// The caller makes the column's data visible to the wave first.
 template <int N>
-THX_DEV void wave_fft(float2* col, int colOff, float2* scratch, const float2* __restrict__ tw, float s,
-                      int lane)
+THX_DEV void wave_fft(float2* col, int off, const float2* __restrict__ tw, float s, int lane)
 {
-    float2* res;
-    int resOff;
-    fft_stages<N, 1>(col, colOff, scratch, 0, tw, s, lane, &res, &resOff);
-    if (res != col) {
-        for (int i = lane; i < N; i += 64) col[(i + colOff) & (N - 1)] = scratch[i];
-        wave_lds_sync();
-    }
+    fft_stages<N, 1>(col, off, tw, s, lane);
 }
 
 }  // namespace thx

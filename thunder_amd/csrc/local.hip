@@ -170,21 +170,7 @@ THX_DEV Cell quad_bcast_cell(const Cell& c)
 
 // Pair form of the y-pair gather (LAYOUT_YPAIR2): lane j of a pair reads
 // element x0 + j of slices z0 and z0 + 1 (two 16-B loads); the pair's two
-// lanes meet on the same 32-B pieces, so a sample costs two accesses with
-// half the lanes of the quad form.  Returns this lane's weighted part.
-THX_DEV float2 ypair_pair_part(const float4* __restrict__ yp, int vdim, const Cell& c, int j)
-{
-    const int nColFT = vdim / 2 + 1;
-    const size_t e0 = ((size_t)wrap_idx(c.z0, vdim) * vdim + wrap_idx(c.y0, vdim)) * nColFT + c.x0 + j;
-    const size_t e1 = ((size_t)wrap_idx(c.z0 + 1, vdim) * vdim + wrap_idx(c.y0, vdim)) * nColFT + c.x0 + j;
-    const float4 q0 = yp[e0], q1 = yp[e1];
-    const float wx = j ? c.dx : 1.f - c.dx;
-    const float wa = wx * (1.f - c.dz), wb = wx * c.dz;
-    const float w00 = wa * (1.f - c.dy), w01 = wa * c.dy, w10 = wb * (1.f - c.dy), w11 = wb * c.dy;
-    const float re = q0.x * w00 + q0.z * w01 + q1.x * w10 + q1.z * w11;
-    const float im = q0.y * w00 + q0.w * w01 + q1.y * w10 + q1.w * w11;
-    return make_float2(re, c.conj ? -im : im);
-}
+// lanes meet on the same 32-B pieces, so a sample costs two accesses.
 // A pair-form sample as its rotating lane hands it to the pair: the two
 // slices' element offsets (32-bit: the y-pair copy has < 2^31 elements up to
 // vdim 1024) and the fractions, the Hermitian fold in dx's sign bit -- five
@@ -210,31 +196,10 @@ THX_DEV PCell pcell_of(float x, float y, float z, int vdim)
     c.dz = z - fz;
     return c;
 }
-// lane j of the pair: element x0 + j of slices z0 and z0 + 1.  RSRC: the
-// y-pair copy through a buffer descriptor (32-bit byte offsets, no 64-bit
-// address arithmetic; the copy must be < 4 GiB -- ypair_bytes_ok)
-#ifndef THX_PAIR_BUF
-#define THX_PAIR_BUF 0
-#endif
-struct YpSrc {
-    const float4* p;
-#if THX_PAIR_BUF
-    __amdgpu_buffer_rsrc_t r;
-#endif
-};
-THX_DEV float4 yp_load(const YpSrc& y, unsigned e)
+// lane j of the pair: element x0 + j of slices z0 and z0 + 1
+THX_DEV float2 ypair_pcell_part(const float4* __restrict__ yp, const PCell& c, int j)
 {
-#if THX_PAIR_BUF
-    typedef float f32x4v_ __attribute__((ext_vector_type(4)));
-    const f32x4v_ v = __builtin_amdgcn_raw_buffer_load_b128(y.r, e * 16u, 0, 0);
-    return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return y.p[e];
-#endif
-}
-THX_DEV float2 ypair_pcell_part(const YpSrc& yp, const PCell& c, int j)
-{
-    const float4 q0 = yp_load(yp, c.e0 + (unsigned)j), q1 = yp_load(yp, c.e1 + (unsigned)j);
+    const float4 q0 = yp[c.e0 + (unsigned)j], q1 = yp[c.e1 + (unsigned)j];
     const bool conj = (__float_as_uint(c.dx) >> 31) != 0;
     const float dx = fabsf(c.dx);
     const float wx = j ? dx : 1.f - dx;
@@ -267,20 +232,6 @@ THX_DEV PCell pair_bcast_pcell(const PCell& c)
     o.dz = __int_as_float(pair_bcast<IT>(__float_as_int(c.dz)));
     return o;
 }
-template <int IT>
-THX_DEV Cell pair_bcast_cell(const Cell& c)
-{
-    Cell o;
-    o.x0 = pair_bcast<IT>(c.x0);
-    o.y0 = pair_bcast<IT>(c.y0);
-    o.z0 = pair_bcast<IT>(c.z0);
-    o.dx = __int_as_float(pair_bcast<IT>(__float_as_int(c.dx)));
-    o.dy = __int_as_float(pair_bcast<IT>(__float_as_int(c.dy)));
-    o.dz = __int_as_float(pair_bcast<IT>(__float_as_int(c.dz)));
-    o.conj = pair_bcast<IT>((int)c.conj) != 0;
-    return o;
-}
-
 // sum over the lanes of each quad (DPP quad permutations), every lane gets it
 THX_DEV float quad_sum(float v)
 {
@@ -293,7 +244,7 @@ THX_DEV float quad_sum(float v)
 // cell-expanded copy (1, quad-cooperative gathers, no LDS boxes) and its
 // y-pair copy (2, thx_volume_ypair: element (x, y, z) holds v(x, y, z) and
 // v(x, y + 1, z), so a trilinear cell is two 32-B pieces, gathered by lane
-// pairs -- ypair_pair_part).
+// pairs -- ypair_pcell_part).
 enum { LAYOUT_FT = 0, LAYOUT_CELLS = 1, LAYOUT_YPAIR2 = 2 };
 // layouts gathered quad-cooperatively (no LDS boxes, no patch records)
 constexpr bool coop_layout(int l) { return l == LAYOUT_CELLS; }
@@ -819,16 +770,6 @@ k_local_fused(const float2* __restrict__ vol,
     }
     // classification: image l projects its own class's volume
     if (cls) vol += (size_t)cls[l] * volStride;
-    YpSrc ysrc;
-    ysrc.p = reinterpret_cast<const float4*>(vol);
-#if THX_PAIR_BUF
-    if (LAYOUT == LAYOUT_YPAIR2)
-        ysrc.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(vol), (short)0,
-                                                   (int)(unsigned)min((size_t)0xFFFFFFF0u,
-                                                                      (size_t)16 * (vdim / 2 + 1) * vdim * vdim),
-                                                   0x00020000);
-#endif
-    (void)ysrc;
     static_assert(CS || NCT == 1, "column tiles per workgroup: CTF search only");
     constexpr int BOXC = BIGBOX ? BOX_CAP_BIG : BOX_CAP;
     constexpr int NITC = BOXC / 4 / THREADS;
@@ -883,14 +824,7 @@ k_local_fused(const float2* __restrict__ vol,
         quat_to_mat(q, mm);
         for (int k = 0; k < 6; k++) m[k] = mm[k];
     }
-#ifndef THX_PAIR_F32ROT
-#define THX_PAIR_F32ROT 0
-#endif
-    // A/B: the pair path's rotation in FP32 (the reference rotates in FP64)
-    float mf[6];
-#pragma unroll
-    for (int k = 0; k < 6; k++) mf[k] = (float)m[k];
-    (void)mf;
+
     // columns: translations, or (t, d) pairs for CS (nT counts the columns)
     if (tid < NC) {
         const int t = CS ? (t0 + tid) / nD : t0 + tid;
@@ -1104,41 +1038,17 @@ k_local_fused(const float2* __restrict__ vol,
         // 4s, 4s + 2) from the h = 0 pairs, (4s + 1, 4s + 3) from the h = 1 pairs.
         auto pair_step = [&](int s) {
             const int j = lane & 1, h = (lane >> 5) & 1;
-#ifndef THX_PAIR_PCELL
-#define THX_PAIR_PCELL 1
-#endif
-#if THX_PAIR_PCELL
             PCell mine;
             {
-                const float2 xyf = sXY[4 * s + h + 2 * j];
-#if THX_PAIR_F32ROT
-                const float fx = xyf.x, fy = xyf.y;
-                mine = pcell_of(fmaf(mf[0], fx, mf[3] * fy), fmaf(mf[1], fx, mf[4] * fy),
-                                fmaf(mf[2], fx, mf[5] * fy), vdim);
-#else
-                const double2 xy = make_double2(xyf.x, xyf.y);
+                const double2 xy = make_double2(sXY[4 * s + h + 2 * j].x, sXY[4 * s + h + 2 * j].y);
                 mine = pcell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                 (float)(m[2] * xy.x + m[5] * xy.y), vdim);
-#endif
             }
-#else
-            Cell mine;
-            {
-                const double2 xy = make_double2(sXY[4 * s + h + 2 * j].x, sXY[4 * s + h + 2 * j].y);
-                mine = cell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
-                               (float)(m[2] * xy.x + m[5] * xy.y));
-            }
-#endif
             float2 P[2];
 #pragma unroll
             for (int it = 0; it < 2; it++) {
-#if THX_PAIR_PCELL
                 const PCell c = it == 0 ? pair_bcast_pcell<0>(mine) : pair_bcast_pcell<1>(mine);
-                const float2 v = ypair_pcell_part(ysrc, c, j);
-#else
-                const Cell c = it == 0 ? pair_bcast_cell<0>(mine) : pair_bcast_cell<1>(mine);
-                const float2 v = ypair_pair_part(reinterpret_cast<const float4*>(vol), vdim, c, j);
-#endif
+                const float2 v = ypair_pcell_part(reinterpret_cast<const float4*>(vol), c, j);
                 P[it] = make_float2(v.x + pair_swap(v.x), v.y + pair_swap(v.y));
             }
             if (!CS)
@@ -1165,15 +1075,14 @@ k_local_fused(const float2* __restrict__ vol,
         };
         if (PAIR) {
             // every step of the iteration, no padding branch (a padding step
-            // adds exactly zero: U = V = b = 0), fully unrolled so that the
-            // loads of later steps can be issued before earlier steps reduce:
-            // 90.1k vs 87.5k images/s with the per-step branch
-            // (profiles/r04_pair_pipe_ab.jsonl; an explicit two-step software
-            // pipeline needs 112 VGPRs, 4 waves per SIMD: 83k)
-#ifndef THX_PAIR_UNROLL
-#define THX_PAIR_UNROLL 2
-#endif
-#pragma unroll THX_PAIR_UNROLL
+            // adds exactly zero: U = V = b = 0; 90.1k vs 87.5k images/s with
+            // the per-step branch, profiles/r04_pair_pipe_ab.jsonl), two steps
+            // per unrolled body: with the packed cells a full unroll hoists
+            // more loads than 80 VGPRs hold (62 spills); unrolled twice: phases
+            // 8.67 vs 9.26 ms for the round-3 cells, full unroll with FP32
+            // rotations 8.71, with buffer-descriptor loads 8.66, full unroll at
+            // 8 waves 8.98 (profiles/r04_pair_ab.jsonl)
+#pragma unroll 2
             for (int s = 0; s < 4 * PP; s++) pair_step(s);
         } else if (COOP) {
 // all four steps unrolled: 16 cell reads in flight per wave (C5 +3-4 %,
@@ -1509,7 +1418,6 @@ size_t rec_bytes(int nImg, int nR, int nVisit)
 }  // namespace
 
 namespace thx {
-bool ypair_bytes_ok(int vdim);
 
 size_t patch_rec_bytes(int nImg, int nR, int nVisit) { return rec_bytes(nImg, nR, nVisit); }
 
@@ -1605,9 +1513,6 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     if (nImg == 0) return THX_OK;
     THX_CHECK_ARG(!ypair || (volLayout == LAYOUT_FT && pxOrder && !nD),
                   "thx_local_phase_routed: a y-pair copy goes with the half-complex layout and pxOrder");
-    THX_CHECK_ARG((volLayout != LAYOUT_YPAIR2 && !ypair) || thx::ypair_bytes_ok(vdim),
-                  "thx_local_phase: the y-pair copy of vdim %d exceeds the 4 GiB its gathers address",
-                  vdim);
     const int nVisit = pxOrder ? nOrd : nPxl;
     THX_CHECK_ARG(workspace && wsBytes >= thx_local_phase_workspace(nImg, nR, nCol, nVisit),
                   "thx_local_phase: workspace too small");
@@ -1807,13 +1712,6 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
 
 // whether local_phase_impl routes a phase on the device (half-complex layout,
 // no CTF search, 64 KiB boxes) -- the phases that can use a y-pair copy
-// the pair-form kernel addresses its y-pair copy through a buffer
-// descriptor with 32-bit byte offsets: vdim <= 812
-bool ypair_bytes_ok(int vdim)
-{
-    return (size_t)16 * (vdim / 2 + 1) * vdim * vdim <= 0xFFFFFFF0ull;
-}
-
 bool phase_routed(int volLayout, int pf, int nPxl, int nD)
 {
     return volLayout == LAYOUT_FT && !nD &&

@@ -54,7 +54,6 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       const double* pD = nullptr, float* wD = nullptr,
                       const float* ypair = nullptr, int* routeOut = nullptr);
 bool phase_routed(int volLayout, int pf, int nPxl, int nD);
-bool ypair_bytes_ok(int vdim);
 int pf_symmetrise_launch(int nImg, int mR, double* quat, int anchorMode, const double* anchor,
                          const double* symQ, int nSym, uint64_t seed, uint32_t stream,
                          const int* done, hipStream_t s);
@@ -1317,8 +1316,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.topD = k.take<int>(on * nImg);
     // the y-pair copy of every class's projectee for the device route's
     // pair-form kernel (phases whose LDS boxes do not pay)
-    const bool yp = !c.volCells && !twoD && mLD == 0 && thx::phase_routed(0, c.pf, nPxl, 0) &&
-                    thx::ypair_bytes_ok(c.vdim);
+    const bool yp = !c.volCells && !twoD && mLD == 0 && thx::phase_routed(0, c.pf, nPxl, 0);
     p.ypair = yp ? k.take<float>((size_t)4 * (c.vdim / 2 + 1) * c.vdim * c.vdim * nK) : nullptr;
     p.bytes = k.off + 256;
     return p;

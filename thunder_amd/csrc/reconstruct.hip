@@ -343,10 +343,10 @@ constexpr int EV_WAVES = 4;
 bool even_ok(int vdim) { return vdim == 64 || vdim == 128 || vdim == 256 || vdim == 512; }
 
 template <int N>
-constexpr size_t even_col_lds() { return (size_t)(EV_CT * N + EV_WAVES * N) * sizeof(float2); }
+constexpr size_t even_col_lds() { return (size_t)EV_CT * thx::fft_pitch<N>() * sizeof(float2); }
 
 template <int N>
-constexpr size_t even_row_lds() { return (size_t)EV_WAVES * 2 * N * sizeof(float2); }
+constexpr size_t even_row_lds() { return (size_t)EV_WAVES * thx::fft_pitch<N>() * sizeof(float2); }
 
 // T on the kx = 0 and kx = N / 2 planes := (T(k) + T(-k)) / 2
 __global__ void k_sym_planes(float* __restrict__ T, int vdim)
@@ -379,24 +379,24 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G
                                                          const float2* __restrict__ tw)
 {
     extern __shared__ float2 sm[];
-    constexpr int H = N / 2 + 1, M = N - 1;
-    float2* tile = sm;                                   // [EV_CT][N], column c rotated by c
+    constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>();
+    float2* tile = sm;                                   // [EV_CT][P], column c rotated by c
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    float2* scr = sm + EV_CT * N + wv * N;
     const int kx0 = blockIdx.x * EV_CT, ky = blockIdx.y;
     const int ncol = min(EV_CT, H - kx0);
-    const int c = tid % EV_CT, rr = tid / EV_CT;         // row mapping: column c, rows rr + 16 i
+    const int c = tid % EV_CT, rr = tid / EV_CT;         // row mapping: column c, rows rr + RSTEP i
     constexpr int RSTEP = 64 * EV_WAVES / EV_CT;
     const int jy = ky < N / 2 ? ky : ky - N;
     const int ix = kx0 + c;
+    float2* col = tile + c * P;
     if (!INIT) {
         for (int nz = rr; nz < H; nz += RSTEP) {
             const float2 v = c < ncol ? G[((size_t)nz * N + ky) * H + ix] : make_float2(0.f, 0.f);
-            tile[c * N + ((nz + c) & M)] = v;
-            if (nz > 0 && nz < N / 2) tile[c * N + ((N - nz + c) & M)] = make_float2(v.x, -v.y);
+            col[thx::fft_slot<N>(nz, c)] = v;
+            if (nz > 0 && nz < N / 2) col[thx::fft_slot<N>(N - nz, c)] = make_float2(v.x, -v.y);
         }
         __syncthreads();
-        for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * N, cc, scr, tw, -1.f, lane);
+        for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, tw, -1.f, lane);
         __syncthreads();
     }
     float dmax = 0.f;
@@ -404,23 +404,24 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G
         for (int kz = rr; kz < N; kz += RSTEP) {
             const size_t e = ((size_t)kz * N + ky) * H + ix;
             float w = W[e];
+            const int slot = thx::fft_slot<N>(kz, c);
             if (!INIT) {
                 const int jz = kz < N / 2 ? kz : kz - N;
                 if (ix * ix + jy * jy + jz * jz < r2) {
-                    const float m = fabsf(tile[c * N + ((kz + c) & M)].x);
+                    const float m = fabsf(col[slot].x);
                     w = w / fmaxf(m, 1e-6f);
                     W[e] = w;
                     dmax = fmaxf(dmax, fabsf(m - 1.f));
                 }
             }
-            tile[c * N + ((kz + c) & M)] = make_float2(T[e] * w, 0.f);
+            col[slot] = make_float2(T[e] * w, 0.f);
         }
     }
     __syncthreads();
-    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * N, cc, scr, tw, 1.f, lane);
+    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, tw, 1.f, lane);
     __syncthreads();
     if (c < ncol)
-        for (int nz = rr; nz < H; nz += RSTEP) G[((size_t)nz * N + ky) * H + ix] = tile[c * N + ((nz + c) & M)];
+        for (int nz = rr; nz < H; nz += RSTEP) G[((size_t)nz * N + ky) * H + ix] = col[thx::fft_slot<N>(nz, c)];
     if (!INIT) {
         dmax = wave_max(dmax);
         __shared__ float sMax[EV_WAVES];
@@ -439,22 +440,22 @@ template <int N, int S>
 __global__ void __launch_bounds__(64 * EV_WAVES) k_even_y(float2* __restrict__ G, const float2* __restrict__ tw)
 {
     extern __shared__ float2 sm[];
-    constexpr int H = N / 2 + 1, M = N - 1;
+    constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>();
     float2* tile = sm;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    float2* scr = sm + EV_CT * N + wv * N;
     const int kx0 = blockIdx.x * EV_CT, nz = blockIdx.y;
     const int ncol = min(EV_CT, H - kx0);
     const int c = tid % EV_CT, rr = tid / EV_CT;
     constexpr int RSTEP = 64 * EV_WAVES / EV_CT;
     float2* base = G + (size_t)nz * N * H + kx0 + c;
+    float2* col = tile + c * P;
     if (c < ncol)
-        for (int y = rr; y < N; y += RSTEP) tile[c * N + ((y + c) & M)] = base[(size_t)y * H];
+        for (int y = rr; y < N; y += RSTEP) col[thx::fft_slot<N>(y, c)] = base[(size_t)y * H];
     __syncthreads();
-    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * N, cc, scr, tw, (float)S, lane);
+    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, tw, (float)S, lane);
     __syncthreads();
     if (c < ncol)
-        for (int y = rr; y < N; y += RSTEP) base[(size_t)y * H] = tile[c * N + ((y + c) & M)];
+        for (int y = rr; y < N; y += RSTEP) base[(size_t)y * H] = col[thx::fft_slot<N>(y, c)];
 }
 
 // x rows (nz < H, ny): the Hermitian kx-half -> C2R (+) -> times the kernel
@@ -464,30 +465,30 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_x(float2* __restrict__ G
                                                          const float2* __restrict__ tw)
 {
     extern __shared__ float2 sm[];
-    constexpr int H = N / 2 + 1;
+    constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const long row = (long)blockIdx.x * EV_WAVES + wv;
     if (row >= (long)H * N) return;
-    float2* buf = sm + wv * 2 * N;
-    float2* scr = buf + N;
+    float2* buf = sm + wv * P;
     float2* g = G + row * H;
     for (int x = lane; x < H; x += 64) {
         const float2 v = g[x];
-        buf[x] = v;
-        if (x > 0 && x < N / 2) buf[N - x] = make_float2(v.x, -v.y);
+        buf[thx::fft_slot<N>(x, 0)] = v;
+        if (x > 0 && x < N / 2) buf[thx::fft_slot<N>(N - x, 0)] = make_float2(v.x, -v.y);
     }
     thx::wave_lds_sync();
-    thx::wave_fft<N>(buf, 0, scr, tw, 1.f, lane);
+    thx::wave_fft<N>(buf, 0, tw, 1.f, lane);
     const int nz = (int)(row / N), ny = (int)(row % N);
     const int ay = ny <= N / 2 ? ny : N - ny;
     const float* o = oct + ((size_t)nz * H + ay) * H;
     for (int x = lane; x < N; x += 64) {
         const int ax = x <= N / 2 ? x : N - x;
-        buf[x] = make_float2(buf[x].x * o[ax], 0.f);
+        const int sl = thx::fft_slot<N>(x, 0);
+        buf[sl] = make_float2(buf[sl].x * o[ax], 0.f);
     }
     thx::wave_lds_sync();
-    thx::wave_fft<N>(buf, 0, scr, tw, -1.f, lane);
-    for (int x = lane; x < H; x += 64) g[x] = buf[x];
+    thx::wave_fft<N>(buf, 0, tw, -1.f, lane);
+    for (int x = lane; x < H; x += 64) g[x] = buf[thx::fft_slot<N>(x, 0)];
 }
 
 template <int N>

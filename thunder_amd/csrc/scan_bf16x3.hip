@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(256) k_scan_bias(const float* __restrict__ Bc,
 // LDS stages of the chunk pipeline: chunk ck + STAGES - 1 is copied while
 // chunk ck is multiplied, so each copy has STAGES - 1 chunks to land
 #ifndef SCAN_STAGES
-#define SCAN_STAGES 3
+#define SCAN_STAGES 2
 #endif
 
 template <int N>
