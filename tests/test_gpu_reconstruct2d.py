@@ -150,9 +150,12 @@ def test_c1_two_iterations_on_gpu():
         info = (it, its, [bool(np.isfinite(rec[k]).all()) for k in range(K1)],
                 [float(np.nanstd(rec[k])) for k in range(K1)], np.bincount(cls.cpu().numpy(), minlength=K1))
         assert np.all(np.isfinite(corr)) and min(corr) > 0.9, (corr, info)
+        # the next references: the reconstructed classes at the references'
+        # scale -- the solve returns irfft2 of F / T (FFT::bw's 1 / size), i.e.
+        # the generating images / vdim under _projectee2d's 1 / vdim
         pad = np.zeros_like(imgs)
         o = (N1 * PF1 - N1) // 2
-        pad[:, o:o + N1, o:o + N1] = rec
+        pad[:, o:o + N1, o:o + N1] = rec * (N1 * PF1)
         refs = _projectee2d(pad)
     assert np.mean(classes[0] == cls_true) >= 0.9
     assert np.mean(classes[1] == cls_true) >= 0.9

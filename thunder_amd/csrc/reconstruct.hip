@@ -342,11 +342,21 @@ constexpr int EV_WAVES = 4;
 
 bool even_ok(int vdim) { return vdim == 64 || vdim == 128 || vdim == 256 || vdim == 512; }
 
+// LDS: the padded columns (rows) and the twiddle table
 template <int N>
-constexpr size_t even_col_lds() { return (size_t)EV_CT * thx::fft_pitch<N>() * sizeof(float2); }
+constexpr size_t even_col_lds() { return (size_t)(EV_CT * thx::fft_pitch<N>() + N) * sizeof(float2); }
 
 template <int N>
-constexpr size_t even_row_lds() { return (size_t)EV_WAVES * thx::fft_pitch<N>() * sizeof(float2); }
+constexpr size_t even_row_lds() { return (size_t)(EV_WAVES * thx::fft_pitch<N>() + N) * sizeof(float2); }
+
+// the twiddle table into LDS (the stages read it at the L1-missing strides
+// of k r N / (Ns R); from global memory each stage waited on L2)
+template <int N>
+THX_DEV const float2* even_twiddles(float2* sTw, const float2* __restrict__ tw)
+{
+    for (int q = threadIdx.x; q < N; q += blockDim.x) sTw[q] = tw[q];
+    return sTw;
+}
 
 // T on the kx = 0 and kx = N / 2 planes := (T(k) + T(-k)) / 2
 __global__ void k_sym_planes(float* __restrict__ T, int vdim)
@@ -381,6 +391,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G
     extern __shared__ float2 sm[];
     constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>();
     float2* tile = sm;                                   // [EV_CT][P], column c rotated by c
+    const float2* stw = even_twiddles<N>(sm + EV_CT * P, tw);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int kx0 = blockIdx.x * EV_CT, ky = blockIdx.y;
     const int ncol = min(EV_CT, H - kx0);
@@ -396,7 +407,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G
             if (nz > 0 && nz < N / 2) col[thx::fft_slot<N>(N - nz, c)] = make_float2(v.x, -v.y);
         }
         __syncthreads();
-        for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, tw, -1.f, lane);
+        for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, stw, -1.f, lane);
         __syncthreads();
     }
     float dmax = 0.f;
@@ -418,7 +429,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G
         }
     }
     __syncthreads();
-    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, tw, 1.f, lane);
+    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, stw, 1.f, lane);
     __syncthreads();
     if (c < ncol)
         for (int nz = rr; nz < H; nz += RSTEP) G[((size_t)nz * N + ky) * H + ix] = col[thx::fft_slot<N>(nz, c)];
@@ -442,6 +453,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_y(float2* __restrict__ G
     extern __shared__ float2 sm[];
     constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>();
     float2* tile = sm;
+    const float2* stw = even_twiddles<N>(sm + EV_CT * P, tw);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int kx0 = blockIdx.x * EV_CT, nz = blockIdx.y;
     const int ncol = min(EV_CT, H - kx0);
@@ -452,7 +464,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_y(float2* __restrict__ G
     if (c < ncol)
         for (int y = rr; y < N; y += RSTEP) col[thx::fft_slot<N>(y, c)] = base[(size_t)y * H];
     __syncthreads();
-    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, tw, (float)S, lane);
+    for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, stw, (float)S, lane);
     __syncthreads();
     if (c < ncol)
         for (int y = rr; y < N; y += RSTEP) base[(size_t)y * H] = col[thx::fft_slot<N>(y, c)];
@@ -467,6 +479,8 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_x(float2* __restrict__ G
     extern __shared__ float2 sm[];
     constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const float2* stw = even_twiddles<N>(sm + EV_WAVES * P, tw);
+    __syncthreads();
     const long row = (long)blockIdx.x * EV_WAVES + wv;
     if (row >= (long)H * N) return;
     float2* buf = sm + wv * P;
@@ -477,7 +491,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_x(float2* __restrict__ G
         if (x > 0 && x < N / 2) buf[thx::fft_slot<N>(N - x, 0)] = make_float2(v.x, -v.y);
     }
     thx::wave_lds_sync();
-    thx::wave_fft<N>(buf, 0, tw, 1.f, lane);
+    thx::wave_fft<N>(buf, 0, stw, 1.f, lane);
     const int nz = (int)(row / N), ny = (int)(row % N);
     const int ay = ny <= N / 2 ? ny : N - ny;
     const float* o = oct + ((size_t)nz * H + ay) * H;
@@ -487,7 +501,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_x(float2* __restrict__ G
         buf[sl] = make_float2(buf[sl].x * o[ax], 0.f);
     }
     thx::wave_lds_sync();
-    thx::wave_fft<N>(buf, 0, tw, -1.f, lane);
+    thx::wave_fft<N>(buf, 0, stw, -1.f, lane);
     for (int x = lane; x < H; x += 64) g[x] = buf[thx::fft_slot<N>(x, 0)];
 }
 
