@@ -114,8 +114,13 @@ def test_c1_two_iterations_on_gpu():
     for l in range(n):
         P[l] = ops.project2d(cl[cls_true[l]].contiguous(), T_(np.array([[np.cos(th[l]), np.sin(th[l])]])),
                              px)[0]
-    dat, sig = synth.noisy_images(ctf * P * ops.trans_table(T_(tt), px), px.iSig, N1 // 2 + 1, snr=10.0,
-                                  seed=85)
+    # white noise (one sigma^2 over the pixel set, as in a micrograph): the
+    # high shells are noise-dominated, so the second expectation weighs the
+    # reconstructed classes' noisy high shells by their real reliability
+    # (per-shell SNR noise would trust them 10:1 and classify on the solve's
+    # high-frequency residue -- tools/diag/c1_frc.py)
+    dat, sig = synth.noisy_images(ctf * P * ops.trans_table(T_(tt), px), px.iSig, N1 // 2 + 1, snr=3.0,
+                                  seed=85, white=True)
     # the full-resolution pixel set for the insert (rU = N / 2 - 2, the
     # reconstruction's maxRadius) and the images there
     pxi = ops.PixelSet(N1, PF1, N1 // 2 - 2, 0, device=DEV)
@@ -125,7 +130,7 @@ def test_c1_two_iterations_on_gpu():
         Pi[l] = ops.project2d(cl[cls_true[l]].contiguous(),
                               T_(np.array([[np.cos(th[l]), np.sin(th[l])]])), pxi)[0]
     dati, _ = synth.noisy_images(ctfi * Pi * ops.trans_table(T_(tt), pxi), pxi.iSig, N1 // 2 + 1,
-                                 snr=10.0, seed=86)
+                                 snr=3.0, seed=86, white=True)
     refs = cl
     classes = []
     for it in range(2):

@@ -378,10 +378,24 @@ __global__ void k_sym_planes(float* __restrict__ T, int vdim)
     }
 }
 
+// blockIdx.x -> tile (-1: past the end) with runs of consecutive tiles on
+// one XCD: dispatch deals workgroups round-robin over the 8 XCDs, and the
+// kx-neighbouring tiles of the column passes share the 128-byte lines of
+// T and W (a tile row of floats is 64 bytes), read once per XCD's L2.
+THX_DEV int even_tile(int ntiles)
+{
+    const int per = (ntiles + 7) / 8;
+    const int t = (int)(blockIdx.x % 8) * per + (int)(blockIdx.x / 8);
+    return t < ntiles ? t : -1;
+}
+
 // z columns.  INIT: C = T W (W as k_init_w left it) -> R2C (+) along z.
 // Otherwise first the C2R (-) along z of G's Hermitian nz-half: the balanced
 // C, whose |C| updates W inside the sphere (and the max | |C| - 1 |), then the
-// same as INIT.  Grid (ceil(H / EV_CT), N): a tile of EV_CT kx columns at one ky.
+// same as INIT.  A block: a tile of EV_CT kx columns at one ky (even_tile).
+// Every global load of a thread (its G rows, then its T and W rows) is
+// issued before the first LDS write, so the T / W latency hides behind the
+// C2R instead of being paid once per kz.
 template <int N, bool INIT>
 __global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G, float* __restrict__ W,
                                                          const float* __restrict__ T, int r2,
@@ -389,50 +403,77 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G
                                                          const float2* __restrict__ tw)
 {
     extern __shared__ float2 sm[];
-    constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>();
+    constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>(), NT = (H + EV_CT - 1) / EV_CT;
+    constexpr int RSTEP = 64 * EV_WAVES / EV_CT;
+    constexpr int NZ = N / RSTEP, NG = (H + RSTEP - 1) / RSTEP;   // rows per thread
     float2* tile = sm;                                   // [EV_CT][P], column c rotated by c
     const float2* stw = even_twiddles<N>(sm + EV_CT * P, tw);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int kx0 = blockIdx.x * EV_CT, ky = blockIdx.y;
+    const int t = even_tile(NT * N);
+    const int kx0 = (t % NT) * EV_CT, ky = t / NT;
     const int ncol = min(EV_CT, H - kx0);
     const int c = tid % EV_CT, rr = tid / EV_CT;         // row mapping: column c, rows rr + RSTEP i
-    constexpr int RSTEP = 64 * EV_WAVES / EV_CT;
+    const bool on = c < ncol;
     const int jy = ky < N / 2 ? ky : ky - N;
     const int ix = kx0 + c;
     float2* col = tile + c * P;
+    float2 g[INIT ? 1 : NG];
     if (!INIT) {
-        for (int nz = rr; nz < H; nz += RSTEP) {
-            const float2 v = c < ncol ? G[((size_t)nz * N + ky) * H + ix] : make_float2(0.f, 0.f);
-            col[thx::fft_slot<N>(nz, c)] = v;
-            if (nz > 0 && nz < N / 2) col[thx::fft_slot<N>(N - nz, c)] = make_float2(v.x, -v.y);
+#pragma unroll
+        for (int i = 0; i < NG; i++) {
+            const int nz = rr + i * RSTEP;
+            g[i] = on && nz < H ? G[((size_t)nz * N + ky) * H + ix] : make_float2(0.f, 0.f);
+        }
+    }
+    float w[NZ], tv[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; i++) {
+        const size_t e = ((size_t)(rr + i * RSTEP) * N + ky) * H + ix;
+        w[i] = on ? W[e] : 0.f;
+        tv[i] = on ? T[e] : 0.f;
+    }
+    if (!INIT) {
+#pragma unroll
+        for (int i = 0; i < NG; i++) {
+            const int nz = rr + i * RSTEP;
+            if (nz < H) {
+                col[thx::fft_slot<N>(nz, c)] = g[i];
+                if (nz > 0 && nz < N / 2) col[thx::fft_slot<N>(N - nz, c)] = make_float2(g[i].x, -g[i].y);
+            }
         }
         __syncthreads();
         for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, stw, -1.f, lane);
         __syncthreads();
     }
     float dmax = 0.f;
-    if (c < ncol) {
-        for (int kz = rr; kz < N; kz += RSTEP) {
-            const size_t e = ((size_t)kz * N + ky) * H + ix;
-            float w = W[e];
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < NZ; i++) {
+            const int kz = rr + i * RSTEP;
             const int slot = thx::fft_slot<N>(kz, c);
+            float wi = w[i];
             if (!INIT) {
                 const int jz = kz < N / 2 ? kz : kz - N;
                 if (ix * ix + jy * jy + jz * jz < r2) {
                     const float m = fabsf(col[slot].x);
-                    w = w / fmaxf(m, 1e-6f);
-                    W[e] = w;
+                    wi = wi / fmaxf(m, 1e-6f);
+                    W[((size_t)kz * N + ky) * H + ix] = wi;
                     dmax = fmaxf(dmax, fabsf(m - 1.f));
                 }
             }
-            col[slot] = make_float2(T[e] * w, 0.f);
+            col[slot] = make_float2(tv[i] * wi, 0.f);
         }
     }
     __syncthreads();
     for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, stw, 1.f, lane);
     __syncthreads();
-    if (c < ncol)
-        for (int nz = rr; nz < H; nz += RSTEP) G[((size_t)nz * N + ky) * H + ix] = col[thx::fft_slot<N>(nz, c)];
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < NG; i++) {
+            const int nz = rr + i * RSTEP;
+            if (nz < H) G[((size_t)nz * N + ky) * H + ix] = col[thx::fft_slot<N>(nz, c)];
+        }
+    }
     if (!INIT) {
         dmax = wave_max(dmax);
         __shared__ float sMax[EV_WAVES];
@@ -446,38 +487,48 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G
     }
 }
 
-// y columns: C2C along y, sign S.  Grid (ceil(H / EV_CT), H): one nz per row of tiles.
+// y columns: C2C along y, sign S.  A block: a tile of EV_CT kx columns at one nz.
 template <int N, int S>
 __global__ void __launch_bounds__(64 * EV_WAVES) k_even_y(float2* __restrict__ G, const float2* __restrict__ tw)
 {
     extern __shared__ float2 sm[];
-    constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>();
+    constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>(), NT = (H + EV_CT - 1) / EV_CT;
+    constexpr int RSTEP = 64 * EV_WAVES / EV_CT, NY = N / RSTEP;
+    const int t = even_tile(NT * H);
+    if (t < 0) return;
     float2* tile = sm;
     const float2* stw = even_twiddles<N>(sm + EV_CT * P, tw);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int kx0 = blockIdx.x * EV_CT, nz = blockIdx.y;
+    const int kx0 = (t % NT) * EV_CT, nz = t / NT;
     const int ncol = min(EV_CT, H - kx0);
     const int c = tid % EV_CT, rr = tid / EV_CT;
-    constexpr int RSTEP = 64 * EV_WAVES / EV_CT;
+    const bool on = c < ncol;
     float2* base = G + (size_t)nz * N * H + kx0 + c;
     float2* col = tile + c * P;
-    if (c < ncol)
-        for (int y = rr; y < N; y += RSTEP) col[thx::fft_slot<N>(y, c)] = base[(size_t)y * H];
+    float2 v[NY];
+#pragma unroll
+    for (int i = 0; i < NY; i++) v[i] = on ? base[(size_t)(rr + i * RSTEP) * H] : make_float2(0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < NY; i++) col[thx::fft_slot<N>(rr + i * RSTEP, c)] = v[i];
     __syncthreads();
     for (int cc = wv; cc < ncol; cc += EV_WAVES) thx::wave_fft<N>(tile + cc * P, cc, stw, (float)S, lane);
     __syncthreads();
-    if (c < ncol)
-        for (int y = rr; y < N; y += RSTEP) base[(size_t)y * H] = col[thx::fft_slot<N>(y, c)];
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < NY; i++) base[(size_t)(rr + i * RSTEP) * H] = col[thx::fft_slot<N>(rr + i * RSTEP, c)];
+    }
 }
 
 // x rows (nz < H, ny): the Hermitian kx-half -> C2R (+) -> times the kernel
-// octant (1 / N^3 and 1 / nf included) -> R2C (-), in place.  One wave per row.
+// octant (1 / N^3 and 1 / nf included) -> R2C (-), in place.  One wave per
+// row; the row and its octant row are loaded before the first transform.
 template <int N>
 __global__ void __launch_bounds__(64 * EV_WAVES) k_even_x(float2* __restrict__ G, const float* __restrict__ oct,
                                                          const float2* __restrict__ tw)
 {
     extern __shared__ float2 sm[];
     constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>();
+    constexpr int NX = (H + 63) / 64, NO = N / 64 > 0 ? N / 64 : 1;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const float2* stw = even_twiddles<N>(sm + EV_WAVES * P, tw);
     __syncthreads();
@@ -485,24 +536,46 @@ __global__ void __launch_bounds__(64 * EV_WAVES) k_even_x(float2* __restrict__ G
     if (row >= (long)H * N) return;
     float2* buf = sm + wv * P;
     float2* g = G + row * H;
-    for (int x = lane; x < H; x += 64) {
-        const float2 v = g[x];
-        buf[thx::fft_slot<N>(x, 0)] = v;
-        if (x > 0 && x < N / 2) buf[thx::fft_slot<N>(N - x, 0)] = make_float2(v.x, -v.y);
-    }
-    thx::wave_lds_sync();
-    thx::wave_fft<N>(buf, 0, stw, 1.f, lane);
     const int nz = (int)(row / N), ny = (int)(row % N);
     const int ay = ny <= N / 2 ? ny : N - ny;
     const float* o = oct + ((size_t)nz * H + ay) * H;
-    for (int x = lane; x < N; x += 64) {
-        const int ax = x <= N / 2 ? x : N - x;
-        const int sl = thx::fft_slot<N>(x, 0);
-        buf[sl] = make_float2(buf[sl].x * o[ax], 0.f);
+    float2 v[NX];
+    float ov[NO];
+#pragma unroll
+    for (int i = 0; i < NX; i++) {
+        const int x = lane + 64 * i;
+        v[i] = x < H ? g[x] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < NO; i++) {
+        const int x = lane + 64 * i;
+        ov[i] = x < N ? o[x <= N / 2 ? x : N - x] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < NX; i++) {
+        const int x = lane + 64 * i;
+        if (x < H) {
+            buf[thx::fft_slot<N>(x, 0)] = v[i];
+            if (x > 0 && x < N / 2) buf[thx::fft_slot<N>(N - x, 0)] = make_float2(v[i].x, -v[i].y);
+        }
+    }
+    thx::wave_lds_sync();
+    thx::wave_fft<N>(buf, 0, stw, 1.f, lane);
+#pragma unroll
+    for (int i = 0; i < NO; i++) {
+        const int x = lane + 64 * i;
+        if (x < N) {
+            const int sl = thx::fft_slot<N>(x, 0);
+            buf[sl] = make_float2(buf[sl].x * ov[i], 0.f);
+        }
     }
     thx::wave_lds_sync();
     thx::wave_fft<N>(buf, 0, stw, -1.f, lane);
-    for (int x = lane; x < H; x += 64) g[x] = buf[thx::fft_slot<N>(x, 0)];
+#pragma unroll
+    for (int i = 0; i < NX; i++) {
+        const int x = lane + 64 * i;
+        if (x < H) g[x] = buf[thx::fft_slot<N>(x, 0)];
+    }
 }
 
 template <int N>
@@ -511,7 +584,9 @@ int even_iteration_n(float2* G, float* W, const float* T, const float* oct, int 
 {
     constexpr int H = N / 2 + 1;
     const dim3 b(64 * EV_WAVES);
-    const dim3 gz((H + EV_CT - 1) / EV_CT, N), gy((H + EV_CT - 1) / EV_CT, H);
+    constexpr int NT = (H + EV_CT - 1) / EV_CT;
+    static_assert(NT * N % 8 == 0, "k_even_z: whole runs of tiles per XCD (no early exit before its barriers)");
+    const dim3 gz(NT * N), gy((NT * H + 7) / 8 * 8);
     const dim3 gx((unsigned)(((long)H * N + EV_WAVES - 1) / EV_WAVES));
     constexpr size_t lc = even_col_lds<N>(), lr = even_row_lds<N>();
     static std::atomic<unsigned> set[5];

@@ -110,10 +110,12 @@ def ctf_attrs(n, seed=5, pixel_size=1.32):
     return a
 
 
-def noisy_images(signal, iSig, n_shell, snr=0.05, seed=6):
+def noisy_images(signal, iSig, n_shell, snr=0.05, seed=6, white=False):
     """signal: complex [nImg, nPxl] (ctf * shifted projection).  Returns
     (dat, sigRcp) with per-shell noise power sigma^2 = <|signal|^2>_shell / snr
-    and sigRcp = -1 / (2 sigma^2) (the _sigRcp of src/Optimiser.cpp:5242)."""
+    (white: one sigma^2 = <|signal|^2> / snr over the pixel set, the
+    micrograph-like case where the high shells are noise-dominated) and
+    sigRcp = -1 / (2 sigma^2) (the _sigRcp of src/Optimiser.cpp:5242)."""
     dev = signal.device
     sh = torch.as_tensor(iSig, dtype=torch.long, device=dev)
     p = (signal.real ** 2 + signal.imag ** 2).mean(dim=0)
@@ -122,6 +124,8 @@ def noisy_images(signal, iSig, n_shell, snr=0.05, seed=6):
         0, sh, torch.ones_like(p, dtype=torch.float64))
     shell_pow = (num / cnt.clamp(min=1)).clamp(min=1e-12)
     sigma2 = (shell_pow / snr).float()[sh]                     # [nPxl]
+    if white:
+        sigma2 = torch.full_like(sigma2, float(p.mean()) / snr)
     g = torch.Generator(device=dev).manual_seed(seed)
     noise = torch.complex(torch.randn(signal.shape, generator=g, device=dev),
                           torch.randn(signal.shape, generator=g, device=dev))

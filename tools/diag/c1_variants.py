@@ -17,7 +17,7 @@ from thunder_amd import ops, synth  # noqa: E402
 DEV, T_, N1, PF1, K1 = t.DEV, t.T_, t.N1, t.PF1, t.K1
 
 
-def run(snr=10.0, n=400, m_reco=4, fsc=None, ru_search=16):
+def run(snr=10.0, n=400, m_reco=4, fsc=None, ru_search=16, white=False, lp=None):
     imgs = t._class_images(K1, 81)
     cl = t._projectee2d(imgs)
     px = ops.PixelSet(N1, PF1, ru_search, 1, device=DEV)
@@ -37,7 +37,7 @@ def run(snr=10.0, n=400, m_reco=4, fsc=None, ru_search=16):
             P[l] = ops.project2d(cl[cls_true[l]].contiguous(),
                                  T_(np.array([[np.cos(th[l]), np.sin(th[l])]])), pxs)[0]
         d, s = synth.noisy_images(c * P * ops.trans_table(T_(tt), pxs), pxs.iSig, N1 // 2 + 1, snr=snr,
-                                  seed=seed)
+                                  seed=seed, white=white)
         return d, c, s
     dat, ctf, sig = images(px, 85)
     pxi = ops.PixelSet(N1, PF1, N1 // 2 - 2, 0, device=DEV)
@@ -58,7 +58,12 @@ def run(snr=10.0, n=400, m_reco=4, fsc=None, ru_search=16):
                      torch.full((n,), 1.0 / m_reco, dtype=torch.float32, device=DEV), pxi, nc=nc)
         ops.prepare_tf2d(hm)
         o, its = ops.reconstruct2d(hm, N1, PF1, fsc=fsc)
-        rec = np.fft.fftshift(o.cpu().numpy(), axes=(-2, -1))
+        rec = o.cpu().numpy()
+        if lp is not None:      # the references low-passed to shell lp (as a resolution limit)
+            fy = np.fft.fftfreq(N1)[:, None] * N1
+            fx = np.fft.fftfreq(N1)[None, :] * N1
+            rec = np.fft.ifft2(np.fft.fft2(rec) * (np.hypot(fy, fx) <= lp)).real
+        rec = np.fft.fftshift(rec, axes=(-2, -1))
         corr = [round(float(np.corrcoef(rec[k].ravel(), gen[k].ravel())[0, 1]), 3) for k in range(K1)]
         out.append((it, acc, hist.tolist(), corr, [round(float(rec[k].std() * N1 * PF1 / gen[k].std()), 3)
                                                    for k in range(K1)]))
@@ -69,7 +74,7 @@ def run(snr=10.0, n=400, m_reco=4, fsc=None, ru_search=16):
     return out
 
 
-for kw in ({}, {"snr": 50.0}, {"n": 800}, {"m_reco": 16}, {"ru_search": 24},
-           {"fsc": np.stack([np.linspace(0.999, 0.5, N1 // 2 + 1)] * K1)}):
+for kw in ({"white": True}, {"white": True, "snr": 3.0}, {"white": True, "snr": 1.0},
+           {"white": True, "ru_search": 24}, {"lp": 10}, {"lp": 12}):
     for row in run(**kw):
         print(kw if not isinstance(kw.get("fsc"), np.ndarray) else "fsc", row)
