@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define THX_ABI_VERSION 7
+#define THX_ABI_VERSION 8
 
 enum {
     THX_OK = 0,
@@ -235,6 +235,18 @@ int thx_local_phase_routed(const thx_local_sel* sel, const float* vol,
                            int idim, int nImg, float* wC, float* wR, float* wT,
                            float* baseL, float* dvp, int* route, void* workspace,
                            size_t wsBytes, thx_stream_t stream);
+
+/* The image order thx_expectation's 3D phases use (the active list of
+ * thx_local_phase_sel): images stably sorted by the Morton code (16 + 16 bits)
+ * of the octahedral map of their slice normal n = R(q) e_z, q = the first
+ * particle quat[l][0] of the cloud, n and -n one plane (n_z >= 0).  The
+ * workgroups in flight then gather from one slab of the projectee, which
+ * stays in an XCD's L2; per-image results do not depend on the order.
+ * ord (device, nImg ints) receives the permutation; workspace >=
+ * thx_view_order_workspace(nImg) bytes. */
+size_t thx_view_order_workspace(int nImg);
+int thx_view_order(int nImg, int mLR, const double* quat, int* ord, void* workspace,
+                   size_t wsBytes, thx_stream_t stream);
 
 /* ---------------------------------------------------- CTF search (a2/a9) ---
  * SEARCH_TYPE_CTF: the local phase over nD defocus samples per image.

@@ -35,7 +35,7 @@ def test_exports_every_declared_symbol(L):
 
 
 def test_abi_version(L):
-    assert L.thx_abi_version() == 7
+    assert L.thx_abi_version() == 8
 
 
 def test_pixel_tile_order(L):

@@ -26,6 +26,8 @@ SIGNATURES = {
     "thx_global_scan": (_c_int, [_p, _c_int, _p, _c_int, _p, _p, _p, _c_int, _c_int, _p, _p,
                                  _c_int, _c_int, _p, _p, _p, _p, _c_int, _p, _c_size, _p]),
     "thx_local_phase_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
+    "thx_view_order_workspace": (_c_size, [_c_int]),
+    "thx_view_order": (_c_int, [_c_int, _c_int, _p, _p, _p, _c_size, _p]),
     "thx_volume_cells": (_c_int, [_p, _c_int, _p, _p]),
     "thx_pixel_tile_order": (_c_int, [_p, _p, _c_int, _c_int, _p, _p]),
     "thx_local_phase": (_c_int, [_p, _c_int, _c_int, _c_int, _p, _c_int, _p, _c_int, _p, _p, _p, _p, _p,

@@ -57,7 +57,15 @@ bool phase_routed(int volLayout, int pf, int nPxl, int nD);
 int pf_symmetrise_launch(int nImg, int mR, double* quat, int anchorMode, const double* anchor,
                          const double* symQ, int nSym, uint64_t seed, uint32_t stream,
                          const int* done, hipStream_t s);
+size_t view_order_tmp_bytes(int nImg);
+int view_order(int nImg, int mLR, const double* quat, unsigned* keys, unsigned* keysOut, int* idx,
+               int* ord, void* tmp, size_t tmpBytes, hipStream_t s);
 }
+
+// the 3D phases visit the images in view order (order.hip); 0 for A/B builds
+#ifndef THX_VIEW_ORDER
+#define THX_VIEW_ORDER 1
+#endif
 
 namespace {
 
@@ -1051,9 +1059,10 @@ __global__ void k_pf_converge(int nImg, int phase, int minPhase, int lastPhase,
 }
 
 // Active-image list: act[0 .. *nAct) = the images with done == 0, in order
-// (one workgroup, ballot prefix per wave).
+// (ord: in the order ord lists them; one workgroup, ballot prefix per wave).
 __global__ void __launch_bounds__(1024) k_compact(int nImg, const int* __restrict__ done,
-                                                  int* __restrict__ act, int* __restrict__ nAct)
+                                                  int* __restrict__ act, int* __restrict__ nAct,
+                                                  const int* __restrict__ ord = nullptr)
 {
     __shared__ int sW[16];
     __shared__ int sBase;
@@ -1062,14 +1071,15 @@ __global__ void __launch_bounds__(1024) k_compact(int nImg, const int* __restric
     __syncthreads();
     for (int b = 0; b < nImg; b += 1024) {
         const int i = b + tid;
-        const bool f = i < nImg && !(done && done[i]);
+        const int img = i < nImg ? (ord ? ord[i] : i) : 0;
+        const bool f = i < nImg && !(done && done[img]);
         const unsigned long long m = __ballot(f);
         const int pre = __popcll(m & ((1ull << lane) - 1ull));
         if (lane == 0) sW[wv] = __popcll(m);
         __syncthreads();
         int off = sBase;
         for (int w = 0; w < wv; w++) off += sW[w];
-        if (f) act[off + pre] = i;
+        if (f) act[off + pre] = img;
         __syncthreads();
         if (tid == 0)
             for (int w = 0; w < 16; w++) sBase += sW[w];
@@ -1243,6 +1253,8 @@ struct Plan {
     double* meanQ;                           // k_pf_mean's perturbation mean
     float* wC; float* wR; float* wT; float* base; double* pC;
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
+    unsigned* ordKey; unsigned* ordKeyOut; int* ordIdx; int* ord;   // view order (order.hip)
+    void* ordTmp; size_t ordTmpBytes;
     double* bestR; double* bestT;                        // convergence: smallest variR / variT
     void* localWs; size_t localWsBytes;
     float* ypair;                        // y-pair projectees (thx_volume_ypair), per class
@@ -1297,6 +1309,13 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.done = k.take<int>(nImg);
     p.act = k.take<int>(nImg);
     p.nAct = k.take<int>(1);
+    const size_t nOrd = THX_VIEW_ORDER && !twoD ? (size_t)nImg : 0;
+    p.ordKey = k.take<unsigned>(nOrd);
+    p.ordKeyOut = k.take<unsigned>(nOrd);
+    p.ordIdx = k.take<int>(nOrd);
+    p.ord = k.take<int>(nOrd);
+    p.ordTmpBytes = nOrd ? thx::view_order_tmp_bytes(nImg) : 0;
+    p.ordTmp = k.take<char>(p.ordTmpBytes);
     p.bestR = k.take<double>(nImg);
     p.bestT = k.take<double>(nImg);
     p.localWsBytes = twoD ? thx_local_phase2d_d_workspace(nImg, c.mLR, c.mLT, mLD)
@@ -1776,11 +1795,19 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     const float* phaseVol = c.volCells ? c.volCells : vol;
     const int phaseLayout = c.volCells ? 1 : 0;
     thx_local_sel sel{nullptr, nullptr, clsSel, (long long)dimSize};
-    if (c.converge) {
+    // 3D phases visit the images in view order (order.hip), through the
+    // active list; results per image are unchanged
+    const int* ord = nullptr;
+    if (THX_VIEW_ORDER && !twoD && nPh > 0) {
+        THX_RET(thx::view_order(nImg, c.mLR, quat, p.ordKey, p.ordKeyOut, p.ordIdx, p.ord, p.ordTmp,
+                                p.ordTmpBytes, s));
+        ord = p.ord;
+    }
+    if (c.converge || ord) {
         THX_HIP(hipMemsetAsync(p.done, 0, sizeof(int) * nImg, s));
-        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
+        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct, ord);
         THX_LAUNCH_CHECK();
-        done = p.done;
+        if (c.converge) done = p.done;
         sel.active = p.act;
         sel.nActive = p.nAct;
     }
@@ -1905,7 +1932,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                phase0 + nPh - 1, p.kv, p.sv, p.bestR, p.bestT, p.done, nPD,
                                cs ? p.sdD : nullptr, cs ? p.bestD : nullptr, (int)twoD);
             THX_LAUNCH_CHECK();
-            hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct);
+            hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct, ord);
             THX_LAUNCH_CHECK();
             if (phase >= c.minPhase) {
                 int left = 0;

@@ -317,6 +317,32 @@ __global__ void __launch_bounds__(256) k_scan_bias(const float* __restrict__ Bc,
     }
 }
 
+// max / sum over the 32 lanes sharing lane >> 5 (the translation columns of
+// one accumulator row): DPP inside each row of 16 lanes, then the row pairs
+// (0, 1) and (2, 3) through v_permlane16_swap -- no ds_bpermute round trips
+// through the LDS pipe (the shuffles were 320 of them per wave, each waited
+// on).  Lane n == 0's sum is the one stored.
+#ifndef SCAN_DPP_REDUCE
+#define SCAN_DPP_REDUCE 1
+#endif
+template <bool MAX>
+THX_DEV float half_reduce(float v)
+{
+#if SCAN_DPP_REDUCE
+    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false)));
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false)));
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false)));
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false)));
+    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return op(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+#else
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v = MAX ? fmaxf(v, __shfl_xor(v, o, 64)) : v + __shfl_xor(v, o, 64);
+    return v;
+#endif
+}
+
 // LDS stages of the chunk pipeline: chunk ck + STAGES - 1 is copied while
 // chunk ck is multiplied, so each copy has STAGES - 1 chunks to land
 #ifndef SCAN_STAGES
@@ -549,8 +575,7 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                 acc[a][f][j] = d;
                 if (f * 32 + n < nT) mx = fmaxf(mx, d);
             }
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+            mx = half_reduce<true>(mx);
             if (!rValid) mx = -INFINITY;
             float sR = 0.f;
 #pragma unroll
@@ -559,8 +584,7 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                 acc[a][f][j] = e;
                 sR += e * pTv[f];
             }
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) sR += __shfl_xor(sR, o, 64);
+            sR = half_reduce<false>(sR);
             if (n == 0) {
                 sMax[w * 64 + row] = mx;
                 if (rValid && l < nImg) wRp[(size_t)l * nR + r] = make_float2(mx, sR);

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Scan-only A/B: tools/microbench.py scan once per library per round, the
+# libraries interleaved over ROUNDS rounds, one JSON line each to
+# gpurun_out/ab/TAG_scan.jsonl.   tools/scan_ab.sh TAG ROUNDS NAME ...
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+tag=$1; rounds=$2; shift 2
+O=$R/gpurun_out/ab
+mkdir -p $O
+for k in $(seq $rounds); do
+  for t in "$@"; do
+    lib=$R/thunder_amd/ab/lib_$t.so
+    [ $t = prod ] && lib=$R/thunder_amd/libthunder_amd.so
+    echo -n "{\"tag\": \"$t\", \"round\": $k, \"run\": " >> $O/${tag}_scan.jsonl
+    THX_LIB=$lib timeout -k 10 120 python -u $R/tools/microbench.py scan | tail -1 >> $O/${tag}_scan.jsonl
+    echo "}" >> $O/${tag}_scan.jsonl
+  done
+done
