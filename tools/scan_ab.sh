@@ -11,8 +11,7 @@ for k in $(seq $rounds); do
   for t in "$@"; do
     lib=$R/thunder_amd/ab/lib_$t.so
     [ $t = prod ] && lib=$R/thunder_amd/libthunder_amd.so
-    echo -n "{\"tag\": \"$t\", \"round\": $k, \"run\": " >> $O/${tag}_scan.jsonl
-    THX_LIB=$lib timeout -k 10 120 python -u $R/tools/microbench.py scan | tail -1 >> $O/${tag}_scan.jsonl
-    echo "}" >> $O/${tag}_scan.jsonl
+    run=$(THX_LIB=$lib timeout -k 10 120 python -u $R/tools/microbench.py scan | tail -1)
+    echo "{\"tag\": \"$t\", \"round\": $k, \"run\": $run}" >> $O/${tag}_scan.jsonl
   done
 done
