@@ -322,13 +322,9 @@ __global__ void __launch_bounds__(256) k_scan_bias(const float* __restrict__ Bc,
 // (0, 1) and (2, 3) through v_permlane16_swap -- no ds_bpermute round trips
 // through the LDS pipe (the shuffles were 320 of them per wave, each waited
 // on).  Lane n == 0's sum is the one stored.
-#ifndef SCAN_DPP_REDUCE
-#define SCAN_DPP_REDUCE 1
-#endif
 template <bool MAX>
 THX_DEV float half_reduce(float v)
 {
-#if SCAN_DPP_REDUCE
     auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
     v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false)));
     v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false)));
@@ -336,17 +332,7 @@ THX_DEV float half_reduce(float v)
     v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false)));
     const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     return op(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-#else
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) v = MAX ? fmaxf(v, __shfl_xor(v, o, 64)) : v + __shfl_xor(v, o, 64);
-    return v;
-#endif
 }
-
-// the software-pipelined BF16X3 chunk body (0: the plain one, A/B)
-#ifndef SCAN_PIPE
-#define SCAN_PIPE 0
-#endif
 
 // LDS stages of the chunk pipeline: chunk ck + STAGES - 1 is copied while
 // chunk ck is multiplied, so each copy has STAGES - 1 chunks to land
@@ -490,138 +476,58 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
         const uint16_t* sTl = reinterpret_cast<const uint16_t*>(stage + S::TL_OFF);
         const float2* sA = reinterpret_cast<const float2*>(stage + S::A_OFF);
         const float2* sP = reinterpret_cast<const float2*>(stage + S::P_OFF);
-        if constexpr (MODE == BF16X3 && SCAN_PIPE) {
-            // Software-pipelined: the w of step s + 1 (both image halves) is
-            // formed while the 6 NF MFMAs of step s issue, in program order
-            // between them (sched_barrier fences): a wave issues in order and
-            // an MFMA blocks the instructions behind it until the matrix
-            // pipe takes it, so VALU placed after an MFMA chain would wait
-            // for the whole chain.  The T fragments of f + 1 are read while
-            // f multiplies.  Per accumulator the products keep their order
-            // (hi hi, hi lo, lo hi; step s before s + 1).
-            struct Ops { f32x4v p01, p23, a01[2], a23[2]; };
-            auto load_ops = [&](int s, Ops& o) {
-                const int px0 = 8 * s + 4 * h;
-                o.p01 = *reinterpret_cast<const f32x4v*>(sP + w * KC + px0);
-                o.p23 = *reinterpret_cast<const f32x4v*>(sP + w * KC + px0 + 2);
+#pragma unroll
+        for (int s = 0; s < KC / 8; s++) {
+            // A fragments: w = a conj(P_r) for images a*32 + n, pixels 8s+4h+{0..3}
+            const int px0 = 8 * s + 4 * h;
+            const f32x4v p01 = *reinterpret_cast<const f32x4v*>(sP + w * KC + px0);
+            const f32x4v p23 = *reinterpret_cast<const f32x4v*>(sP + w * KC + px0 + 2);
+            const float pr[4] = {p01.x, p01.z, p23.x, p23.z};
+            const float pi[4] = {p01.y, p01.w, p23.y, p23.w};
+            // w fragments of image half a (hi, lo split in registers)
+            auto make_w = [&](int a, HV& wh, HV& wl) {
+                const float2* rowA = sA + (a * 32 + n) * APITCH + px0;
+                const f32x4v a01 = *reinterpret_cast<const f32x4v*>(rowA);
+                const f32x4v a23 = *reinterpret_cast<const f32x4v*>(rowA + 2);
+                const float ar[4] = {a01.x, a01.z, a23.x, a23.z};
+                const float ai[4] = {a01.y, a01.w, a23.y, a23.w};
+#pragma unroll
+                for (int qd = 0; qd < 4; qd++) {
+                    const float wr = ar[qd] * pr[qd] + ai[qd] * pi[qd];
+                    const float wi = ai[qd] * pr[qd] - ar[qd] * pi[qd];
+                    H x0, x1;
+                    split16(wr, x0, x1); wh[2 * qd] = x0; wl[2 * qd] = x1;
+                    split16(wi, x0, x1); wh[2 * qd + 1] = x0; wl[2 * qd + 1] = x1;
+                }
+            };
+            if constexpr (MODE == BF16X3) {
+                // one image half at a time (register budget of the three products)
 #pragma unroll
                 for (int a = 0; a < 2; a++) {
-                    const float2* rowA = sA + (a * 32 + n) * APITCH + px0;
-                    o.a01[a] = *reinterpret_cast<const f32x4v*>(rowA);
-                    o.a23[a] = *reinterpret_cast<const f32x4v*>(rowA + 2);
-                }
-            };
-            // pixel qd of half a: w = a conj(P), split into the hi / lo fragments
-            auto w_piece = [&](const Ops& o, int a, int qd, HV (&wh)[2], HV (&wl)[2]) {
-                const f32x4v pv = qd < 2 ? o.p01 : o.p23, av = qd < 2 ? o.a01[a] : o.a23[a];
-                const float pr = (qd & 1) ? pv.z : pv.x, pi = (qd & 1) ? pv.w : pv.y;
-                const float ar = (qd & 1) ? av.z : av.x, ai = (qd & 1) ? av.w : av.y;
-                const float wr = ar * pr + ai * pi;
-                const float wi = ai * pr - ar * pi;
-                H x0, x1;
-                split16(wr, x0, x1); wh[a][2 * qd] = x0; wl[a][2 * qd] = x1;
-                split16(wi, x0, x1); wh[a][2 * qd + 1] = x0; wl[a][2 * qd + 1] = x1;
-            };
-            auto t_frag = [&](int f, int s, HV& th, HV& tl) {
-                const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
-                th = *reinterpret_cast<const HV*>(sTh + row);
-                tl = *reinterpret_cast<const HV*>(sTl + row);
-            };
-            HV wh[2], wl[2];
-            {
-                Ops o;
-                load_ops(0, o);
+                    HV wh, wl;
+                    make_w(a, wh, wl);
 #pragma unroll
-                for (int k = 0; k < 8; k++) w_piece(o, k >> 2, k & 3, wh, wl);
-            }
-#pragma unroll
-            for (int s = 0; s < KC / 8; s++) {
-                const bool nxt = s + 1 < KC / 8;
-                Ops on;
-                if (nxt) load_ops(s + 1, on);
-                HV nh[2], nl[2];
-                HV th, tl;
-                t_frag(0, s, th, tl);
-#pragma unroll
-                for (int f = 0; f < NF; f++) {
-                    HV th2, tl2;
-                    if (f + 1 < NF) t_frag(f + 1, s, th2, tl2);
-                    acc[0][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[0], th, acc[0][f], 0, 0, 0);
-                    acc[1][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[1], th, acc[1][f], 0, 0, 0);
-                    acc[0][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[0], tl, acc[0][f], 0, 0, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (nxt && 2 * f < 8) w_piece(on, (2 * f) >> 2, (2 * f) & 3, nh, nl);
-                    __builtin_amdgcn_sched_barrier(0);
-                    acc[1][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh[1], tl, acc[1][f], 0, 0, 0);
-                    acc[0][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[0], th, acc[0][f], 0, 0, 0);
-                    acc[1][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl[1], th, acc[1][f], 0, 0, 0);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (nxt && 2 * f + 1 < 8) w_piece(on, (2 * f + 1) >> 2, (2 * f + 1) & 3, nh, nl);
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (f + 1 < NF) { th = th2; tl = tl2; }
-                }
-                if (nxt) {
-                    // NF < 4 leaves pieces for after the chain
-#pragma unroll
-                    for (int k = 2 * NF; k < 8; k++) w_piece(on, k >> 2, k & 3, nh, nl);
-#pragma unroll
-                    for (int a = 0; a < 2; a++) { wh[a] = nh[a]; wl[a] = nl[a]; }
-                }
-            }
-        } else {
-    #pragma unroll
-            for (int s = 0; s < KC / 8; s++) {
-                // A fragments: w = a conj(P_r) for images a*32 + n, pixels 8s+4h+{0..3}
-                const int px0 = 8 * s + 4 * h;
-                const f32x4v p01 = *reinterpret_cast<const f32x4v*>(sP + w * KC + px0);
-                const f32x4v p23 = *reinterpret_cast<const f32x4v*>(sP + w * KC + px0 + 2);
-                const float pr[4] = {p01.x, p01.z, p23.x, p23.z};
-                const float pi[4] = {p01.y, p01.w, p23.y, p23.w};
-                // w fragments of image half a (hi, lo split in registers)
-                auto make_w = [&](int a, HV& wh, HV& wl) {
-                    const float2* rowA = sA + (a * 32 + n) * APITCH + px0;
-                    const f32x4v a01 = *reinterpret_cast<const f32x4v*>(rowA);
-                    const f32x4v a23 = *reinterpret_cast<const f32x4v*>(rowA + 2);
-                    const float ar[4] = {a01.x, a01.z, a23.x, a23.z};
-                    const float ai[4] = {a01.y, a01.w, a23.y, a23.w};
-    #pragma unroll
-                    for (int qd = 0; qd < 4; qd++) {
-                        const float wr = ar[qd] * pr[qd] + ai[qd] * pi[qd];
-                        const float wi = ai[qd] * pr[qd] - ar[qd] * pi[qd];
-                        H x0, x1;
-                        split16(wr, x0, x1); wh[2 * qd] = x0; wl[2 * qd] = x1;
-                        split16(wi, x0, x1); wh[2 * qd + 1] = x0; wl[2 * qd + 1] = x1;
-                    }
-                };
-                if constexpr (MODE == BF16X3) {
-                    // one image half at a time (register budget of the three products)
-    #pragma unroll
-                    for (int a = 0; a < 2; a++) {
-                        HV wh, wl;
-                        make_w(a, wh, wl);
-    #pragma unroll
-                        for (int f = 0; f < NF; f++) {
-                            const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
-                            const HV th = *reinterpret_cast<const HV*>(sTh + row);
-                            const HV tl = *reinterpret_cast<const HV*>(sTl + row);
-                            acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, th, acc[a][f], 0, 0, 0);
-                            acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, tl, acc[a][f], 0, 0, 0);
-                            acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, th, acc[a][f], 0, 0, 0);
-                        }
-                    }
-                } else {
-                    HV wh[2], wl[2];
-                    make_w(0, wh[0], wl[0]);
-                    make_w(1, wh[1], wl[1]);
-    #pragma unroll
                     for (int f = 0; f < NF; f++) {
                         const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
                         const HV th = *reinterpret_cast<const HV*>(sTh + row);
-    #pragma unroll
-                        for (int a = 0; a < 2; a++) {
-                            acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[a], th, acc[a][f], 0, 0, 0);
-                            acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl[a], th, acc[a][f], 0, 0, 0);
-                        }
+                        const HV tl = *reinterpret_cast<const HV*>(sTl + row);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, th, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, tl, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, th, acc[a][f], 0, 0, 0);
+                    }
+                }
+            } else {
+                HV wh[2], wl[2];
+                make_w(0, wh[0], wl[0]);
+                make_w(1, wh[1], wl[1]);
+#pragma unroll
+                for (int f = 0; f < NF; f++) {
+                    const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
+                    const HV th = *reinterpret_cast<const HV*>(sTh + row);
+#pragma unroll
+                    for (int a = 0; a < 2; a++) {
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[a], th, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl[a], th, acc[a][f], 0, 0, 0);
                     }
                 }
             }
