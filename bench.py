@@ -658,19 +658,27 @@ def main():
             # box pf N), FSC of the reconstructed maps
             # (a first call makes the hipFFT plans -- kernels compiled at run
             # time on a fresh box -- which stay cached for later iterations)
-            # the two hemispheres' solves on two streams from two host threads
-            # (per-stream hipFFT plans and workspaces: they overlap)
+            # the two hemispheres' solves: one after the other on one stream
+            # (each solve is HBM-bound: r04q measured two streams from two host
+            # threads at 2.7x one solve, worse than serial), and, for the
+            # record, on two streams from two host threads (per-stream hipFFT
+            # plans and workspaces)
             import threading
             streams = [torch.cuda.Stream(dev) for _ in recs]
             recs_out = [None] * len(recs)
             T0 = [r_.hm.T.clone() for r_ in recs]
+
+            def reset_T():
+                for r_, t0 in zip(recs, T0):
+                    r_.hm.T.copy_(t0)                 # thx_reconstruct modifies T in place
+                torch.cuda.synchronize()
 
             def solve(k):
                 with torch.cuda.stream(streams[k]):
                     recs_out[k] = ops.reconstruct(recs[k].hm, N, pf)
                 streams[k].synchronize()
 
-            def both():
+            def both_concurrent():
                 th = [threading.Thread(target=solve, args=(k,)) for k in range(len(recs))]
                 for t_ in th:
                     t_.start()
@@ -678,14 +686,23 @@ def main():
                     t_.join()
                 torch.cuda.synchronize()
 
-            both()                                    # plans per stream (first call)
-            for r_, t0 in zip(recs, T0):
-                r_.hm.T.copy_(t0)                     # thx_reconstruct modifies T in place
-            torch.cuda.synchronize()
+            def both_serial():
+                for k in range(len(recs)):
+                    recs_out[k] = ops.reconstruct(recs[k].hm, N, pf)
+                torch.cuda.synchronize()
+
+            both_concurrent()                         # plans per stream (first call)
+            reset_T()
+            both_serial()                             # this stream's plans
+            reset_T()
             t1 = time.perf_counter()
-            both()
-            extras["reconstruct_ms_per_halfmap"] = (time.perf_counter() - t1) * 1e3 / 2
+            both_concurrent()
             extras["reconstruct_ms_two_halfmaps_concurrent"] = (time.perf_counter() - t1) * 1e3
+            reset_T()
+            t1 = time.perf_counter()
+            both_serial()
+            extras["reconstruct_ms_two_halfmaps"] = (time.perf_counter() - t1) * 1e3
+            extras["reconstruct_ms_per_halfmap"] = extras["reconstruct_ms_two_halfmaps"] / 2
             extras["reconstruct_balancing_iterations"] = [o[2] for o in recs_out]
             # one half-map's solve alone, for the concurrency ratio
             hm1 = ops.HalfMap(recs[0].hm.vdim, dev)
