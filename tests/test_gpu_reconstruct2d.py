@@ -118,7 +118,7 @@ def test_c1_two_iterations_on_gpu():
     # high shells are noise-dominated, so the second expectation weighs the
     # reconstructed classes' noisy high shells by their real reliability
     # (per-shell SNR noise would trust them 10:1 and classify on the solve's
-    # high-frequency residue -- tools/diag/c1_frc.py)
+    # high-frequency residue -- tools/diag_c1_frc.py)
     dat, sig = synth.noisy_images(ctf * P * ops.trans_table(T_(tt), px), px.iSig, N1 // 2 + 1, snr=3.0,
                                   seed=85, white=True)
     # the full-resolution pixel set for the insert (rU = N / 2 - 2, the

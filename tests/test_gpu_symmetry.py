@@ -176,7 +176,7 @@ def test_expectation_with_symmetry_recovers_poses():
     R, Q = ops.symmetry(sym)
     vol = synth.projectee(synth.blob_volume(N, n_blobs=10, seed=4, sym_R=R, device=DEV), pf)
     # rU 12: the global search's resolution (at rU 20 the 1500-rotation grid
-    # is too coarse for both the C4 and the C1 search; tools/diag/sym_expect.py)
+    # is too coarse for both the C4 and the C1 search)
     px = ops.PixelSet(N, pf, 12, 1, device=DEV)
     mS, nR, nT = ops.global_sample_sizes(1500, n_sym_elem=len(Q))
     assert (mS, nR) == (6000, 1500)
