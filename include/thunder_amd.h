@@ -237,8 +237,8 @@ int thx_local_phase_routed(const thx_local_sel* sel, const float* vol,
                            size_t wsBytes, thx_stream_t stream);
 
 /* The image order thx_expectation's 3D phases use (the active list of
- * thx_local_phase_sel): images stably sorted by the Morton code (16 + 16 bits)
- * of the octahedral map of their slice normal n = R(q) e_z, q = the first
+ * thx_local_phase_sel): images stably sorted by the Hilbert index (16-bit
+ * cells) of the octahedral map of their slice normal n = R(q) e_z, q = the first
  * particle quat[l][0] of the cloud, n and -n one plane (n_z >= 0).  The
  * workgroups in flight then gather from one slab of the projectee, which
  * stays in an XCD's L2; per-image results do not depend on the order.

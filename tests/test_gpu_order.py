@@ -1,7 +1,7 @@
 """thx_view_order (csrc/order.hip): the image order of the 3D phases, against
 a numpy restatement of its key -- slice normal n = R(q) e_z (quat_to_mat of
 common.h, rotate3D of src/Geometry/Euler.cpp:181-189), n_z >= 0, octahedral
-map, 16 + 16-bit Morton code -- and a stable sort."""
+map, 16-bit cells, their Hilbert index -- and a stable sort."""
 import numpy as np
 import pytest
 import torch
@@ -26,11 +26,21 @@ def _keys(q, cells=False):
     qv = np.clip((n[:, 1] / s + 1) * 32768, 0, 65535).astype(np.uint64)
     if cells:
         return qu.astype(np.int64), qv.astype(np.int64)
-    key = np.zeros(len(q), dtype=np.uint64)
-    for b in range(16):
-        key |= ((qu >> b) & 1) << (2 * b)
-        key |= ((qv >> b) & 1) << (2 * b + 1)
-    return key
+    return np.array([_hilbert(int(x), int(y)) for x, y in zip(qu, qv)], dtype=np.uint64)
+
+
+def _hilbert(x, y, n=1 << 16):
+    """xy -> index on the Hilbert curve of an n x n grid."""
+    d, s = 0, n // 2
+    while s > 0:
+        rx, ry = int(x & s > 0), int(y & s > 0)
+        d += s * s * ((3 * rx) ^ ry)
+        if ry == 0:
+            if rx == 1:
+                x, y = n - 1 - x, n - 1 - y
+            x, y = y, x
+        s //= 2
+    return d
 
 
 def _order(quat):

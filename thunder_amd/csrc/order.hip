@@ -18,7 +18,11 @@
 
 namespace {
 
-// 16-bit Morton interleave
+// index of (x, y) on the Hilbert curve through the 2^16 x 2^16 grid (its
+// runs of consecutive indices are connected, where a Morton order's jump)
+#ifndef THX_VIEW_HILBERT
+#define THX_VIEW_HILBERT 1
+#endif
 THX_DEV unsigned spread16(unsigned v)
 {
     v &= 0xffffu;
@@ -28,10 +32,26 @@ THX_DEV unsigned spread16(unsigned v)
     v = (v | (v << 1)) & 0x55555555u;
     return v;
 }
+THX_DEV unsigned curve16(unsigned x, unsigned y)
+{
+    if (!THX_VIEW_HILBERT) return spread16(x) | (spread16(y) << 1);
+    constexpr unsigned N = 1u << 16;
+    unsigned d = 0;
+    for (unsigned s = N / 2; s > 0; s >>= 1) {
+        const unsigned rx = (x & s) ? 1u : 0u, ry = (y & s) ? 1u : 0u;
+        d += s * s * ((3u * rx) ^ ry);
+        if (ry == 0) {
+            if (rx == 1) { x = N - 1 - x; y = N - 1 - y; }
+            const unsigned t = x; x = y; y = t;
+        }
+    }
+    return d;
+}
 
 // key of image l: the slice normal n = R(q) e_z of the cloud's first
 // particle (column 2 of quat_to_mat's column-major R), n and -n being one
-// plane (n_z >= 0), octahedral map onto [-1, 1]^2, Morton code of 16 + 16 bits
+// plane (n_z >= 0), octahedral map onto [-1, 1]^2, 16-bit cells, their
+// Hilbert index
 __global__ void __launch_bounds__(256) k_view_key(int nImg, int mLR, const double* __restrict__ quat,
                                                   unsigned* __restrict__ key, int* __restrict__ idx)
 {
@@ -44,7 +64,7 @@ __global__ void __launch_bounds__(256) k_view_key(int nImg, int mLR, const doubl
     const double s = fabs(nx) + fabs(ny) + nz;
     const double u = s > 0.0 ? nx / s : 0.0, v = s > 0.0 ? ny / s : 0.0;
     auto q16 = [](double t) { return (unsigned)fmin(65535.0, fmax(0.0, (t + 1.0) * 32768.0)); };
-    key[l] = spread16(q16(u)) | (spread16(q16(v)) << 1);
+    key[l] = curve16(q16(u), q16(v));
     idx[l] = l;
 }
 
