@@ -92,18 +92,19 @@ def single(rd, wr, name, grid, factor, shape, per=1):
 
 
 def routed_phase(rd, wr, grid, factor, shape):
-    """Bytes per routed bench phase: its two k_local_fused<0> dispatches
-    (staged / box-less variant) plus its y-pair dispatch (k_local_fused<4>,
-    the pair form; <3> the quad form); the kernels not chosen exit at entry."""
+    """Bytes per routed bench phase: its staged half-complex dispatch
+    (k_local_fused<0>) plus, with a y-pair copy, the pair-form dispatch
+    (k_local_fused<2>, LAYOUT_YPAIR2) or, without, the box-less <0> variant;
+    the kernel not chosen exits at entry."""
     r0 = [v for n, g, v in rd if "k_local_fused<0," in n and g == grid]
     w0 = [v for n, g, v in wr if "k_local_fused<0," in n and g == grid]
-    r3 = [v for n, g, v in rd if ("k_local_fused<3," in n or "k_local_fused<4," in n) and g == grid]
-    w3 = [v for n, g, v in wr if ("k_local_fused<3," in n or "k_local_fused<4," in n) and g == grid]
+    r2 = [v for n, g, v in rd if "k_local_fused<2," in n and g == grid]
+    w2 = [v for n, g, v in wr if "k_local_fused<2," in n and g == grid]
     if not r0 or not w0:
         return None
-    nph = len(r0) // 2
-    return _entry((sum(r0) + sum(r3)) / nph, (sum(w0) + sum(w3)) / nph, factor, nph,
-                  ["k_local_fused<0,", "k_local_fused<4,"], shape)
+    nph = len(r2) if r2 else len(r0) // 2
+    return _entry((sum(r0) + sum(r2)) / nph, (sum(w0) + sum(w2)) / nph, factor, nph,
+                  ["k_local_fused<0,", "k_local_fused<2,"], shape)
 
 
 def sliced(rd, wr, name, grid, k, per, factor, shape, pair=1):
