@@ -337,15 +337,7 @@ __global__ void __launch_bounds__(CF_THREADS) k_col_fft(float2* __restrict__ a, 
 #ifndef EVEN_BALANCE
 #define EVEN_BALANCE 1             // 0: the hipFFT loop everywhere (A/B builds)
 #endif
-#ifndef EV_CT_COLS
-#define EV_CT_COLS 16
-#endif
-constexpr int EV_CT = EV_CT_COLS;  // columns per tile of the column passes
-#ifdef EV_WPE
-#define EV_OCC __attribute__((amdgpu_waves_per_eu(EV_WPE)))
-#else
-#define EV_OCC
-#endif
+constexpr int EV_CT = 16;          // columns per tile of the column passes
 constexpr int EV_WAVES = 4;
 
 bool even_ok(int vdim) { return vdim == 64 || vdim == 128 || vdim == 256 || vdim == 512; }
@@ -405,7 +397,7 @@ THX_DEV int even_tile(int ntiles)
 // issued before the first LDS write, so the T / W latency hides behind the
 // C2R instead of being paid once per kz.
 template <int N, bool INIT>
-__global__ void __launch_bounds__(64 * EV_WAVES) EV_OCC k_even_z(float2* __restrict__ G, float* __restrict__ W,
+__global__ void __launch_bounds__(64 * EV_WAVES) k_even_z(float2* __restrict__ G, float* __restrict__ W,
                                                          const float* __restrict__ T, int r2,
                                                          unsigned* __restrict__ diffBits,
                                                          const float2* __restrict__ tw)
@@ -497,7 +489,7 @@ __global__ void __launch_bounds__(64 * EV_WAVES) EV_OCC k_even_z(float2* __restr
 
 // y columns: C2C along y, sign S.  A block: a tile of EV_CT kx columns at one nz.
 template <int N, int S>
-__global__ void __launch_bounds__(64 * EV_WAVES) EV_OCC k_even_y(float2* __restrict__ G, const float2* __restrict__ tw)
+__global__ void __launch_bounds__(64 * EV_WAVES) k_even_y(float2* __restrict__ G, const float2* __restrict__ tw)
 {
     extern __shared__ float2 sm[];
     constexpr int H = N / 2 + 1, P = thx::fft_pitch<N>(), NT = (H + EV_CT - 1) / EV_CT;
