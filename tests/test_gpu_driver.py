@@ -189,6 +189,23 @@ def test_local_search_fixed_phases_is_reproducible(local_stack):
     assert (outs[0][6] == 2).all()      # phases 0, 1, 2
 
 
+@pytest.mark.parametrize("converge", [False, True])
+def test_view_order_leaves_every_image_unchanged(local_stack, monkeypatch, converge):
+    """thx_view_order (csrc/order.hip) only changes which workgroup takes
+    which image in the 3D phases: with the order (default) and without
+    (THX_VIEW_ORDER=0) the driver returns bit-identical particles, priors,
+    scores, classes and phase counts -- global search, fixed phases and the
+    stopping rule."""
+    s = local_stack
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("THX_VIEW_ORDER", flag)
+        e = ex.Expectation(s["vol"], s["px"], s["gset"], n_phase=4, seed=12, converge=converge)
+        outs.append([x.clone() for x in e.run(s["dat"], s["ctf"], s["sig"])])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_global_converge_matches_fixed_quality(local_stack):
     """The stopping rule ends every image between phase 11 and 99 and keeps
     the grid-pose recovery of the fixed 10-phase run."""

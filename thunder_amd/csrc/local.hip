@@ -1491,7 +1491,8 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
                             float* wR, float* wT, float* baseL, float* dvp, void* workspace,
                             size_t wsBytes, thx_stream_t stream, int nD = 0,
                             const double* pD = nullptr, float* wD = nullptr,
-                            const float* ypair = nullptr, int* routeOut = nullptr)
+                            const float* ypair = nullptr, int* routeOut = nullptr,
+                            const int* const* routeSample = nullptr)
 {
     THX_CHECK_ARG(nR > 0 && nT > 0 && nPxl > 0 && nImg >= 0 && vdim > 0 && pf > 0 && nD >= 0,
                   "thx_local_phase: bad sizes");
@@ -1534,9 +1535,15 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     if (routed) {
         THX_HIP(hipMemsetAsync(route, 0, 2 * sizeof(int), s));
         THX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(route + 2), ypair ? 1 : 0, 1, s));
+        // the route's sample: every ROUTE_SAMPLE-th entry of the active list,
+        // or of the list the caller names (routeSample = {list, count}, both
+        // null = every image in index order), so that a reordered active list
+        // does not change the sample and with it the kernel
+        const int* sAct = routeSample ? routeSample[0] : act;
+        const int* sNAct = routeSample ? routeSample[1] : nAct;
         hipLaunchKernelGGL(k_patch_boxes, dim3((unsigned)thx::cdiv(nImg, ROUTE_SAMPLE) * nRT),
                            dim3(64 * PB_WAVES), 0, s, quat, nR, iCol, iRow, pxOrder, nVisit, pf, vdim,
-                           rec, act, nAct, route, 1);
+                           rec, sAct, sNAct, route, 1);
         THX_LAUNCH_CHECK();
         if (routeOut) {
             hipLaunchKernelGGL(k_route_out, dim3(1), dim3(64), 0, s, route, routeOut);
@@ -1702,12 +1709,13 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       const int* iCol, const int* iRow, const int* pxOrder, int nOrd, int nPxl,
                       int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
                       void* workspace, size_t wsBytes, thx_stream_t stream, int nD,
-                      const double* pD, float* wD, const float* ypair, int* routeOut)
+                      const double* pD, float* wD, const float* ypair, int* routeOut,
+                      const int* const* routeSample)
 {
     return local_phase_impl(sel, evBeg, evEnd, vol, volLayout, vdim, pf, quat, nR, trans, nT, pC,
                             pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg,
                             wC, wR, wT, baseL, nullptr, workspace, wsBytes, stream, nD, pD, wD,
-                            ypair, routeOut);
+                            ypair, routeOut, routeSample);
 }
 
 // whether local_phase_impl routes a phase on the device (half-complex layout,

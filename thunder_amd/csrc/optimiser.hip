@@ -52,7 +52,8 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
                       void* workspace, size_t wsBytes, thx_stream_t stream, int nD = 0,
                       const double* pD = nullptr, float* wD = nullptr,
-                      const float* ypair = nullptr, int* routeOut = nullptr);
+                      const float* ypair = nullptr, int* routeOut = nullptr,
+                      const int* const* routeSample = nullptr);
 bool phase_routed(int volLayout, int pf, int nPxl, int nD);
 int pf_symmetrise_launch(int nImg, int mR, double* quat, int anchorMode, const double* anchor,
                          const double* symQ, int nSym, uint64_t seed, uint32_t stream,
@@ -66,6 +67,13 @@ int view_order(int nImg, int mLR, const double* quat, unsigned* keys, unsigned* 
 #ifndef THX_VIEW_ORDER
 #define THX_VIEW_ORDER 1
 #endif
+// THX_VIEW_ORDER=0 in the environment turns it off per call (the test that
+// the order leaves every image's result unchanged compares both)
+static bool view_order_on()
+{
+    const char* e = std::getenv("THX_VIEW_ORDER");
+    return !(e && e[0] == '0');
+}
 
 namespace {
 
@@ -1253,6 +1261,7 @@ struct Plan {
     double* meanQ;                           // k_pf_mean's perturbation mean
     float* wC; float* wR; float* wT; float* base; double* pC;
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
+    int* actIdx; int* nActIdx;           // the active list in index order (route samples)
     unsigned* ordKey; unsigned* ordKeyOut; int* ordIdx; int* ord;   // view order (order.hip)
     void* ordTmp; size_t ordTmpBytes;
     double* bestR; double* bestT;                        // convergence: smallest variR / variT
@@ -1309,6 +1318,8 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.done = k.take<int>(nImg);
     p.act = k.take<int>(nImg);
     p.nAct = k.take<int>(1);
+    p.actIdx = k.take<int>(nImg);
+    p.nActIdx = k.take<int>(1);
     const size_t nOrd = THX_VIEW_ORDER && !twoD ? (size_t)nImg : 0;
     p.ordKey = k.take<unsigned>(nOrd);
     p.ordKeyOut = k.take<unsigned>(nOrd);
@@ -1798,15 +1809,26 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     // 3D phases visit the images in view order (order.hip), through the
     // active list; results per image are unchanged
     const int* ord = nullptr;
-    if (THX_VIEW_ORDER && !twoD && nPh > 0) {
+    if (THX_VIEW_ORDER && !twoD && nPh > 0 && view_order_on()) {
         THX_RET(thx::view_order(nImg, c.mLR, quat, p.ordKey, p.ordKeyOut, p.ordIdx, p.ord, p.ordTmp,
                                 p.ordTmpBytes, s));
         ord = p.ord;
     }
+    // the route samples images in index order whatever the visiting order
+    // (the kernel a phase runs must not depend on it): every image without
+    // the stopping rule, the index-ordered active list with it
+    const int* sampleNone[2] = {nullptr, nullptr};
+    const int* sampleIdx[2] = {p.actIdx, p.nActIdx};
+    const int* const* routeSample = ord ? (c.converge ? sampleIdx : sampleNone) : nullptr;
     if (c.converge || ord) {
         THX_HIP(hipMemsetAsync(p.done, 0, sizeof(int) * nImg, s));
         hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct, ord);
         THX_LAUNCH_CHECK();
+        if (ord && c.converge) {
+            hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.actIdx, p.nActIdx,
+                               nullptr);
+            THX_LAUNCH_CHECK();
+        }
         if (c.converge) done = p.done;
         sel.active = p.act;
         sel.nActive = p.nAct;
@@ -1866,7 +1888,8 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                        dat, cs ? p.ctfD : ctf, sigRcp, iCol, iRow, pxOrder, nOrd,
                                        nPxl, c.idim, nImg, p.wC, p.wR, p.wT, p.base, p.localWs,
                                        p.localWsBytes, stream, mLD, cs ? cs->pD : nullptr, p.wD,
-                                       p.ypair, pi < c.nPhaseRoute ? c.phaseRoute + pi : nullptr));
+                                       p.ypair, pi < c.nPhaseRoute ? c.phaseRoute + pi : nullptr,
+                                       routeSample));
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
                            p.peakR, 0, nullptr, 0, done, rankDiv);
         THX_LAUNCH_CHECK();
@@ -1934,6 +1957,11 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             THX_LAUNCH_CHECK();
             hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.act, p.nAct, ord);
             THX_LAUNCH_CHECK();
+            if (ord) {
+                hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, nImg, p.done, p.actIdx,
+                                   p.nActIdx, nullptr);
+                THX_LAUNCH_CHECK();
+            }
             if (phase >= c.minPhase) {
                 int left = 0;
                 THX_HIP(hipMemcpyAsync(&left, p.nAct, sizeof(int), hipMemcpyDeviceToHost, s));
