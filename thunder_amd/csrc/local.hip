@@ -180,7 +180,29 @@ struct PCell {
     unsigned e0, e1;
     float dx, dy, dz;
 };
-THX_DEV PCell pcell_of(float x, float y, float z, int vdim)
+// index of element (x, y, z) of the whole y-pair copy (thx_volume_ypair),
+// nc = vdim / 2 + 1
+THX_DEV unsigned ypair_elem(unsigned z, unsigned y, unsigned x, unsigned vdim, unsigned nc)
+{
+    return (z * vdim + y) * nc + x;
+}
+// THX_YPAIR_ZIL: in the compact ball slices z and z + 1 (z + R even) are
+// interleaved element by element, so for such z0 a sample's four 16-B
+// elements (x0, x0 + 1 of both slices) are one contiguous 64-B piece
+#ifndef THX_YPAIR_ZIL
+#define THX_YPAIR_ZIL 1
+#endif
+// ballR > 0: the copy is the compact ball of thx::volume_ypair_ball --
+// elements (x, y, z), 0 <= x < ballR + 2, -ballR <= y, z < ballR + 2, no
+// wrap (every tap of the pixel ring lies inside)
+THX_DEV unsigned ypair_ball_elem(int z, int y, int x, int ballR)
+{
+    const unsigned Y = 2u * ballR + 2u, X = (unsigned)ballR + 2u;
+    const unsigned zc = (unsigned)(z + ballR), yc = (unsigned)(y + ballR);
+    return THX_YPAIR_ZIL ? (((zc >> 1) * Y + yc) * X + (unsigned)x) * 2u + (zc & 1u)
+                         : (zc * Y + yc) * X + (unsigned)x;
+}
+THX_DEV PCell pcell_of(float x, float y, float z, int vdim, int ballR = 0)
 {
     const bool conj = !(x >= 0.f);
     if (conj) { x = -x; y = -y; z = -z; }
@@ -189,17 +211,24 @@ THX_DEV PCell pcell_of(float x, float y, float z, int vdim)
     const unsigned nc = (unsigned)(vdim / 2 + 1);
     const unsigned yw = (unsigned)wrap_idx(y0, vdim);
     PCell c;
-    c.e0 = ((unsigned)wrap_idx(z0, vdim) * (unsigned)vdim + yw) * nc + (unsigned)x0;
-    c.e1 = ((unsigned)wrap_idx(z0 + 1, vdim) * (unsigned)vdim + yw) * nc + (unsigned)x0;
+    if (ballR > 0) {
+        c.e0 = ypair_ball_elem(z0, y0, x0, ballR);
+        c.e1 = ypair_ball_elem(z0 + 1, y0, x0, ballR);
+    } else {
+        c.e0 = ypair_elem((unsigned)wrap_idx(z0, vdim), yw, (unsigned)x0, (unsigned)vdim, nc);
+        c.e1 = ypair_elem((unsigned)wrap_idx(z0 + 1, vdim), yw, (unsigned)x0, (unsigned)vdim, nc);
+    }
     c.dx = __uint_as_float(__float_as_uint(x - fx) | (conj ? 0x80000000u : 0u));
     c.dy = y - fy;
     c.dz = z - fz;
     return c;
 }
 // lane j of the pair: element x0 + j of slices z0 and z0 + 1
-THX_DEV float2 ypair_pcell_part(const float4* __restrict__ yp, const PCell& c, int j)
+// (xs: the element stride of x -- 2 in the z-interleaved ball, else 1)
+THX_DEV float2 ypair_pcell_part(const float4* __restrict__ yp, const PCell& c, int j, unsigned xs)
 {
-    const float4 q0 = yp[c.e0 + (unsigned)j], q1 = yp[c.e1 + (unsigned)j];
+    const unsigned dj = xs * (unsigned)j;   // element x0 + j
+    const float4 q0 = yp[c.e0 + dj], q1 = yp[c.e1 + dj];
     const bool conj = (__float_as_uint(c.dx) >> 31) != 0;
     const float dx = fabsf(c.dx);
     const float wx = j ? dx : 1.f - dx;
@@ -758,7 +787,8 @@ k_local_fused(const float2* __restrict__ vol,
                                                             float* __restrict__ wR = nullptr,
                                                             float* __restrict__ wT = nullptr,
                                                             float* __restrict__ baseL = nullptr,
-                                                            const int* __restrict__ route = nullptr)
+                                                            const int* __restrict__ route = nullptr,
+                                                            int ballR = 0)
 {
     // routed phases launch the staged and the box-less kernel; one exits
     if (route && route_pick(route) != (LAYOUT == LAYOUT_YPAIR2 ? ROUTE_YPAIR
@@ -1036,19 +1066,20 @@ k_local_fused(const float2* __restrict__ vol,
         // r at pixels 4s + h (it 0) and 4s + h + 2 (it 1); lane j rotates the
         // it = j sample and the pair shares the cells.  MFMA A rows: (pixels
         // 4s, 4s + 2) from the h = 0 pairs, (4s + 1, 4s + 3) from the h = 1 pairs.
+        const unsigned yxs = ballR > 0 && THX_YPAIR_ZIL ? 2u : 1u;   // x stride of the copy's elements
         auto pair_step = [&](int s) {
             const int j = lane & 1, h = (lane >> 5) & 1;
             PCell mine;
             {
                 const double2 xy = make_double2(sXY[4 * s + h + 2 * j].x, sXY[4 * s + h + 2 * j].y);
                 mine = pcell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
-                                (float)(m[2] * xy.x + m[5] * xy.y), vdim);
+                                (float)(m[2] * xy.x + m[5] * xy.y), vdim, ballR);
             }
             float2 P[2];
 #pragma unroll
             for (int it = 0; it < 2; it++) {
                 const PCell c = it == 0 ? pair_bcast_pcell<0>(mine) : pair_bcast_pcell<1>(mine);
-                const float2 v = ypair_pcell_part(reinterpret_cast<const float4*>(vol), c, j);
+                const float2 v = ypair_pcell_part(reinterpret_cast<const float4*>(vol), c, j, yxs);
                 P[it] = make_float2(v.x + pair_swap(v.x), v.y + pair_swap(v.y));
             }
             if (!CS)
@@ -1404,7 +1435,29 @@ __global__ void __launch_bounds__(256) k_volume_ypair(const float2* __restrict__
         const int j = (int)(jk % vdim), k = (int)(jk / vdim);
         const int j1 = j + 1 == vdim ? 0 : j + 1;
         const float2 a = vol[q], b = vol[((size_t)k * vdim + j1) * nColFT + i];
-        yp[q] = make_float4(a.x, a.y, b.x, b.y);
+        yp[ypair_elem((unsigned)k, (unsigned)j, (unsigned)i, (unsigned)vdim, (unsigned)nColFT)] =
+            make_float4(a.x, a.y, b.x, b.y);
+    }
+}
+
+// the compact ball of the y-pair copy (ypair_ball_elem): elements
+// (x, y, z), 0 <= x < R + 2, -R <= y, z < R + 2, from the half-complex
+// volume with its wrap
+__global__ void __launch_bounds__(256) k_volume_ypair_ball(const float2* __restrict__ vol, int vdim,
+                                                           int R, float4* __restrict__ yp)
+{
+    const int nColFT = vdim / 2 + 1;
+    const int X = R + 2, Y = 2 * R + 2;
+    const long n = (long)X * Y * Y;
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
+         q += (long)gridDim.x * blockDim.x) {
+        const int x = (int)(q % X);
+        const long yz = q / X;
+        const int y = (int)(yz % Y) - R, z = (int)(yz / Y) - R;
+        const int zw = wrap_idx(z, vdim), yw = wrap_idx(y, vdim), yw1 = wrap_idx(y + 1, vdim);
+        const float2 a = x < nColFT ? vol[((size_t)zw * vdim + yw) * nColFT + x] : make_float2(0.f, 0.f);
+        const float2 b = x < nColFT ? vol[((size_t)zw * vdim + yw1) * nColFT + x] : make_float2(0.f, 0.f);
+        yp[ypair_ball_elem(z, y, x, R)] = make_float4(a.x, a.y, b.x, b.y);
     }
 }
 
@@ -1453,6 +1506,8 @@ int launch_patch_boxes(const double* quat, int nR, const int* iCol, const int* i
     return THX_OK;
 }
 
+size_t ypair_ball_elems(int R);
+
 }  // namespace thx
 
 extern "C" int thx_volume_cells(const float* vol, int vdim, float* cells,
@@ -1492,7 +1547,7 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
                             size_t wsBytes, thx_stream_t stream, int nD = 0,
                             const double* pD = nullptr, float* wD = nullptr,
                             const float* ypair = nullptr, int* routeOut = nullptr,
-                            const int* const* routeSample = nullptr)
+                            const int* const* routeSample = nullptr, int ypairR = 0)
 {
     THX_CHECK_ARG(nR > 0 && nT > 0 && nPxl > 0 && nImg >= 0 && vdim > 0 && pf > 0 && nD >= 0,
                   "thx_local_phase: bad sizes");
@@ -1582,7 +1637,7 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
                            vdim, pf, quat, nR, trans, nCol, reinterpret_cast<const float2*>(dat),
                            ctf, sigRcp, iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, d, act, nAct,
                            cls, vs, nD, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           nullptr);
+                           nullptr, 0);
         THX_LAUNCH_CHECK();
         if (evEnd) THX_HIP(hipEventRecord(evEnd, s));
         hipLaunchKernelGGL(k_local_weights_d, dim3(nImg), dim3(256), 0, s, d, nR, nT, nD, pC, pR,
@@ -1604,7 +1659,7 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
                            pf, quat, nR, trans, nT, reinterpret_cast<const float2*>(dat), ctf, sigRcp,
                            iCol, iRow, pxOrder, nVisit, nPxl, idim, rec, fuse ? dvp : d, act, nAct,
                            cls, vs, 1, pC, pR, pT, fuse ? wC : nullptr, fuse ? wR : nullptr,
-                           fuse ? wT : nullptr, fuse ? baseL : nullptr, rt);
+                           fuse ? wT : nullptr, fuse ? baseL : nullptr, rt, 0);
     };
     if (routed) {
         // two launches, the staged kernel and (with a y-pair copy) the pair-form
@@ -1616,9 +1671,9 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
                                reinterpret_cast<const float2*>(ypair), vdim, pf, quat, nR, trans, nT,
                                reinterpret_cast<const float2*>(dat), ctf, sigRcp, iCol, iRow, pxOrder,
                                nVisit, nPxl, idim, rec, fuse ? dvp : d, act, nAct, cls,
-                               cls ? 2 * vs : 0L, 1, pC, pR, pT, fuse ? wC : nullptr,
-                               fuse ? wR : nullptr, fuse ? wT : nullptr, fuse ? baseL : nullptr,
-                               route);
+                               cls ? (ypairR > 0 ? 2L * (long)thx::ypair_ball_elems(ypairR) : 2 * vs) : 0L, 1,
+                               pC, pR, pT, fuse ? wC : nullptr, fuse ? wR : nullptr,
+                               fuse ? wT : nullptr, fuse ? baseL : nullptr, route, ypairR);
         } else {
             launch(k_local_fused<LAYOUT_FT, false, 1, false, false>, route);
         }
@@ -1702,6 +1757,19 @@ extern "C" int thx_local_phase_routed(const thx_local_sel* sel, const float* vol
 
 namespace thx {
 // the driver's phase launch, with optional events around k_local_fused
+// float4 elements of the compact y-pair ball of radius R
+size_t ypair_ball_elems(int R) { return (size_t)(R + 2) * (2 * R + 2) * (2 * R + 2); }
+
+int volume_ypair_ball(const float* vol, int vdim, int R, float* ypair, hipStream_t s)
+{
+    THX_CHECK_ARG(vol && ypair && vdim > 0 && vdim % 2 == 0 && R > 0 && R + 2 <= vdim / 2 + 1,
+                  "volume_ypair_ball: bad arguments");
+    hipLaunchKernelGGL(k_volume_ypair_ball, dim3(2048), dim3(256), 0, s,
+                       reinterpret_cast<const float2*>(vol), vdim, R, reinterpret_cast<float4*>(ypair));
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
 int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evEnd,
                       const float* vol, int volLayout, int vdim, int pf, const double* quat, int nR,
                       const double* trans, int nT, const double* pC, const double* pR,
@@ -1710,12 +1778,12 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       int idim, int nImg, float* wC, float* wR, float* wT, float* baseL,
                       void* workspace, size_t wsBytes, thx_stream_t stream, int nD,
                       const double* pD, float* wD, const float* ypair, int* routeOut,
-                      const int* const* routeSample)
+                      const int* const* routeSample, int ypairR)
 {
     return local_phase_impl(sel, evBeg, evEnd, vol, volLayout, vdim, pf, quat, nR, trans, nT, pC,
                             pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim, nImg,
                             wC, wR, wT, baseL, nullptr, workspace, wsBytes, stream, nD, pD, wD,
-                            ypair, routeOut, routeSample);
+                            ypair, routeOut, routeSample, ypairR);
 }
 
 // whether local_phase_impl routes a phase on the device (half-complex layout,

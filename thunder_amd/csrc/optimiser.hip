@@ -53,7 +53,9 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
                       void* workspace, size_t wsBytes, thx_stream_t stream, int nD = 0,
                       const double* pD = nullptr, float* wD = nullptr,
                       const float* ypair = nullptr, int* routeOut = nullptr,
-                      const int* const* routeSample = nullptr);
+                      const int* const* routeSample = nullptr, int ypairR = 0);
+size_t ypair_ball_elems(int R);
+int volume_ypair_ball(const float* vol, int vdim, int R, float* ypair, hipStream_t s);
 bool phase_routed(int volLayout, int pf, int nPxl, int nD);
 int pf_symmetrise_launch(int nImg, int mR, double* quat, int anchorMode, const double* anchor,
                          const double* symQ, int nSym, uint64_t seed, uint32_t stream,
@@ -61,6 +63,26 @@ int pf_symmetrise_launch(int nImg, int mR, double* quat, int anchorMode, const d
 size_t view_order_tmp_bytes(int nImg);
 int view_order(int nImg, int mLR, const double* quat, unsigned* keys, unsigned* keysOut, int* idx,
                int* ord, void* tmp, size_t tmpBytes, hipStream_t s);
+}
+
+// the driver's y-pair copy as the compact ball of the pixel ring (local.hip
+// ypair_ball_elem); 0 for A/B builds
+#ifndef THX_YPAIR_BALL
+#define THX_YPAIR_BALL 1
+#endif
+
+// max iCol^2 + iRow^2 over the pixel set (one workgroup)
+__global__ void __launch_bounds__(256) k_max_r2(const int* __restrict__ iCol,
+                                                const int* __restrict__ iRow, int nPxl,
+                                                int* __restrict__ out)
+{
+    __shared__ int sm[4];
+    int m = 0;
+    for (int i = threadIdx.x; i < nPxl; i += 256) m = max(m, iCol[i] * iCol[i] + iRow[i] * iRow[i]);
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) *out = max(max(sm[0], sm[1]), max(sm[2], sm[3]));
 }
 
 // the 3D phases visit the images in view order (order.hip); 0 for A/B builds
@@ -1262,6 +1284,7 @@ struct Plan {
     float* wC; float* wR; float* wT; float* base; double* pC;
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
     int* actIdx; int* nActIdx;           // the active list in index order (route samples)
+    int* maxR2;                          // max iCol^2 + iRow^2 of the pixel set
     unsigned* ordKey; unsigned* ordKeyOut; int* ordIdx; int* ord;   // view order (order.hip)
     void* ordTmp; size_t ordTmpBytes;
     double* bestR; double* bestT;                        // convergence: smallest variR / variT
@@ -1319,6 +1342,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.act = k.take<int>(nImg);
     p.nAct = k.take<int>(1);
     p.actIdx = k.take<int>(nImg);
+    p.maxR2 = k.take<int>(1);
     p.nActIdx = k.take<int>(1);
     const size_t nOrd = THX_VIEW_ORDER && !twoD ? (size_t)nImg : 0;
     p.ordKey = k.take<unsigned>(nOrd);
@@ -1705,10 +1729,30 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     int* clsD = cls ? cls : p.cls;
     int* nPD = nPhaseOut ? nPhaseOut : p.nP;
     const int* clsSel = nK > 1 ? clsD : nullptr;    // rows / volumes picked per image
-    if (p.ypair)
-        for (int k = 0; k < nK; k++)
-            THX_RET(thx_volume_ypair(vol + 2 * dimSize * k, c.vdim,
-                                     p.ypair + 4 * dimSize * k, stream));
+    // the y-pair copy: the compact ball around the pixel ring (radius pf
+    // r_max + 2 voxels, no wrap, a few MB instead of the whole 2x volume:
+    // its pages stay in the TLBs and its lines in one region), or the whole
+    // copy when the ball is the volume
+    int ypairR = 0;
+    if (p.ypair) {
+        if (THX_YPAIR_BALL) {
+            hipLaunchKernelGGL(k_max_r2, dim3(1), dim3(256), 0, s, iCol, iRow, nPxl, p.maxR2);
+            THX_LAUNCH_CHECK();
+            int r2 = 0;
+            THX_HIP(hipMemcpyAsync(&r2, p.maxR2, sizeof(int), hipMemcpyDeviceToHost, s));
+            THX_HIP(hipStreamSynchronize(s));
+            const int R = (int)std::ceil(c.pf * std::sqrt((double)r2)) + 2;
+            if (R + 2 <= c.vdim / 2 + 1) ypairR = R;
+        }
+        for (int k = 0; k < nK; k++) {
+            if (ypairR > 0)
+                THX_RET(thx::volume_ypair_ball(vol + 2 * dimSize * k, c.vdim, ypairR,
+                                               p.ypair + 4 * thx::ypair_ball_elems(ypairR) * k, s));
+            else
+                THX_RET(thx_volume_ypair(vol + 2 * dimSize * k, c.vdim, p.ypair + 4 * dimSize * k,
+                                         stream));
+        }
+    }
 
     if (global) {
         // ---- global scan of every class (ExpectRotran + ExpectProject + ExpectGlobal3D
@@ -1889,7 +1933,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                        nPxl, c.idim, nImg, p.wC, p.wR, p.wT, p.base, p.localWs,
                                        p.localWsBytes, stream, mLD, cs ? cs->pD : nullptr, p.wD,
                                        p.ypair, pi < c.nPhaseRoute ? c.phaseRoute + pi : nullptr,
-                                       routeSample));
+                                       routeSample, ypairR));
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.mLR, p.wR, c.mLR,
                            p.peakR, 0, nullptr, 0, done, rankDiv);
         THX_LAUNCH_CHECK();
