@@ -1742,7 +1742,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             THX_HIP(hipMemcpyAsync(&r2, p.maxR2, sizeof(int), hipMemcpyDeviceToHost, s));
             THX_HIP(hipStreamSynchronize(s));
             const int R = (int)std::ceil(c.pf * std::sqrt((double)r2)) + 2;
-            if (R + 2 <= c.vdim / 2 + 1) ypairR = R;
+            if (R + 2 <= c.vdim / 2 + 1 && thx::ypair_ball_elems(R) <= dimSize) ypairR = R;
         }
         for (int k = 0; k < nK; k++) {
             if (ypairR > 0)
