@@ -509,7 +509,8 @@ def main():
             "peak_source": roof_src or "MI355X_MICROARCH.md L2", **line_fields,
             "kernel": f"k_local_fused (particle-filter phase, nPxl={px.n}, {mR}x{mT}, {nL} images "
                       "per launch), routed on the device per phase: the staged half-complex kernel "
-                      "<0> where the LDS boxes pay, else the pair-form y-pair kernel <4>",
+                      "<0> where the LDS boxes pay, else the pair-form y-pair kernel <2> on the "
+                      "driver's compact z-interleaved y-pair ball",
             "launch_ms": t_launch * 1e3, "launches_timed": len(local_ms),
             "launch_ms_by_phase": [round(float(np.mean(local_ms[k::a.phases])), 3)
                                    for k in range(a.phases)] if len(local_ms) == a.phases * a.steps else None,
@@ -518,8 +519,8 @@ def main():
             "fp32_TFLOPs": achieved, "fp32_frac": achieved / PEAK_FP32_TFLOPS,
             "tap_bytes_per_launch": tap_bytes,
             "note": "HIP events recorded by the driver on its launch stream around every "
-                    "phase's routed k_local_fused launches of the timed steps (three dispatches, "
-                    "two exit at entry; rocprof lists them per variant); achieved = 64 B of taps per "
+                    "phase's routed k_local_fused launches of the timed steps (two dispatches, "
+                    "one exits at entry; rocprof lists them per variant); achieved = 64 B of taps per "
                     "rotation-pixel (SURVEY 8(d)) per launch / launch time, peak = the L2 -> L1 "
                     "line bandwidth for random 16-B row pieces (tools/probes/l2_roof.hip, = the "
                     "guide's L2 figure); each tap row piece costs a 128-B line unless L1 or the "
