@@ -286,8 +286,11 @@ int thx_volume_cells(const float* vol, int vdim, float* cells,
                      thx_stream_t stream);
 
 /* The y-pair copy of a half-complex projectee (thx_local_phase volLayout 2):
- * element (x, y, z) = (v(x, y, z), v(x, y + 1, z)), rows wrapped, 16 B; a
- * trilinear cell is two 32-B pieces.  ypair: 4 dimSize floats. */
+ * element (x, y, z) holds v(x, y, z) and v(x, (y + 1) mod vdim, z) (16 B), so
+ * a trilinear cell is two 32-B pieces; the slices z, z + 1 of each even z are
+ * interleaved element by element -- element (x, y, z) sits at index
+ * ((z / 2 * vdim + y) * (vdim / 2 + 1) + x) * 2 + z % 2 -- so for even z0 a
+ * cell is one contiguous 64-B piece.  ypair: 4 dimSize floats (ABI 8). */
 int thx_volume_ypair(const float* vol, int vdim, float* ypair, thx_stream_t stream);
 
 /* ----------------------------------------------------------------- a10 ---

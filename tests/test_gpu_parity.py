@@ -526,12 +526,14 @@ def test_empty_batches(orc, stack):
 
 def test_volume_ypair_layout():
     """thx_volume_ypair against the layout its header states: element
-    (z, y, x) = (v(z, y, x), v(z, (y + 1) mod vdim, x))."""
+    (x, y, z) = (v(x, y, z), v(x, (y + 1) mod vdim, z)), the slices z, z+1
+    of each even z interleaved: yp[z // 2, y, x, z % 2]."""
     vdim = 24
     g = torch.Generator().manual_seed(3)
     vol = torch.complex(torch.randn(vdim, vdim, vdim // 2 + 1, generator=g),
                         torch.randn(vdim, vdim, vdim // 2 + 1, generator=g)).to(DEV)
     yp = ops.volume_ypair(vol).cpu()
     v = vol.cpu()
-    assert torch.equal(yp[..., 0], v)
-    assert torch.equal(yp[..., 1], torch.roll(v, -1, dims=1))
+    for zl in (0, 1):
+        assert torch.equal(yp[:, :, :, zl, 0], v[zl::2])
+        assert torch.equal(yp[:, :, :, zl, 1], torch.roll(v, -1, dims=1)[zl::2])

@@ -182,9 +182,17 @@ struct PCell {
 };
 // index of element (x, y, z) of the whole y-pair copy (thx_volume_ypair),
 // nc = vdim / 2 + 1
+// THX_YPAIR_WZIL: the whole copy with its slices z, z+1 (z even)
+// interleaved element by element as in the ball: for even z0 a sample's
+// four 16-B elements are one contiguous 64-B piece (full resolution, box
+// 256: 14.0 -> 12.1 ms at 1.5 deg, 18.4 -> 16.0 at 2 deg, 27.5 -> 23.0 at 3,
+// profiles/r04_fullres_wzil_ab.jsonl)
+#ifndef THX_YPAIR_WZIL
+#define THX_YPAIR_WZIL 1
+#endif
 THX_DEV unsigned ypair_elem(unsigned z, unsigned y, unsigned x, unsigned vdim, unsigned nc)
 {
-    return (z * vdim + y) * nc + x;
+    return THX_YPAIR_WZIL ? (((z >> 1) * vdim + y) * nc + x) * 2u + (z & 1u) : (z * vdim + y) * nc + x;
 }
 // THX_YPAIR_ZIL: in the compact ball slices z and z + 1 (z + R even) are
 // interleaved element by element, so for such z0 a sample's four 16-B
@@ -1066,7 +1074,7 @@ k_local_fused(const float2* __restrict__ vol,
         // r at pixels 4s + h (it 0) and 4s + h + 2 (it 1); lane j rotates the
         // it = j sample and the pair shares the cells.  MFMA A rows: (pixels
         // 4s, 4s + 2) from the h = 0 pairs, (4s + 1, 4s + 3) from the h = 1 pairs.
-        const unsigned yxs = ballR > 0 && THX_YPAIR_ZIL ? 2u : 1u;   // x stride of the copy's elements
+        const unsigned yxs = ballR > 0 ? (THX_YPAIR_ZIL ? 2u : 1u) : (THX_YPAIR_WZIL ? 2u : 1u);   // x stride of the copy's elements
         auto pair_step = [&](int s) {
             const int j = lane & 1, h = (lane >> 5) & 1;
             PCell mine;

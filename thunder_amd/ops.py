@@ -302,7 +302,7 @@ def _layout(vol, cells, ypair=None):
     if cells is not None and ypair is not None:
         raise ValueError("cells and ypair are alternatives")
     if ypair is not None:
-        _req(ypair, torch.complex64, tuple(vol.shape) + (2,), "ypair")
+        _req(ypair, torch.complex64, _ypair_shape(vol), "ypair")
         return 2, ypair
     if cells is not None:
         _req(cells, torch.complex64, tuple(vol.shape) + (8,), "cells")
@@ -310,11 +310,18 @@ def _layout(vol, cells, ypair=None):
     return 0, vol
 
 
+def _ypair_shape(vol):
+    """[vdim/2, vdim, vdim/2+1, 2 (z parity), 2 (y, y+1)] of thx_volume_ypair."""
+    vdim = vol.shape[0]
+    return (vdim // 2, vdim, vol.shape[2], 2, 2)
+
+
 def volume_ypair(vol):
-    """y-pair copy [vdim, vdim, vdim/2+1, 2]: element (x, y, z) = (v(x, y, z),
-    v(x, y+1, z)), so a trilinear cell is two 32-B pieces (thx_volume_ypair)."""
+    """y-pair copy (thx_volume_ypair): yp[zp, y, x, zl] = (v(x, y, z), v(x, y+1, z))
+    for z = 2 zp + zl -- the slices z, z+1 of each even z interleaved, so a
+    trilinear cell at even z0 is one 64-B piece, else two 32-B pieces."""
     vdim = _vol_dim(vol)
-    out = torch.empty(tuple(vol.shape) + (2,), dtype=torch.complex64, device=vol.device)
+    out = torch.empty(_ypair_shape(vol), dtype=torch.complex64, device=vol.device)
     check(lib().thx_volume_ypair(_ptr(vol), vdim, _ptr(out), _stream(vol.device)),
           "thx_volume_ypair")
     return out
@@ -342,7 +349,7 @@ def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False
     _req(pR, torch.float64, (nImg, nR), "pR")
     _req(pT, torch.float64, (nImg, nT), "pT")
     if routed and ypair is not None:
-        _req(ypair, torch.complex64, tuple(vol.shape) + (2,), "ypair")
+        _req(ypair, torch.complex64, _ypair_shape(vol), "ypair")
     wC = torch.empty(nImg, dtype=torch.float32, device=dev)
     wR = torch.empty(nImg, nR, dtype=torch.float32, device=dev)
     wT = torch.empty(nImg, nT, dtype=torch.float32, device=dev)
