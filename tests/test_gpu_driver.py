@@ -206,6 +206,21 @@ def test_view_order_leaves_every_image_unchanged(local_stack, monkeypatch, conve
         assert torch.equal(a, b)
 
 
+def test_ypair_ball_leaves_every_image_unchanged(local_stack, monkeypatch):
+    """The driver's compact y-pair ball (slices interleaved, no wrap) reads
+    the same taps with the same weights as the whole copy: with the ball
+    (default) and without (THX_YPAIR_BALL=0) the driver returns bit-identical
+    particles, priors, scores and classes."""
+    s = local_stack
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("THX_YPAIR_BALL", flag)
+        e = ex.Expectation(s["vol"], s["px"], s["gset"], n_phase=4, seed=13)
+        outs.append([x.clone() for x in e.run(s["dat"], s["ctf"], s["sig"])])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_global_converge_matches_fixed_quality(local_stack):
     """The stopping rule ends every image between phase 11 and 99 and keeps
     the grid-pose recovery of the fixed 10-phase run."""

@@ -91,11 +91,12 @@ __global__ void __launch_bounds__(256) k_max_r2(const int* __restrict__ iCol,
 #endif
 // THX_VIEW_ORDER=0 in the environment turns it off per call (the test that
 // the order leaves every image's result unchanged compares both)
-static bool view_order_on()
+static bool env_on(const char* name)
 {
-    const char* e = std::getenv("THX_VIEW_ORDER");
+    const char* e = std::getenv(name);
     return !(e && e[0] == '0');
 }
+static bool view_order_on() { return env_on("THX_VIEW_ORDER"); }
 
 namespace {
 
@@ -1735,7 +1736,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     // copy when the ball is the volume
     int ypairR = 0;
     if (p.ypair) {
-        if (THX_YPAIR_BALL) {
+        if (THX_YPAIR_BALL && env_on("THX_YPAIR_BALL")) {
             hipLaunchKernelGGL(k_max_r2, dim3(1), dim3(256), 0, s, iCol, iRow, nPxl, p.maxR2);
             THX_LAUNCH_CHECK();
             int r2 = 0;
