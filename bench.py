@@ -65,8 +65,9 @@ def parse():
     p.add_argument("--box", type=int, default=256)
     p.add_argument("--nr", type=int, default=2000)
     p.add_argument("--phases", type=int, default=10)
-    p.add_argument("--algo", type=int, default=2,
-                   help="global-scan algorithm: 0 direct, 1 FP32 MFMA, 2 bf16x3 MFMA")
+    p.add_argument("--algo", type=int, default=4,
+                   help="global-scan algorithm: 0 direct, 1 FP32 MFMA, 2 bf16x3 MFMA, "
+                        "4 bf16x6 MFMA (exact three-way split of the FP32 operands)")
     p.add_argument("--shuffle", type=int, default=1,
                    help="1: shuffle the support before resampling (Particle::resample)")
     p.add_argument("--perturb-mean", default="acg", choices=["acg", "top"],
@@ -163,7 +164,8 @@ def scan_roofline(vol, px, gset, dat, ctf, sig, algo, reps=3):
     """Average duration of the global-scan launch sequence (HIP events on the
     launch stream) priced against the matrix-core roof of its dtype:
     algo 1 = FP32 MFMA (4 flop per image x rotation x translation x pixel),
-    algo 2 = bf16 MFMA, three products per FP32 product (12 bf16 flop)."""
+    algo 2 = bf16 MFMA, three products per FP32 product (12 bf16 flop),
+    algo 4 = bf16 MFMA, six products per FP32 product (24 bf16 flop)."""
     dev = dat.device
     q, t, pR, pT = gset
     nImg, nR, nT = dat.shape[0], len(q), len(t)
@@ -175,8 +177,8 @@ def scan_roofline(vol, px, gset, dat, ctf, sig, algo, reps=3):
                        reps, st)
     pad = lambda v, m: (v + m - 1) // m * m
     elems = float(pad(nImg, 64)) * pad(nR, 4) * pad(nT, 32) * pad(px.n, 16)
-    issued = (12.0 if algo == 2 else 4.0) * elems
-    peak = PEAK_BF16_MFMA_TFLOPS if algo == 2 else PEAK_FP32_MFMA_TFLOPS
+    issued = {2: 12.0, 4: 24.0}.get(algo, 4.0) * elems
+    peak = PEAK_BF16_MFMA_TFLOPS if algo in (2, 4) else PEAK_FP32_MFMA_TFLOPS
     algorithmic = 15.0 * nImg * nR * nT * px.n      # SURVEY §8(d), direct formulation
     return sec, issued, algorithmic, peak
 
@@ -528,12 +530,13 @@ def main():
                     "while the algorithmic rate is a fraction of it"}
 
     if not a.no_extras:
-        # ---- secondary: the global scan (bf16x3 MFMA) and its FP32-MFMA twin
+        # ---- secondary: the global scan (bf16x6 MFMA) and its FP32-MFMA twin
         nRoof = min(ROOF_IMAGES, a.images)
         sec, issued, algorithmic, peak = scan_roofline(vol, px, gset, dat[:nRoof], ctf[:nRoof],
                                                        sig[:nRoof], a.algo)
-        kname = {1: "k_scan_mfma (fp32 32x32x2)", 2: "k_scan_split<BF16X3> (bf16 32x32x16, 3-product split)"}
-        tr, tr_src = launch_traffic("scan_4096", a.algo == 2 and nRoof == 4096
+        kname = {1: "k_scan_mfma (fp32 32x32x2)", 2: "k_scan_split<BF16X3> (bf16 32x32x16, 3-product split)",
+                 4: "k_scan_split<BF16X6> (bf16 32x32x16, exact 3-way split, 6 products)"}
+        tr, tr_src = launch_traffic("scan_4096", a.algo == 4 and nRoof == 4096
                                     and a.nr == 2000 and N == 256)
         extras["roofline_scan"] = {
             "bound": "mfma", "achieved": issued / sec / 1e12, "peak": peak, "unit": "TFLOP/s",
@@ -543,8 +546,9 @@ def main():
             "launch_ms": sec * 1e3, "images_per_launch": nRoof,
             "algorithmic_equiv_tflops": algorithmic / sec / 1e12,
             "note": "achieved = issued matrix-core flops after the expansion of |d-cTP|^2 into a "
-                    "GEMM (4 fp32 flop, or 3x4 bf16 flop, per image x rotation x translation x "
-                    "pixel); algorithmic_equiv uses the direct 15-flop count of SURVEY 8(d)"}
+                    "GEMM (4 fp32 flop, or 6x4 bf16 flop for bf16x6, per image x rotation x "
+                    "translation x pixel); algorithmic_equiv uses the direct 15-flop count of "
+                    "SURVEY 8(d)"}
         sec1, issued1, _, _ = scan_roofline(vol, px, gset, dat[:nRoof], ctf[:nRoof], sig[:nRoof], 1)
         extras["roofline_scan"]["fp32_mfma_launch_ms"] = sec1 * 1e3
         extras["roofline_scan"]["fp32_mfma_frac"] = issued1 / sec1 / 1e12 / PEAK_FP32_MFMA_TFLOPS
@@ -733,7 +737,11 @@ def main():
                 "value": value, "unit": "particle-images/s", "n_gpus": a.gpus, "steps": a.steps,
                 "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None,
-                "dtype": "f32" if a.algo == 1 else "f32 (global scan: bf16x3 split, fp32 accumulate)",
+                "dtype": {1: "f32", 4: "f32 (global scan: FP32 operands split exactly into three bf16, "
+                               "six products -- dropped terms <= 2^-26 |w||T|, below an FP32 product's "
+                               "rounding -- FP32 accumulation, cancellation-guarded direct FP32 "
+                               "recompute; phases: FP32)"}.get(
+                    a.algo, "f32 with a bf16x3 global scan (narrower than FP32)"),
                 "data": "synthetic (seeded Gaussian-blob volume, CTF-modulated noisy projections, SNR 0.05)",
                 "config": {"workload": f"C3: 3D refine box {N}, {a.nr} rotation x {len(gset[1])} "
                                        f"translation global scan at rU={rU} (nPxl={px.n}) + "

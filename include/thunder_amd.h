@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define THX_ABI_VERSION 8
+#define THX_ABI_VERSION 9
 
 enum {
     THX_OK = 0,
@@ -143,9 +143,14 @@ int thx_dvp(const float* rotP, int nR, const float* traP, int nT,
  * classes when the baseline rises (kernel_setBaseLine, Kernel.cu:1096-1128).
  * algo: 0 = direct per-pixel formulation, materialised dvp;
  *       1 = fused FP32 MFMA formulation;
- *       2 = bf16 MFMA, three-product split (bf16x3);
- *       3 = fp16 MFMA, two-product split of w against an fp16 T (fp16x2);
- *       2 and 3 fall back to 1 when nT > 160.
+ *       2 = bf16 MFMA, three-product split (bf16x3, ~2^-16 per product);
+ *       4 = bf16 MFMA, exact three-way split of both FP32 operands and six
+ *           products (bf16x6: every dropped term <= 2^-26 |w||T|, below the
+ *           FP32 rounding of a product) -- the expectation driver's default;
+ *       (3, fp16x2, was retired in ABI 9);
+ *       2 and 4 run the cancellation guard (samples whose expanded form
+ *       A + B + X cancels by more than 4x are recomputed in the direct form)
+ *       and fall back to 1 when nT > 160.
  * workspace: >= thx_global_scan_workspace(...) bytes of device memory. */
 size_t thx_global_scan_workspace(int nImg, int nR, int nT, int nPxl, int algo);
 int thx_global_scan(const float* rotP, int nR, const float* traP, int nT,
@@ -154,6 +159,19 @@ int thx_global_scan(const float* rotP, int nR, const float* traP, int nT,
                     int kIdx, int nK, float* wC, float* wR, float* wT,
                     float* baseL, int algo, void* workspace, size_t wsBytes,
                     thx_stream_t stream);
+
+/* thx_global_scan for algo 2 or 4 with two debug controls (ABI 9): dvp
+ * [nImg][nR][nT] receives every sample's final log-likelihood (the value the
+ * marginals are formed from), for the element-wise dump-compare of
+ * gpu/src/cuthunder.cu:2247-2271; guard = the cancellation ratio above which
+ * a sample is recomputed in the direct form (thx_global_scan uses 4; 0 turns
+ * the guard off).  nT <= 160. */
+int thx_global_scan_dvp(const float* rotP, int nR, const float* traP, int nT,
+                        const float* dat, const float* ctf, const float* sigRcp,
+                        int nImg, int nPxl, const double* pR, const double* pT,
+                        int kIdx, int nK, float* wC, float* wR, float* wT,
+                        float* baseL, int algo, float guard, float* dvp,
+                        void* workspace, size_t wsBytes, thx_stream_t stream);
 
 /* --------------------------------------------------------- a6 + a7 + a9 ---
  * One particle-filter phase for a batch of images, each with its own
@@ -818,17 +836,24 @@ int thx_event_pairs_destroy(void* events, int n);
  * device, as cuthunder deals batches round-robin over every visible GPU
  * (gpu/src/cuthunder.cu:2002-2198, 5570-5826); insert partial half-maps are
  * summed onto the first device.  The devices (also what thx_getAviDevice
- * reports to the per-image local path), THX_DEVICES unset: one device per
- * process, (local rank % GPU count), when the launcher's environment says
- * several processes share the node (LOCAL_WORLD_SIZE /
- * OMPI_COMM_WORLD_LOCAL_SIZE / MPI_LOCALNRANKS / SLURM_NTASKS_PER_NODE > 1
- * with LOCAL_RANK / OMPI_COMM_WORLD_LOCAL_RANK / MPI_LOCALRANKID /
- * SLURM_LOCALID), otherwise every visible GPU; THX_DEVICES=all / local /
- * current (the caller's current device) / a list ("0,2,5") forces one.  A
- * hemisphere communicator passed to the insert adapters must live on the
- * first of these devices (checked: THX_ERR_ARG otherwise).  This returns the
- * list (devs may be NULL when cap is 0). */
+ * reports to the per-image local path), THX_DEVICES unset: every visible
+ * GPU, as the reference's getAviDevice -- except when the launcher's
+ * environment puts at least as many processes on the node as there are GPUs
+ * (LOCAL_WORLD_SIZE / OMPI_COMM_WORLD_LOCAL_SIZE / MPI_LOCALNRANKS /
+ * SLURM_NTASKS_PER_NODE >= the GPU count, with LOCAL_RANK /
+ * OMPI_COMM_WORLD_LOCAL_RANK / MPI_LOCALRANKID / SLURM_LOCALID): then one
+ * device per process, (local rank % GPU count) (ABI 9; THUNDER's master +
+ * two hemisphere ranks on an 8-GPU node keep all eight); THX_DEVICES=all /
+ * local / current (the caller's current device) / a list ("0,2,5") forces
+ * one.  A hemisphere communicator passed to the insert adapters must live on
+ * the first of these devices (checked: THX_ERR_ARG otherwise).  This returns
+ * the list (devs may be NULL when cap is 0). */
 int thx_adapter_devices(int* devs, int cap, int* n);
+/* The same policy as a pure function of its inputs (no device call): nVisible
+ * GPUs, current device cur, THX_DEVICES value env (NULL = unset), the
+ * launcher's local process count / local rank (-1 = unknown). */
+int thx_adapter_device_policy(int nVisible, int cur, const char* env, int localSize,
+                              int localRank, int* devs, int cap, int* n);
 /* hipSetDevice for C++ callers without HIP headers (e.g. before
  * thx_rccl_comm_init, whose communicator lives on the current device). */
 int thx_set_device(int dev);

@@ -29,17 +29,15 @@ def test_scan_algorithms_agree_at_metric_config(c3):
     traP = ops.trans_table(torch.as_tensor(t, device=DEV), px)
     pRd, pTd = torch.as_tensor(pR, device=DEV), torch.as_tensor(pT, device=DEV)
     res = {a: [x.cpu().numpy() for x in ops.global_scan(rotP, traP, c3["dat"], c3["ctf"], c3["sig"],
-                                                         pRd, pTd, algo=a)] for a in (0, 1, 2, 3)}
+                                                         pRd, pTd, algo=a)] for a in (0, 1, 2, 4)}
     ref = res[0]
-    for a in (1, 2, 3):
+    for a in (1, 2, 4):
         wC, wR, wT, base = res[a]
         assert np.allclose(base, ref[3], rtol=1e-5, atol=0)
         for x, y in ((wR, ref[1]), (wT, ref[2]), (wC, ref[0])):
             m = y >= 1e-4 * y.max(axis=-1, keepdims=True)
             rel = np.abs(x - y)[m] / y[m]
-            # fp16x2 (algo 3) carries the fp16 rounding of T: |d dvp| ~ 2e-3
-            # absolute (5e-6 relative), i.e. ~0.5 % on exp(dvp - base)
-            assert rel.max() < (1e-2 if a == 3 else 2e-3), (a, rel.max())
+            assert rel.max() < 2e-3, (a, rel.max())
 
 
 def test_dvp_matches_oracle_subset(orc, c3):

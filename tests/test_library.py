@@ -35,7 +35,7 @@ def test_exports_every_declared_symbol(L):
 
 
 def test_abi_version(L):
-    assert L.thx_abi_version() == 8
+    assert L.thx_abi_version() == 9
 
 
 def test_pixel_tile_order(L):
@@ -206,3 +206,49 @@ def test_ctf_search_entry_points_validate_without_gpu(L):
     # the global sample set producer
     assert L.thx_global_sample_set(0, 151, 10.0, 1, dummy, dummy, dummy, dummy, None) == bad
     assert L.thx_global_sample_set(10, 1, 10.0, 1, dummy, dummy, dummy, dummy, None) == bad
+
+
+def _policy(L, n, env=None, size=-1, rank=-1, cur=0):
+    out = (ctypes.c_int * 16)()
+    cnt = ctypes.c_int(0)
+    st = L.thx_adapter_device_policy(n, cur, env.encode() if env is not None else None, size, rank,
+                                     out, 16, ctypes.byref(cnt))
+    assert st == 0
+    return list(out[:cnt.value])
+
+
+def test_adapter_device_policy(L):
+    """THX_DEVICES unset: every visible GPU, as cuthunder's getAviDevice --
+    including THUNDER's master + two hemisphere ranks (LOCAL_WORLD_SIZE=3) on
+    an 8-GPU node; one device per process only when the node runs at least
+    one process per GPU."""
+    assert _policy(L, 8) == list(range(8))
+    for rank in range(3):
+        assert _policy(L, 8, size=3, rank=rank) == list(range(8))
+    assert _policy(L, 8, size=8, rank=5) == [5]
+    assert _policy(L, 8, size=16, rank=13) == [5]
+    assert _policy(L, 1, size=3, rank=2) == [0]
+    assert _policy(L, 8, env="local", size=3, rank=2) == [2]
+    assert _policy(L, 8, env="current", cur=6) == [6]
+    assert _policy(L, 8, env="all", size=8, rank=1) == list(range(8))
+    assert _policy(L, 8, env="0,3") == [0, 3]
+    out = (ctypes.c_int * 4)()
+    cnt = ctypes.c_int(0)
+    assert L.thx_adapter_device_policy(8, 0, b"9", -1, -1, out, 4, ctypes.byref(cnt)) != 0
+    assert L.thx_adapter_device_policy(0, 0, None, -1, -1, out, 4, ctypes.byref(cnt)) != 0
+
+
+def test_global_scan_dvp_validates_without_gpu(L):
+    """thx_global_scan_dvp (ABI 9): only the split algorithms (2, 4) keep a
+    per-sample dump; a negative guard, a NULL dump and the retired fp16x2
+    (algo 3) are refused before any device work."""
+    p = ctypes.c_void_p(16)
+    args = lambda algo, guard, dvp: (p, 2000, p, 151, p, p, p, 8, 870, p, p, 0, 1, p, p, p, p, algo,
+                                     ctypes.c_float(guard), dvp, p, ctypes.c_size_t(1 << 40), None)
+    assert L.thx_global_scan_dvp(*args(1, 4.0, p)) != 0
+    assert L.thx_global_scan_dvp(*args(3, 4.0, p)) != 0
+    assert L.thx_global_scan_dvp(*args(4, -1.0, p)) != 0
+    assert L.thx_global_scan_dvp(*args(4, 4.0, None)) != 0
+    assert L.thx_global_scan(p, 2000, p, 151, p, p, p, 8, 870, p, p, 0, 1, p, p, p, p, 3, p,
+                             ctypes.c_size_t(1 << 40), None) != 0
+    assert L.thx_global_scan_workspace(8, 2000, 151, 870, 4) > 0

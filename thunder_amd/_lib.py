@@ -25,6 +25,9 @@ SIGNATURES = {
     "thx_global_scan_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int, _c_int]),
     "thx_global_scan": (_c_int, [_p, _c_int, _p, _c_int, _p, _p, _p, _c_int, _c_int, _p, _p,
                                  _c_int, _c_int, _p, _p, _p, _p, _c_int, _p, _c_size, _p]),
+    "thx_global_scan_dvp": (_c_int, [_p, _c_int, _p, _c_int, _p, _p, _p, _c_int, _c_int, _p, _p,
+                                     _c_int, _c_int, _p, _p, _p, _p, _c_int, ctypes.c_float, _p, _p,
+                                     _c_size, _p]),
     "thx_local_phase_workspace": (_c_size, [_c_int, _c_int, _c_int, _c_int]),
     "thx_view_order_workspace": (_c_size, [_c_int]),
     "thx_view_order": (_c_int, [_c_int, _c_int, _p, _p, _p, _c_size, _p]),
@@ -108,6 +111,7 @@ SIGNATURES = {
     "thx_insert2d_d": (_c_int, [_p, _p, _p, _p, _c_int, _c_int, _p, _p, _p, _p, _p, _p, _p, _p,
                                 _c_int, _c_int, _p, _p, _c_int, _c_int, _p]),
     "thx_adapter_devices": (_c_int, [_p, _c_int, _p]),
+    "thx_adapter_device_policy": (_c_int, [_c_int, _c_int, ctypes.c_char_p, _c_int, _c_int, _p, _c_int, _p]),
     "thx_set_device": (_c_int, [_c_int]),
     "thx_img_stats": (_c_int, [_p, _c_int, _c_int, _c_int, _c_float, _p, _p, _p]),
     "thx_img_finish": (_c_int, [_p, _c_int, _c_int, _c_float, _c_float, _c_int, _c_float,

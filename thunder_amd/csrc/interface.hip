@@ -31,6 +31,10 @@ using thx::on_devices;
 
 namespace {
 
+// the global scan of the batch adapters: bf16x6 (FP32-equivalent products,
+// cancellation-guarded), the expectation driver's default
+constexpr int kScanAlgo = 4;
+
 template <typename T>
 __global__ void k_add(T* __restrict__ dst, const T* __restrict__ src, size_t n)
 {
@@ -114,27 +118,27 @@ static int local_size_env()
 }
 
 // The devices the batch adapters spread work over and getAviDevice reports
-// (see the file comment): THX_DEVICES unset -> one device per process, (local
-// rank % count), when the launcher put several processes on this node, else
-// every visible GPU (the reference's one-rank-per-node layout); "current" ->
-// the caller's current device; "local" -> (local rank % count); "all" ->
-// every visible GPU; "0,3" -> a list.
-int adapter_devices(std::vector<int>& devs)
+// (see the file comment), from the visible device count, the caller's current
+// device, THX_DEVICES and the launcher's local process count / rank:
+//   THX_DEVICES unset -> every visible GPU (the reference's getAviDevice), except
+//     when the launcher placed at least as many processes on this node as there
+//     are GPUs: then one device per process, (local rank % count) -- a
+//     one-process-per-GPU launch must not pile every rank onto every GPU, while
+//     THUNDER's master + two hemisphere ranks on an 8-GPU node keep all eight;
+//   "current" -> the caller's current device; "local" -> (local rank % count);
+//   "all" -> every visible GPU; "0,3" -> a list.
+int device_policy(int n, int cur, const char* env, int localSize, int localRank,
+                  std::vector<int>& devs)
 {
     devs.clear();
-    int n = 0, cur = 0;
-    THX_HIP(hipGetDeviceCount(&n));
-    THX_HIP(hipGetDevice(&cur));
     THX_CHECK_ARG(n > 0, "no HIP device");
-    const char* env = std::getenv("THX_DEVICES");
     if (env && std::strcmp(env, "current") == 0) {
         devs.push_back(cur);
         return THX_OK;
     }
-    const bool several = local_size_env() > 1 && local_rank_env() >= 0;
-    if ((env && std::strcmp(env, "local") == 0) || ((!env || !*env) && several)) {
-        const int lr = local_rank_env();
-        devs.push_back(lr >= 0 ? lr % n : cur);
+    const bool perGpu = localSize > 1 && localSize >= n && localRank >= 0;
+    if ((env && std::strcmp(env, "local") == 0) || ((!env || !*env) && perGpu)) {
+        devs.push_back(localRank >= 0 ? localRank % n : cur);
         return THX_OK;
     }
     if (env && *env && std::strcmp(env, "all") != 0) {
@@ -155,7 +159,28 @@ int adapter_devices(std::vector<int>& devs)
     return THX_OK;
 }
 
+int adapter_devices(std::vector<int>& devs)
+{
+    int n = 0, cur = 0;
+    THX_HIP(hipGetDeviceCount(&n));
+    THX_HIP(hipGetDevice(&cur));
+    return device_policy(n, cur, std::getenv("THX_DEVICES"), local_size_env(), local_rank_env(),
+                         devs);
+}
+
 }  // namespace thx
+
+// the policy alone, for host tests (no device calls)
+extern "C" int thx_adapter_device_policy(int nVisible, int cur, const char* env, int localSize,
+                                         int localRank, int* devs, int cap, int* n)
+{
+    THX_CHECK_ARG(n && (cap == 0 || devs), "thx_adapter_device_policy: bad arguments");
+    std::vector<int> d;
+    THX_RET(thx::device_policy(nVisible, cur, env, localSize, localRank, d));
+    *n = (int)d.size();
+    for (int k = 0; k < (int)d.size() && k < cap; k++) devs[k] = d[k];
+    return THX_OK;
+}
 
 using thx::adapter_devices;
 
@@ -254,7 +279,7 @@ extern "C" int thx_ExpectGlobal3D(const float* rotP, const float* traP,
         const int n = l1 - l0;
         if (n <= 0) return THX_OK;
         const size_t nPx = (size_t)n * npxl, o = (size_t)l0 * npxl;
-        const size_t ws = thx_global_scan_workspace(n, nR, nT, npxl, 1);
+        const size_t ws = thx_global_scan_workspace(n, nR, nT, npxl, kScanAlgo);
         DBuf dRot, dTra, dDat, dCtf, dSig, dWC, dWR, dWT, dPR, dPT, dBase, dWs;
         THX_DALLOC(dRot, sizeof(float) * 2 * (size_t)nR * npxl);
         THX_DALLOC(dTra, sizeof(float) * 2 * (size_t)nT * npxl);
@@ -287,7 +312,7 @@ extern "C" int thx_ExpectGlobal3D(const float* rotP, const float* traP,
         THX_RET(thx_global_scan(dRot.as<float>(), nR, dTra.as<float>(), nT, dDat.as<float>(),
                                 dCtf.as<float>(), dSig.as<float>(), n, npxl, dPR.as<double>(),
                                 dPT.as<double>(), kIdx, nK, dWC.as<float>(), dWR.as<float>(),
-                                dWT.as<float>(), dBase.as<float>(), 1, dWs.p, ws, nullptr));
+                                dWT.as<float>(), dBase.as<float>(), kScanAlgo, dWs.p, ws, nullptr));
         THX_HIP(hipMemcpy(wC + (size_t)l0 * nK, dWC.p, sizeof(float) * (size_t)n * nK,
                           hipMemcpyDeviceToHost));
         THX_HIP(hipMemcpy(wR + (size_t)l0 * nK * nR, dWR.p, sizeof(float) * (size_t)n * nK * nR,
@@ -564,7 +589,7 @@ extern "C" int thx_ExpectGlobal2D(const float* vol, const float* datP, const flo
         const int n = l1 - l0;
         if (n <= 0) return THX_OK;
         const size_t nPx = (size_t)n * npxl, o = (size_t)l0 * npxl;
-        const size_t ws = thx_global_scan_workspace(n, nR, nT, npxl, 1);
+        const size_t ws = thx_global_scan_workspace(n, nR, nT, npxl, kScanAlgo);
         DBuf dV, dRot, dTr, dTra, dDat, dCtf, dSig, dWC, dWR, dWT, dPR, dPT, dBase, dWs, dRP, dIc, dIr;
         THX_DALLOC(dV, sizeof(float) * 2 * img * nK);
         THX_DALLOC(dRot, sizeof(double) * 2 * nR);
@@ -602,7 +627,7 @@ extern "C" int thx_ExpectGlobal2D(const float* vol, const float* datP, const flo
             THX_RET(thx_global_scan(dRP.as<float>(), nR, dTra.as<float>(), nT, dDat.as<float>(),
                                     dCtf.as<float>(), dSig.as<float>(), n, npxl, dPR.as<double>(),
                                     dPT.as<double>(), k, nK, dWC.as<float>(), dWR.as<float>(),
-                                    dWT.as<float>(), dBase.as<float>(), 1, dWs.p, ws, nullptr));
+                                    dWT.as<float>(), dBase.as<float>(), kScanAlgo, dWs.p, ws, nullptr));
         }
         THX_HIP(hipMemcpy(wC + (size_t)l0 * nK, dWC.p, sizeof(float) * (size_t)n * nK,
                           hipMemcpyDeviceToHost));

@@ -138,28 +138,31 @@ int scan_mfma(const float* rotP, int nR, const float* traP, int nT,
               int nK, float* wC, float* wR, float* wT, float* baseL,
               void* workspace, size_t wsBytes, hipStream_t stream);
 size_t scan_mfma_workspace(int nImg, int nR, int nT, int nPxl);
-int scan_bf16x3(const float* rotP, int nR, const float* traP, int nT,
-                const float* dat, const float* ctf, const float* sigRcp,
-                int nImg, int nPxl, const double* pR, const double* pT, int kIdx,
-                int nK, float* wC, float* wR, float* wT, float* baseL,
-                void* workspace, size_t wsBytes, hipStream_t stream);
-int scan_f16x2(const float* rotP, int nR, const float* traP, int nT,
-               const float* dat, const float* ctf, const float* sigRcp,
-               int nImg, int nPxl, const double* pR, const double* pT, int kIdx,
-               int nK, float* wC, float* wR, float* wT, float* baseL,
-               void* workspace, size_t wsBytes, hipStream_t stream);
+int scan_split_algo(int algo, const float* rotP, int nR, const float* traP, int nT,
+                    const float* dat, const float* ctf, const float* sigRcp, int nImg, int nPxl,
+                    const double* pR, const double* pT, int kIdx, int nK, float* wC, float* wR,
+                    float* wT, float* baseL, float guard, float* dvpOut, void* workspace,
+                    size_t wsBytes, hipStream_t s);
 size_t scan_split_workspace(int nImg, int nR, int nT, int nPxl);
+float scan_guard_default();
 }  // namespace thx
 
 extern "C" size_t thx_global_scan_workspace(int nImg, int nR, int nT, int nPxl,
                                             int algo)
 {
     if (algo == 1) return thx::scan_mfma_workspace(nImg, nR, nT, nPxl);
-    if (algo == 2 || algo == 3) return thx::scan_split_workspace(nImg, nR, nT, nPxl);
+    if (algo == 2 || algo == 4) return thx::scan_split_workspace(nImg, nR, nT, nPxl);
     thx::Carver c(nullptr, 0);
     c.take<float>((size_t)nImg * nR * nT);
     return c.off + 256;
 }
+
+#define SCAN_ARGS_CHECK()                                                                    \
+    THX_CHECK_ARG(nR > 0 && nT > 0 && nImg >= 0 && nPxl > 0,                                 \
+                  "thx_global_scan: bad sizes nR=%d nT=%d nImg=%d nPxl=%d", nR, nT, nImg,    \
+                  nPxl);                                                                     \
+    THX_CHECK_ARG(nK >= 1 && kIdx >= 0 && kIdx < nK, "thx_global_scan: bad kIdx=%d nK=%d",  \
+                  kIdx, nK)
 
 extern "C" int thx_global_scan(const float* rotP, int nR, const float* traP,
                                int nT, const float* dat, const float* ctf,
@@ -169,12 +172,9 @@ extern "C" int thx_global_scan(const float* rotP, int nR, const float* traP,
                                float* baseL, int algo, void* workspace,
                                size_t wsBytes, thx_stream_t stream)
 {
-    THX_CHECK_ARG(nR > 0 && nT > 0 && nImg >= 0 && nPxl > 0,
-                  "thx_global_scan: bad sizes nR=%d nT=%d nImg=%d nPxl=%d", nR,
-                  nT, nImg, nPxl);
-    THX_CHECK_ARG(nK >= 1 && kIdx >= 0 && kIdx < nK,
-                  "thx_global_scan: bad kIdx=%d nK=%d", kIdx, nK);
-    THX_CHECK_ARG(algo >= 0 && algo <= 3, "thx_global_scan: algo must be 0, 1, 2 or 3");
+    SCAN_ARGS_CHECK();
+    THX_CHECK_ARG(algo >= 0 && algo <= 4 && algo != 3,
+                  "thx_global_scan: algo must be 0, 1, 2 or 4 (3, fp16x2, was retired in ABI 9)");
     THX_CHECK_ARG(wsBytes >= thx_global_scan_workspace(nImg, nR, nT, nPxl, algo),
                   "thx_global_scan: workspace too small");
     if (nImg == 0) return THX_OK;
@@ -183,14 +183,10 @@ extern "C" int thx_global_scan(const float* rotP, int nR, const float* traP,
         return thx::scan_mfma(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl,
                               pR, pT, kIdx, nK, wC, wR, wT, baseL, workspace,
                               wsBytes, s);
-    if (algo == 2)
-        return thx::scan_bf16x3(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl,
-                                pR, pT, kIdx, nK, wC, wR, wT, baseL, workspace,
-                                wsBytes, s);
-    if (algo == 3)
-        return thx::scan_f16x2(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl,
-                               pR, pT, kIdx, nK, wC, wR, wT, baseL, workspace,
-                               wsBytes, s);
+    if (algo >= 2)
+        return thx::scan_split_algo(algo, rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR,
+                                    pT, kIdx, nK, wC, wR, wT, baseL, thx::scan_guard_default(),
+                                    nullptr, workspace, wsBytes, s);
     thx::Carver c(workspace, wsBytes);
     float* dvp = c.take<float>((size_t)nImg * nR * nT);
     for (int l0 = 0; l0 < nImg; l0 += 65535) {
@@ -204,4 +200,23 @@ extern "C" int thx_global_scan(const float* rotP, int nR, const float* traP,
                        nT, pR, pT, kIdx, nK, wC, wR, wT, baseL);
     THX_LAUNCH_CHECK();
     return THX_OK;
+}
+
+extern "C" int thx_global_scan_dvp(const float* rotP, int nR, const float* traP, int nT,
+                                   const float* dat, const float* ctf, const float* sigRcp,
+                                   int nImg, int nPxl, const double* pR, const double* pT,
+                                   int kIdx, int nK, float* wC, float* wR, float* wT,
+                                   float* baseL, int algo, float guard, float* dvp,
+                                   void* workspace, size_t wsBytes, thx_stream_t stream)
+{
+    SCAN_ARGS_CHECK();
+    THX_CHECK_ARG(algo == 2 || algo == 4, "thx_global_scan_dvp: algo must be 2 or 4");
+    THX_CHECK_ARG(guard >= 0.f, "thx_global_scan_dvp: guard must be >= 0");
+    THX_CHECK_ARG(dvp != nullptr, "thx_global_scan_dvp: dvp is NULL");
+    THX_CHECK_ARG(wsBytes >= thx_global_scan_workspace(nImg, nR, nT, nPxl, algo),
+                  "thx_global_scan_dvp: workspace too small");
+    if (nImg == 0) return THX_OK;
+    return thx::scan_split_algo(algo, rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT,
+                                kIdx, nK, wC, wR, wT, baseL, guard, dvp, workspace, wsBytes,
+                                thx::as_stream(stream));
 }

@@ -1,11 +1,12 @@
-// scan_bf16x3.hip -- a7 + a8 on 16-bit matrix cores: the global scan's cross
+// scan_split.hip -- a7 + a8 on 16-bit matrix cores: the global scan's cross
 // term with FP32 operands split into 16-bit pieces.
+//   algo 4 (BF16X6, the product path): every FP32 operand split EXACTLY into
+//                    three bf16 (x = hi + mid + lo: 8 + 8 + 8 significant
+//                    bits), six products (hh, hm, mh, hl, mm, lh); the three
+//                    dropped (ml, lm, ll) are <= 2^-26 |w||T|, below the FP32
+//                    rounding of one product (2^-24); FP32 accumulation;
 //   algo 2 (BF16X3): bf16 hi/lo of both operands, three products
 //                    (hi hi + hi lo + lo hi), ~2^-16 relative per product;
-//   algo 3 (F16X2):  fp16 hi/lo of the generated operand w, the translation
-//                    table T (|T| = 1) as ONE fp16 plane, two products
-//                    (w_hi T + w_lo T): 2/3 of the matrix work, error set by
-//                    the fp16 rounding of T (<= 2^-12 per component).
 //
 // Same expansion as algo 1 (scan_mfma.hip): with |T| = 1
 //   dvp[l][r][t] = A_l + B[l][r] + X[l][r][t],  A_l = sum s|d|^2,
@@ -17,9 +18,7 @@
 // operand w = a conj(P_r) is formed per (image tile, rotation) in registers
 // and split there.  Each generated A fragment is reused across all NF
 // translation fragments, and each T fragment read from LDS feeds both image
-// fragments of the wave.  The fp16 form needs range: a is pre-scaled per
-// image by an exact power of two 2^e_l so that max |w| <= 2^14, and X is
-// scaled back by 2^-e_l in the epilogue (exact).
+// fragments of the wave.
 //
 // Workgroup = 8 waves = 8 rotations x 64 images; each wave owns a
 // 64-image x NT_PAD-translation tile of ONE rotation (2 x NF accumulators
@@ -36,13 +35,20 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-enum Mode { BF16X3 = 0, F16X2 = 1 };
+enum Mode { BF16X3 = 0, BF16X6 = 2 };
+typedef __bf16 H;
+typedef bf16x8 HV;
 
-template <int MODE> struct Elt;
-template <> struct Elt<BF16X3> { typedef __bf16 T; typedef bf16x8 V; };
-template <> struct Elt<F16X2> { typedef _Float16 T; typedef f16x8 V; };
+// planes of the translation table staged per chunk
+template <int MODE> constexpr int nplane() { return MODE == BF16X6 ? 3 : 2; }
+
+// Cancellation guard of the expanded form dvp = (A + B) + X: where
+// |A| + |B| + |X| > SCAN_GUARD |dvp| (signal-dominated samples near the true
+// pose) the expansion loses log2 of that ratio in bits to cancellation, so
+// those samples are recomputed in the reference's direct form.
+constexpr float SCAN_GUARD = 4.f;
+constexpr int GCAP = 32;   // guard list entries per wave and round
 
 #ifndef SCAN_KC
 #define SCAN_KC 16
@@ -58,8 +64,6 @@ constexpr int THREADS = 64 * ROT_TILE;
 constexpr int NWAVE = ROT_TILE;
 constexpr int TROW = KC * 2 + 8;  // 16-bit elements per translation row of the T tile (80 B)
 constexpr int APITCH = KC + 2;    // float2 per image row of the a tile (144 B: aligned, conflict-free b128)
-constexpr int PMAX_BLOCKS = 256;
-constexpr float WMAX = 16384.f;   // fp16 range budget of the scaled w
 
 inline int pad_to(int v, int m) { return (v + m - 1) / m * m; }
 
@@ -81,15 +85,13 @@ Dims dims(int nImg, int nR, int nT, int nPxl)
 }
 
 struct WS {
-    float2* Ac;     // [nCk][nImgPad][APITCH]  a = -2 s c d (x 2^e_l for F16X2), LDS image
+    float2* Ac;     // [nCk][nImgPad][APITCH]  a = -2 s c d, LDS image
     float* Bc;      // [nCk][nImgPad][KC]   b = s c^2
     float* Aconst;  // [nImgPad]
-    float* amax;    // [nImgPad]   max_i |a.re| + |a.im|
-    float* scale;   // [nImgPad]   2^e_l
-    float* pmaxB;   // [PMAX_BLOCKS]
     float* bias;    // [nImgPad][nRBias]  B[l][r]
     uint16_t* Thi;  // [nCk][nTPad][TROW]   T split, (re, im) interleaved, LDS image
-    uint16_t* Tlo;
+    uint16_t* Tlo;  //   second plane (lo of bf16x3, mid of bf16x6)
+    uint16_t* Tl2;  //   third plane (lo of bf16x6)
     float2* Pc;     // [nCk][nRB * ROT_TILE][KC]  projections, chunk-major
     float2* wRp;    // [nImg][nR]
     float* pM;      // [nRB][nImgPad]
@@ -105,12 +107,10 @@ WS carve(void* base, const Dims& d)
     w.Ac = c.take<float2>((size_t)d.nCk * d.nImgPad * APITCH);
     w.Bc = c.take<float>((size_t)d.nPxlPad * d.nImgPad);
     w.Aconst = c.take<float>(d.nImgPad);
-    w.amax = c.take<float>(d.nImgPad);
-    w.scale = c.take<float>(d.nImgPad);
-    w.pmaxB = c.take<float>(PMAX_BLOCKS);
     w.bias = c.take<float>((size_t)d.nImgPad * d.nRBias);
     w.Thi = c.take<uint16_t>((size_t)d.nCk * d.nTPad * TROW);
     w.Tlo = c.take<uint16_t>((size_t)d.nCk * d.nTPad * TROW);
+    w.Tl2 = c.take<uint16_t>((size_t)d.nCk * d.nTPad * TROW);
     w.Pc = c.take<float2>((size_t)d.nCk * d.nRB * ROT_TILE * KC);
     w.wRp = c.take<float2>((size_t)d.nImg * d.nR);
     w.pM = c.take<float>((size_t)d.nRB * d.nImgPad);
@@ -127,82 +127,42 @@ THX_DEV void split16(float x, H& hi, H& lo)
     lo = (H)(x - (float)hi);
 }
 
-// Per image: A_l = sum s|d|^2 and max |a| (a = -2 s c d) for the fp16 scale.
+// x = hi + mid + lo exactly: hi takes the top 8 significant bits, the
+// residual x - hi (exact in FP32) keeps at most 16, mid the next 8, and the
+// residual after mid (again exact) at most 8, which lo holds exactly.
+THX_DEV void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo)
+{
+    hi = (__bf16)x;
+    const float r = x - (float)hi;
+    mid = (__bf16)r;
+    lo = (__bf16)(r - (float)mid);
+}
+
+// Per image: A_l = sum s|d|^2
 __global__ void __launch_bounds__(256) k_prep_aconst(const float2* __restrict__ dat,
-                                                     const float* __restrict__ ctf,
                                                      const float* __restrict__ sig, int nImg,
                                                      int nPxl, int nImgPad,
-                                                     float* __restrict__ Aconst,
-                                                     float* __restrict__ amax)
+                                                     float* __restrict__ Aconst)
 {
     const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (l >= nImgPad) return;
-    float a = 0.f, m = 0.f;
+    float a = 0.f;
     if (l < nImg)
         for (int i = lane; i < nPxl; i += 64) {
             const size_t s = (size_t)l * nPxl + i;
             const float2 d = dat[s];
-            const float sg = sig[s];
-            a += sg * (d.x * d.x + d.y * d.y);
-            const float k = -2.f * sg * ctf[s];
-            m = fmaxf(m, fabsf(k * d.x) + fabsf(k * d.y));
+            a += sig[s] * (d.x * d.x + d.y * d.y);
         }
     a = wave_sum(a);
-    m = wave_max(m);
-    if (lane == 0) {
-        Aconst[l] = a;
-        amax[l] = m;
-    }
+    if (lane == 0) Aconst[l] = a;
 }
 
-// Block maxima of |P.re| + |P.im| over the shared projections.
-__global__ void __launch_bounds__(256) k_prep_pmax(const float2* __restrict__ rotP, long n,
-                                                   float* __restrict__ pmaxB)
-{
-    __shared__ float sm[4];
-    float m = 0.f;
-    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
-         q += (long)gridDim.x * blockDim.x) {
-        const float2 p = rotP[q];
-        m = fmaxf(m, fabsf(p.x) + fabsf(p.y));
-    }
-    m = wave_max(m);
-    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) pmaxB[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
-}
-
-// scale_l = 2^e_l with max |w| = amax_l pmax 2^e_l <= WMAX (F16X2), 1 (BF16X3).
-__global__ void __launch_bounds__(256) k_prep_scale(const float* __restrict__ amax,
-                                                    const float* __restrict__ pmaxB, int nImgPad,
-                                                    int fp16, float* __restrict__ scale)
-{
-    __shared__ float sP;
-    if (threadIdx.x < 64) {
-        float m = 0.f;
-        for (int b = threadIdx.x; b < PMAX_BLOCKS; b += 64) m = fmaxf(m, pmaxB[b]);
-        m = wave_max(m);
-        if (threadIdx.x == 0) sP = m;
-    }
-    __syncthreads();
-    for (int l = blockIdx.x * blockDim.x + threadIdx.x; l < nImgPad; l += gridDim.x * blockDim.x) {
-        float s = 1.f;
-        const float wm = amax[l] * sP;
-        if (fp16 && wm > 0.f && wm == wm) {
-            int e;
-            frexpf(WMAX / wm, &e);                 // WMAX / wm = f 2^e, f in [0.5, 1)
-            s = ldexpf(1.f, max(-100, min(100, e - 1)));
-        }
-        scale[l] = s;
-    }
-}
-
-// a (scaled), b in pixel-chunked image rows; pixel fastest so writes are contiguous
+// a, b in pixel-chunked image rows; pixel fastest so writes are contiguous
 __global__ void __launch_bounds__(256) k_prep_img(const float2* __restrict__ dat,
                                                   const float* __restrict__ ctf,
                                                   const float* __restrict__ sig,
-                                                  const float* __restrict__ scale, int nImg,
+                                                  int nImg,
                                                   int nPxl, int nImgPad, int nPxlPad,
                                                   float2* __restrict__ Ac,
                                                   float* __restrict__ Bc)
@@ -218,8 +178,7 @@ __global__ void __launch_bounds__(256) k_prep_img(const float2* __restrict__ dat
             const float2 d = dat[s];
             const float c = ctf[s], sg = sig[s];
             const float k = -2.f * sg * c;
-            const float sc = scale[l];
-            a = make_float2((k * d.x) * sc, (k * d.y) * sc);
+            a = make_float2(k * d.x, k * d.y);
             b = sg * c * c;
         }
         Ac[((size_t)(i / KC) * nImgPad + l) * APITCH + (i % KC)] = a;
@@ -248,9 +207,9 @@ __global__ void __launch_bounds__(256) k_prep_tsplit(const float2* __restrict__ 
                                                      int nPxl, int nTPad, int nPxlPad,
                                                      uint16_t* __restrict__ Thi,
                                                      uint16_t* __restrict__ Tlo,
+                                                     uint16_t* __restrict__ Tl2,
                                                      float* __restrict__ pTf)
 {
-    typedef typename Elt<MODE>::T H;
     const long n = (long)nTPad * nPxlPad;
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
          q += (long)gridDim.x * blockDim.x) {
@@ -258,12 +217,24 @@ __global__ void __launch_bounds__(256) k_prep_tsplit(const float2* __restrict__ 
         const float2 v = (t < nT && i < nPxl) ? traP[(size_t)t * nPxl + i] : make_float2(0.f, 0.f);
         const size_t o = ((size_t)(i / KC) * nTPad + t) * TROW + (i % KC) * 2;
         H h, lo;
-        split16(v.x, h, lo);
-        Thi[o] = __builtin_bit_cast(uint16_t, h);
-        Tlo[o] = __builtin_bit_cast(uint16_t, lo);
-        split16(v.y, h, lo);
-        Thi[o + 1] = __builtin_bit_cast(uint16_t, h);
-        Tlo[o + 1] = __builtin_bit_cast(uint16_t, lo);
+        if constexpr (MODE == BF16X6) {
+            H m;
+            split3(v.x, h, m, lo);
+            Thi[o] = __builtin_bit_cast(uint16_t, h);
+            Tlo[o] = __builtin_bit_cast(uint16_t, m);
+            Tl2[o] = __builtin_bit_cast(uint16_t, lo);
+            split3(v.y, h, m, lo);
+            Thi[o + 1] = __builtin_bit_cast(uint16_t, h);
+            Tlo[o + 1] = __builtin_bit_cast(uint16_t, m);
+            Tl2[o + 1] = __builtin_bit_cast(uint16_t, lo);
+        } else {
+            split16(v.x, h, lo);
+            Thi[o] = __builtin_bit_cast(uint16_t, h);
+            Tlo[o] = __builtin_bit_cast(uint16_t, lo);
+            split16(v.y, h, lo);
+            Thi[o + 1] = __builtin_bit_cast(uint16_t, h);
+            Tlo[o + 1] = __builtin_bit_cast(uint16_t, lo);
+        }
         if (i == 0) pTf[t] = t < nT ? (float)pT[t] : 0.f;
     }
 }
@@ -349,7 +320,7 @@ THX_DEV void wait_vm()
 template <int MODE, int NF>
 struct Smem {
     static constexpr int NTP = NF * 32;
-    static constexpr int NPLANE = MODE == BF16X3 ? 2 : 1;
+    static constexpr int NPLANE = nplane<MODE>();
     static constexpr int T_H = NTP * TROW;                 // 16-bit elements per plane
     static constexpr int A_F2 = IMG_TILE * APITCH;         // float2
     static constexpr int P_F2 = ROT_TILE * KC;             // float2
@@ -363,11 +334,12 @@ struct Smem {
     static constexpr int P_PC = P_F2 * 8 / 16;             // 16-B pieces of the P rows
     static constexpr int PQ = (P_PC + 63) / 64;
     static constexpr int NQ = NPLANE * TQ + AQ + PQ;
-    static constexpr int TL_OFF = TQ * 1024;               // bytes: lo plane, a tile, P rows
+    static constexpr int TL_OFF = TQ * 1024;               // bytes: second / third plane, a tile, P rows
+    static constexpr int TL2_OFF = 2 * TQ * 1024;
     static constexpr int A_OFF = NPLANE * TQ * 1024;
     static constexpr int P_OFF = (NPLANE * TQ + AQ) * 1024;
     static constexpr int STAGE_B = NQ * 1024;
-    static constexpr int EPI_B = (ROT_TILE * 64 * 3 + 64 + ROT_TILE * 8 * NTP) * 4;
+    static constexpr int EPI_B = (ROT_TILE * 64 * 3 + 64 + ROT_TILE * 8 * NTP + ROT_TILE * GCAP) * 4;
     static constexpr int TOTAL_B = SCAN_STAGES * STAGE_B > EPI_B ? SCAN_STAGES * STAGE_B : EPI_B;
 };
 
@@ -380,13 +352,140 @@ THX_DEV void dma16(const void* g, void* ldsBase)
         (__attribute__((address_space(3))) void*)ldsBase, 16, 0, 0);
 }
 
+// The reference's direct form of one sample (logDataVSPrior_m_huabin,
+// src/Optimiser.cpp:9187-9213, with the T P product of :756-826 first):
+// per pixel ctf (T P), d minus it, |.|^2 times sigRcp, in FP32 without
+// contraction; the pixels strided over the wave's lanes, then a wave sum.
+// Used by the cancellation guard for the few samples it flags.
+THX_DEV float direct_dvp(const float2* __restrict__ dat,
+                                                      const float* __restrict__ ctf,
+                                                      const float* __restrict__ sig,
+                                                      const float2* __restrict__ traP,
+                                                      const float2* __restrict__ rotP,
+                                                      int nPxl, int l, int r, int t)
+{
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    const float2* D = dat + (size_t)l * nPxl;
+    const float* C = ctf + (size_t)l * nPxl;
+    const float* S = sig + (size_t)l * nPxl;
+    const float2* Tt = traP + (size_t)t * nPxl;
+    const float2* Pr = rotP + (size_t)r * nPxl;
+    float acc = 0.f;
+    for (int i = lane; i < nPxl; i += 64) {
+        const float2 tp = Tt[i], p = Pr[i], d = D[i];
+        const float c = C[i], sg = S[i];
+        const float pr = tp.x * p.x - tp.y * p.y;
+        const float pi = tp.x * p.y + tp.y * p.x;
+        const float er = d.x - c * pr;
+        const float ei = d.y - c * pi;
+        acc += (er * er + ei * ei) * sg;
+    }
+    return wave_sum(acc);
+}
+
+struct Guard {
+    const float2* dat;
+    const float* ctf;
+    const float* sig;
+    const float2* traP;
+    const float2* rotP;
+    float kmax;       // <= 0: off
+    float* dvpOut;    // optional [nImg][nR][nT] dump of the final dvp
+};
+
+// The cancellation guard over one wave's tile acc[2][NF] (16 rows x 32
+// translation columns per accumulator, values already dvp = X + (A + B)).
+// A sample is flagged when |A| + |B| + |X| > kmax |dvp|.  Flagged samples are
+// recomputed by the whole wave (direct_dvp) in rounds of at most GCAP into a
+// per-wave LDS list, then every flagged lane picks its value up by its rank --
+// the accumulator registers are only ever indexed at compile time.
+template <int NF>
+THX_DEV void guard_tile(f32x16 (&acc)[2][NF], const Guard& gd, const float* sABw,
+                        const float* sBiasw, float* sVal, int l0,
+                        int r, bool rValid, int nImg, int nT, int nPxl)
+{
+    const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
+    unsigned fw[NF];              // bit q = a * 16 + j of translation fragment f
+#pragma unroll
+    for (int f = 0; f < NF; f++) fw[f] = 0;
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int row = a * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
+            const float b = sBiasw[row], ab = sABw[row];
+            const bool ok = rValid && l0 + row < nImg;
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                const float d = acc[a][f][j];
+                const float x = d - b;   // X up to one rounding: the flag is a ratio test
+                if (ok && f * 32 + n < nT && ab + fabsf(x) > gd.kmax * fabsf(d))
+                    fw[f] |= 1u << (a * 16 + j);
+            }
+        }
+    unsigned any = 0;
+#pragma unroll
+    for (int f = 0; f < NF; f++) any |= fw[f];
+    while (__ballot(any != 0)) {
+        unsigned pw[NF];          // the entries of this round
+#pragma unroll
+        for (int f = 0; f < NF; f++) pw[f] = 0;
+        int cnt = 0;
+        for (int q = 0; q < 32 && cnt < GCAP; q++) {
+#pragma unroll
+            for (int f = 0; f < NF; f++) {
+                uint64_t m = __ballot((fw[f] >> q) & 1u);
+                while (m && cnt < GCAP) {
+                    const int L = __builtin_ctzll(m);
+                    const int j = q & 15;
+                    const int lL = l0 + (q >> 4) * 32 + (j & 3) + 8 * (j >> 2) + 4 * (L >> 5);
+                    const float v = direct_dvp(gd.dat, gd.ctf, gd.sig, gd.traP, gd.rotP, nPxl, lL, r,
+                                               f * 32 + (L & 31));
+                    if (lane == 0) sVal[cnt] = v;
+                    if (lane == L) {
+                        fw[f] &= ~(1u << q);
+                        pw[f] |= 1u << q;
+                    }
+                    cnt++;
+                    m &= m - 1;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // entries were appended in (q, f, lane) order: a lane's slot is the
+        // count of earlier (q, f) groups plus the processed lanes below it
+        int base = 0;
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+#pragma unroll
+                for (int f = 0; f < NF; f++) {
+                    const bool mine = (pw[f] >> (a * 16 + j)) & 1u;
+                    const uint64_t m = __ballot(mine);
+                    if (m) {
+                        if (mine)
+                            acc[a][f][j] = sVal[base + __builtin_amdgcn_mbcnt_hi(
+                                (unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0))];
+                        base += __builtin_popcountll(m);
+                    }
+                }
+        __builtin_amdgcn_wave_barrier();
+        any = 0;
+#pragma unroll
+        for (int f = 0; f < NF; f++) any |= fw[f];
+    }
+}
+
 template <int MODE, int NF>
 __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2))) k_scan_split(const float2* __restrict__ Ac,
                                                         const float* __restrict__ Aconst,
-                                                        const float* __restrict__ scale,
                                                         const float* __restrict__ bias,
                                                         const uint16_t* __restrict__ Thi,
                                                         const uint16_t* __restrict__ Tlo,
+                                                        const uint16_t* __restrict__ Tl2,
                                                         const float2* __restrict__ Pc,
                                                         const float* __restrict__ pTf,
                                                         const double* __restrict__ pR,
@@ -395,10 +494,8 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                                                         int nRBias, int nIT,
                                                         float2* __restrict__ wRp,
                                                         float* __restrict__ pM,
-                                                        float* __restrict__ pWT)
+                                                        float* __restrict__ pWT, Guard gd)
 {
-    typedef typename Elt<MODE>::T H;
-    typedef typename Elt<MODE>::V HV;
     using S = Smem<MODE, NF>;
     constexpr int NTP = S::NTP;
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -433,6 +530,7 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
     auto issue_chunk = [&](int ck, char* stage) {
         const char* gTh = reinterpret_cast<const char*>(Thi + (size_t)ck * nTPad * TROW);
         const char* gTl = reinterpret_cast<const char*>(Tlo + (size_t)ck * nTPad * TROW);
+        const char* gT2 = reinterpret_cast<const char*>(Tl2 + (size_t)ck * nTPad * TROW);
         const char* gA = reinterpret_cast<const char*>(Ac + ((size_t)ck * nImgPad + l0) * APITCH);
         const char* gP = reinterpret_cast<const char*>(Pc + ((size_t)ck * nRBk + rb) * ROT_TILE * KC);
 #pragma unroll
@@ -442,7 +540,8 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                 const char* g;
                 int pc, lim;
                 if (q < S::TQ) { g = gTh; pc = q * 64; lim = S::T_PC; }
-                else if (MODE == BF16X3 && q < 2 * S::TQ) { g = gTl; pc = (q - S::TQ) * 64; lim = S::T_PC; }
+                else if (S::NPLANE >= 2 && q < 2 * S::TQ) { g = gTl; pc = (q - S::TQ) * 64; lim = S::T_PC; }
+                else if (S::NPLANE >= 3 && q < 3 * S::TQ) { g = gT2; pc = (q - 2 * S::TQ) * 64; lim = S::T_PC; }
                 else if (q < S::NQ - S::PQ) { g = gA; pc = (q - S::NPLANE * S::TQ) * 64; lim = S::A_PC; }
                 else { g = gP; pc = (q - (S::NQ - S::PQ)) * 64; lim = S::P_PC; }
                 if (pc + lane < lim) dma16(g + (size_t)(pc + lane) * 16, stage + q * 1024);
@@ -500,7 +599,47 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                     split16(wi, x0, x1); wh[2 * qd + 1] = x0; wl[2 * qd + 1] = x1;
                 }
             };
-            if constexpr (MODE == BF16X3) {
+            if constexpr (MODE == BF16X6) {
+                // both image halves' w in three pieces (24 VGPRs), then per
+                // translation fragment the three T planes feed 2 x 6 products
+                // (smallest first into the running FP32 sum)
+                const uint16_t* sT2 = reinterpret_cast<const uint16_t*>(stage + S::TL2_OFF);
+                HV wp[2][3];
+#pragma unroll
+                for (int a = 0; a < 2; a++) {
+                    const float2* rowA = sA + (a * 32 + n) * APITCH + px0;
+                    const f32x4v a01 = *reinterpret_cast<const f32x4v*>(rowA);
+                    const f32x4v a23 = *reinterpret_cast<const f32x4v*>(rowA + 2);
+                    const float ar[4] = {a01.x, a01.z, a23.x, a23.z};
+                    const float ai[4] = {a01.y, a01.w, a23.y, a23.w};
+#pragma unroll
+                    for (int qd = 0; qd < 4; qd++) {
+                        const float wr = ar[qd] * pr[qd] + ai[qd] * pi[qd];
+                        const float wi = ai[qd] * pr[qd] - ar[qd] * pi[qd];
+                        H x0, x1, x2;
+                        split3(wr, x0, x1, x2);
+                        wp[a][0][2 * qd] = x0; wp[a][1][2 * qd] = x1; wp[a][2][2 * qd] = x2;
+                        split3(wi, x0, x1, x2);
+                        wp[a][0][2 * qd + 1] = x0; wp[a][1][2 * qd + 1] = x1; wp[a][2][2 * qd + 1] = x2;
+                    }
+                }
+#pragma unroll
+                for (int f = 0; f < NF; f++) {
+                    const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
+                    const HV th = *reinterpret_cast<const HV*>(sTh + row);
+                    const HV tm = *reinterpret_cast<const HV*>(sTl + row);
+                    const HV tl = *reinterpret_cast<const HV*>(sT2 + row);
+#pragma unroll
+                    for (int a = 0; a < 2; a++) {
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][2], th, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][1], tm, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][0], tl, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][1], th, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][0], tm, acc[a][f], 0, 0, 0);
+                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][0], th, acc[a][f], 0, 0, 0);
+                    }
+                }
+            } else if constexpr (MODE == BF16X3) {
                 // one image half at a time (register budget of the three products)
 #pragma unroll
                 for (int a = 0; a < 2; a++) {
@@ -516,20 +655,6 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                         acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, th, acc[a][f], 0, 0, 0);
                     }
                 }
-            } else {
-                HV wh[2], wl[2];
-                make_w(0, wh[0], wl[0]);
-                make_w(1, wh[1], wl[1]);
-#pragma unroll
-                for (int f = 0; f < NF; f++) {
-                    const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
-                    const HV th = *reinterpret_cast<const HV*>(sTh + row);
-#pragma unroll
-                    for (int a = 0; a < 2; a++) {
-                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh[a], th, acc[a][f], 0, 0, 0);
-                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl[a], th, acc[a][f], 0, 0, 0);
-                    }
-                }
             }
         }
         // chunk ck + 1 must have landed; the newer copy may stay in flight
@@ -539,12 +664,16 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
 
     // ------------------------------------------------------------ epilogue
     float* sBias = reinterpret_cast<float*>(lds);      // [8 waves][64]  A_l + B[l][r]
-    float* sInv = sBias + ROT_TILE * 64;               // [64]           2^-e_l
-    float* sMax = sInv + ROT_TILE * 64;                // [8 waves][64 rows]
+    float* sMax = sBias + ROT_TILE * 64;               // [8 waves][64 rows]
     float* sRowM = sMax + ROT_TILE * 64;               // [64]           max over the tile's rotations
-    float* sT = sRowM + 64;                            // [8 waves][8 rows][NTP] scaled terms
-    sBias[w * 64 + lane] = Aconst[l0 + lane] + (rValid ? bias[(size_t)(l0 + lane) * nRBias + r] : 0.f);
-    if (w == 0) sInv[lane] = 1.f / scale[l0 + lane];
+    float* sAB = sRowM + 64;                           // [8 waves][64]  |A_l| + |B[l][r]|
+    float* sT = sAB + ROT_TILE * 64;                   // [8 waves][8 rows][NTP] scaled terms
+    float* sGVal = sT + ROT_TILE * 8 * NTP;            // [8 waves][GCAP] guard list
+    {
+        const float A = Aconst[l0 + lane], B = rValid ? bias[(size_t)(l0 + lane) * nRBias + r] : 0.f;
+        sBias[w * 64 + lane] = A + B;
+        sAB[w * 64 + lane] = fabsf(A) + fabsf(B);
+    }
     __syncthreads();
 
     float pTv[NF];
@@ -557,15 +686,26 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             const int row = a * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
+            const float b = sBias[w * 64 + row];
+#pragma unroll
+            for (int f = 0; f < NF; f++) acc[a][f][j] += b;
+        }
+    if (gd.kmax > 0.f) guard_tile<NF>(acc, gd, sAB + w * 64, sBias + w * 64, sGVal + w * GCAP, l0, r, rValid, nImg, nT, nPxl);
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int row = a * 32 + (j & 3) + 8 * (j >> 2) + 4 * h;
             const int l = l0 + row;
-            const float b = sBias[w * 64 + row], inv = sInv[row];
+            if (gd.dvpOut && rValid && l < nImg) {
+#pragma unroll
+                for (int f = 0; f < NF; f++)
+                    if (f * 32 + n < nT) gd.dvpOut[((size_t)l * nR + r) * nT + f * 32 + n] = acc[a][f][j];
+            }
             float mx = -INFINITY;
 #pragma unroll
-            for (int f = 0; f < NF; f++) {
-                const float d = acc[a][f][j] * inv + b;
-                acc[a][f][j] = d;
-                if (f * 32 + n < nT) mx = fmaxf(mx, d);
-            }
+            for (int f = 0; f < NF; f++)
+                if (f * 32 + n < nT) mx = fmaxf(mx, acc[a][f][j]);
             mx = half_reduce<true>(mx);
             if (!rValid) mx = -INFINITY;
             float sR = 0.f;
@@ -664,7 +804,7 @@ __global__ void __launch_bounds__(256) k_scan_combine_bf(const float2* __restric
 }
 
 template <int MODE, int NF>
-int launch_main(const WS& ws, const Dims& d, const float* rotP, const double* pR, hipStream_t s)
+int launch_main(const WS& ws, const Dims& d, const double* pR, const Guard& gd, hipStream_t s)
 {
     const int nIT = d.nImgPad / IMG_TILE;
     dim3 grid((unsigned)(8 * thx::cdiv(nIT * d.nRB, 8)));
@@ -674,9 +814,9 @@ int launch_main(const WS& ws, const Dims& d, const float* rotP, const double* pR
     const int st = thx::set_max_lds(reinterpret_cast<const void*>(k_scan_split<MODE, NF>), lds, ldsSet);
     if (st != THX_OK) return st;
     hipLaunchKernelGGL((k_scan_split<MODE, NF>), grid, dim3(THREADS), lds, s, ws.Ac, ws.Aconst,
-                       ws.scale, ws.bias, ws.Thi, ws.Tlo, ws.Pc,
+                       ws.bias, ws.Thi, ws.Tlo, ws.Tl2, ws.Pc,
                        ws.pTf, pR, d.nImg, d.nR, d.nT, d.nPxl, d.nImgPad, d.nPxlPad, d.nTPad,
-                       d.nRBias, nIT, ws.wRp, ws.pM, ws.pWT);
+                       d.nRBias, nIT, ws.wRp, ws.pM, ws.pWT, gd);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
@@ -685,7 +825,8 @@ template <int MODE>
 int scan_split(const float* rotP, int nR, const float* traP, int nT, const float* dat,
                const float* ctf, const float* sigRcp, int nImg, int nPxl, const double* pR,
                const double* pT, int kIdx, int nK, float* wC, float* wR, float* wT,
-               float* baseL, void* workspace, size_t wsBytes, hipStream_t s)
+               float* baseL, float guard, float* dvpOut, void* workspace, size_t wsBytes,
+               hipStream_t s)
 {
     const Dims d = dims(nImg, nR, nT, nPxl);
     THX_CHECK_ARG(d.nRB <= 65535 && d.nRBias / 64 <= 65535, "thx_global_scan: grid too large");
@@ -693,16 +834,10 @@ int scan_split(const float* rotP, int nR, const float* traP, int nT, const float
     THX_CHECK_ARG(ws.bytes <= wsBytes, "thx_global_scan: workspace too small");
     const float2* dat2 = reinterpret_cast<const float2*>(dat);
     const float2* rot2 = reinterpret_cast<const float2*>(rotP);
-    hipLaunchKernelGGL(k_prep_aconst, dim3(thx::cdiv(d.nImgPad, 4)), dim3(256), 0, s, dat2, ctf,
-                       sigRcp, nImg, nPxl, d.nImgPad, ws.Aconst, ws.amax);
+    hipLaunchKernelGGL(k_prep_aconst, dim3(thx::cdiv(d.nImgPad, 4)), dim3(256), 0, s, dat2, sigRcp,
+                       nImg, nPxl, d.nImgPad, ws.Aconst);
     THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_pmax, dim3(PMAX_BLOCKS), dim3(256), 0, s, rot2, (long)nR * nPxl,
-                       ws.pmaxB);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_scale, dim3(thx::cdiv(d.nImgPad, 256)), dim3(256), 0, s, ws.amax,
-                       ws.pmaxB, d.nImgPad, MODE == F16X2 ? 1 : 0, ws.scale);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_img, dim3(2048), dim3(256), 0, s, dat2, ctf, sigRcp, ws.scale, nImg,
+    hipLaunchKernelGGL(k_prep_img, dim3(2048), dim3(256), 0, s, dat2, ctf, sigRcp, nImg,
                        nPxl, d.nImgPad, d.nPxlPad, ws.Ac, ws.Bc);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_prep_pchunk, dim3(2048), dim3(256), 0, s, rot2, nR, nPxl,
@@ -710,18 +845,19 @@ int scan_split(const float* rotP, int nR, const float* traP, int nT, const float
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_prep_tsplit<MODE>, dim3(512), dim3(256), 0, s,
                        reinterpret_cast<const float2*>(traP), pT, nT, nPxl, d.nTPad, d.nPxlPad,
-                       ws.Thi, ws.Tlo, ws.pTf);
+                       ws.Thi, ws.Tlo, ws.Tl2, ws.pTf);
     THX_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_scan_bias, dim3(d.nImgPad / 64, d.nRBias / 64), dim3(256), 0, s, ws.Bc,
                        rot2, nR, nPxl, d.nImgPad, d.nCk, d.nRBias, ws.bias);
     THX_LAUNCH_CHECK();
+    const Guard gd{dat2, ctf, sigRcp, reinterpret_cast<const float2*>(traP), rot2, guard, dvpOut};
     int st;
     switch (d.nTPad / 32) {
-        case 1: st = launch_main<MODE, 1>(ws, d, rotP, pR, s); break;
-        case 2: st = launch_main<MODE, 2>(ws, d, rotP, pR, s); break;
-        case 3: st = launch_main<MODE, 3>(ws, d, rotP, pR, s); break;
-        case 4: st = launch_main<MODE, 4>(ws, d, rotP, pR, s); break;
-        default: st = launch_main<MODE, 5>(ws, d, rotP, pR, s); break;
+        case 1: st = launch_main<MODE, 1>(ws, d, pR, gd, s); break;
+        case 2: st = launch_main<MODE, 2>(ws, d, pR, gd, s); break;
+        case 3: st = launch_main<MODE, 3>(ws, d, pR, gd, s); break;
+        case 4: st = launch_main<MODE, 4>(ws, d, pR, gd, s); break;
+        default: st = launch_main<MODE, 5>(ws, d, pR, gd, s); break;
     }
     if (st != THX_OK) return st;
     hipLaunchKernelGGL(k_scan_combine_bf, dim3(nImg), dim3(256), sizeof(float) * d.nRB, s,
@@ -749,28 +885,28 @@ size_t scan_split_workspace(int nImg, int nR, int nT, int nPxl)
     return carve(nullptr, d).bytes;
 }
 
-int scan_bf16x3(const float* rotP, int nR, const float* traP, int nT, const float* dat,
-                const float* ctf, const float* sigRcp, int nImg, int nPxl, const double* pR,
-                const double* pT, int kIdx, int nK, float* wC, float* wR, float* wT,
-                float* baseL, void* workspace, size_t wsBytes, hipStream_t s)
-{
-    if (pad_to(nT, 32) > 160)
-        return scan_mfma(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx, nK,
-                         wC, wR, wT, baseL, workspace, wsBytes, s);
-    return scan_split<BF16X3>(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx,
-                              nK, wC, wR, wT, baseL, workspace, wsBytes, s);
-}
+float scan_guard_default() { return SCAN_GUARD; }
 
-int scan_f16x2(const float* rotP, int nR, const float* traP, int nT, const float* dat,
-               const float* ctf, const float* sigRcp, int nImg, int nPxl, const double* pR,
-               const double* pT, int kIdx, int nK, float* wC, float* wR, float* wT,
-               float* baseL, void* workspace, size_t wsBytes, hipStream_t s)
+// algo 2 (bf16x3), 4 (bf16x6); guard = the cancellation ratio
+// above which a sample is recomputed directly (0 = off); dvpOut (optional)
+// receives every sample's final dvp
+int scan_split_algo(int algo, const float* rotP, int nR, const float* traP, int nT,
+                    const float* dat, const float* ctf, const float* sigRcp, int nImg, int nPxl,
+                    const double* pR, const double* pT, int kIdx, int nK, float* wC, float* wR,
+                    float* wT, float* baseL, float guard, float* dvpOut, void* workspace,
+                    size_t wsBytes, hipStream_t s)
 {
-    if (pad_to(nT, 32) > 160)
+    if (pad_to(nT, 32) > 160) {
+        THX_CHECK_ARG(dvpOut == nullptr,
+                      "thx_global_scan_dvp: nT = %d > 160 runs the FP32-MFMA scan, which keeps no dvp", nT);
         return scan_mfma(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx, nK,
                          wC, wR, wT, baseL, workspace, wsBytes, s);
-    return scan_split<F16X2>(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx,
-                             nK, wC, wR, wT, baseL, workspace, wsBytes, s);
+    }
+    if (algo == 2)
+        return scan_split<BF16X3>(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx,
+                                  nK, wC, wR, wT, baseL, guard, dvpOut, workspace, wsBytes, s);
+    return scan_split<BF16X6>(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx, nK,
+                              wC, wR, wT, baseL, guard, dvpOut, workspace, wsBytes, s);
 }
 
 }  // namespace thx

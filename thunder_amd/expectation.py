@@ -85,7 +85,7 @@ class Expectation:
     """
 
     def __init__(self, vol, px, gset=None, mLR=125, mLT=9, n_phase=10, perturb=0.5,
-                 trans_s=10.0, trans_search_factor=0.25, algo=2, seed=7, shuffle=True,
+                 trans_s=10.0, trans_search_factor=0.25, algo=4, seed=7, shuffle=True,
                  search="global", converge=False, perturb_mean="acg", acg_iters=100,
                  perturb_large=2.0, large_first=False, min_phase=None, max_phase=None,
                  mLD=9, ctf_refine_s=0.01, perturb_ctf=0.5, cells="auto", mode="3d", sym=None):

@@ -256,9 +256,13 @@ def dvp(rotP, traP, dat, ctf_, sig):
 
 
 # ------------------------------------------------------------- a7 + a8
-def global_scan(rotP, traP, dat, ctf_, sig, pR, pT, kIdx=0, nK=1, state=None, algo=2):
+def global_scan(rotP, traP, dat, ctf_, sig, pR, pT, kIdx=0, nK=1, state=None, algo=4, guard=None,
+                want_dvp=False):
     """ExpectGlobal3D: returns (wC [nImg,nK], wR [nImg,nK,nR], wT [nImg,nK,nT], baseL [nImg]).
-    algo: 0 direct, 1 FP32 MFMA, 2 bf16x3 MFMA (default, as the expectation driver), 3 fp16x2."""
+    algo: 0 direct, 1 FP32 MFMA, 2 bf16x3 MFMA, 3 fp16x2, 4 bf16x6 MFMA (default, as the
+    expectation driver).  want_dvp (algo 2-4): also return every sample's final dvp
+    [nImg, nR, nT] (thx_global_scan_dvp); guard: the cancellation ratio of the
+    direct-form recompute (None = the library's default, 0 = off)."""
     nImg, nPxl = _images(dat, ctf_, sig)
     nR, nT = rotP.shape[0], traP.shape[0]
     dev = dat.device
@@ -280,6 +284,14 @@ def global_scan(rotP, traP, dat, ctf_, sig, pR, pT, kIdx=0, nK=1, state=None, al
     _req(baseL, torch.float32, (nImg,), "baseL")
     nbytes = lib().thx_global_scan_workspace(nImg, nR, nT, nPxl, algo)
     ws = workspace(nbytes, dev)
+    if want_dvp or guard is not None:
+        dvp = torch.empty(nImg, nR, nT, dtype=torch.float32, device=dev)
+        check(lib().thx_global_scan_dvp(_ptr(rotP), nR, _ptr(traP), nT, _ptr(dat), _ptr(ctf_),
+                                        _ptr(sig), nImg, nPxl, _ptr(pR), _ptr(pT), kIdx, nK,
+                                        _ptr(wC), _ptr(wR), _ptr(wT), _ptr(baseL), algo,
+                                        4.0 if guard is None else float(guard), _ptr(dvp),
+                                        _ptr(ws), ws.numel(), _stream(dev)), "thx_global_scan_dvp")
+        return (wC, wR, wT, baseL, dvp) if want_dvp else (wC, wR, wT, baseL)
     check(lib().thx_global_scan(_ptr(rotP), nR, _ptr(traP), nT, _ptr(dat), _ptr(ctf_), _ptr(sig),
                                 nImg, nPxl, _ptr(pR), _ptr(pT), kIdx, nK, _ptr(wC), _ptr(wR),
                                 _ptr(wT), _ptr(baseL), algo, _ptr(ws), ws.numel(), _stream(dev)),
