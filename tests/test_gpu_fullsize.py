@@ -92,3 +92,24 @@ def test_full_resolution_phase_matches_oracle(orc, c3, layout, spread):
                                  dat[l].cpu().numpy(), ctf[l].cpu().numpy(), sig[l].cpu().numpy(),
                                  pxh, N)
         assert np.max(np.abs(d[l] - rd) / np.abs(rd)) < 1e-5
+
+
+@pytest.mark.parametrize("algo", [2, 4])
+def test_split_scan_every_tile_row_matches_direct(c3, algo):
+    """A whole 64-image tile (both 32-row halves of every MFMA operand, all 16
+    accumulator rows per lane) of the split scans' dumped dvp against the
+    direct formulation (thx_dvp) at 1e-5, and a repeated call bit-identical.
+    A schedule of the bf16x6 main loop once corrupted rows 16-31 of each half
+    nondeterministically ("bf16x6 scan"): this is the guard."""
+    q, t, pR, pT = synth.global_sample_set(2000, seed=2)
+    px = c3["px"]
+    assert c3["dat"].shape[0] == 64
+    rotP = ops.project3d(c3["vol"], ops.rotmat(torch.as_tensor(q, device=DEV)), px)
+    traP = ops.trans_table(torch.as_tensor(t, device=DEV), px)
+    pRd, pTd = torch.as_tensor(pR, device=DEV), torch.as_tensor(pT, device=DEV)
+    ref = ops.dvp(rotP, traP, c3["dat"], c3["ctf"], c3["sig"]).cpu().numpy().astype(np.float64)
+    runs = [ops.global_scan(rotP, traP, c3["dat"], c3["ctf"], c3["sig"], pRd, pTd, algo=algo,
+                            want_dvp=True)[4].cpu().numpy() for _ in range(2)]
+    rel = (np.abs(runs[0] - ref) / np.abs(ref)).reshape(64, -1).max(1)
+    assert rel.max() < 1e-5, np.nonzero(rel >= 1e-5)[0]
+    assert np.array_equal(runs[0], runs[1])

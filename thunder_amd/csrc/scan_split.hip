@@ -604,9 +604,7 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                 // translation fragment the three T planes feed 2 x 6 products
                 // (smallest first into the running FP32 sum)
                 const uint16_t* sT2 = reinterpret_cast<const uint16_t*>(stage + S::TL2_OFF);
-                HV wp[2][3];
-#pragma unroll
-                for (int a = 0; a < 2; a++) {
+                auto make_w3 = [&](int a, HV (&wq)[3]) {
                     const float2* rowA = sA + (a * 32 + n) * APITCH + px0;
                     const f32x4v a01 = *reinterpret_cast<const f32x4v*>(rowA);
                     const f32x4v a23 = *reinterpret_cast<const f32x4v*>(rowA + 2);
@@ -618,11 +616,22 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                         const float wi = ai[qd] * pr[qd] - ar[qd] * pi[qd];
                         H x0, x1, x2;
                         split3(wr, x0, x1, x2);
-                        wp[a][0][2 * qd] = x0; wp[a][1][2 * qd] = x1; wp[a][2][2 * qd] = x2;
+                        wq[0][2 * qd] = x0; wq[1][2 * qd] = x1; wq[2][2 * qd] = x2;
                         split3(wi, x0, x1, x2);
-                        wp[a][0][2 * qd + 1] = x0; wp[a][1][2 * qd + 1] = x1; wp[a][2][2 * qd + 1] = x2;
+                        wq[0][2 * qd + 1] = x0; wq[1][2 * qd + 1] = x1; wq[2][2 * qd + 1] = x2;
                     }
-                }
+                };
+                auto mma6 = [&](f32x16& c, const HV (&wq)[3], const HV& th, const HV& tm, const HV& tl) {
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq[2], th, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq[1], tm, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq[0], tl, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq[1], th, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq[0], tm, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq[0], th, c, 0, 0, 0);
+                };
+                HV wp[2][3];
+                make_w3(0, wp[0]);
+                make_w3(1, wp[1]);
 #pragma unroll
                 for (int f = 0; f < NF; f++) {
                     const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
@@ -630,14 +639,7 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                     const HV tm = *reinterpret_cast<const HV*>(sTl + row);
                     const HV tl = *reinterpret_cast<const HV*>(sT2 + row);
 #pragma unroll
-                    for (int a = 0; a < 2; a++) {
-                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][2], th, acc[a][f], 0, 0, 0);
-                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][1], tm, acc[a][f], 0, 0, 0);
-                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][0], tl, acc[a][f], 0, 0, 0);
-                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][1], th, acc[a][f], 0, 0, 0);
-                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][0], tm, acc[a][f], 0, 0, 0);
-                        acc[a][f] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wp[a][0], th, acc[a][f], 0, 0, 0);
-                    }
+                    for (int a = 0; a < 2; a++) mma6(acc[a][f], wp[a], th, tm, tl);
                 }
             } else if constexpr (MODE == BF16X3) {
                 // one image half at a time (register budget of the three products)

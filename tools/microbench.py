@@ -54,7 +54,7 @@ def main():
     p.add_argument("--images", type=int, default=4096)
     p.add_argument("--cells", type=int, default=0)
     p.add_argument("--ypair", type=int, default=0, help="local: gather from ops.volume_ypair(vol)")
-    p.add_argument("--algo", type=int, default=2)
+    p.add_argument("--algo", type=int, default=4)
     p.add_argument("--nr", type=int, default=2000)
     p.add_argument("--mreco", type=int, default=100)
     p.add_argument("--reps", type=int, default=5)
