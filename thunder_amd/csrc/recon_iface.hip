@@ -56,7 +56,8 @@ using thx::DeviceGuard;
 namespace {
 
 constexpr double PI_2_REF = 6.28318530717959;   // PI_2 (gpu/include/acc/Constructor.cuh:35)
-constexpr float DIFF_C_THRES = 1e-2f, DIFF_C_DECREASE_THRES = 0.95f;   // include/Reconstructor.h:65-69
+// double, as the reference's macros: float diffC is promoted before the compare
+constexpr double DIFF_C_THRES = 1e-2, DIFF_C_DECREASE_THRES = 0.95;   // include/Reconstructor.h:65-69
 constexpr int N_DIFF_C_NO_DECREASE = 2;
 
 #define GRID_STRIDE(q, n) \
@@ -362,8 +363,8 @@ int expose_wt(int gpuIdx, const float* T, float* W, const float* tab, float step
         THX_RET(to_host(&bits, dDiff.p, sizeof(unsigned)));
         diffCPrev = diffC;
         std::memcpy(&diffC, &bits, sizeof(float));
-        noDec = diffC > diffCPrev * DIFF_C_DECREASE_THRES ? noDec + 1 : 0;
-        if (diffC < DIFF_C_THRES || (m >= minIter && noDec == N_DIFF_C_NO_DECREASE)) break;
+        noDec = (double)diffC > (double)diffCPrev * DIFF_C_DECREASE_THRES ? noDec + 1 : 0;
+        if ((double)diffC < DIFF_C_THRES || (m >= minIter && noDec == N_DIFF_C_NO_DECREASE)) break;
     }
     if (nIter) *nIter = m < maxIter ? m + 1 : maxIter;
     return to_host(W, dW.p, sizeof(float) * n);
@@ -540,15 +541,25 @@ extern "C" int thx_AllocDevicePoint(int gpuIdx, float** dev_C, float** dev_W, fl
     *dev_C = *dev_W = *dev_T = *dev_tab = *devMax = nullptr;
     if (devDiff) *devDiff = nullptr;      // RECONSTRUCTOR_CHECK_C_AVERAGE is off (include/Config.h:101)
     if (devCount) *devCount = nullptr;
-    // the C buffer also holds the dim^3 real-space C of ExposeForConvC
-    THX_HIP(hipMalloc((void**)dev_C, std::max(sizeof(float2) * n, sizeof(float) * rl_size(dim, 3))));
-    THX_HIP(hipMalloc((void**)dev_W, sizeof(float) * n));
-    THX_HIP(hipMalloc((void**)dev_T, sizeof(float) * n));
-    THX_HIP(hipMalloc((void**)dev_tab, sizeof(float) * tabSize));
-    THX_HIP(hipMalloc((void**)devMax, sizeof(unsigned)));
     for (int i = 0; i < streamNum; i++) stream[i] = nullptr;
+    // all or nothing: the buffers are handed to the out-pointers only once
+    // every allocation (and the stream) succeeded; on a failure the DBufs free
+    // what was allocated and the outputs stay null
+    DBuf C, W, T, tab, mx;
+    // the C buffer also holds the dim^3 real-space C of ExposeForConvC
+    THX_DALLOC(C, std::max(sizeof(float2) * n, sizeof(float) * rl_size(dim, 3)));
+    THX_DALLOC(W, sizeof(float) * n);
+    THX_DALLOC(T, sizeof(float) * n);
+    THX_DALLOC(tab, sizeof(float) * tabSize);
+    THX_DALLOC(mx, sizeof(unsigned));
     hipStream_t s = nullptr;
     THX_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    auto release = [](DBuf& b) { void* p = b.p; b.p = nullptr; return p; };
+    *dev_C = static_cast<float*>(release(C));
+    *dev_W = static_cast<float*>(release(W));
+    *dev_T = static_cast<float*>(release(T));
+    *dev_tab = static_cast<float*>(release(tab));
+    *devMax = static_cast<float*>(release(mx));
     stream[0] = s;
     return THX_OK;
 }

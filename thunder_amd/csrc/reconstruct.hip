@@ -967,9 +967,9 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
             diffPrev = diffC;
             diffC = __builtin_bit_cast(float, *bits);
             if (diffOut) diffOut[m] = diffC;
-            if (diffC > diffPrev * 0.95f) nNoDec += 1;            // DIFF_C_DECREASE_THRES
+            if ((double)diffC > (double)diffPrev * 0.95) nNoDec += 1;   // DIFF_C_DECREASE_THRES (double)
             else nNoDec = 0;
-            if (diffC < 1e-2f || (m >= 10 && nNoDec == 2)) {       // DIFF_C_THRES, MIN_N_ITER, N_DIFF_C_NO_DECREASE
+            if ((double)diffC < 1e-2 || (m >= 10 && nNoDec == 2)) {  // DIFF_C_THRES, MIN_N_ITER, N_DIFF_C_NO_DECREASE
                 m++;
                 break;
             }
@@ -1333,9 +1333,9 @@ extern "C" int thx_reconstruct2d(const float* F, float* T, int nK, int N, int pf
                 prev[c] = diffC[c];
                 diffC[c] = __builtin_bit_cast(float, bits[c]);
                 iters[c] = m + 1;
-                if (diffC[c] > prev[c] * 0.95f) nNoDec[c] += 1;        // DIFF_C_DECREASE_THRES
+                if ((double)diffC[c] > (double)prev[c] * 0.95) nNoDec[c] += 1;   // DIFF_C_DECREASE_THRES (double)
                 else nNoDec[c] = 0;
-                if (diffC[c] < 1e-2f || (m >= 10 && nNoDec[c] == 2)) act[c] = 0;
+                if ((double)diffC[c] < 1e-2 || (m >= 10 && nNoDec[c] == 2)) act[c] = 0;
                 any = any || act[c];
             }
             if (!any) break;

@@ -363,6 +363,11 @@ extern "C" int thx_symmetrize_ft(const float* src, float* dst, int isComplex, in
     THX_CHECK_ARG(src && dst && src != dst && vdim > 0 && vdim % 2 == 0 && nSymElem >= 0 &&
                       nSymElem <= SYM_MAX && (nSymElem == 0 || R),
                   "thx_symmetrize_ft: bad arguments");
+    // a voxel within r interpolates at x0 + 1 <= r + 1: still inside the
+    // vdim / 2 + 1 half-complex columns only while r <= vdim / 2 - 1
+    THX_CHECK_ARG(r >= 0 && r <= vdim / 2 - 1,
+                  "thx_symmetrize_ft: radius %g past the half box %d (taps would leave the row)", r,
+                  vdim / 2 - 1);
     hipStream_t s = thx::as_stream(stream);
     const long n = (long)(vdim / 2 + 1) * vdim * vdim;
     const unsigned grid = (unsigned)std::min<long>(thx::cdiv(n, 256), 65536L);
@@ -391,6 +396,9 @@ extern "C" int thx_prepare_tf(float* F, float* T, int vdim, const double* R, int
                   "thx_prepare_tf: bad arguments");
     THX_CHECK_ARG(workspace && wsBytes >= thx_prepare_tf_workspace(vdim),
                   "thx_prepare_tf: workspace too small");
+    THX_CHECK_ARG((long)maxRadius * pf + 1 <= vdim / 2 - 1,
+                  "thx_prepare_tf: maxRadius * pf + 1 = %ld past the half box %d", (long)maxRadius * pf + 1,
+                  vdim / 2 - 1);
     hipStream_t s = thx::as_stream(stream);
     const long n = (long)(vdim / 2 + 1) * vdim * vdim;
     thx::Carver k(workspace, wsBytes);
