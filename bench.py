@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--cpu-images", type=int, default=4096,
                    help="images of the CPU-baseline sample (median of 3 runs)")
     p.add_argument("--no-extras", action="store_true", help="skip insert / all-reduce / local roofline")
+    p.add_argument("--no-rooflines", action="store_true",
+                   help="keep the insert and the round end (all-reduce, reconstruction, FSC) but "
+                        "skip the secondary rooflines (scan, full-resolution phase and insert)")
     return p.parse_args()
 
 
@@ -529,7 +532,7 @@ def main():
                     "LDS patch box serves it, so the line traffic (PMC, l2_line_*) runs at the roof "
                     "while the algorithmic rate is a fraction of it"}
 
-    if not a.no_extras:
+    if not a.no_extras and not a.no_rooflines:
         # ---- secondary: the global scan (bf16x6 MFMA) and its FP32-MFMA twin
         nRoof = min(ROOF_IMAGES, a.images)
         sec, issued, algorithmic, peak = scan_roofline(vol, px, gset, dat[:nRoof], ctf[:nRoof],
@@ -589,6 +592,7 @@ def main():
             "launch_ms": lsec * 1e3, "by_cloud": clouds}
         extras["insert_fullres"] = insert_fullres(vol, N, pf, dev)
 
+    if not a.no_extras:
         # ---- insert (mReco = 100) into the two hemispheres' half-maps, the
         # per-hemisphere RCCL all-reduce, FSC between the half-maps
         quat, trans = outs[0][0], outs[0][1]

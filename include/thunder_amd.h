@@ -254,6 +254,28 @@ int thx_local_phase_routed(const thx_local_sel* sel, const float* vol,
                            float* baseL, float* dvp, int* route, void* workspace,
                            size_t wsBytes, thx_stream_t stream);
 
+/* The compact y-pair ball the expectation driver gathers from (ABI 9; the
+ * copy every bench phase reads): elements (x, y, z), 0 <= x < R + 2,
+ * -R <= y, z < R + 2, each (v(x, y, z), v(x, y+1, z)) without wrap, the
+ * slices z, z+1 (z + R even) interleaved element by element; R = ceil(pf
+ * r_max) + 2 for a pixel ring of radius r_max (max sqrt(iCol^2 + iRow^2)).
+ * thx_ypair_ball_elems(R): float4 elements of the ball (0 for R <= 0). */
+size_t thx_ypair_ball_elems(int R);
+int thx_volume_ypair_ball(const float* vol, int vdim, int R, float* ball, thx_stream_t stream);
+/* thx_local_phase_routed with the ball as its y-pair copy (the driver's
+ * call); checks on the device's pixel set that pf r_max + 2 <= ballR (one
+ * read-back, so not graph-capturable) before any gather. */
+int thx_local_phase_routed_ball(const thx_local_sel* sel, const float* vol,
+                                const float* ball, int ballR, int vdim, int pf,
+                                const double* quat, int nR, const double* trans, int nT,
+                                const double* pC, const double* pR, const double* pT,
+                                const float* dat, const float* ctf, const float* sigRcp,
+                                const int* iCol, const int* iRow, const int* pxOrder,
+                                int nOrd, int nPxl, int idim, int nImg, float* wC,
+                                float* wR, float* wT, float* baseL, float* dvp,
+                                int* route, void* workspace, size_t wsBytes,
+                                thx_stream_t stream);
+
 /* The image order thx_expectation's 3D phases use (the active list of
  * thx_local_phase_sel): images stably sorted by the Hilbert index (16-bit
  * cells) of the octahedral map of their slice normal n = R(q) e_z, q = the first

@@ -58,7 +58,7 @@ def _scan_vs_oracle(orc, vol, px, pxh, N, pf, gset, dat, ctf, sig, algo):
 
 
 def _phase_vs_oracle(orc, vol, px, pxh, N, pf, quat, trans, dat, ctf, sig, cells=None, tol=1e-5,
-                     ypair=None, routed=False):
+                     ypair=None, routed=False, ball=None, ball_r=0):
     """The phase in the given layout (routed: thx_local_phase_routed, whose
     kernel choice is returned) against orc.local_phase image by image."""
     nImg, mR = quat.shape[:2]
@@ -66,7 +66,8 @@ def _phase_vs_oracle(orc, vol, px, pxh, N, pf, quat, trans, dat, ctf, sig, cells
     pR = np.full((nImg, mR), 1.0 / mR)
     pT = np.full((nImg, mT), 1.0 / mT)
     out = ops.local_phase(vol, T(quat), T(trans), T(np.ones(nImg)), T(pR), T(pT), dat, ctf, sig, px,
-                          want_dvp=True, cells=cells, ypair=ypair, routed=routed)
+                          want_dvp=True, cells=cells, ypair=ypair, routed=routed, ball=ball,
+                          ball_r=ball_r)
     wC, wR, wT, base, d = out[:5]
     d, wR, wT, base = d.cpu().numpy(), wR.cpu().numpy(), wT.cpu().numpy(), base.cpu().numpy()
     vnp = vol.cpu().numpy()
@@ -157,22 +158,65 @@ def test_c3_fp32_scan_matches_oracle(orc, c3):
                     c3["ctf"][:n].contiguous(), c3["sig"][:n].contiguous(), algo=1)
 
 
-@pytest.mark.parametrize("layout", ["halfcomplex", "ypair", "routed"])
+@pytest.mark.parametrize("layout", ["halfcomplex", "ypair", "routed", "ball"])
 def test_c3_local_phase_bench_clouds_match_oracle(orc, c3, layout):
     """The half-complex layout, the pair-form y-pair kernel (the one every
-    bench phase runs) and the device route with a y-pair copy at the bench's
-    cloud widths (3, 10 and 30 degrees), 125 x 9: dvp 1e-5 against the
-    oracle; the route takes the y-pair kernel for the wide clouds."""
+    bench phase runs), the device route with a y-pair copy and the route on
+    the driver's compact ball (thx_local_phase_routed_ball: the copy the bench
+    gathers from, R = ceil(pf r_max) + 2 = 53 at rU 24) at the bench's cloud
+    widths (3, 10 and 30 degrees), 125 x 9: dvp 1e-5 against the oracle; the
+    route takes the y-pair kernel for the wide clouds."""
     rng = np.random.default_rng(8)
     pxh = orc.pixel_set(256, 2, 24, 1)
-    yp = ops.volume_ypair(c3["vol"]) if layout != "halfcomplex" else None
+    yp = ops.volume_ypair(c3["vol"]) if layout in ("ypair", "routed") else None
+    kw = {}
+    if layout == "ball":
+        R = ops.ypair_ball_radius(c3["px"])
+        assert R == 53
+        kw = dict(ball=ops.volume_ypair_ball(c3["vol"], R), ball_r=R)
     for spread in (3.0, 10.0, 30.0):
         quat = synth.clustered_quaternions(16, 125, spread, rng)
         trans = rng.standard_normal((16, 9, 2)) * 2
         r = _phase_vs_oracle(orc, c3["vol"], c3["px"], pxh, 256, 2, quat, trans, c3["dat"], c3["ctf"],
-                             c3["sig"], ypair=yp, routed=layout == "routed")
-        if layout == "routed" and spread >= 10:
+                             c3["sig"], ypair=yp, routed=layout in ("routed", "ball"), **kw)
+        if layout in ("routed", "ball") and spread >= 10:
             assert r == 2, (spread, r)
+
+
+def test_ball_at_high_resolution_matches_oracle(orc, c3):
+    """The compact ball where it is largest and still smaller than the
+    volume: box 256, rU 100 (nPxl 15.6k, R = 203 of the 257 x-columns), 1.5
+    and 3 degree clouds -- thx_local_phase_routed_ball against the oracle at
+    1e-5.  (At the full-resolution radius rU 126 the ball would be the whole
+    volume, so the driver passes the whole y-pair copy, covered by
+    test_gpu_fullsize / the C5 test.)"""
+    from bench import make_stack
+    px, dat, ctf, sig, *_ = make_stack(256, 2, 100, 1, 4, DEV, seed=33, vol=c3["vol"])
+    pxh = orc.pixel_set(256, 2, 100, 1)
+    R = ops.ypair_ball_radius(px)
+    assert R + 2 <= 257 and px.n > 15000
+    ball = ops.volume_ypair_ball(c3["vol"], R)
+    rng = np.random.default_rng(9)
+    for spread in (1.5, 3.0):
+        quat = synth.clustered_quaternions(4, 125, spread, rng)
+        trans = rng.standard_normal((4, 9, 2))
+        r = _phase_vs_oracle(orc, c3["vol"], px, pxh, 256, 2, quat, trans, dat, ctf, sig, routed=True,
+                             ball=ball, ball_r=R)
+        assert r in (0, 2)
+
+
+def test_ball_rejects_a_radius_the_ring_does_not_fit(c3):
+    """pf r_max + 2 > ballR would gather outside the ball: refused before any
+    launch (thx_local_phase_routed_ball reads the ring radius back)."""
+    R = ops.ypair_ball_radius(c3["px"])
+    ball = ops.volume_ypair_ball(c3["vol"], R - 1)
+    one = lambda *sh: torch.ones(*sh, dtype=torch.float64, device=DEV)
+    q = T(synth.clustered_quaternions(2, 8, 3.0, np.random.default_rng(1)))
+    t = torch.zeros(2, 3, 2, dtype=torch.float64, device=DEV)
+    with pytest.raises(RuntimeError, match="needs ballR"):
+        ops.local_phase(c3["vol"], q, t, one(2), one(2, 8), one(2, 3), c3["dat"][:2].contiguous(),
+                        c3["ctf"][:2].contiguous(), c3["sig"][:2].contiguous(), c3["px"],
+                        routed=True, ball=ball, ball_r=R - 1)
 
 
 def test_c3_driver_routes_bench_phases_to_ypair(c3):

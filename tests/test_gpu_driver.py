@@ -210,13 +210,19 @@ def test_ypair_ball_leaves_every_image_unchanged(local_stack, monkeypatch):
     """The driver's compact y-pair ball (slices interleaved, no wrap) reads
     the same taps with the same weights as the whole copy: with the ball
     (default) and without (THX_YPAIR_BALL=0) the driver returns bit-identical
-    particles, priors, scores and classes."""
+    particles, priors, scores and classes.  The stack is the bench's SNR
+    (0.05), whose wide clouds the device route sends to the y-pair kernel in
+    every phase -- asserted, so the ball is really read."""
+    from bench import make_stack
     s = local_stack
+    _, dat, ctf, sig, *_ = make_stack(N5, 2, RU5, 1, 256, DEV, seed=77, vol=s["vol"])
     outs = []
     for flag in ("1", "0"):
         monkeypatch.setenv("THX_YPAIR_BALL", flag)
         e = ex.Expectation(s["vol"], s["px"], s["gset"], n_phase=4, seed=13)
-        outs.append([x.clone() for x in e.run(s["dat"], s["ctf"], s["sig"])])
+        routes = e.track_routes(4)
+        outs.append([x.clone() for x in e.run(dat, ctf, sig)])
+        assert routes.cpu().tolist() == [2] * 4, (flag, routes.cpu().tolist())
     for a, b in zip(*outs):
         assert torch.equal(a, b)
 

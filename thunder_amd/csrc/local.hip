@@ -1763,8 +1763,70 @@ extern "C" int thx_local_phase_routed(const thx_local_sel* sel, const float* vol
                             nullptr, ypair, route);
 }
 
+// max iCol^2 + iRow^2 over the pixel set (one workgroup)
+__global__ void __launch_bounds__(256) k_ring_r2(const int* __restrict__ iCol,
+                                                 const int* __restrict__ iRow, int nPxl,
+                                                 int* __restrict__ out)
+{
+    __shared__ int sm[4];
+    int m = 0;
+    for (int i = threadIdx.x; i < nPxl; i += 256) m = max(m, iCol[i] * iCol[i] + iRow[i] * iRow[i]);
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) *out = max(max(sm[0], sm[1]), max(sm[2], sm[3]));
+}
+
+extern "C" size_t thx_ypair_ball_elems(int R)
+{
+    return R > 0 ? (size_t)(R + 2) * (2 * R + 2) * (2 * R + 2) : 0;
+}
+
+extern "C" int thx_volume_ypair_ball(const float* vol, int vdim, int R, float* ball,
+                                     thx_stream_t stream)
+{
+    THX_CHECK_ARG(vol && ball && vdim > 0 && vdim % 2 == 0 && R > 0 && R + 2 <= vdim / 2 + 1,
+                  "thx_volume_ypair_ball: bad arguments (R = %d, vdim = %d)", R, vdim);
+    hipLaunchKernelGGL(k_volume_ypair_ball, dim3(2048), dim3(256), 0, thx::as_stream(stream),
+                       reinterpret_cast<const float2*>(vol), vdim, R, reinterpret_cast<float4*>(ball));
+    THX_LAUNCH_CHECK();
+    return THX_OK;
+}
+
+extern "C" int thx_local_phase_routed_ball(const thx_local_sel* sel, const float* vol,
+                                           const float* ball, int ballR, int vdim, int pf,
+                                           const double* quat, int nR, const double* trans, int nT,
+                                           const double* pC, const double* pR, const double* pT,
+                                           const float* dat, const float* ctf, const float* sigRcp,
+                                           const int* iCol, const int* iRow, const int* pxOrder,
+                                           int nOrd, int nPxl, int idim, int nImg, float* wC,
+                                           float* wR, float* wT, float* baseL, float* dvp,
+                                           int* route, void* workspace, size_t wsBytes,
+                                           thx_stream_t stream)
+{
+    THX_CHECK_ARG(pxOrder && ball && ballR > 0 && ballR + 2 <= vdim / 2 + 1 && nPxl > 0 && iCol && iRow,
+                  "thx_local_phase_routed_ball: bad arguments");
+    // every tap must fall inside the ball: pf r_max + 2 <= R, checked on the
+    // pixel set itself (one read-back)
+    hipStream_t s = thx::as_stream(stream);
+    thx::Carver c(workspace, wsBytes);
+    int* r2d = c.take<int>(1);
+    THX_CHECK_ARG(c.ok(), "thx_local_phase_routed_ball: workspace too small");
+    hipLaunchKernelGGL(k_ring_r2, dim3(1), dim3(256), 0, s, iCol, iRow, nPxl, r2d);
+    THX_LAUNCH_CHECK();
+    int r2 = 0;
+    THX_HIP(hipMemcpyAsync(&r2, r2d, sizeof(int), hipMemcpyDeviceToHost, s));
+    THX_HIP(hipStreamSynchronize(s));
+    THX_CHECK_ARG(pf * std::sqrt((double)r2) + 2 <= ballR,
+                  "thx_local_phase_routed_ball: the pixel ring (pf r_max = %g) needs ballR >= %d",
+                  pf * std::sqrt((double)r2), (int)std::ceil(pf * std::sqrt((double)r2)) + 2);
+    return local_phase_impl(sel, nullptr, nullptr, vol, LAYOUT_FT, vdim, pf, quat, nR, trans, nT,
+                            pC, pR, pT, dat, ctf, sigRcp, iCol, iRow, pxOrder, nOrd, nPxl, idim,
+                            nImg, wC, wR, wT, baseL, dvp, workspace, wsBytes, stream, 0, nullptr,
+                            nullptr, ball, route, nullptr, ballR);
+}
+
 namespace thx {
-// the driver's phase launch, with optional events around k_local_fused
 // float4 elements of the compact y-pair ball of radius R
 size_t ypair_ball_elems(int R) { return (size_t)(R + 2) * (2 * R + 2) * (2 * R + 2); }
 

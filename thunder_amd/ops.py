@@ -339,13 +339,36 @@ def volume_ypair(vol):
     return out
 
 
+def ypair_ball_radius(px):
+    """R of the driver's compact y-pair ball for a pixel set: ceil(pf r_max) + 2."""
+    r2 = int(np.max(px.iCol.astype(np.int64) ** 2 + px.iRow.astype(np.int64) ** 2))
+    return int(math.ceil(px.pf * math.sqrt(r2))) + 2
+
+
+def volume_ypair_ball(vol, R):
+    """thx_volume_ypair_ball: the compact y-pair ball of radius R the driver
+    gathers from ([elements, 2] complex64: (v(x, y, z), v(x, y+1, z)))."""
+    vdim = _vol_dim(vol)
+    n = lib().thx_ypair_ball_elems(R)
+    out = torch.empty(n, 2, dtype=torch.complex64, device=vol.device)
+    check(lib().thx_volume_ypair_ball(_ptr(vol), vdim, R, _ptr(out), _stream(vol.device)),
+          "thx_volume_ypair_ball")
+    return out
+
+
 def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False, cells=None,
-                tiled=True, ypair=None, routed=False):
+                tiled=True, ypair=None, routed=False, ball=None, ball_r=0):
     """cells / ypair: optional thx_volume_cells / thx_volume_ypair copy of vol.
     tiled: visit pixels in px.order (LDS-staged neighbourhoods) instead of set order.
     routed: the device route of thx_local_phase_routed (vol half-complex, ypair
     optional, pxOrder), which then also returns the kernel it picked (0 staged,
-    1 box-less, 2 y-pair, -1 not routed) as a sixth value."""
+    1 box-less, 2 y-pair, -1 not routed) as a sixth value; with ball (the
+    volume_ypair_ball of radius ball_r) instead of ypair, the driver's
+    thx_local_phase_routed_ball."""
+    if ball is not None:
+        if not routed or ypair is not None or ball_r <= 0:
+            raise ValueError("ball: routed phase with ball_r > 0 and no ypair")
+        _req(ball, torch.complex64, (lib().thx_ypair_ball_elems(ball_r), 2), "ball")
     vdim = _vol_dim(vol)
     layout, src = (0, vol) if routed else _layout(vol, cells, ypair)
     if routed and (cells is not None or not tiled):
@@ -372,6 +395,18 @@ def local_phase(vol, quat, trans, pC, pR, pT, dat, ctf_, sig, px, want_dvp=False
                                                    len(px.order) if tiled else nPxl), dev)
     for l0 in range(0, nImg, 65535):
         nb = min(65535, nImg - l0)
+        if routed and ball is not None:
+            check(lib().thx_local_phase_routed_ball(None, _ptr(vol), _ptr(ball), ball_r, vdim, px.pf,
+                                                    _ptr(quat[l0:]), nR, _ptr(trans[l0:]), nT,
+                                                    _ptr(pC[l0:]), _ptr(pR[l0:]), _ptr(pT[l0:]),
+                                                    _ptr(dat[l0:]), _ptr(ctf_[l0:]), _ptr(sig[l0:]),
+                                                    _ptr(px.d_iCol), _ptr(px.d_iRow), _ptr(px.d_order),
+                                                    len(px.order), nPxl, px.idim, nb, _ptr(wC[l0:]),
+                                                    _ptr(wR[l0:]), _ptr(wT[l0:]), _ptr(base[l0:]),
+                                                    _ptr(d[l0:]) if d is not None else None, _ptr(route),
+                                                    _ptr(ws), ws.numel(), _stream(dev)),
+                  "thx_local_phase_routed_ball")
+            continue
         if routed:
             check(lib().thx_local_phase_routed(None, _ptr(vol), _ptr(ypair) if ypair is not None else None,
                                                vdim, px.pf, _ptr(quat[l0:]), nR, _ptr(trans[l0:]), nT,
