@@ -569,26 +569,50 @@ def main():
 
         # ---- secondary: the north-star full-resolution phase against HBM
         lr = local_roofline(vol, N, pf, dev)
-        tr, tr_src = launch_traffic("local_fullres_512", N == 256)
         lbytes = lr["algo_bytes"]
         frac = lambda ms: lbytes / (ms / 1e3) / 1e9 / PEAK_HBM_GBS
+        # the PMC bytes of the same dispatches (tools/traffic.py: per cloud and
+        # layout, exact 64 / 128-B split where the pmc3 pass has it)
+        lt = traffic.get("local_fullres_512") if N == 256 else None
         clouds = []
         lays = ("halfcomplex", "cells", "ypair")
         for row in lr["clouds"]:
             best = min(lays, key=lambda k: row[k + "_ms"])
-            clouds.append({**{k: (round(v, 3) if isinstance(v, float) else v) for k, v in row.items()},
-                           **{"frac_" + k: round(frac(row[k + "_ms"]), 3) for k in lays},
-                           "best": best})
+            c = {**{k: (round(v, 3) if isinstance(v, float) else v) for k, v in row.items()},
+                 **{"algorithmic_frac_" + k: round(frac(row[k + "_ms"]), 3) for k in lays},
+                 "best": best}
+            key = "uniform" if row["spread_deg"] == "uniform" else f"{float(row['spread_deg']):.1f}"
+            pm = (lt or {}).get(key, {})
+            for k in lays:
+                if k in pm:
+                    tb = pm[k]["traffic_bytes"] / (row[k + "_ms"] / 1e3) / 1e12
+                    c["hbm_TBps_" + k] = round(tb, 3)
+                    c["hbm_frac_" + k] = round(tb * 1e3 / PEAK_HBM_GBS, 3)
+                    c["hbm_bytes_exact_" + k] = "exact_read" in pm[k]
+            clouds.append(c)
         head = clouds[0]
-        lsec = min(head[k + "_ms"] for k in lays) / 1e3
+        best = head["best"]
+        lsec = head[best + "_ms"] / 1e3
+        hk = "uniform" if head["spread_deg"] == "uniform" else f"{float(head['spread_deg']):.1f}"
+        pm = ((lt or {}).get(hk) or {}).get(best)
+        tr = pm["traffic_bytes"] if pm else None
+        hbm = tr / lsec / 1e9 if tr else None
         extras["roofline_local"] = {
-            "bound": "hbm", "achieved": lbytes / lsec / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": lbytes / lsec / 1e9 / PEAK_HBM_GBS, "traffic": tr,
-            "traffic_unit": "bytes per launch (HBM, PMC)", "traffic_source": tr_src,
+            "bound": "hbm", "achieved": hbm, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": hbm / PEAK_HBM_GBS if hbm else None, "traffic": tr,
+            "traffic_unit": "bytes per launch (HBM / fabric reads + writes, PMC, of the same "
+                            "kernel, cloud and layout as the time)",
+            "traffic_source": f"{traffic_src}: local_fullres_512/{hk}/{best}" if tr else None,
             "algorithmic_bytes": lbytes,
+            "algorithmic_GBps": lbytes / lsec / 1e9,
+            "algorithmic_frac": lbytes / lsec / 1e9 / PEAK_HBM_GBS,
             "kernel": f"local phase full-res (nPxl={lr['nPxl']}, 125x9, {lr['n_img']} images), "
                       f"{head['spread_deg']} deg local-search clouds, the faster projectee layout "
-                      f"({head['best']}); every cloud and layout in by_cloud",
+                      f"({best}); every cloud and layout in by_cloud",
+            "note": "achieved / frac = PMC bytes moved between L2 and the fabric (HBM, MALL "
+                    "hits included) per launch / launch time; algorithmic_* = 64 B of taps per "
+                    "rotation-pixel + 16 B per pixel (SURVEY 8(d)) / launch time, which L2 / MALL "
+                    "reuse of the narrow clouds can lift past what HBM delivers",
             "launch_ms": lsec * 1e3, "by_cloud": clouds}
         extras["insert_fullres"] = insert_fullres(vol, N, pf, dev)
 

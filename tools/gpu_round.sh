@@ -27,10 +27,16 @@ for s in $steps; do
           -d $O/prof_extras -o run -- python3 $R/bench.py --steps 1 --warmup 0 \
           --no-cpu-baseline > $O/prof_extras.json 2> $O/prof_extras.err) ;;
     pmc)
-      # HBM bytes: FETCH_SIZE and WRITE_SIZE need separate passes (TCC slots)
+      # HBM bytes: FETCH_SIZE and WRITE_SIZE need separate passes (TCC slots);
+      # pass 3 the exact 64 / 128-B request split when the box lists the
+      # 128-B counter (rocprofv3 -L), pass 4 the L2 hit rate
+      (cd /tmp && timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1) || true
+      P3="TCC_HIT_sum TCC_MISS_sum"
+      grep -q "TCC_EA0_RDREQ_128B" $O/counters.txt && P3="TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum"
       i=0
-      for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+      for P in "FETCH_SIZE" "WRITE_SIZE" "$P3" "TCC_HIT_sum TCC_MISS_sum"; do
         i=$((i+1))
+        [ $i = 4 ] && [ "$P3" = "$P" ] && break
         (cd /tmp && timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv \
             --kernel-include-regex "k_scan|k_local|k_patch|k_insert|k_prep" \
             -d $O/pmc$i -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline \

@@ -6,12 +6,16 @@ on `bench.py --steps 1 --warmup 0`).
 A "launch" is the whole launch sequence the bench times with HIP events
 (local_bench: the single k_local_fused<0> dispatch of a bench phase):
   scan  : k_prep_aconst .. k_scan_combine_bf of one thx_global_scan call whose
-          k_scan_split grid is the 4096-image grid (bench.scan_roofline);
-  local : k_patch_boxes .. k_local_fused of one thx_local_phase call of
-          bench.local_roofline (full resolution, 512 images): the clustered
-          cloud in the half-complex layout (first four 512-image
-          k_local_fused<0> sequences), and the 3-degree and uniform clouds in
-          the cell layout (k_local_fused<1>, 4 launches per cloud).
+          k_scan_pu grid is the 4096-image grid (bench.scan_roofline);
+  local : one thx_local_phase call of bench.local_roofline (full resolution,
+          512 images, grid 512 x 512): per cloud (1.5, 2, 3 degrees, uniform)
+          four launches (timed_events: one warm-up + 3) in each layout, in the
+          order half-complex (k_local_fused<0>, not routed: one dispatch),
+          cells (k_local_fused<1>), y-pair (k_local_fused<2>) -- sliced per
+          cloud and layout so each by_cloud time of the bench pairs with the
+          traffic of the same dispatches;
+  local_bench : the bench step's routed phase (k_local_fused<0> staged
+          variant, exits at entry, + k_local_fused<2>) over 12 500 images.
 Bytes: FETCH_SIZE is 64 B per memory-side read request (TCC_EA0_RDREQ x 64),
 whatever the request's size.  profiles/r02_fetch_calibration.json measured
 what that means per access shape on gfx950: wide coalesced reads (128-B
@@ -120,50 +124,73 @@ def sliced(rd, wr, name, grid, k, per, factor, shape, pair=1):
                   shape)
 
 
-def exact_split(tag, name, grid):
+def exact_split(tag, name, grid, k=None, per=None):
     """64 B x (RDREQ - RDREQ_128B) + 128 B x RDREQ_128B per dispatch, from a
-    pmc3 pass, or None."""
+    pmc3 pass, or None; k / per: the k-th run of `per` dispatches only."""
     p = os.path.join(tag, "pmc3", "run_counter_collection.csv")
     if not os.path.exists(p):
         return None
     req = [v for n, g, v in dispatches(p, "TCC_EA0_RDREQ_sum") if name in n and g == grid]
     big = [v for n, g, v in dispatches(p, "TCC_EA0_RDREQ_128B_sum") if name in n and g == grid]
+    if k is not None:
+        req, big = req[k * per:(k + 1) * per], big[k * per:(k + 1) * per]
     if not req or not big:
         return None
     a, b = sum(req) / len(req), sum(big) / len(big)
     return {"read_bytes": 64 * (a - b) + 128 * b, "requests": a, "requests_128B": b}
 
 
+CLOUDS = ("1.5", "2.0", "3.0", "uniform")          # bench.local_roofline spreads
+LAYOUTS = (("halfcomplex", "k_local_fused<0,", 2, "staged box rows (128-B requests) + 16-B row taps"),
+           ("cells", "k_local_fused<1,", 1, "64-B cell gathers"),
+           ("ypair", "k_local_fused<2,", 1, "32-B / 64-B y-pair pieces"))
+
+
+def local_fullres(tag, rd, wr):
+    """Per cloud and layout: bytes per launch of the full-resolution phase, the
+    FETCH_SIZE factor of the dominant access shape, and the exact 64 / 128-B
+    split where the pmc3 pass has it (then read_bytes is exact)."""
+    out = {}
+    for k, cl in enumerate(CLOUDS):
+        row = {}
+        for lay, name, factor, shape in LAYOUTS:
+            e = sliced(rd, wr, name, 512 * 512, k, 4, factor, shape)
+            if e is None:
+                continue
+            ex = exact_split(tag, name, 512 * 512, k, 4)
+            if ex:
+                e["exact_read"] = ex
+                e["read_bytes"] = ex["read_bytes"]
+                e["traffic_bytes"] = ex["read_bytes"] + e["write_bytes"]
+            row[lay] = e
+        out[cl] = row
+    return out
+
+
 def main():
     tag, out = sys.argv[1], sys.argv[2]
     rd = dispatches(os.path.join(tag, "pmc1", "run_counter_collection.csv"), "FETCH_SIZE")
     wr = dispatches(os.path.join(tag, "pmc2", "run_counter_collection.csv"), "WRITE_SIZE")
-    scan_grid = (4096 // 64) * 250 * 512          # k_scan_split grid at 4096 images, nR 2000
+    # the bf16x6 scan kernel's grid at 4096 images, nR 2000 (8 tiles of 256
+    # rotations x 4096 images, 512 threads each)
+    scan_grid = 4096 * 8 * 512
     res = {
         "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({tag}), "
                   "FETCH_SIZE x2 on gfx950",
         "scan_4096": summarise(rd, wr, "k_prep_aconst", "k_scan_combine_bf",
-                               lambda g: any("k_scan_split" in n and gr == scan_grid
+                               lambda g: any("k_scan_pu" in n and gr == scan_grid
                                              for n, gr, _ in g), 2, "streaming (128-B requests)"),
-        # bench.local_roofline: per cloud (1.5 deg, 3 deg, uniform) 4 launches
-        # half-complex (k_patch_boxes + k_local_fused<0>), then 4 cell-layout
-        # launches (k_local_fused<1> alone)
-        # a routed half-complex phase is two dispatches (staged / box-less
-        # variant, one exits at entry): the grid is 512 workgroups x 512 threads
-        "local_fullres_512": sliced(rd, wr, "k_local_fused<0,", 512 * 512, 0, 4, 2,
-                                    "staged box rows (128-B requests) + 16-B row taps", pair=2),
-        "local_fullres_512_3deg_cells": sliced(rd, wr, "k_local_fused<1,", 512 * 512, 1, 4, 1,
-                                               "64-B cell gathers"),
-        "local_fullres_512_uniform_cells": sliced(rd, wr, "k_local_fused<1,", 512 * 512, 2, 4, 1,
-                                                  "64-B cell gathers"),
+        # bench.local_roofline, every cloud and layout (not routed: one
+        # dispatch per launch)
+        "local_fullres_512": local_fullres(tag, rd, wr),
         # the bench step's dominant kernel: one k_local_fused<0> launch per
         # phase over the whole 12 500-image batch (grid 12500 x 1 x 1 of 512)
         "local_bench": routed_phase(rd, wr, 12500 * 512, 2,
                                     "16-B row taps / 32-B y-pair pieces"),
     }
-    ex = exact_split(tag, "k_local_fused<0,", 12500 * 512)
+    ex = exact_split(tag, "k_local_fused<2,", 12500 * 512)
     if ex and res["local_bench"]:
-        res["local_bench"]["exact_read"] = ex
+        res["local_bench"]["exact_read_ypair"] = ex
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
