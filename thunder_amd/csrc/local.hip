@@ -182,24 +182,17 @@ struct PCell {
 };
 // index of element (x, y, z) of the whole y-pair copy (thx_volume_ypair),
 // nc = vdim / 2 + 1
-// THX_YPAIR_WZIL: the whole copy with its slices z, z+1 (z even)
-// interleaved element by element as in the ball: for even z0 a sample's
-// four 16-B elements are one contiguous 64-B piece (full resolution, box
-// 256: 14.0 -> 12.1 ms at 1.5 deg, 18.4 -> 16.0 at 2 deg, 27.5 -> 23.0 at 3,
-// profiles/r04_fullres_wzil_ab.jsonl)
-#ifndef THX_YPAIR_WZIL
-#define THX_YPAIR_WZIL 1
-#endif
+// The whole y-pair copy has its slices z, z+1 (z even) interleaved element
+// by element as in the ball: for even z0 a sample's four 16-B elements are
+// one contiguous 64-B piece (full resolution, box 256: 14.0 -> 12.1 ms at 1.5
+// deg, 18.4 -> 16.0 at 2 deg, 27.5 -> 23.0 at 3, profiles/r04_fullres_wzil_ab.jsonl)
 THX_DEV unsigned ypair_elem(unsigned z, unsigned y, unsigned x, unsigned vdim, unsigned nc)
 {
-    return THX_YPAIR_WZIL ? (((z >> 1) * vdim + y) * nc + x) * 2u + (z & 1u) : (z * vdim + y) * nc + x;
+    return (((z >> 1) * vdim + y) * nc + x) * 2u + (z & 1u);
 }
-// THX_YPAIR_ZIL: in the compact ball slices z and z + 1 (z + R even) are
-// interleaved element by element, so for such z0 a sample's four 16-B
-// elements (x0, x0 + 1 of both slices) are one contiguous 64-B piece
-#ifndef THX_YPAIR_ZIL
-#define THX_YPAIR_ZIL 1
-#endif
+// In the compact ball slices z and z + 1 (z + R even) are interleaved element
+// by element, so for such z0 a sample's four 16-B elements (x0, x0 + 1 of
+// both slices) are one contiguous 64-B piece
 // ballR > 0: the copy is the compact ball of thx::volume_ypair_ball --
 // elements (x, y, z), 0 <= x < ballR + 2, -ballR <= y, z < ballR + 2, no
 // wrap (every tap of the pixel ring lies inside)
@@ -207,8 +200,7 @@ THX_DEV unsigned ypair_ball_elem(int z, int y, int x, int ballR)
 {
     const unsigned Y = 2u * ballR + 2u, X = (unsigned)ballR + 2u;
     const unsigned zc = (unsigned)(z + ballR), yc = (unsigned)(y + ballR);
-    return THX_YPAIR_ZIL ? (((zc >> 1) * Y + yc) * X + (unsigned)x) * 2u + (zc & 1u)
-                         : (zc * Y + yc) * X + (unsigned)x;
+    return (((zc >> 1) * Y + yc) * X + (unsigned)x) * 2u + (zc & 1u);
 }
 THX_DEV PCell pcell_of(float x, float y, float z, int vdim, int ballR = 0)
 {
@@ -382,14 +374,12 @@ THX_DEV int store_rec(const int (&e)[12], int ic0, int ir0, int vdim, int* __res
 
 // Route of a phase (FT layout, 64 KiB boxes): a sample of the images' patch
 // records is counted first (route[0] patches whose box fits, route[1]
-// patches); below THX_STAGE_MIN_PCT per cent staged, the phase gathers every
+// patches); below STAGE_MIN_PCT per cent staged, the phase gathers every
 // patch from L2 with the box-less kernel (6 waves per SIMD instead of 4, no
 // records), otherwise records are built for all images and the staged kernel
 // runs.  Both kernels are launched; the one not chosen exits at entry, so the
 // choice needs no host round trip.
-#ifndef THX_STAGE_MIN_PCT
-#define THX_STAGE_MIN_PCT 50
-#endif
+constexpr int STAGE_MIN_PCT = 50;
 constexpr int ROUTE_SAMPLE = 16;   // every 16th image's records are counted
 
 // Third route (round 3): when the caller supplies a y-pair copy (route[2] =
@@ -404,7 +394,7 @@ constexpr int ROUTE_SAMPLE = 16;   // every 16th image's records are counted
 constexpr int ROUTE_STAGED = 0, ROUTE_NOBOX = 1, ROUTE_YPAIR = 2;
 THX_DEV bool route_nostage(const int* __restrict__ route)
 {
-    return (long)route[0] * 100 < (long)THX_STAGE_MIN_PCT * route[1];
+    return (long)route[0] * 100 < (long)STAGE_MIN_PCT * route[1];
 }
 THX_DEV int route_pick(const int* __restrict__ route)
 {
@@ -418,12 +408,6 @@ __global__ void k_route_out(const int* __restrict__ route, int* __restrict__ out
     if (threadIdx.x == 0) *out = route_pick(route);
 }
 
-#ifndef THX_SKIP_PAD
-#define THX_SKIP_PAD 1
-#endif
-#ifndef THX_LOCAL_SORT
-#define THX_LOCAL_SORT 1
-#endif
 
 // 3D Morton code of three 10-bit coordinates.
 THX_DEV unsigned morton3(unsigned x, unsigned y, unsigned z)
@@ -453,7 +437,7 @@ THX_DEV void rotation_slots(const double* __restrict__ q4, int nRl, int tid,
 {
     if (tid < RT) {
         unsigned key = ~0u;
-        if (THX_LOCAL_SORT && tid < nRl) {
+        if (tid < nRl) {
             const double a0 = q4[0], a1 = -q4[1], a2 = -q4[2], a3 = -q4[3];   // conj(q_0)
             const double* b = q4 + 4 * tid;
             double w = a0 * b[0] - a1 * b[1] - a2 * b[2] - a3 * b[3];
@@ -755,12 +739,12 @@ THX_DEV float2 interp_box(const float2* __restrict__ box, int nx, int sp, int of
 // A CS workgroup covers NCT column tiles of 16 (up to 96 (t, d) columns), so
 // the projection -- the expensive part -- is gathered once for all of them;
 // each step then issues 4 NCT MFMAs against NCT accumulators.
-#ifndef THX_NOBOX_WAVES
-#define THX_NOBOX_WAVES 6
-#endif
-#ifndef THX_PAIR_WAVES
-#define THX_PAIR_WAVES THX_NOBOX_WAVES
-#endif
+// the big-box kernel from a pixel ring of BIGBOX_MIN_R projectee voxels on
+// (C5 full resolution; profiles/r02_local_bigbox_ab.jsonl)
+constexpr double BIGBOX_MIN_R = 300;
+// box-less and y-pair kernels: 6 waves per SIMD (4 / 5 / 8 measured slower,
+// profiles/r03_nobox_waves_ab.jsonl, r04_pair_waves_ball_ab.jsonl)
+constexpr int NOBOX_WAVES = 6;
 template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false, bool STAGE = true>
 // non-CS: two workgroups per CU (LDS-bound), 4 waves per SIMD, 128 VGPRs;
 // CS: the NCT accumulators and CTF prefetches need the 256-VGPR budget;
@@ -768,7 +752,7 @@ template <int LAYOUT, bool CS = false, int NCT = 1, bool BIGBOX = false, bool ST
 // no LDS box (cell layout, or STAGE = false): no box prefetch registers, so
 // 6 waves per SIMD (three workgroups per CU) for the L2 gathers
 __global__ void __launch_bounds__(THREADS)
-__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : LAYOUT == LAYOUT_YPAIR2 ? THX_PAIR_WAVES : (coop_layout(LAYOUT) || !STAGE) ? THX_NOBOX_WAVES : 4)))
+__attribute__((amdgpu_waves_per_eu((CS || BIGBOX) ? 2 : (coop_layout(LAYOUT) || LAYOUT == LAYOUT_YPAIR2 || !STAGE) ? NOBOX_WAVES : 4)))
 k_local_fused(const float2* __restrict__ vol,
                                                             int vdim, int pf,
                                                             const double* __restrict__ quat,
@@ -825,10 +809,7 @@ k_local_fused(const float2* __restrict__ vol,
     // barriers, 4 PP independent steps between them); CS keeps one.  PP 2:
     // full-res cells -2.5 %, the bench's phases unchanged; PP 4 needs two
     // image-tile elements per thread and spills (profiles/r03_nobox_pp_ab.jsonl)
-#ifndef THX_NOBOX_PP
-#define THX_NOBOX_PP 2
-#endif
-    constexpr int PP = (coop_layout(LAYOUT) || PAIR || !STAGE) && !CS ? THX_NOBOX_PP : 1;
+    constexpr int PP = (coop_layout(LAYOUT) || PAIR || !STAGE) && !CS ? 2 : 1;
     constexpr int PKC = PP * KC;                        // pixels per iteration
     constexpr int NE = (PKC * TT + THREADS - 1) / THREADS;   // image-tile elements per thread
     const int r0 = blockIdx.y * RT, t0 = blockIdx.z * NC;
@@ -1011,8 +992,7 @@ k_local_fused(const float2* __restrict__ vol,
         // a step whose four pixels are all padding adds exactly zero (U = V = b
         // = 0): skipped, wave-uniformly
         auto pad_step = [&](int s) {
-            return THX_SKIP_PAD &&
-                   !(sValid[4 * s] | sValid[4 * s + 1] | sValid[4 * s + 2] | sValid[4 * s + 3]);
+            return !(sValid[4 * s] | sValid[4 * s + 1] | sValid[4 * s + 2] | sValid[4 * s + 3]);
         };
         // COOP step: quad r of the wave evaluates rotation 16 wv + r at the four
         // pixels 4s + p, one cooperative cell read each, summed over the quad;
@@ -1074,7 +1054,7 @@ k_local_fused(const float2* __restrict__ vol,
         // r at pixels 4s + h (it 0) and 4s + h + 2 (it 1); lane j rotates the
         // it = j sample and the pair shares the cells.  MFMA A rows: (pixels
         // 4s, 4s + 2) from the h = 0 pairs, (4s + 1, 4s + 3) from the h = 1 pairs.
-        const unsigned yxs = ballR > 0 ? (THX_YPAIR_ZIL ? 2u : 1u) : (THX_YPAIR_WZIL ? 2u : 1u);   // x stride of the copy's elements
+        constexpr unsigned yxs = 2u;   // x stride of the copy's elements (slices interleaved)
         auto pair_step = [&](int s) {
             const int j = lane & 1, h = (lane >> 5) & 1;
             PCell mine;
@@ -1126,10 +1106,7 @@ k_local_fused(const float2* __restrict__ vol,
         } else if (COOP) {
 // all four steps unrolled: 16 cell reads in flight per wave (C5 +3-4 %,
 // full-res 1.5-3 deg 2-5 % over 2; profiles/r03_coop_unroll_ab.jsonl)
-#ifndef THX_COOP_UNROLL
-#define THX_COOP_UNROLL 4
-#endif
-#pragma unroll THX_COOP_UNROLL
+#pragma unroll 4
             for (int s = 0; s < 4 * PP; s++) {
                 if (pad_step(s)) continue;
                 coop_step(s);
@@ -1586,11 +1563,8 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     int* route = ws.take<int>(64);
     hipStream_t s = thx::as_stream(stream);
     // big LDS boxes for large full-resolution pixel sets: the ring's outer
-    // radius in projectee voxels, pf sqrt(2 nPxl / pi), past THX_BIGBOX_MIN_R
-#ifndef THX_BIGBOX_MIN_R
-#define THX_BIGBOX_MIN_R 300
-#endif
-    const bool big = pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R;
+    // radius in projectee voxels, pf sqrt(2 nPxl / pi), past BIGBOX_MIN_R
+    const bool big = pf * std::sqrt(2.0 * nPxl / M_PI) >= BIGBOX_MIN_R;
     // the staged / box-less (or y-pair) route of a half-complex phase, chosen
     // on the device from a sample of the patch records (route_pick)
     const bool routed = volLayout == LAYOUT_FT && !nD && !big;
@@ -1626,12 +1600,9 @@ static int local_phase_impl(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent
     if (evBeg) THX_HIP(hipEventRecord(evBeg, s));
     if (nD) {
         // all (t, d) columns of a workgroup in NCT tiles (one gather of the
-        // projection), up to 96 per workgroup; THX_CS_NCT caps it (A/B builds)
-#ifndef THX_CS_NCT
-#define THX_CS_NCT 6
-#endif
+        // projection), up to 96 per workgroup
         const int need = (int)thx::cdiv(nCol, TT);
-        const int nct = THX_CS_NCT == 1 ? 1 : need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 6;
+        const int nct = need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 6;
         auto pick = [&](auto c1, auto c2, auto c4, auto c6) {
             return nct == 1 ? c1 : nct == 2 ? c2 : nct == 4 ? c4 : c6;
         };
@@ -1861,6 +1832,6 @@ int local_phase_timed(const thx_local_sel* sel, hipEvent_t evBeg, hipEvent_t evE
 bool phase_routed(int volLayout, int pf, int nPxl, int nD)
 {
     return volLayout == LAYOUT_FT && !nD &&
-           !(pf * std::sqrt(2.0 * nPxl / M_PI) >= THX_BIGBOX_MIN_R);
+           !(pf * std::sqrt(2.0 * nPxl / M_PI) >= BIGBOX_MIN_R);
 }
 }  // namespace thx

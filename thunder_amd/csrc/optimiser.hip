@@ -65,12 +65,6 @@ int view_order(int nImg, int mLR, const double* quat, unsigned* keys, unsigned* 
                int* ord, void* tmp, size_t tmpBytes, hipStream_t s);
 }
 
-// the driver's y-pair copy as the compact ball of the pixel ring (local.hip
-// ypair_ball_elem); 0 for A/B builds
-#ifndef THX_YPAIR_BALL
-#define THX_YPAIR_BALL 1
-#endif
-
 // max iCol^2 + iRow^2 over the pixel set (one workgroup)
 __global__ void __launch_bounds__(256) k_max_r2(const int* __restrict__ iCol,
                                                 const int* __restrict__ iRow, int nPxl,
@@ -85,12 +79,10 @@ __global__ void __launch_bounds__(256) k_max_r2(const int* __restrict__ iCol,
     if (threadIdx.x == 0) *out = max(max(sm[0], sm[1]), max(sm[2], sm[3]));
 }
 
-// the 3D phases visit the images in view order (order.hip); 0 for A/B builds
-#ifndef THX_VIEW_ORDER
-#define THX_VIEW_ORDER 1
-#endif
-// THX_VIEW_ORDER=0 in the environment turns it off per call (the test that
-// the order leaves every image's result unchanged compares both)
+// the 3D phases visit the images in view order (order.hip) and gather from
+// the compact y-pair ball; THX_VIEW_ORDER=0 / THX_YPAIR_BALL=0 in the
+// environment turn either off per call (the tests that they leave every
+// image's result unchanged compare both)
 static bool env_on(const char* name)
 {
     const char* e = std::getenv(name);
@@ -1345,7 +1337,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.actIdx = k.take<int>(nImg);
     p.maxR2 = k.take<int>(1);
     p.nActIdx = k.take<int>(1);
-    const size_t nOrd = THX_VIEW_ORDER && !twoD ? (size_t)nImg : 0;
+    const size_t nOrd = !twoD ? (size_t)nImg : 0;
     p.ordKey = k.take<unsigned>(nOrd);
     p.ordKeyOut = k.take<unsigned>(nOrd);
     p.ordIdx = k.take<int>(nOrd);
@@ -1736,7 +1728,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     // copy when the ball is the volume
     int ypairR = 0;
     if (p.ypair) {
-        if (THX_YPAIR_BALL && env_on("THX_YPAIR_BALL")) {
+        if (env_on("THX_YPAIR_BALL")) {
             hipLaunchKernelGGL(k_max_r2, dim3(1), dim3(256), 0, s, iCol, iRow, nPxl, p.maxR2);
             THX_LAUNCH_CHECK();
             int r2 = 0;
@@ -1854,7 +1846,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     // 3D phases visit the images in view order (order.hip), through the
     // active list; results per image are unchanged
     const int* ord = nullptr;
-    if (THX_VIEW_ORDER && !twoD && nPh > 0 && view_order_on()) {
+    if (!twoD && nPh > 0 && view_order_on()) {
         THX_RET(thx::view_order(nImg, c.mLR, quat, p.ordKey, p.ordKeyOut, p.ordIdx, p.ord, p.ordTmp,
                                 p.ordTmpBytes, s));
         ord = p.ord;

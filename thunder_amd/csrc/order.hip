@@ -20,21 +20,8 @@ namespace {
 
 // index of (x, y) on the Hilbert curve through the 2^16 x 2^16 grid (its
 // runs of consecutive indices are connected, where a Morton order's jump)
-#ifndef THX_VIEW_HILBERT
-#define THX_VIEW_HILBERT 1
-#endif
-THX_DEV unsigned spread16(unsigned v)
-{
-    v &= 0xffffu;
-    v = (v | (v << 8)) & 0x00ff00ffu;
-    v = (v | (v << 4)) & 0x0f0f0f0fu;
-    v = (v | (v << 2)) & 0x33333333u;
-    v = (v | (v << 1)) & 0x55555555u;
-    return v;
-}
 THX_DEV unsigned curve16(unsigned x, unsigned y)
 {
-    if (!THX_VIEW_HILBERT) return spread16(x) | (spread16(y) << 1);
     constexpr unsigned N = 1u << 16;
     unsigned d = 0;
     for (unsigned s = N / 2; s > 0; s >>= 1) {
