@@ -917,7 +917,7 @@ struct PUWS {
     float* Aconst;  // [nImgPad]
     float* bias;    // [nImgPad][nRBias]
     uint16_t* Pf;   // [nRPad / 32][nKS][3][64][8]  P split, fragment order
-    float2* Tp;     // [nTPad][nPxlPad]  T, zero-padded
+    float2* Tp;     // [nCk][nTPad][KC]  T, chunk-major, zero-padded
     float* pTf;     // [nTPad]
     float2* wRp;    // [nImg][nR]
     float* pM;      // [nRT][nImgPad]
@@ -975,7 +975,8 @@ __global__ void __launch_bounds__(256) k_prep_pfrag(const float2* __restrict__ r
     }
 }
 
-// T rows zero-padded to nPxlPad (and to nTPad rows) for 16-B group loads
+// T chunk-major and zero-padded, Tc[ck][t][KC] (nTPad rows): one chunk is
+// one contiguous LDS-DMA image of nTPad x 128 B
 __global__ void __launch_bounds__(256) k_prep_tpad(const float2* __restrict__ traP,
                                                    const double* __restrict__ pT, int nT, int nPxl,
                                                    int nTPad, int nPxlPad, float2* __restrict__ Tp,
@@ -985,7 +986,8 @@ __global__ void __launch_bounds__(256) k_prep_tpad(const float2* __restrict__ tr
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
          q += (long)gridDim.x * blockDim.x) {
         const int i = (int)(q % nPxlPad), t = (int)(q / nPxlPad);
-        Tp[q] = (t < nT && i < nPxl) ? traP[(size_t)t * nPxl + i] : make_float2(0.f, 0.f);
+        Tp[((size_t)(i / KC) * nTPad + t) * KC + i % KC] =
+            (t < nT && i < nPxl) ? traP[(size_t)t * nPxl + i] : make_float2(0.f, 0.f);
         if (i == 0) pTf[t] = t < nT ? (float)pT[t] : 0.f;
     }
 }
@@ -997,10 +999,18 @@ struct PUSmem {
     static constexpr int BUF_B = 3 * PLANE_B;
     static constexpr int NG = NTP * (KC / 4);             // 4-pixel groups per chunk
     static constexpr int GPT = (NG + PU_THREADS - 1) / PU_THREADS;
+    // the chunk's T (NTP rows of KC complex) and a (KC complex) land by
+    // LDS-DMA one chunk ahead: two stages after the two U buffers
+    static constexpr int T_B = NTP * KC * 8;
+    static constexpr int TQ = T_B / 1024;                 // 1-KiB DMA wave instructions
+    static_assert(T_B % 1024 == 0, "whole DMA instructions per T chunk");
+    static constexpr int STG_B = T_B + 1024;              // + the a chunk (128 B used)
+    static constexpr int STG_OFF = 2 * BUF_B;
     // epilogue: A + B and |A| + |B| per rotation, per-wave maxima and column
     // sums, the guard lists
     static constexpr int EPI_B = (2 * PU_RT + PU_WAVES + PU_WAVES * NTP + PU_WAVES * GCAP) * 4;
-    static constexpr int TOTAL_B = 2 * BUF_B > EPI_B ? 2 * BUF_B : EPI_B;
+    static constexpr int MAIN_B = STG_OFF + 2 * STG_B;
+    static constexpr int TOTAL_B = MAIN_B > EPI_B ? MAIN_B : EPI_B;
 };
 
 template <int NF>
@@ -1034,36 +1044,45 @@ k_scan_pu(const uint16_t* __restrict__ Pf, const float2* __restrict__ Tp,
 #pragma unroll
         for (int j = 0; j < 16; j++) acc[f][j] = 0.f;
 
-    // U formation: group g = tid + k PU_THREADS -> translation row g >> 2,
-    // pixels 4 (g & 3) .. +3 of the chunk; every group of a thread has the
-    // same four pixels (PU_THREADS = 0 mod 4), so a is loaded once
-    const int q4 = tid & 3;
-    struct In {
-        f32x4v a01, a23;
-        f32x4v t01[S::GPT], t23[S::GPT];
-    };
-    auto load_in = [&](int ck, In& in) {
-        const float2* ap = Ac + ((size_t)ck * nImgPad + l) * APITCH + 4 * q4;
-        in.a01 = *reinterpret_cast<const f32x4v*>(ap);
-        in.a23 = *reinterpret_cast<const f32x4v*>(ap + 2);
+    // Chunk staging: T (nTPad rows x KC complex, chunk-major in global) and
+    // the image's a (KC complex) by LDS-DMA into stage ck & 1, issued one
+    // chunk ahead, so no register holds a long-latency load across a barrier
+    // (hipcc drains vmcnt before every __syncthreads()).
+    auto stage_at = [&](int ck) { return lds + S::STG_OFF + (ck & 1) * S::STG_B; };
+    auto issue_stage = [&](int ck) {
+        const char* gT = reinterpret_cast<const char*>(Tp + (size_t)ck * NTP * KC);
+        const char* gA = reinterpret_cast<const char*>(Ac + ((size_t)ck * nImgPad + l) * APITCH);
+        char* st = stage_at(ck);
 #pragma unroll
-        for (int k = 0; k < S::GPT; k++) {
-            const int g = tid + k * PU_THREADS;
-            const int t = g < S::NG ? g >> 2 : 0;
-            const float2* tp = Tp + (size_t)t * nPxlPad + ck * KC + 4 * q4;
-            in.t01[k] = *reinterpret_cast<const f32x4v*>(tp);
-            in.t23[k] = *reinterpret_cast<const f32x4v*>(tp + 2);
+        for (int u = 0; u < (S::TQ + 1 + PU_WAVES - 1) / PU_WAVES; u++) {
+            const int q = u * PU_WAVES + w;                 // wave-uniform instruction
+            if (q < S::TQ) dma16(gT + (size_t)(q * 64 + lane) * 16, st + q * 1024);
+            else if (q == S::TQ && lane < KC / 2) dma16(gA + lane * 16, st + S::T_B);
         }
     };
-    auto form_u = [&](const In& in, char* buf) {
-        const float ar[4] = {in.a01.x, in.a01.z, in.a23.x, in.a23.z};
-        const float ai[4] = {in.a01.y, in.a01.w, in.a23.y, in.a23.w};
+    // U formation from stage ck & 1 into U buffer ck & 1: group g = tid + k
+    // PU_THREADS -> translation row g >> 2, pixels 4 (g & 3) .. +3 of the
+    // chunk; every group of a thread has the same four pixels (PU_THREADS = 0
+    // mod 4), so a is read once
+    const int q4 = tid & 3;
+    auto form_u = [&](int ck) {
+        const char* st = stage_at(ck);
+        char* buf = lds + (ck & 1) * S::BUF_B;
+        const float2* sTc = reinterpret_cast<const float2*>(st);
+        const float2* sAc = reinterpret_cast<const float2*>(st + S::T_B) + 4 * q4;
+        const f32x4v a01 = *reinterpret_cast<const f32x4v*>(sAc);
+        const f32x4v a23 = *reinterpret_cast<const f32x4v*>(sAc + 2);
+        const float ar[4] = {a01.x, a01.z, a23.x, a23.z};
+        const float ai[4] = {a01.y, a01.w, a23.y, a23.w};
 #pragma unroll
         for (int k = 0; k < S::GPT; k++) {
             const int g = tid + k * PU_THREADS;
             if (S::NG % PU_THREADS != 0 && g >= S::NG) break;
-            const float tr[4] = {in.t01[k].x, in.t01[k].z, in.t23[k].x, in.t23[k].z};
-            const float ti[4] = {in.t01[k].y, in.t01[k].w, in.t23[k].y, in.t23[k].w};
+            const float2* tp = sTc + (g >> 2) * KC + 4 * q4;
+            const f32x4v t01 = *reinterpret_cast<const f32x4v*>(tp);
+            const f32x4v t23 = *reinterpret_cast<const f32x4v*>(tp + 2);
+            const float tr[4] = {t01.x, t01.z, t23.x, t23.z};
+            const float ti[4] = {t01.y, t01.w, t23.y, t23.w};
             HV hi, mid, lo;
 #pragma unroll
             for (int u = 0; u < 4; u++) {
@@ -1089,46 +1108,57 @@ k_scan_pu(const uint16_t* __restrict__ Pf, const float2* __restrict__ Tp,
             for (int pl = 0; pl < 3; pl++) p[s][pl] = Pw[((size_t)(2 * ck + s) * 3 + pl) * 64];
     };
 
-    In in;
+    // prologue: stage 0 landed, U 0 formed, stage 1 in flight
     HV pc[2][3], pn[2][3];
-    load_in(0, in);
+    issue_stage(0);
     load_p(0, pc);
-    form_u(in, lds);
-    if (nCk > 1) load_in(1, in);
+    wait_vm<0>();
     __syncthreads();
+    form_u(0);
+    if (nCk > 1) issue_stage(1);
+    __syncthreads();
+    // iteration ck: stage ck + 2 issued into the stage U ck consumed last
+    // iteration (it lands by this iteration's barrier, which drains vmcnt);
+    // MFMAs on U ck & 1; U ck + 1 formed from stage (ck + 1) & 1 (landed at
+    // the previous barrier) into the other buffer between the two k-steps
     for (int ck = 0; ck < nCk; ck++) {
         const bool more = ck + 1 < nCk;
+        if (ck + 2 < nCk) issue_stage(ck + 2);
         if (more) load_p(ck + 1, pn);
         const char* buf = lds + (ck & 1) * S::BUF_B;
+        // the U fragments of fragment f + 1 are read before f's six MFMAs
+        auto load_u = [&](int s, int f, HV (&u)[3]) {
+            const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
+#pragma unroll
+            for (int pl = 0; pl < 3; pl++)
+                u[pl] = *reinterpret_cast<const HV*>(reinterpret_cast<const uint16_t*>(buf + pl * S::PLANE_B) + row);
+        };
 #pragma unroll
         for (int s = 0; s < 2; s++) {
+            if (s == 1 && more) form_u(ck + 1);
+            HV u[2][3];
+            load_u(s, 0, u[0]);
 #pragma unroll
             for (int f = 0; f < NF; f++) {
-                const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
-                const HV uh = *reinterpret_cast<const HV*>(reinterpret_cast<const uint16_t*>(buf) + row);
-                const HV um = *reinterpret_cast<const HV*>(reinterpret_cast<const uint16_t*>(buf + S::PLANE_B) + row);
-                const HV ul = *reinterpret_cast<const HV*>(reinterpret_cast<const uint16_t*>(buf + 2 * S::PLANE_B) + row);
+                if (f + 1 < NF) load_u(s, f + 1, u[(f + 1) & 1]);
+                const HV(&uf)[3] = u[f & 1];
                 f32x16& c = acc[f];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][2], uh, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][1], um, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][0], ul, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][1], uh, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][0], um, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][0], uh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][2], uf[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][1], uf[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][0], uf[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][1], uf[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][0], uf[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][0], uf[0], c, 0, 0, 0);
             }
         }
-        if (more) {
-            // chunk ck + 1's U into the other buffer (its last readers finished
-            // at the previous barrier), then chunk ck + 2's inputs in flight
-            form_u(in, lds + ((ck + 1) & 1) * S::BUF_B);
-            if (ck + 2 < nCk) load_in(ck + 2, in);
+        __syncthreads();      // U ck + 1 written, stage ck + 2 landed
+        if (more)
 #pragma unroll
             for (int s = 0; s < 2; s++)
 #pragma unroll
                 for (int pl = 0; pl < 3; pl++) pc[s][pl] = pn[s][pl];
-        }
-        __syncthreads();
     }
+    __syncthreads();
 
     // ------------------------------------------------------------ epilogue
     float* sBias = reinterpret_cast<float*>(lds);       // [256]  A_l + B[l][r]
