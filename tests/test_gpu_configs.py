@@ -163,7 +163,7 @@ def test_c3_local_phase_bench_clouds_match_oracle(orc, c3, layout):
     """The half-complex layout, the pair-form y-pair kernel (the one every
     bench phase runs), the device route with a y-pair copy and the route on
     the driver's compact ball (thx_local_phase_routed_ball: the copy the bench
-    gathers from, R = ceil(pf r_max) + 2 = 53 at rU 24) at the bench's cloud
+    gathers from, R = ceil(pf r_max) + 2 = 49 at rU 24) at the bench's cloud
     widths (3, 10 and 30 degrees), 125 x 9: dvp 1e-5 against the oracle; the
     route takes the y-pair kernel for the wide clouds."""
     rng = np.random.default_rng(8)
@@ -172,7 +172,7 @@ def test_c3_local_phase_bench_clouds_match_oracle(orc, c3, layout):
     kw = {}
     if layout == "ball":
         R = ops.ypair_ball_radius(c3["px"])
-        assert R == 53
+        assert R == 49
         kw = dict(ball=ops.volume_ypair_ball(c3["vol"], R), ball_r=R)
     for spread in (3.0, 10.0, 30.0):
         quat = synth.clustered_quaternions(16, 125, spread, rng)

@@ -387,7 +387,7 @@ def test_host_adapters_match_device_ops(orc, stack):
     dat, ctf, sig = (np.ascontiguousarray(s[k]) for k in ("dat", "ctf", "sig"))
     assert L.thx_ExpectGlobal3D(P(rotP), P(traP), P(dat), P(ctf), P(sig), P(wC), P(wR), P(wT),
                                 P(pR), P(pT), P(base), 0, 1, nR, nT, n, nImg) == 0
-    ref = ops.global_scan(g_rot, g_tra, T(dat), T(ctf), T(sig), T(pR), T(pT), algo=1)
+    ref = ops.global_scan(g_rot, g_tra, T(dat), T(ctf), T(sig), T(pR), T(pT), algo=4)
     assert np.array_equal(wR, ref[1].cpu().numpy().reshape(-1))
     assert np.array_equal(base, ref[3].cpu().numpy())
     # InsertFT

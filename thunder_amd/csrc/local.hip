@@ -238,31 +238,28 @@ THX_DEV float2 ypair_pcell_part(const float4* __restrict__ yp, const PCell& c, i
     const float im = q0.y * w00 + q0.w * w01 + q1.y * w10 + q1.w * w11;
     return make_float2(re, conj ? -im : im);
 }
-// Pairs are lanes L and L ^ 16 (rows 2i and 2i + 1 of 16 lanes).
-// v_permlane16_swap(x, x) returns the even row's x to both rows in [0] and the
-// odd row's x in [1]: the pair's two values in one VALU op.
-THX_DEV void pair_both(unsigned x, unsigned& x0, unsigned& x1)
+// the pair's other lane's value (DPP quad_perm [1, 0, 3, 2])
+THX_DEV float pair_swap(float v)
 {
-    const auto sw = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-    x0 = sw[0];
-    x1 = sw[1];
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));
 }
-// sum of the pair's two values, the even row's first (the same on both lanes)
-THX_DEV float pair_sum(float v)
+// lane IT of each pair, to both lanes (quad_perm [IT, IT, 2 + IT, 2 + IT])
+template <int IT>
+THX_DEV int pair_bcast(int v)
 {
-    unsigned a, b;
-    pair_both(__float_as_uint(v), a, b);
-    return __uint_as_float(a) + __uint_as_float(b);
+    return __builtin_amdgcn_update_dpp(0, v, IT | (IT << 2) | ((2 + IT) << 4) | ((2 + IT) << 6), 0xf,
+                                       0xf, false);
 }
-// the cells of the pair's two samples (it 0 from the even-row lane) on both lanes
-THX_DEV void pair_cells(const PCell& mine, PCell (&c)[2])
+template <int IT>
+THX_DEV PCell pair_bcast_pcell(const PCell& c)
 {
-    unsigned a, b;
-    pair_both(mine.e0, a, b); c[0].e0 = a; c[1].e0 = b;
-    pair_both(mine.e1, a, b); c[0].e1 = a; c[1].e1 = b;
-    pair_both(__float_as_uint(mine.dx), a, b); c[0].dx = __uint_as_float(a); c[1].dx = __uint_as_float(b);
-    pair_both(__float_as_uint(mine.dy), a, b); c[0].dy = __uint_as_float(a); c[1].dy = __uint_as_float(b);
-    pair_both(__float_as_uint(mine.dz), a, b); c[0].dz = __uint_as_float(a); c[1].dz = __uint_as_float(b);
+    PCell o;
+    o.e0 = (unsigned)pair_bcast<IT>((int)c.e0);
+    o.e1 = (unsigned)pair_bcast<IT>((int)c.e1);
+    o.dx = __int_as_float(pair_bcast<IT>(__float_as_int(c.dx)));
+    o.dy = __int_as_float(pair_bcast<IT>(__float_as_int(c.dy)));
+    o.dz = __int_as_float(pair_bcast<IT>(__float_as_int(c.dz)));
+    return o;
 }
 // sum over the lanes of each quad (DPP quad permutations), every lane gets it
 THX_DEV float quad_sum(float v)
@@ -838,8 +835,9 @@ k_local_fused(const float2* __restrict__ vol,
     double m[6];
     {
         // COOP: lane 4 r + j works on rotation slot 16 wv + r (its quad's sample)
-        // PAIR: lane 16 k + r works on rotation slot 16 wv + r (as the MFMA A rows)
-        const int r = r0 + slot_rotation(sPerm, COOP ? wv * 16 + (lane >> 2) : rl, nRl);
+        // PAIR: lane 2 k + j works on rotation slot 16 wv + (k & 15)
+        const int r = r0 + slot_rotation(sPerm, COOP ? wv * 16 + (lane >> 2)
+                                                : PAIR ? wv * 16 + ((lane >> 1) & 15) : rl, nRl);
         double q[4], mm[9];
         for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
         quat_to_mat(q, mm);
@@ -1052,36 +1050,39 @@ k_local_fused(const float2* __restrict__ vol,
                 }
             }
         };
-        // PAIR step: lanes r + 32 G + 16 j (j = 0, 1: a pair 16 lanes apart, G =
-        // lane >> 5) evaluate rotation 16 wv + r at pixels 4s + 2G (it 0) and
-        // 4s + 2G + 1 (it 1); lane j rotates the it = j sample, v_permlane16_swap
-        // hands both cells to both lanes and sums the two half-cells, and each
-        // lane then already holds its MFMA A element: component j of it 0 (a1:
-        // pixels 4s, 4s + 2) and of it 1 (a2: 4s + 1, 4s + 3) at row r, k = 2G +
-        // j -- no ds_bpermute (round 4 paired adjacent lanes and regrouped
-        // through four ds_bpermute per step).
+        // PAIR step: pair (r, h) = lanes 2 (16 h + r) + j evaluates rotation 16 wv +
+        // r at pixels 4s + h (it 0) and 4s + h + 2 (it 1); lane j rotates the
+        // it = j sample and the pair shares the cells.  MFMA A rows: (pixels
+        // 4s, 4s + 2) from the h = 0 pairs, (4s + 1, 4s + 3) from the h = 1 pairs.
         constexpr unsigned yxs = 2u;   // x stride of the copy's elements (slices interleaved)
         auto pair_step = [&](int s) {
-            const int j = (lane >> 4) & 1, G = lane >> 5;
+            const int j = lane & 1, h = (lane >> 5) & 1;
             PCell mine;
             {
-                const double2 xy = make_double2(sXY[4 * s + 2 * G + j].x, sXY[4 * s + 2 * G + j].y);
+                const double2 xy = make_double2(sXY[4 * s + h + 2 * j].x, sXY[4 * s + h + 2 * j].y);
                 mine = pcell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                 (float)(m[2] * xy.x + m[5] * xy.y), vdim, ballR);
             }
-            PCell c[2];
-            pair_cells(mine, c);
             float2 P[2];
 #pragma unroll
             for (int it = 0; it < 2; it++) {
-                const float2 v = ypair_pcell_part(reinterpret_cast<const float4*>(vol), c[it], j, yxs);
-                P[it] = make_float2(pair_sum(v.x), pair_sum(v.y));
+                const PCell c = it == 0 ? pair_bcast_pcell<0>(mine) : pair_bcast_pcell<1>(mine);
+                const float2 v = ypair_pcell_part(reinterpret_cast<const float4*>(vol), c, j, yxs);
+                P[it] = make_float2(v.x + pair_swap(v.x), v.y + pair_swap(v.y));
             }
             if (!CS)
 #pragma unroll
                 for (int it = 0; it < 2; it++)
-                    bias += sBq[4 * s + 2 * G + it] * (P[it].x * P[it].x + P[it].y * P[it].y);
-            const float a1 = j ? P[0].y : P[0].x, a2 = j ? P[1].y : P[1].x;
+                    bias += sBq[4 * s + h + 2 * it] * (P[it].x * P[it].x + P[it].y * P[it].y);
+            // A[r][kk]: kk < 2 -> component kk of it 0, kk >= 2 -> component kk - 2 of it 1,
+            // from lane 2 r + (kk & 1) (a1: h = 0 pairs) or 32 + 2 r + (kk & 1) (a2: h = 1)
+            const float c0 = j ? P[0].y : P[0].x, c1 = j ? P[1].y : P[1].x;
+            const int sa = (2 * (lane & 15) + (kk & 1)) * 4;
+            const float t10 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(c0)));
+            const float t11 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(c1)));
+            const float t20 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa + 128, __float_as_int(c0)));
+            const float t21 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa + 128, __float_as_int(c1)));
+            const float a1 = kk < 2 ? t10 : t11, a2 = kk < 2 ? t20 : t21;
             const int q0 = 4 * s + (kk < 2 ? 0 : 2), q1 = q0 + 1;
 #pragma unroll
             for (int ct = 0; ct < NCT; ct++) {
@@ -1142,9 +1143,8 @@ k_local_fused(const float2* __restrict__ vol,
     // B_r: the four pixel slots of a rotation are lanes l, l + 16, l + 32, l + 48
     // (COOP: every lane of quad r holds rotation r's whole sum)
     if (PAIR) {
-        // rotation r's pixels are split over the pairs G = 0 (lane r) and G = 1
-        // (lane 32 + r); both lanes of a pair hold the same sums
-        bias = __shfl(bias, lane & 15, 64) + __shfl(bias, 32 + (lane & 15), 64);
+        // rotation r's pixels are split over the pairs (r, h = 0) and (r, h = 1)
+        bias = __shfl(bias, 2 * (lane & 15), 64) + __shfl(bias, 32 + 2 * (lane & 15), 64);
     } else if (COOP) {
         bias = __shfl(bias, 4 * (lane & 15), 64);
     } else {
