@@ -151,7 +151,7 @@ extern "C" size_t thx_global_scan_workspace(int nImg, int nR, int nT, int nPxl,
                                             int algo)
 {
     if (algo == 1) return thx::scan_mfma_workspace(nImg, nR, nT, nPxl);
-    if (algo == 2 || algo == 4 || algo == 5) return thx::scan_split_workspace(nImg, nR, nT, nPxl);
+    if (algo == 2 || algo == 4) return thx::scan_split_workspace(nImg, nR, nT, nPxl);
     thx::Carver c(nullptr, 0);
     c.take<float>((size_t)nImg * nR * nT);
     return c.off + 256;
@@ -173,7 +173,7 @@ extern "C" int thx_global_scan(const float* rotP, int nR, const float* traP,
                                size_t wsBytes, thx_stream_t stream)
 {
     SCAN_ARGS_CHECK();
-    THX_CHECK_ARG(algo >= 0 && algo <= 5 && algo != 3,
+    THX_CHECK_ARG(algo >= 0 && algo <= 4 && algo != 3,
                   "thx_global_scan: algo must be 0, 1, 2 or 4 (3, fp16x2, was retired in ABI 9)");
     THX_CHECK_ARG(wsBytes >= thx_global_scan_workspace(nImg, nR, nT, nPxl, algo),
                   "thx_global_scan: workspace too small");
@@ -210,7 +210,7 @@ extern "C" int thx_global_scan_dvp(const float* rotP, int nR, const float* traP,
                                    void* workspace, size_t wsBytes, thx_stream_t stream)
 {
     SCAN_ARGS_CHECK();
-    THX_CHECK_ARG(algo == 2 || algo == 4 || algo == 5, "thx_global_scan_dvp: algo must be 2 or 4");
+    THX_CHECK_ARG(algo == 2 || algo == 4, "thx_global_scan_dvp: algo must be 2 or 4");
     THX_CHECK_ARG(guard >= 0.f, "thx_global_scan_dvp: guard must be >= 0");
     THX_CHECK_ARG(dvp != nullptr, "thx_global_scan_dvp: dvp is NULL");
     THX_CHECK_ARG(wsBytes >= thx_global_scan_workspace(nImg, nR, nT, nPxl, algo),

@@ -35,6 +35,8 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 enum Mode { BF16X3 = 0, BF16X6 = 2 };
 typedef __bf16 H;
@@ -136,6 +138,18 @@ THX_DEV void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo)
     const float r = x - (float)hi;
     mid = (__bf16)r;
     lo = (__bf16)(r - (float)mid);
+}
+
+// split3 of a (re, im) pair, each level one packed round (v_cvt_pk_bf16_f32),
+// two unpacking bit operations and one packed subtraction: the same three
+// planes as split3 on each component, (re, im) interleaved per plane
+THX_DEV void split3x2(float x, float y, uint32_t& hi, uint32_t& mid, uint32_t& lo)
+{
+    auto pk = [](float a, float b) { return __builtin_bit_cast(uint32_t, bf16x2{(__bf16)a, (__bf16)b}); };
+    hi = pk(x, y);
+    const float rx = x - __uint_as_float(hi << 16), ry = y - __uint_as_float(hi & 0xffff0000u);
+    mid = pk(rx, ry);
+    lo = pk(rx - __uint_as_float(mid << 16), ry - __uint_as_float(mid & 0xffff0000u));
 }
 
 // Per image: A_l = sum s|d|^2
@@ -612,16 +626,18 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                     const f32x4v a23 = *reinterpret_cast<const f32x4v*>(rowA + 2);
                     const float ar[4] = {a01.x, a01.z, a23.x, a23.z};
                     const float ai[4] = {a01.y, a01.w, a23.y, a23.w};
+                    u32x4 hq, mq, lq;
 #pragma unroll
                     for (int qd = 0; qd < 4; qd++) {
                         const float wr = ar[qd] * pr[qd] + ai[qd] * pi[qd];
                         const float wi = ai[qd] * pr[qd] - ar[qd] * pi[qd];
-                        H x0, x1, x2;
-                        split3(wr, x0, x1, x2);
-                        wq[0][2 * qd] = x0; wq[1][2 * qd] = x1; wq[2][2 * qd] = x2;
-                        split3(wi, x0, x1, x2);
-                        wq[0][2 * qd + 1] = x0; wq[1][2 * qd + 1] = x1; wq[2][2 * qd + 1] = x2;
+                        uint32_t x0, x1, x2;
+                        split3x2(wr, wi, x0, x1, x2);
+                        hq[qd] = x0; mq[qd] = x1; lq[qd] = x2;
                     }
+                    wq[0] = __builtin_bit_cast(HV, hq);
+                    wq[1] = __builtin_bit_cast(HV, mq);
+                    wq[2] = __builtin_bit_cast(HV, lq);
                 };
                 auto mma6 = [&](f32x16& c, const HV (&wq)[3], const HV& th, const HV& tm, const HV& tl) {
                     c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq[2], th, c, 0, 0, 0);
@@ -874,442 +890,6 @@ int scan_split(const float* rotP, int nR, const float* traP, int nT, const float
     return THX_OK;
 }
 
-// ---------------------------------------------------------------- algo 4
-// bf16x6, rotation-major: per image l the cross term is the GEMM
-//   X[r][t] = sum_i Re(conj(P_ri) U_ti),   U_ti = a_li conj(T_ti),
-// A = the projections P (rotations x 2 nPxl, split ONCE per call into three
-// bf16 planes, stored in MFMA-fragment order so a wave's fragment is one
-// contiguous 1 KiB load), B = U (translations x 2 nPxl), formed per
-// (image, 16-pixel chunk) by the whole workgroup into LDS and split there.
-// U is shared by the 8 waves (256 rotations) of the workgroup, so its VALU
-// cost is spread over 8 x 60 MFMAs per chunk -- in the image-major k_scan_split
-// every wave formed its own w = a conj(P_r) for 30 MFMAs.  Each XCD walks its
-// own run of (rotation tile, image) pairs tile-major, so the tile's P planes
-// (256 x 880 x 12 B = 2.7 MB at C3) stay in that XCD's L2 while the images
-// stream through.
-constexpr int PU_WAVES = 8;
-constexpr int PU_RT = 32 * PU_WAVES;         // rotations per workgroup, one A fragment per wave
-constexpr int PU_THREADS = 64 * PU_WAVES;
-static_assert(KC == 16, "U chunks of 16 pixels: four groups of four pixels per translation row");
-
-struct PUDims {
-    int nImg, nR, nT, nPxl, nImgPad, nPxlPad, nTPad, nRPad, nRT, nCk, nKS, nRBias;
-};
-
-PUDims pu_dims(int nImg, int nR, int nT, int nPxl)
-{
-    PUDims d;
-    d.nImg = nImg; d.nR = nR; d.nT = nT; d.nPxl = nPxl;
-    d.nImgPad = pad_to(nImg, 64);
-    d.nPxlPad = pad_to(nPxl, KC);
-    d.nTPad = pad_to(nT, 32);
-    d.nRPad = pad_to(nR, PU_RT);
-    d.nRT = d.nRPad / PU_RT;
-    d.nCk = d.nPxlPad / KC;
-    d.nKS = d.nPxlPad / 8;
-    d.nRBias = d.nRPad;
-    return d;
-}
-
-struct PUWS {
-    float2* Ac;     // [nCk][nImgPad][APITCH]  a = -2 s c d (k_prep_img)
-    float* Bc;      // [nCk][nImgPad][KC]      b = s c^2
-    float* Aconst;  // [nImgPad]
-    float* bias;    // [nImgPad][nRBias]
-    uint16_t* Pf;   // [nRPad / 32][nKS][3][64][8]  P split, fragment order
-    float2* Tp;     // [nCk][nTPad][KC]  T, chunk-major, zero-padded
-    float* pTf;     // [nTPad]
-    float2* wRp;    // [nImg][nR]
-    float* pM;      // [nRT][nImgPad]
-    float* pWT;     // [nRT][nImgPad][nTPad]
-    size_t bytes;
-};
-
-PUWS pu_carve(void* base, const PUDims& d)
-{
-    thx::Carver c(base, ~size_t(0));
-    PUWS w;
-    w.Ac = c.take<float2>((size_t)d.nCk * d.nImgPad * APITCH);
-    w.Bc = c.take<float>((size_t)d.nPxlPad * d.nImgPad);
-    w.Aconst = c.take<float>(d.nImgPad);
-    w.bias = c.take<float>((size_t)d.nImgPad * d.nRBias);
-    w.Pf = c.take<uint16_t>((size_t)d.nRPad * d.nPxlPad * 2 * 3);
-    w.Tp = c.take<float2>((size_t)d.nTPad * d.nPxlPad);
-    w.pTf = c.take<float>(d.nTPad);
-    w.wRp = c.take<float2>((size_t)d.nImg * d.nR);
-    w.pM = c.take<float>((size_t)d.nRT * d.nImgPad);
-    w.pWT = c.take<float>((size_t)d.nRT * d.nImgPad * d.nTPad);
-    w.bytes = c.off + 256;
-    return w;
-}
-
-// P split into three bf16 planes in the A-fragment order of
-// v_mfma_f32_32x32x16_bf16: fragment (rf, ks), lane L holds A[row = L & 31]
-// [k = 8 (L >> 5) + j], k = 2 q + c -> pixel 8 ks + 4 (L >> 5) + q, component c
-__global__ void __launch_bounds__(256) k_prep_pfrag(const float2* __restrict__ rotP, int nR,
-                                                    int nPxl, int nRF, int nKS,
-                                                    uint16_t* __restrict__ Pf)
-{
-    const long n = (long)nRF * nKS * 64;
-    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
-         q += (long)gridDim.x * blockDim.x) {
-        const int L = (int)(q & 63);
-        const long fk = q >> 6;
-        const int ks = (int)(fk % nKS), rf = (int)(fk / nKS);
-        const int r = rf * 32 + (L & 31), px0 = ks * 8 + 4 * (L >> 5);
-        HV hi, mid, lo;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int i = px0 + u;
-            const float2 v = (r < nR && i < nPxl) ? rotP[(size_t)r * nPxl + i] : make_float2(0.f, 0.f);
-            H x0, x1, x2;
-            split3(v.x, x0, x1, x2);
-            hi[2 * u] = x0; mid[2 * u] = x1; lo[2 * u] = x2;
-            split3(v.y, x0, x1, x2);
-            hi[2 * u + 1] = x0; mid[2 * u + 1] = x1; lo[2 * u + 1] = x2;
-        }
-        HV* out = reinterpret_cast<HV*>(Pf + (fk * 3) * 512) + L;
-        out[0] = hi;
-        out[64] = mid;
-        out[128] = lo;
-    }
-}
-
-// T chunk-major and zero-padded, Tc[ck][t][KC] (nTPad rows): one chunk is
-// one contiguous LDS-DMA image of nTPad x 128 B
-__global__ void __launch_bounds__(256) k_prep_tpad(const float2* __restrict__ traP,
-                                                   const double* __restrict__ pT, int nT, int nPxl,
-                                                   int nTPad, int nPxlPad, float2* __restrict__ Tp,
-                                                   float* __restrict__ pTf)
-{
-    const long n = (long)nTPad * nPxlPad;
-    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
-         q += (long)gridDim.x * blockDim.x) {
-        const int i = (int)(q % nPxlPad), t = (int)(q / nPxlPad);
-        Tp[((size_t)(i / KC) * nTPad + t) * KC + i % KC] =
-            (t < nT && i < nPxl) ? traP[(size_t)t * nPxl + i] : make_float2(0.f, 0.f);
-        if (i == 0) pTf[t] = t < nT ? (float)pT[t] : 0.f;
-    }
-}
-
-template <int NF>
-struct PUSmem {
-    static constexpr int NTP = NF * 32;
-    static constexpr int PLANE_B = NTP * TROW * 2;       // one bf16 plane of U, rows of TROW
-    static constexpr int BUF_B = 3 * PLANE_B;
-    static constexpr int NG = NTP * (KC / 4);             // 4-pixel groups per chunk
-    static constexpr int GPT = (NG + PU_THREADS - 1) / PU_THREADS;
-    // the chunk's T (NTP rows of KC complex) and a (KC complex) land by
-    // LDS-DMA one chunk ahead: two stages after the two U buffers
-    static constexpr int T_B = NTP * KC * 8;
-    static constexpr int TQ = T_B / 1024;                 // 1-KiB DMA wave instructions
-    static_assert(T_B % 1024 == 0, "whole DMA instructions per T chunk");
-    static constexpr int STG_B = T_B + 1024;              // + the a chunk (128 B used)
-    static constexpr int STG_OFF = 2 * BUF_B;
-    // epilogue: A + B and |A| + |B| per rotation, per-wave maxima and column
-    // sums, the guard lists
-    static constexpr int EPI_B = (2 * PU_RT + PU_WAVES + PU_WAVES * NTP + PU_WAVES * GCAP) * 4;
-    static constexpr int MAIN_B = STG_OFF + 2 * STG_B;
-    static constexpr int TOTAL_B = MAIN_B > EPI_B ? MAIN_B : EPI_B;
-};
-
-template <int NF>
-__global__ void __launch_bounds__(PU_THREADS) __attribute__((amdgpu_waves_per_eu(2)))
-k_scan_pu(const uint16_t* __restrict__ Pf, const float2* __restrict__ Tp,
-          const float2* __restrict__ Ac, const float* __restrict__ Aconst,
-          const float* __restrict__ bias, const float* __restrict__ pTf,
-          const double* __restrict__ pR, int nImg, int nR, int nT, int nPxl, int nImgPad,
-          int nPxlPad, int nRBias, int nRT, float2* __restrict__ wRp, float* __restrict__ pM,
-          float* __restrict__ pWT, Guard gd)
-{
-    using S = PUSmem<NF>;
-    constexpr int NTP = S::NTP;
-    extern __shared__ __attribute__((aligned(16))) char lds[];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int n = lane & 31, h = lane >> 5;
-    // XCD b % 8 walks its own contiguous run of (rotation tile, image) pairs,
-    // tile-major: one tile's P planes stay in that XCD's L2
-    const int nB = nImg * nRT;
-    const int per = (nB + 7) / 8;
-    const int pq = (blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (pq >= nB) return;
-    const int rt = pq / nImg, l = pq % nImg;
-    const int r0 = rt * PU_RT + w * 32;                  // this wave's first rotation
-    const int nKS = nPxlPad / 8, nCk = nPxlPad / KC;
-    const HV* Pw = reinterpret_cast<const HV*>(Pf) + (size_t)(rt * PU_WAVES + w) * nKS * 3 * 64 + lane;
-
-    f32x16 acc[NF];
-#pragma unroll
-    for (int f = 0; f < NF; f++)
-#pragma unroll
-        for (int j = 0; j < 16; j++) acc[f][j] = 0.f;
-
-    // Chunk staging: T (nTPad rows x KC complex, chunk-major in global) and
-    // the image's a (KC complex) by LDS-DMA into stage ck & 1, issued one
-    // chunk ahead, so no register holds a long-latency load across a barrier
-    // (hipcc drains vmcnt before every __syncthreads()).
-    auto stage_at = [&](int ck) { return lds + S::STG_OFF + (ck & 1) * S::STG_B; };
-    auto issue_stage = [&](int ck) {
-        const char* gT = reinterpret_cast<const char*>(Tp + (size_t)ck * NTP * KC);
-        const char* gA = reinterpret_cast<const char*>(Ac + ((size_t)ck * nImgPad + l) * APITCH);
-        char* st = stage_at(ck);
-#pragma unroll
-        for (int u = 0; u < (S::TQ + 1 + PU_WAVES - 1) / PU_WAVES; u++) {
-            const int q = u * PU_WAVES + w;                 // wave-uniform instruction
-            if (q < S::TQ) dma16(gT + (size_t)(q * 64 + lane) * 16, st + q * 1024);
-            else if (q == S::TQ && lane < KC / 2) dma16(gA + lane * 16, st + S::T_B);
-        }
-    };
-    // U formation from stage ck & 1 into U buffer ck & 1: group g = tid + k
-    // PU_THREADS -> translation row g >> 2, pixels 4 (g & 3) .. +3 of the
-    // chunk; every group of a thread has the same four pixels (PU_THREADS = 0
-    // mod 4), so a is read once
-    const int q4 = tid & 3;
-    auto form_u = [&](int ck) {
-        const char* st = stage_at(ck);
-        char* buf = lds + (ck & 1) * S::BUF_B;
-        const float2* sTc = reinterpret_cast<const float2*>(st);
-        const float2* sAc = reinterpret_cast<const float2*>(st + S::T_B) + 4 * q4;
-        const f32x4v a01 = *reinterpret_cast<const f32x4v*>(sAc);
-        const f32x4v a23 = *reinterpret_cast<const f32x4v*>(sAc + 2);
-        const float ar[4] = {a01.x, a01.z, a23.x, a23.z};
-        const float ai[4] = {a01.y, a01.w, a23.y, a23.w};
-#pragma unroll
-        for (int k = 0; k < S::GPT; k++) {
-            const int g = tid + k * PU_THREADS;
-            if (S::NG % PU_THREADS != 0 && g >= S::NG) break;
-            const float2* tp = sTc + (g >> 2) * KC + 4 * q4;
-            const f32x4v t01 = *reinterpret_cast<const f32x4v*>(tp);
-            const f32x4v t23 = *reinterpret_cast<const f32x4v*>(tp + 2);
-            const float tr[4] = {t01.x, t01.z, t23.x, t23.z};
-            const float ti[4] = {t01.y, t01.w, t23.y, t23.w};
-            HV hi, mid, lo;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const float ur = ar[u] * tr[u] + ai[u] * ti[u];      // a conj(T)
-                const float ui = ai[u] * tr[u] - ar[u] * ti[u];
-                H x0, x1, x2;
-                split3(ur, x0, x1, x2);
-                hi[2 * u] = x0; mid[2 * u] = x1; lo[2 * u] = x2;
-                split3(ui, x0, x1, x2);
-                hi[2 * u + 1] = x0; mid[2 * u + 1] = x1; lo[2 * u + 1] = x2;
-            }
-            const int off = (g >> 2) * TROW + 8 * q4;        // bf16 elements in a plane
-            *reinterpret_cast<HV*>(reinterpret_cast<uint16_t*>(buf) + off) = hi;
-            *reinterpret_cast<HV*>(reinterpret_cast<uint16_t*>(buf + S::PLANE_B) + off) = mid;
-            *reinterpret_cast<HV*>(reinterpret_cast<uint16_t*>(buf + 2 * S::PLANE_B) + off) = lo;
-        }
-    };
-    // P fragments of the two k-steps of a chunk, three planes each
-    auto load_p = [&](int ck, HV (&p)[2][3]) {
-#pragma unroll
-        for (int s = 0; s < 2; s++)
-#pragma unroll
-            for (int pl = 0; pl < 3; pl++) p[s][pl] = Pw[((size_t)(2 * ck + s) * 3 + pl) * 64];
-    };
-
-    // prologue: stage 0 landed, U 0 formed, stage 1 in flight
-    HV pc[2][3], pn[2][3];
-    issue_stage(0);
-    load_p(0, pc);
-    wait_vm<0>();
-    __syncthreads();
-    form_u(0);
-    if (nCk > 1) issue_stage(1);
-    __syncthreads();
-    // iteration ck: stage ck + 2 issued into the stage U ck consumed last
-    // iteration (it lands by this iteration's barrier, which drains vmcnt);
-    // MFMAs on U ck & 1; U ck + 1 formed from stage (ck + 1) & 1 (landed at
-    // the previous barrier) into the other buffer between the two k-steps
-    for (int ck = 0; ck < nCk; ck++) {
-        const bool more = ck + 1 < nCk;
-        if (ck + 2 < nCk) issue_stage(ck + 2);
-        if (more) load_p(ck + 1, pn);
-        const char* buf = lds + (ck & 1) * S::BUF_B;
-        // the U fragments of fragment f + 1 are read before f's six MFMAs
-        auto load_u = [&](int s, int f, HV (&u)[3]) {
-            const int row = (f * 32 + n) * TROW + 16 * s + 8 * h;
-#pragma unroll
-            for (int pl = 0; pl < 3; pl++)
-                u[pl] = *reinterpret_cast<const HV*>(reinterpret_cast<const uint16_t*>(buf + pl * S::PLANE_B) + row);
-        };
-#pragma unroll
-        for (int s = 0; s < 2; s++) {
-            if (s == 1 && more) form_u(ck + 1);
-            HV u[2][3];
-            load_u(s, 0, u[0]);
-#pragma unroll
-            for (int f = 0; f < NF; f++) {
-                if (f + 1 < NF) load_u(s, f + 1, u[(f + 1) & 1]);
-                const HV(&uf)[3] = u[f & 1];
-                f32x16& c = acc[f];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][2], uf[0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][1], uf[1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][0], uf[2], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][1], uf[0], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][0], uf[1], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pc[s][0], uf[0], c, 0, 0, 0);
-            }
-        }
-        __syncthreads();      // U ck + 1 written, stage ck + 2 landed
-        if (more)
-#pragma unroll
-            for (int s = 0; s < 2; s++)
-#pragma unroll
-                for (int pl = 0; pl < 3; pl++) pc[s][pl] = pn[s][pl];
-    }
-    __syncthreads();
-
-    // ------------------------------------------------------------ epilogue
-    float* sBias = reinterpret_cast<float*>(lds);       // [256]  A_l + B[l][r]
-    float* sAB = sBias + PU_RT;                          // [256]  |A_l| + |B[l][r]|
-    float* sMaxW = sAB + PU_RT;                          // [8]
-    float* sCol = sMaxW + PU_WAVES;                      // [8][NTP]
-    float* sGVal = sCol + PU_WAVES * NTP;                // [8][GCAP]
-    if (tid < PU_RT) {
-        const int r = rt * PU_RT + tid;
-        const float A = Aconst[l], B = r < nR ? bias[(size_t)l * nRBias + r] : 0.f;
-        sBias[tid] = A + B;
-        sAB[tid] = fabsf(A) + fabsf(B);
-    }
-    __syncthreads();
-    f32x16 (&acc1)[1][NF] = *reinterpret_cast<f32x16 (*)[1][NF]>(&acc);
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const float b = sBias[w * 32 + (j & 3) + 8 * (j >> 2) + 4 * h];
-#pragma unroll
-        for (int f = 0; f < NF; f++) acc[f][j] += b;
-    }
-    if (gd.kmax > 0.f)
-        guard_tile<1, NF>(acc1, gd, sAB + w * 32, sBias + w * 32, sGVal + w * GCAP,
-                          [&](int row) { return make_int2(r0 + row < nR ? l : -1, r0 + row); }, nT, nPxl);
-    float pTv[NF];
-#pragma unroll
-    for (int f = 0; f < NF; f++) pTv[f] = pTf[f * 32 + n];
-    float mxj[16];
-    float wmax = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const int r = r0 + (j & 3) + 8 * (j >> 2) + 4 * h;
-        const bool rOk = r < nR;
-        if (gd.dvpOut && rOk) {
-#pragma unroll
-            for (int f = 0; f < NF; f++)
-                if (f * 32 + n < nT) gd.dvpOut[((size_t)l * nR + r) * nT + f * 32 + n] = acc[f][j];
-        }
-        float mx = -INFINITY;
-#pragma unroll
-        for (int f = 0; f < NF; f++)
-            if (f * 32 + n < nT) mx = fmaxf(mx, acc[f][j]);
-        mx = half_reduce<true>(mx);
-        if (!rOk) mx = -INFINITY;
-        float sR = 0.f;
-#pragma unroll
-        for (int f = 0; f < NF; f++) {
-            const float e = (f * 32 + n < nT && rOk) ? __expf(acc[f][j] - mx) : 0.f;
-            acc[f][j] = e;
-            sR += e * pTv[f];
-        }
-        sR = half_reduce<false>(sR);
-        if (n == 0 && rOk) wRp[(size_t)l * nR + r] = make_float2(mx, sR);
-        mxj[j] = mx;
-        wmax = fmaxf(wmax, mx);
-    }
-    wmax = fmaxf(wmax, __shfl_xor(wmax, 32, 64));
-    if (lane == 0) sMaxW[w] = wmax;
-    __syncthreads();
-    float M = sMaxW[0];
-#pragma unroll
-    for (int k = 1; k < PU_WAVES; k++) M = fmaxf(M, sMaxW[k]);
-    if (tid == 0) pM[(size_t)rt * nImgPad + l] = M;
-    // the t-marginal partial of the tile: each lane sums its rows (the
-    // rotation's scale exp(max_r - M) pR[r]), the two lane halves combine, the
-    // 8 waves add in wave order (deterministic, no atomics)
-    float col[NF];
-#pragma unroll
-    for (int f = 0; f < NF; f++) col[f] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        const int r = r0 + (j & 3) + 8 * (j >> 2) + 4 * h;
-        const float sc = r < nR ? __expf(mxj[j] - M) * (float)pR[r] : 0.f;
-#pragma unroll
-        for (int f = 0; f < NF; f++) col[f] += acc[f][j] * sc;
-    }
-#pragma unroll
-    for (int f = 0; f < NF; f++) {
-        const float v = col[f] + __shfl_xor(col[f], 32, 64);
-        if (h == 0) sCol[w * NTP + f * 32 + n] = v;
-    }
-    __syncthreads();
-    for (int t = tid; t < NTP; t += PU_THREADS) {
-        float sum = 0.f;
-#pragma unroll
-        for (int k = 0; k < PU_WAVES; k++) sum += sCol[k * NTP + t];
-        pWT[((size_t)rt * nImgPad + l) * NTP + t] = sum;
-    }
-}
-
-template <int NF>
-int pu_launch_main(const PUWS& ws, const PUDims& d, const double* pR, const Guard& gd, hipStream_t s)
-{
-    dim3 grid((unsigned)(8 * thx::cdiv((long)d.nImg * d.nRT, 8)));
-    constexpr int lds = PUSmem<NF>::TOTAL_B;
-    static_assert(lds <= 160 * 1024, "U buffers exceed the LDS");
-    static std::atomic<unsigned> ldsSet{0};
-    const int st = thx::set_max_lds(reinterpret_cast<const void*>(k_scan_pu<NF>), lds, ldsSet);
-    if (st != THX_OK) return st;
-    hipLaunchKernelGGL(k_scan_pu<NF>, grid, dim3(PU_THREADS), lds, s, ws.Pf, ws.Tp, ws.Ac, ws.Aconst,
-                       ws.bias, ws.pTf, pR, d.nImg, d.nR, d.nT, d.nPxl, d.nImgPad, d.nPxlPad,
-                       d.nRBias, d.nRT, ws.wRp, ws.pM, ws.pWT, gd);
-    THX_LAUNCH_CHECK();
-    return THX_OK;
-}
-
-int scan_pu(const float* rotP, int nR, const float* traP, int nT, const float* dat,
-            const float* ctf, const float* sigRcp, int nImg, int nPxl, const double* pR,
-            const double* pT, int kIdx, int nK, float* wC, float* wR, float* wT, float* baseL,
-            float guard, float* dvpOut, void* workspace, size_t wsBytes, hipStream_t s)
-{
-    const PUDims d = pu_dims(nImg, nR, nT, nPxl);
-    THX_CHECK_ARG(d.nTPad <= 160, "thx_global_scan: nT = %d > 160 in the bf16x6 kernel", nT);
-    THX_CHECK_ARG((long)nImg * d.nRT < (1L << 31) && d.nRBias / 64 <= 65535,
-                  "thx_global_scan: grid too large");
-    const PUWS ws = pu_carve(workspace, d);
-    THX_CHECK_ARG(ws.bytes <= wsBytes, "thx_global_scan: workspace too small");
-    const float2* dat2 = reinterpret_cast<const float2*>(dat);
-    const float2* rot2 = reinterpret_cast<const float2*>(rotP);
-    hipLaunchKernelGGL(k_prep_aconst, dim3(thx::cdiv(d.nImgPad, 4)), dim3(256), 0, s, dat2, sigRcp,
-                       nImg, nPxl, d.nImgPad, ws.Aconst);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_img, dim3(2048), dim3(256), 0, s, dat2, ctf, sigRcp, nImg,
-                       nPxl, d.nImgPad, d.nPxlPad, ws.Ac, ws.Bc);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_pfrag, dim3(2048), dim3(256), 0, s, rot2, nR, nPxl, d.nRPad / 32,
-                       d.nKS, ws.Pf);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_prep_tpad, dim3(512), dim3(256), 0, s, reinterpret_cast<const float2*>(traP),
-                       pT, nT, nPxl, d.nTPad, d.nPxlPad, ws.Tp, ws.pTf);
-    THX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_scan_bias, dim3(d.nImgPad / 64, d.nRBias / 64), dim3(256), 0, s, ws.Bc,
-                       rot2, nR, nPxl, d.nImgPad, d.nCk, d.nRBias, ws.bias);
-    THX_LAUNCH_CHECK();
-    const Guard gd{dat2, ctf, sigRcp, reinterpret_cast<const float2*>(traP), rot2, guard, dvpOut};
-    int st;
-    switch (d.nTPad / 32) {
-        case 1: st = pu_launch_main<1>(ws, d, pR, gd, s); break;
-        case 2: st = pu_launch_main<2>(ws, d, pR, gd, s); break;
-        case 3: st = pu_launch_main<3>(ws, d, pR, gd, s); break;
-        case 4: st = pu_launch_main<4>(ws, d, pR, gd, s); break;
-        default: st = pu_launch_main<5>(ws, d, pR, gd, s); break;
-    }
-    if (st != THX_OK) return st;
-    hipLaunchKernelGGL(k_scan_combine_bf, dim3(nImg), dim3(256), sizeof(float) * d.nRT, s,
-                       ws.wRp, ws.pM, ws.pWT, pR, nR, nT, d.nTPad, d.nRT, d.nImgPad, kIdx, nK,
-                       wC, wR, wT, baseL);
-    THX_LAUNCH_CHECK();
-    return THX_OK;
-}
-
 }  // namespace
 
 namespace thx {
@@ -1325,7 +905,7 @@ size_t scan_split_workspace(int nImg, int nR, int nT, int nPxl)
 {
     const Dims d = dims(nImg, nR, nT, nPxl);
     if (d.nTPad > 160) return scan_mfma_workspace(nImg, nR, nT, nPxl);
-    return std::max(carve(nullptr, d).bytes, pu_carve(nullptr, pu_dims(nImg, nR, nT, nPxl)).bytes);
+    return carve(nullptr, d).bytes;
 }
 
 float scan_guard_default() { return SCAN_GUARD; }
@@ -1348,9 +928,6 @@ int scan_split_algo(int algo, const float* rotP, int nR, const float* traP, int 
     if (algo == 2)
         return scan_split<BF16X3>(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx,
                                   nK, wC, wR, wT, baseL, guard, dvpOut, workspace, wsBytes, s);
-    if (algo == 4)
-        return scan_pu(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx, nK, wC, wR,
-                       wT, baseL, guard, dvpOut, workspace, wsBytes, s);
     return scan_split<BF16X6>(rotP, nR, traP, nT, dat, ctf, sigRcp, nImg, nPxl, pR, pT, kIdx, nK,
                               wC, wR, wT, baseL, guard, dvpOut, workspace, wsBytes, s);
 }

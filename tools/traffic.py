@@ -6,7 +6,7 @@ on `bench.py --steps 1 --warmup 0`).
 A "launch" is the whole launch sequence the bench times with HIP events
 (local_bench: the single k_local_fused<0> dispatch of a bench phase):
   scan  : k_prep_aconst .. k_scan_combine_bf of one thx_global_scan call whose
-          k_scan_pu grid is the 4096-image grid (bench.scan_roofline);
+          k_scan_split grid is the 4096-image grid (bench.scan_roofline);
   local : one thx_local_phase call of bench.local_roofline (full resolution,
           512 images, grid 512 x 512): per cloud (1.5, 2, 3 degrees, uniform)
           four launches (timed_events: one warm-up + 3) in each layout, in the
@@ -171,14 +171,14 @@ def main():
     tag, out = sys.argv[1], sys.argv[2]
     rd = dispatches(os.path.join(tag, "pmc1", "run_counter_collection.csv"), "FETCH_SIZE")
     wr = dispatches(os.path.join(tag, "pmc2", "run_counter_collection.csv"), "WRITE_SIZE")
-    # the bf16x6 scan kernel's grid at 4096 images, nR 2000 (8 tiles of 256
-    # rotations x 4096 images, 512 threads each)
-    scan_grid = 4096 * 8 * 512
+    # the bf16x6 scan kernel's grid at 4096 images, nR 2000 (64-image tiles x
+    # 250 blocks of 8 rotations, 512 threads each)
+    scan_grid = (4096 // 64) * 250 * 512
     res = {
         "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py ({tag}), "
                   "FETCH_SIZE x2 on gfx950",
         "scan_4096": summarise(rd, wr, "k_prep_aconst", "k_scan_combine_bf",
-                               lambda g: any("k_scan_pu" in n and gr == scan_grid
+                               lambda g: any("k_scan_split" in n and gr == scan_grid
                                              for n, gr, _ in g), 2, "streaming (128-B requests)"),
         # bench.local_roofline, every cloud and layout (not routed: one
         # dispatch per launch)
