@@ -152,7 +152,7 @@ THX_DEV float2 cell_piece(const float4* __restrict__ cells, int vdim, const Cell
 template <int P>
 THX_DEV int quad_bcast(int v)
 {
-    return __builtin_amdgcn_update_dpp(0, v, P | (P << 2) | (P << 4) | (P << 6), 0xf, 0xf, false);
+    return __builtin_amdgcn_mov_dpp(v, P | (P << 2) | (P << 4) | (P << 6), 0xf, 0xf, true);
 }
 template <int P>
 THX_DEV Cell quad_bcast_cell(const Cell& c)
@@ -224,31 +224,41 @@ THX_DEV PCell pcell_of(float x, float y, float z, int vdim, int ballR = 0)
     return c;
 }
 // lane j of the pair: element x0 + j of slices z0 and z0 + 1
-// (xs: the element stride of x -- 2 in the z-interleaved ball, else 1)
-THX_DEV float2 ypair_pcell_part(const float4* __restrict__ yp, const PCell& c, int j, unsigned xs)
+// (xs: the element stride of x -- 2 in the z-interleaved ball, else 1);
+// the loads apart from the interpolation, so a step issues all its loads
+// before the first one is waited on
+struct PTaps { float4 q0, q1; };
+THX_DEV PTaps ypair_pcell_load(const float4* __restrict__ yp, const PCell& c, int j, unsigned xs)
 {
     const unsigned dj = xs * (unsigned)j;   // element x0 + j
-    const float4 q0 = yp[c.e0 + dj], q1 = yp[c.e1 + dj];
+    return PTaps{yp[c.e0 + dj], yp[c.e1 + dj]};
+}
+THX_DEV float2 ypair_pcell_lerp(const PTaps& t, const PCell& c, int j)
+{
+    const float4 q0 = t.q0, q1 = t.q1;
     const bool conj = (__float_as_uint(c.dx) >> 31) != 0;
     const float dx = fabsf(c.dx);
     const float wx = j ? dx : 1.f - dx;
     const float wa = wx * (1.f - c.dz), wb = wx * c.dz;
     const float w00 = wa * (1.f - c.dy), w01 = wa * c.dy, w10 = wb * (1.f - c.dy), w11 = wb * c.dy;
-    const float re = q0.x * w00 + q0.z * w01 + q1.x * w10 + q1.z * w11;
-    const float im = q0.y * w00 + q0.w * w01 + q1.y * w10 + q1.w * w11;
-    return make_float2(re, conj ? -im : im);
+    // (re, im) pairs of the four taps as packed operands (v_pk_fma_f32 with
+    // the weight broadcast), in the order of the scalar sum
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v r = f2v{q0.x, q0.y} * w00 + f2v{q0.z, q0.w} * w01 + f2v{q1.x, q1.y} * w10 +
+                  f2v{q1.z, q1.w} * w11;
+    return make_float2(r.x, conj ? -r.y : r.y);
 }
 // the pair's other lane's value (DPP quad_perm [1, 0, 3, 2])
 THX_DEV float pair_swap(float v)
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, true));
 }
 // lane IT of each pair, to both lanes (quad_perm [IT, IT, 2 + IT, 2 + IT])
 template <int IT>
 THX_DEV int pair_bcast(int v)
 {
-    return __builtin_amdgcn_update_dpp(0, v, IT | (IT << 2) | ((2 + IT) << 4) | ((2 + IT) << 6), 0xf,
-                                       0xf, false);
+    return __builtin_amdgcn_mov_dpp(v, IT | (IT << 2) | ((2 + IT) << 4) | ((2 + IT) << 6), 0xf, 0xf,
+                                    true);
 }
 template <int IT>
 THX_DEV PCell pair_bcast_pcell(const PCell& c)
@@ -264,8 +274,8 @@ THX_DEV PCell pair_bcast_pcell(const PCell& c)
 // sum over the lanes of each quad (DPP quad permutations), every lane gets it
 THX_DEV float quad_sum(float v)
 {
-    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));
-    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false));
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xb1, 0xf, 0xf, true));
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4e, 0xf, 0xf, true));
     return v;
 }
 
@@ -273,7 +283,7 @@ THX_DEV float quad_sum(float v)
 // cell-expanded copy (1, quad-cooperative gathers, no LDS boxes) and its
 // y-pair copy (2, thx_volume_ypair: element (x, y, z) holds v(x, y, z) and
 // v(x, y + 1, z), so a trilinear cell is two 32-B pieces, gathered by lane
-// pairs -- ypair_pcell_part).
+// pairs -- ypair_pcell_load / ypair_pcell_lerp).
 enum { LAYOUT_FT = 0, LAYOUT_CELLS = 1, LAYOUT_YPAIR2 = 2 };
 // layouts gathered quad-cooperatively (no LDS boxes, no patch records)
 constexpr bool coop_layout(int l) { return l == LAYOUT_CELLS; }
@@ -1063,11 +1073,15 @@ k_local_fused(const float2* __restrict__ vol,
                 mine = pcell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                 (float)(m[2] * xy.x + m[5] * xy.y), vdim, ballR);
             }
+            const PCell pc0 = pair_bcast_pcell<0>(mine), pc1 = pair_bcast_pcell<1>(mine);
+            const float4* yp = reinterpret_cast<const float4*>(vol);
+            const PTaps t0 = ypair_pcell_load(yp, pc0, j, yxs), t1 = ypair_pcell_load(yp, pc1, j, yxs);
+            // all four loads in flight before the first interpolation waits
+            __builtin_amdgcn_sched_barrier(0);
             float2 P[2];
 #pragma unroll
             for (int it = 0; it < 2; it++) {
-                const PCell c = it == 0 ? pair_bcast_pcell<0>(mine) : pair_bcast_pcell<1>(mine);
-                const float2 v = ypair_pcell_part(reinterpret_cast<const float4*>(vol), c, j, yxs);
+                const float2 v = ypair_pcell_lerp(it == 0 ? t0 : t1, it == 0 ? pc0 : pc1, j);
                 P[it] = make_float2(v.x + pair_swap(v.x), v.y + pair_swap(v.y));
             }
             if (!CS)

@@ -334,9 +334,6 @@ __global__ void __launch_bounds__(CF_THREADS) k_col_fft(float2* __restrict__ a, 
 // The kx = 0 and kx = N / 2 planes of T are replaced by their Hermitian
 // average first: a C2R reads only that average of those planes (FFTW,
 // hipFFT and numpy's irfftn alike), so the balanced W is unchanged.
-#ifndef EVEN_BALANCE
-#define EVEN_BALANCE 1             // 0: the hipFFT loop everywhere (A/B builds)
-#endif
 constexpr int EV_CT = 16;          // columns per tile of the column passes
 constexpr int EV_WAVES = 4;
 
@@ -938,7 +935,7 @@ extern "C" int thx_reconstruct(const float* F, float* T, int N, int pf, float a,
         THX_LAUNCH_CHECK();
         // the even half-grid loop where its transforms exist, else two hipFFT
         // 3D transforms per iteration
-        const bool even = EVEN_BALANCE && even_ok(vdim) && pl.tw;
+        const bool even = even_ok(vdim) && pl.tw;
         if (even) {
             hipLaunchKernelGGL(k_sym_planes, g, b, 0, s, T, vdim);
             THX_LAUNCH_CHECK();

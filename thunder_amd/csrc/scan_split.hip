@@ -52,16 +52,10 @@ template <int MODE> constexpr int nplane() { return MODE == BF16X6 ? 3 : 2; }
 constexpr float SCAN_GUARD = 4.f;
 constexpr int GCAP = 32;   // guard list entries per wave and round
 
-#ifndef SCAN_KC
-#define SCAN_KC 16
-#endif
-constexpr int KC = SCAN_KC;       // pixels per LDS stage (KC / 8 MFMA k-steps)
+constexpr int KC = 16;            // pixels per LDS stage (KC / 8 MFMA k-steps)
 static_assert(KC % 16 == 0, "whole float4 rows per thread in the stagers");
 constexpr int IMG_TILE = 64;
-#ifndef SCAN_RT
-#define SCAN_RT 8
-#endif
-constexpr int ROT_TILE = SCAN_RT;     // rotations per workgroup, one per wave
+constexpr int ROT_TILE = 8;       // rotations per workgroup, one per wave
 constexpr int THREADS = 64 * ROT_TILE;
 constexpr int NWAVE = ROT_TILE;
 constexpr int TROW = KC * 2 + 8;  // 16-bit elements per translation row of the T tile (80 B)
@@ -321,9 +315,7 @@ THX_DEV float half_reduce(float v)
 
 // LDS stages of the chunk pipeline: chunk ck + STAGES - 1 is copied while
 // chunk ck is multiplied, so each copy has STAGES - 1 chunks to land
-#ifndef SCAN_STAGES
-#define SCAN_STAGES 2
-#endif
+constexpr int SCAN_STAGES = 2;
 
 template <int N>
 THX_DEV void wait_vm()
