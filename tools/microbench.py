@@ -55,6 +55,7 @@ def main():
     p.add_argument("--cells", type=int, default=0)
     p.add_argument("--ypair", type=int, default=0, help="local: gather from ops.volume_ypair(vol)")
     p.add_argument("--algo", type=int, default=4)
+    p.add_argument("--guard", type=float, default=None, help="scan: cancellation guard (None: the default 4, 0: off)")
     p.add_argument("--nr", type=int, default=2000)
     p.add_argument("--mreco", type=int, default=100)
     p.add_argument("--reps", type=int, default=5)
@@ -121,7 +122,7 @@ def main():
         traP = ops.trans_table(torch.as_tensor(t, device=dev), px)
         pRd, pTd = torch.as_tensor(pR, device=dev), torch.as_tensor(pT, device=dev)
         sec = timed_events(lambda: ops.global_scan(rotP, traP, dat, ctf, sig, pRd, pTd,
-                                                   algo=a.algo), a.reps, st)
+                                                   algo=a.algo, guard=a.guard), a.reps, st)
         out.update(ms=sec * 1e3, us_per_image=sec / a.images * 1e6, algo=a.algo)
     else:
         rec = ex.Reconstructor(N, pf, dev)
