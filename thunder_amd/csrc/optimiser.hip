@@ -112,6 +112,16 @@ THX_DEV void qmul(const double* a, const double* b, double* o)
 // pairs (Laplace expansion), upper triangle only, mirrored; det == 0 or a
 // non-finite input gives NaNs (the reference's Eigen inverse of a singular A
 // does too).  ~90 FP64 operations instead of the ~300 of 16 full cofactors.
+// 1 / x from v_rcp_f64 and two Newton steps (within an ulp of the IEEE
+// quotient, a third of its instructions: the fixed-point chains below are
+// latency-bound)
+THX_DEV double rcp_nr(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+
 THX_DEV double inv4(const double* m, double* o)
 {
     const double s0 = m[0] * m[5] - m[4] * m[1], s1 = m[0] * m[6] - m[4] * m[2];
@@ -121,7 +131,7 @@ THX_DEV double inv4(const double* m, double* o)
     const double c3 = m[9] * m[14] - m[13] * m[10], c2 = m[8] * m[15] - m[12] * m[11];
     const double c1 = m[8] * m[14] - m[12] * m[10], c0 = m[8] * m[13] - m[12] * m[9];
     const double det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
-    const double r = det != 0.0 ? 1.0 / det : __builtin_nan("");
+    const double r = det != 0.0 ? rcp_nr(det) : __builtin_nan("");
     o[0] = (m[5] * c5 - m[6] * c4 + m[7] * c3) * r;
     o[1] = (-m[1] * c5 + m[2] * c4 - m[3] * c3) * r;
     o[2] = (m[13] * s5 - m[14] * s4 + m[15] * s3) * r;
@@ -170,8 +180,9 @@ template <int CTRL>
 THX_DEV double dpp_d(double v)
 {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    // every lane's source lies inside its row: no 'old' operand to initialise
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, true);
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
@@ -251,7 +262,7 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
         pack10(Ai, Mp);
         double b[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nf = 0.0;
         auto term = [&](const double* q, double w) {
-            const double r = w / quad10(Mp, q);
+            const double r = w * rcp_nr(quad10(Mp, q));
             int t = 0;
             for (int j = 0; j < 4; j++) {
                 const double qj = q[j] * r;
@@ -281,7 +292,7 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
         nf = group_sum(nf);
         int t = 0;
         for (int j = 0; j < 4; j++)
-            for (int k = j; k < 4; k++, t++) B[4 * j + k] = B[4 * k + j] = b[t] * (4.0 / nf);
+            for (int k = j; k < 4; k++, t++) B[4 * j + k] = B[4 * k + j] = b[t] * (4.0 * rcp_nr(nf));
         double crit = 0.0;
         for (int k = 0; k < 16; k++) crit += fabs(A[k] - B[k]);
         if (!(crit > 1e-3)) return it + 1;
