@@ -1,3 +1,4 @@
+# SQ / TA PMC passes over the bench's k_local_fused launches: tools/pmc_local.sh TAG -> gpurun_out/TAG/{pa,pb}
 set -e
 O=$GRAFT_REPO_ROOT/gpurun_out/$1; mkdir -p $O; export TMPDIR=/tmp
 B="python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-extras --no-cpu-baseline"
