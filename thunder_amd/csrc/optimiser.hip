@@ -1598,6 +1598,10 @@ namespace {
 struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    // the second side stream: the next phase's inferACG mean, forked once the
+    // rotations are resampled, beside the translations' resampling
+    hipStream_t s2 = nullptr;
+    hipEvent_t fork2 = nullptr, join2 = nullptr;
     std::mutex mu;      // calls on one caller stream are ordered anyway
 };
 
@@ -1614,6 +1618,9 @@ int side_stream(hipStream_t main, SideStream** out)
         THX_HIP(hipStreamCreateWithFlags(&n->s, hipStreamNonBlocking));
         THX_HIP(hipEventCreateWithFlags(&n->fork, hipEventDisableTiming));
         THX_HIP(hipEventCreateWithFlags(&n->join, hipEventDisableTiming));
+        THX_HIP(hipStreamCreateWithFlags(&n->s2, hipStreamNonBlocking));
+        THX_HIP(hipEventCreateWithFlags(&n->fork2, hipEventDisableTiming));
+        THX_HIP(hipEventCreateWithFlags(&n->join2, hipEventDisableTiming));
         e = n;
     }
     *out = e;
@@ -1697,14 +1704,31 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         SideStream* side;
         hipStream_t s;
         bool open = false;         // forked and not yet joined into s
+        bool open2 = false;        // the same for the second side stream
         ~SideGuard()
         {
-            if (!open) return;
-            (void)hipEventRecord(side->join, side->s);
-            (void)hipStreamWaitEvent(s, side->join, 0);
-            (void)hipStreamSynchronize(side->s);
+            if (open) {
+                (void)hipEventRecord(side->join, side->s);
+                (void)hipStreamWaitEvent(s, side->join, 0);
+                (void)hipStreamSynchronize(side->s);
+            }
+            if (open2) {
+                (void)hipEventRecord(side->join2, side->s2);
+                (void)hipStreamWaitEvent(s, side->join2, 0);
+                (void)hipStreamSynchronize(side->s2);
+            }
         }
     } sideGuard{side, s};
+    // the next phase's perturbation mean, already running on s2
+    bool meanAhead = false;
+    auto join2 = [&]() -> int {
+        if (sideGuard.open2) {
+            THX_HIP(hipEventRecord(side->join2, side->s2));
+            THX_HIP(hipStreamWaitEvent(s, side->join2, 0));
+            sideGuard.open2 = false;
+        }
+        return THX_OK;
+    };
     auto fork = [&]() -> int {
         sideGuard.open = true;
         THX_HIP(hipEventRecord(side->fork, s));
@@ -1892,9 +1916,14 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                c.seed, (uint32_t)(2000 + phase), done);
             THX_LAUNCH_CHECK();
         } else if (c.perturbMean == 1) {
-            hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat,
-                               c.acgIters, done, p.meanQ, nullptr);
-            THX_LAUNCH_CHECK();
+            if (meanAhead) {
+                THX_RET(join2());      // forked after the last phase's rotation resampling
+                meanAhead = false;
+            } else {
+                hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat,
+                                   c.acgIters, done, p.meanQ, nullptr);
+                THX_LAUNCH_CHECK();
+            }
         }
         if (!twoD) {
             THX_RET(join());     // the spreads of the previous calVari
@@ -1968,6 +1997,18 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, p.tmpQ,
                            (long)c.mLR * 4, c.mLR, p.anc, quat, done);
         THX_LAUNCH_CHECK();
+        // the next phase's perturbation mean needs only the resampled
+        // rotations: it runs on s2 beside the translations' resampling (an
+        // image the stopping rule retires below gets a mean nothing reads)
+        if (!twoD && c.perturbMean == 1 && phase + 1 < phase0 + nPh) {
+            THX_HIP(hipEventRecord(side->fork2, s));
+            THX_HIP(hipStreamWaitEvent(side->s2, side->fork2, 0));
+            sideGuard.open2 = true;
+            hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, side->s2, nImg, c.mLR, quat,
+                               c.acgIters, done, p.meanQ, nullptr);
+            THX_LAUNCH_CHECK();
+            meanAhead = true;
+        }
         hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg,
                            p.tmpQ, (long)c.mLR * 4, p.topR, p.topQ, done);
         THX_LAUNCH_CHECK();
@@ -2018,7 +2059,8 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             }
         }
     }
-    THX_RET(join());     // nothing of this call stays on the side stream
+    THX_RET(join());     // nothing of this call stays on the side streams
+    THX_RET(join2());
     if (!c.converge) {
         hipLaunchKernelGGL(k_fill_int, dim3(64), dim3(256), 0, s, nPD, (long)nImg,
                            phase0 + c.nPhase - 1);
