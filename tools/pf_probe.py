@@ -49,5 +49,6 @@ for name, q in clouds.items():
     quat = torch.as_tensor(np.ascontiguousarray(q), device=dev)
     for cap in (10, 100, 256):
         ms, p50, mx = timed(quat, cap)
-        print(json.dumps({"cloud": name, "cap": cap, "ms": round(ms, 4), "iters_p50": p50,
+        print(json.dumps({"lib": os.path.basename(os.environ.get("THX_LIB", "prod")),
+                          "cloud": name, "cap": cap, "ms": round(ms, 4), "iters_p50": p50,
                           "iters_max": mx}), flush=True)
