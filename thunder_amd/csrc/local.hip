@@ -34,7 +34,10 @@
 // whole launch -- and on pixel 4s + (l >> 4) of step s of a patch.  After a
 // step the (re, im) of the four pixels are regrouped across lane rows with
 // v_permlane16_swap into the A operands of two 16x16x4 MFMAs (k = re, im of
-// two pixels), so the projection tile never goes through LDS.
+// two pixels), so the projection tile never goes through LDS.  The y-pair
+// form (LAYOUT_YPAIR2, the bench's route) maps lanes differently: two lanes
+// per sample, and each tap load covers 8 rotations x the 4 pixels of a step
+// (pair_step), regrouped into the same A operands with ds_bpermute.
 #include <climits>
 
 #include <cmath>
@@ -846,8 +849,10 @@ k_local_fused(const float2* __restrict__ vol,
     {
         // COOP: lane 4 r + j works on rotation slot 16 wv + r (its quad's sample)
         // PAIR: lane 2 k + j works on rotation slot 16 wv + (k & 15)
+        // PAIR: lane 2 k + j (k = r8 + 8 p) works on rotation slot 16 wv + r8 + 8 j
+        const int pairSlot = wv * 16 + ((lane >> 1) & 7) + 8 * (lane & 1);
         const int r = r0 + slot_rotation(sPerm, COOP ? wv * 16 + (lane >> 2)
-                                                : PAIR ? wv * 16 + ((lane >> 1) & 15) : rl, nRl);
+                                                : PAIR ? pairSlot : rl, nRl);
         double q[4], mm[9];
         for (int k = 0; k < 4; k++) q[k] = quat[((size_t)l * nR + r) * 4 + k];
         quat_to_mat(q, mm);
@@ -888,6 +893,7 @@ k_local_fused(const float2* __restrict__ vol,
 #pragma unroll
     for (int ct = 0; ct < NCT; ct++) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
     float bias = 0.f, aConst = 0.f;
+    float biasHi = 0.f;     // PAIR: the bias of rotation r8 + 8 (bias: r8)
     // image-tile elements tid + j THREADS (< PKC TT): pixel bpx + j THREADS / TT
     // of the iteration's PKC, column bt
     constexpr int PSTEP = THREADS / TT;
@@ -1065,18 +1071,24 @@ k_local_fused(const float2* __restrict__ vol,
         // it = j sample and the pair shares the cells.  MFMA A rows: (pixels
         // 4s, 4s + 2) from the h = 0 pairs, (4s + 1, 4s + 3) from the h = 1 pairs.
         constexpr unsigned yxs = 2u;   // x stride of the copy's elements (slices interleaved)
+        // PAIR step, 8 rotations x 4 pixels per load: pair (r8, p) = lanes 2 (r8 + 8 p) + j
+        // evaluates pixel 4s + p for rotations 16 wv + r8 (it 0) and 16 wv + r8 + 8
+        // (it 1); lane j rotates the it = j sample and the pair shares the cells, so
+        // one load instruction covers 8 rotations of a 4-pixel patch row (the
+        // patch's neighbouring pixels share lines where a wide cloud's rotations
+        // do not).  MFMA A rows: rotation rho's (pixels 4s, 4s + 2) from pairs
+        // (rho & 7, 0 / 2), (4s + 1, 4s + 3) from (rho & 7, 1 / 3), it = rho >> 3.
         auto pair_step = [&](int s) {
-            const int j = lane & 1, h = (lane >> 5) & 1;
+            const int j = lane & 1, p = lane >> 4;
             PCell mine;
             {
-                const double2 xy = make_double2(sXY[4 * s + h + 2 * j].x, sXY[4 * s + h + 2 * j].y);
+                const double2 xy = make_double2(sXY[4 * s + p].x, sXY[4 * s + p].y);
                 mine = pcell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                 (float)(m[2] * xy.x + m[5] * xy.y), vdim, ballR);
             }
             const PCell pc0 = pair_bcast_pcell<0>(mine), pc1 = pair_bcast_pcell<1>(mine);
             const float4* yp = reinterpret_cast<const float4*>(vol);
             const PTaps t0 = ypair_pcell_load(yp, pc0, j, yxs), t1 = ypair_pcell_load(yp, pc1, j, yxs);
-            // all four loads in flight before the first interpolation waits
             __builtin_amdgcn_sched_barrier(0);
             float2 P[2];
 #pragma unroll
@@ -1084,19 +1096,19 @@ k_local_fused(const float2* __restrict__ vol,
                 const float2 v = ypair_pcell_lerp(it == 0 ? t0 : t1, it == 0 ? pc0 : pc1, j);
                 P[it] = make_float2(v.x + pair_swap(v.x), v.y + pair_swap(v.y));
             }
-            if (!CS)
-#pragma unroll
-                for (int it = 0; it < 2; it++)
-                    bias += sBq[4 * s + h + 2 * it] * (P[it].x * P[it].x + P[it].y * P[it].y);
-            // A[r][kk]: kk < 2 -> component kk of it 0, kk >= 2 -> component kk - 2 of it 1,
-            // from lane 2 r + (kk & 1) (a1: h = 0 pairs) or 32 + 2 r + (kk & 1) (a2: h = 1)
+            if (!CS) {
+                const float bq = sBq[4 * s + p];
+                bias += bq * (P[0].x * P[0].x + P[0].y * P[0].y);
+                biasHi += bq * (P[1].x * P[1].x + P[1].y * P[1].y);
+            }
             const float c0 = j ? P[0].y : P[0].x, c1 = j ? P[1].y : P[1].x;
-            const int sa = (2 * (lane & 15) + (kk & 1)) * 4;
+            const int rho = lane & 15;
+            const int sa = ((kk & 1) + 2 * (rho & 7) + 16 * (kk < 2 ? 0 : 2)) * 4;
             const float t10 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(c0)));
             const float t11 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa, __float_as_int(c1)));
-            const float t20 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa + 128, __float_as_int(c0)));
-            const float t21 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa + 128, __float_as_int(c1)));
-            const float a1 = kk < 2 ? t10 : t11, a2 = kk < 2 ? t20 : t21;
+            const float t20 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa + 64, __float_as_int(c0)));
+            const float t21 = __int_as_float(__builtin_amdgcn_ds_bpermute(sa + 64, __float_as_int(c1)));
+            const float a1 = rho < 8 ? t10 : t11, a2 = rho < 8 ? t20 : t21;
             const int q0 = 4 * s + (kk < 2 ? 0 : 2), q1 = q0 + 1;
 #pragma unroll
             for (int ct = 0; ct < NCT; ct++) {
@@ -1157,8 +1169,14 @@ k_local_fused(const float2* __restrict__ vol,
     // B_r: the four pixel slots of a rotation are lanes l, l + 16, l + 32, l + 48
     // (COOP: every lane of quad r holds rotation r's whole sum)
     if (PAIR) {
-        // rotation r's pixels are split over the pairs (r, h = 0) and (r, h = 1)
-        bias = __shfl(bias, 2 * (lane & 15), 64) + __shfl(bias, 32 + 2 * (lane & 15), 64);
+        // rotation rho's pixels are split over the pairs (rho & 7, p = 0..3),
+        // its sum in bias (rho < 8) or biasHi
+        bias += __shfl_xor(bias, 16, 64);
+        bias += __shfl_xor(bias, 32, 64);
+        biasHi += __shfl_xor(biasHi, 16, 64);
+        biasHi += __shfl_xor(biasHi, 32, 64);
+        const float lo = __shfl(bias, 2 * (lane & 7), 64), hi = __shfl(biasHi, 2 * (lane & 7), 64);
+        bias = (lane & 8) ? hi : lo;
     } else if (COOP) {
         bias = __shfl(bias, 4 * (lane & 15), 64);
     } else {
