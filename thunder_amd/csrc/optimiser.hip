@@ -13,8 +13,13 @@
 // The reference leaves the particle filter on the host and round-trips to the
 // GPU once per image per phase (gpu/src/cuthunder.cu:2675-3140 with a stream
 // sync at :3140); here every step runs for the whole batch on device and the
-// host only enqueues kernels (nothing synchronises, so the sequence can be
-// captured into a HIP graph).
+// host only enqueues kernels.  The host waits on the device at two points
+// only: one 4-byte read-back per call (the pixel ring's radius, which sizes
+// the compact y-pair ball) and, with the stopping rule on, the count of
+// images left after each phase from minPhase on.  So the phase loop with
+// converge == 0 is stream-ordered end to end, but a whole call is not
+// capturable into a HIP graph (the read-back would have to move into the
+// caller's configuration first).
 //
 // The particle statistics follow Particle / DirectionalStat with the
 // reference's Config.h switches: ACG spreads by inferACG's fixed point,
@@ -1592,8 +1597,8 @@ extern "C" int thx_pf_resample(int nImg, int nIn, int nOut, const double* w, int
 // beside the resampling, the gathers and the next phase's inferACG mean --
 // two latency-bound, low-occupancy kernels side by side.  One side stream
 // and a fork / join event pair per (device, caller stream), made once; the
-// side stream only ever waits on events recorded on the caller's stream, so
-// the whole sequence stays capturable into a HIP graph.
+// side stream only ever waits on events recorded on the caller's stream (a
+// fork / join pattern, the shape HIP graph capture accepts).
 namespace {
 struct SideStream {
     hipStream_t s = nullptr;
