@@ -11,17 +11,19 @@ no collective on the expectation path.  Insert (mReco = 100), the RCCL
 half-map all-reduce (thx_halfmap_allreduce over each hemisphere's ranks) and
 the FSC are timed separately and reported as extra fields.
 
-`roofline` is the dominant kernel of the timed step, k_local_fused<0>
-(the particle-filter phase at global resolution), timed by HIP events the
-driver records around every one of its launches inside the timed region
-(thx_expect_cfg.phaseEvents).  It gathers its taps from the 1.9 MB
-low-resolution ball of the projectee, which stays in L2, so it is priced
-against the L2 -> L1 line bandwidth measured by tools/probes/l2_roof.hip
-(random 16-B row pieces, one 128-B line each: 34.4 TB/s, the guide's L2
-figure): `achieved` = SURVEY §8(d)'s 64 B of taps per rotation-pixel per
-launch / launch time, and the PMC line traffic of the same launches
-(tools/l2_lines.py: TCP_TCC_READ_REQ x 128 B) against the same roof says how
-close the kernel runs to it.  The global scan and the full-resolution phase
+`roofline` is the dominant kernel of the timed step, k_local_fused (the
+particle-filter phase at global resolution, about half the step), timed by
+HIP events the driver records around every one of its launches inside the
+timed region (thx_expect_cfg.phaseEvents).  The device route sends every
+bench phase to the pair-form y-pair kernel k_local_fused<2>, which gathers
+its taps from the driver's compact z-interleaved y-pair ball (8.7 MB at
+rU 24, mostly L2-resident), so it is priced against the L2 -> L1 line
+bandwidth measured by tools/probes/l2_roof.hip (random 16-B row pieces, one
+128-B line each: 34.4 TB/s, the guide's L2 figure): `achieved` = SURVEY
+§8(d)'s 64 B of taps per rotation-pixel per launch / launch time, and the
+PMC line traffic of the same launches (tools/l2_lines.py: TCP_TCC_READ_REQ x
+128 B) against the same roof says how close the kernel runs to it.  The
+global scan and the full-resolution phase
 are reported beside it (roofline_scan, roofline_local).
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]
@@ -84,6 +86,24 @@ def parse():
                    help="keep the insert and the round end (all-reduce, reconstruction, FSC) but "
                         "skip the secondary rooflines (scan, full-resolution phase and insert)")
     return p.parse_args()
+
+
+def rank_layout(world, rank):
+    """What rank `rank` of a `world`-rank job owns (weak scaling):
+    its own batch of synthetic images (seeds per rank), its gold-standard
+    hemisphere (rank % 2, src/Parallel.cpp:26-53), the ranks its half-maps are
+    all-reduced with, and whether it leads its hemisphere (reconstruction, and
+    for A the FSC)."""
+    hemi = rank % 2
+    members = [r for r in range(world) if r % 2 == hemi]
+    from thunder_amd.hemisphere import leads
+    return {"hemisphere": hemi, "hemisphere_ranks": members, "leads": leads(world),
+            "is_lead": rank in leads(world), "image_seed": 5 + 101 * rank, "pf_seed": 7 + rank}
+
+
+def throughput(gpus, images, steps, seconds):
+    """The bench's value: every rank's images over the max-over-ranks time."""
+    return gpus * images * steps / seconds
 
 
 def log(rank, *a):
@@ -382,9 +402,10 @@ def main():
     # reference's rules (thx_global_sample_sizes: nT = 151 at transS 10)
     _, nR, nT = ops.global_sample_sizes(a.nr)
     gset = tuple(x.cpu().numpy() for x in ops.global_sample_set(nR, nT, 10.0, 2, dev))
-    px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, rL, a.images, dev, seed=5 + 101 * rank,
+    lay = rank_layout(world, rank)
+    px, dat, ctf, sig, qtrue, ttrue = make_stack(N, pf, rU, rL, a.images, dev, seed=lay["image_seed"],
                                                  vol=vol)
-    mk = lambda algo: ex.Expectation(vol, px, gset, n_phase=a.phases, algo=algo, seed=7 + rank,
+    mk = lambda algo: ex.Expectation(vol, px, gset, n_phase=a.phases, algo=algo, seed=lay["pf_seed"],
                                      shuffle=bool(a.shuffle), perturb_mean=a.perturb_mean,
                                      acg_iters=a.acg_iters, large_first=bool(a.large_first))
     e = mk(a.algo)
@@ -449,7 +470,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     ms_per_step = el / a.steps * 1e3
-    value = a.gpus * a.images * a.steps / el
+    value = throughput(a.gpus, a.images, a.steps, el)
     local_ms = timer.ms() if timer is not None else []
     if timer is not None:
         timer.close()
@@ -657,8 +678,7 @@ def main():
             torch.cuda.synchronize()
             extras["allreduce_ms"] = (time.perf_counter() - t1) * 1e3
             extras["allreduce_bytes"] = hm_bytes
-            extras["allreduce_ranks_per_hemisphere"] = len([r for r in range(world)
-                                                            if r % 2 == rank % 2])
+            extras["allreduce_ranks_per_hemisphere"] = len(lay["hemisphere_ranks"])
             extras["allreduce_transport"] = re_.transport
             if re_.is_lead:
                 ops.reconstruct(recs[0].hm, N, pf, want_ft=False)   # hipFFT plans (first call)
@@ -766,7 +786,7 @@ def main():
                 "warmup": a.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None,
                 "dtype": {1: "f32", 4: "f32 (global scan: FP32 operands split exactly into three bf16, "
-                               "six products -- dropped terms <= 2^-26 |w||T|, below an FP32 product's "
+                               "six products -- dropped terms <= 2^-24 |w||T| each, comparable to an FP32 product's "
                                "rounding -- FP32 accumulation, cancellation-guarded direct FP32 "
                                "recompute; phases: FP32)"}.get(
                     a.algo, "f32 with a bf16x3 global scan (narrower than FP32)"),

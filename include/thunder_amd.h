@@ -145,8 +145,9 @@ int thx_dvp(const float* rotP, int nR, const float* traP, int nT,
  *       1 = fused FP32 MFMA formulation;
  *       2 = bf16 MFMA, three-product split (bf16x3, ~2^-16 per product);
  *       4 = bf16 MFMA, exact three-way split of both FP32 operands and six
- *           products (bf16x6: every dropped term <= 2^-26 |w||T|, below the
- *           FP32 rounding of a product) -- the expectation driver's default;
+ *           products (bf16x6: the dropped m l and l m are <= 2^-24 |w||T|
+ *           each, about 2^-23 together -- comparable to the FP32 rounding of
+ *           a product) -- the expectation driver's default;
  *       (3, fp16x2, was retired in ABI 9);
  *       2 and 4 run the cancellation guard (samples whose expanded form
  *       A + B + X cancels by more than 4x are recomputed in the direct form)
@@ -161,11 +162,11 @@ int thx_global_scan(const float* rotP, int nR, const float* traP, int nT,
                     thx_stream_t stream);
 
 /* thx_global_scan for algo 2 or 4 with two debug controls (ABI 9): dvp
- * [nImg][nR][nT] receives every sample's final log-likelihood (the value the
- * marginals are formed from), for the element-wise dump-compare of
- * gpu/src/cuthunder.cu:2247-2271; guard = the cancellation ratio above which
- * a sample is recomputed in the direct form (thx_global_scan uses 4; 0 turns
- * the guard off).  nT <= 160. */
+ * [nImg][nR][nT] (optional, NULL = no dump) receives every sample's final
+ * log-likelihood (the value the marginals are formed from), for the
+ * element-wise dump-compare of gpu/src/cuthunder.cu:2247-2271; guard = the
+ * cancellation ratio above which a sample is recomputed in the direct form
+ * (thx_global_scan uses 4; 0 turns the guard off).  A dump needs nT <= 160. */
 int thx_global_scan_dvp(const float* rotP, int nR, const float* traP, int nT,
                         const float* dat, const float* ctf, const float* sigRcp,
                         int nImg, int nPxl, const double* pR, const double* pT,

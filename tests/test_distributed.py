@@ -49,7 +49,7 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_halfmap_allreduce_per_hemisphere(world):
     port = free_port()
     mgr = mp.Manager()
@@ -132,7 +132,7 @@ def _round_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_round_end_fsc_across_ranks(world, orc):
     """bench.py's N > 1 round end (thunder_amd.hemisphere.round_end) on CPU
     tensors over gloo, with the restatement's insert / reconstruction / FSC:
@@ -161,9 +161,51 @@ def test_round_end_fsc_across_ranks(world, orc):
                                                   off, w)))
     ref = _fsc_cpu(*maps).numpy()
     got, cnt0 = out[0]
-    assert got is not None and np.allclose(got.numpy(), ref, rtol=0, atol=1e-9), (got, ref)
+    # two ranks per hemisphere: a + b is the same sum in any order (1e-9);
+    # with four (world 8) gloo's reduction order is not the rank order, the
+    # float32 maps differ by rounding and the balancing may stop an iteration
+    # apart, so the curve is held to the one-call tolerance below
+    assert got is not None and np.allclose(got.numpy(), ref, rtol=0,
+                                           atol=1e-9 if world <= 4 else 1e-2), (got, ref)
     # against one-call hemisphere inserts: the float32 sum order differs, the
     # balancing iterations may stop one step apart -- the curve agrees to 1e-2
     assert np.allclose(got.numpy(), _fsc_cpu(*maps1).numpy(), atol=1e-2)
     assert all(out[r][0] is None for r in range(1, world))
     assert cnt0 == (NIMG_RE // 2) * MRECO_RE and out[1][1] == (NIMG_RE // 2) * MRECO_RE
+
+
+# ---- the driver's 8-GPU run, planned without launching ranks
+def test_bench_plumbing_at_world_8(monkeypatch):
+    """What bench.py does at --gpus 8 (the driver's SCALE run) before any
+    collective: the argument reaches the bench, every rank has its own image
+    seed, the hemispheres are 4 + 4 ranks (rank % 2) led by ranks 0 and 1,
+    RoundEnd builds exactly those groups (torch.distributed.new_group
+    recorded, not called), hemisphere_shard deals any batch to the 8 ranks
+    once, and the value is all ranks' images over the max-over-ranks time."""
+    import sys
+    import bench
+    from thunder_amd import hemisphere as hs
+    from thunder_amd.expectation import hemisphere_shard
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "3", "--warmup", "1"])
+    a = bench.parse()
+    assert (a.gpus, a.steps, a.warmup, a.images) == (8, 3, 1, 12500)
+    lays = [bench.rank_layout(8, r) for r in range(8)]
+    assert [l_["hemisphere"] for l_ in lays] == [0, 1] * 4
+    assert lays[0]["hemisphere_ranks"] == [0, 2, 4, 6] and lays[1]["hemisphere_ranks"] == [1, 3, 5, 7]
+    assert [r for r in range(8) if lays[r]["is_lead"]] == [0, 1]
+    assert len({l_["image_seed"] for l_ in lays}) == 8 and len({l_["pf_seed"] for l_ in lays}) == 8
+    made = []
+    monkeypatch.setattr(dist, "new_group", lambda ranks: made.append(list(ranks)) or tuple(ranks))
+    for r in range(8):
+        made.clear()
+        re_ = hs.RoundEnd(8, r, transport="torch")
+        assert made == [[0, 2, 4, 6], [1, 3, 5, 7], [0, 1]]
+        assert re_.hemi_groups[r % 2] == tuple(lays[r]["hemisphere_ranks"])
+        assert re_.is_lead == (r in (0, 1))
+    for n in (12500, 100000, 7):
+        shards = [list(hemisphere_shard(n, 8, r)) for r in range(8)]
+        assert sorted(i for s_ in shards for i in s_) == list(range(n))
+        assert all(i % 2 == r % 2 for r in range(8) for i in shards[r])
+        sizes = [len(s_) for s_ in shards]
+        assert max(sizes) - min(sizes) <= 2
+    assert bench.throughput(8, 12500, 3, 1.5) == 8 * 12500 * 3 / 1.5

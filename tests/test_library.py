@@ -240,15 +240,17 @@ def test_adapter_device_policy(L):
 
 def test_global_scan_dvp_validates_without_gpu(L):
     """thx_global_scan_dvp (ABI 9): only the split algorithms (2, 4) keep a
-    per-sample dump; a negative guard, a NULL dump and the retired fp16x2
-    (algo 3) are refused before any device work."""
+    per-sample dump; a negative guard and the retired fp16x2 (algo 3) are
+    refused before any device work, with or without a dump (NULL dump = guard
+    control only)."""
     p = ctypes.c_void_p(16)
     args = lambda algo, guard, dvp: (p, 2000, p, 151, p, p, p, 8, 870, p, p, 0, 1, p, p, p, p, algo,
                                      ctypes.c_float(guard), dvp, p, ctypes.c_size_t(1 << 40), None)
     assert L.thx_global_scan_dvp(*args(1, 4.0, p)) != 0
     assert L.thx_global_scan_dvp(*args(3, 4.0, p)) != 0
     assert L.thx_global_scan_dvp(*args(4, -1.0, p)) != 0
-    assert L.thx_global_scan_dvp(*args(4, 4.0, None)) != 0
+    assert L.thx_global_scan_dvp(*args(3, 4.0, None)) != 0
+    assert L.thx_global_scan_dvp(*args(4, -1.0, None)) != 0
     assert L.thx_global_scan(p, 2000, p, 151, p, p, p, 8, 870, p, p, 0, 1, p, p, p, p, 3, p,
                              ctypes.c_size_t(1 << 40), None) != 0
     assert L.thx_global_scan_workspace(8, 2000, 151, 870, 4) > 0

@@ -119,9 +119,14 @@ THX_DEV void qmul(const double* a, const double* b, double* o)
 // does too).  ~90 FP64 operations instead of the ~300 of 16 full cofactors.
 // 1 / x from v_rcp_f64 and two Newton steps (within an ulp of the IEEE
 // quotient, a third of its instructions: the fixed-point chains below are
-// latency-bound)
+// latency-bound).  Outside 2^-1021 <= |x| <= 2^1021 -- zero, infinities, NaN
+// and the operands whose reciprocal leaves the normal range -- the IEEE
+// quotient itself (1 / 0 = inf, 1 / inf = 0, where the Newton steps would
+// give NaN), so degenerate clouds see the reference's division.
 THX_DEV double rcp_nr(double x)
 {
+    const double ax = __builtin_fabs(x);
+    if (!(ax >= 0x1p-1021 && ax <= 0x1p1021)) return 1.0 / x;
     double r = __builtin_amdgcn_rcp(x);
     r = fma(r, fma(-x, r, 1.0), r);
     return fma(r, fma(-x, r, 1.0), r);
@@ -1292,6 +1297,7 @@ struct Plan {
     double* meanQ;                           // k_pf_mean's perturbation mean
     float* wC; float* wR; float* wT; float* base; double* pC;
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
+    int* doneSnap;                       // done as of a side-stream fork (k_pf_mean on s2)
     int* actIdx; int* nActIdx;           // the active list in index order (route samples)
     int* maxR2;                          // max iCol^2 + iRow^2 of the pixel set
     unsigned* ordKey; unsigned* ordKeyOut; int* ordIdx; int* ord;   // view order (order.hip)
@@ -1348,6 +1354,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.cls = k.take<int>(nImg);
     p.nP = k.take<int>(nImg);
     p.done = k.take<int>(nImg);
+    p.doneSnap = k.take<int>(nImg);
     p.act = k.take<int>(nImg);
     p.nAct = k.take<int>(1);
     p.actIdx = k.take<int>(nImg);
@@ -2004,13 +2011,18 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         THX_LAUNCH_CHECK();
         // the next phase's perturbation mean needs only the resampled
         // rotations: it runs on s2 beside the translations' resampling (an
-        // image the stopping rule retires below gets a mean nothing reads)
+        // image the stopping rule retires below gets a mean nothing reads).
+        // It reads the done mask as of the fork (a snapshot), never the
+        // buffer k_pf_converge / k_compact write on s after it.
         if (!twoD && c.perturbMean == 1 && phase + 1 < phase0 + nPh) {
+            if (done)
+                THX_HIP(hipMemcpyAsync(p.doneSnap, done, sizeof(int) * nImg,
+                                       hipMemcpyDeviceToDevice, s));
             THX_HIP(hipEventRecord(side->fork2, s));
             THX_HIP(hipStreamWaitEvent(side->s2, side->fork2, 0));
             sideGuard.open2 = true;
             hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, side->s2, nImg, c.mLR, quat,
-                               c.acgIters, done, p.meanQ, nullptr);
+                               c.acgIters, done ? p.doneSnap : nullptr, p.meanQ, nullptr);
             THX_LAUNCH_CHECK();
             meanAhead = true;
         }

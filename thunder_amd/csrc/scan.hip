@@ -212,7 +212,6 @@ extern "C" int thx_global_scan_dvp(const float* rotP, int nR, const float* traP,
     SCAN_ARGS_CHECK();
     THX_CHECK_ARG(algo == 2 || algo == 4, "thx_global_scan_dvp: algo must be 2 or 4");
     THX_CHECK_ARG(guard >= 0.f, "thx_global_scan_dvp: guard must be >= 0");
-    THX_CHECK_ARG(dvp != nullptr, "thx_global_scan_dvp: dvp is NULL");
     THX_CHECK_ARG(wsBytes >= thx_global_scan_workspace(nImg, nR, nT, nPxl, algo),
                   "thx_global_scan_dvp: workspace too small");
     if (nImg == 0) return THX_OK;

@@ -2,9 +2,11 @@
 // term with FP32 operands split into 16-bit pieces.
 //   algo 4 (BF16X6, the product path): every FP32 operand split EXACTLY into
 //                    three bf16 (x = hi + mid + lo: 8 + 8 + 8 significant
-//                    bits), six products (hh, hm, mh, hl, mm, lh); the three
-//                    dropped (ml, lm, ll) are <= 2^-26 |w||T|, below the FP32
-//                    rounding of one product (2^-24); FP32 accumulation;
+//                    bits, |mid| <= 2^-8 |x|, |lo| <= 2^-16 |x|), six products
+//                    (hh, hm, mh, hl, mm, lh); of the three dropped, ml and lm
+//                    are <= 2^-24 |w||T| each (ll <= 2^-32), about 2^-23
+//                    together: comparable to the FP32 rounding of one product
+//                    (2^-24); FP32 accumulation;
 //   algo 2 (BF16X3): bf16 hi/lo of both operands, three products
 //                    (hi hi + hi lo + lo hi), ~2^-16 relative per product;
 //

@@ -285,11 +285,14 @@ def global_scan(rotP, traP, dat, ctf_, sig, pR, pT, kIdx=0, nK=1, state=None, al
     nbytes = lib().thx_global_scan_workspace(nImg, nR, nT, nPxl, algo)
     ws = workspace(nbytes, dev)
     if want_dvp or guard is not None:
-        dvp = torch.empty(nImg, nR, nT, dtype=torch.float32, device=dev)
+        # the dump only when asked for: a guard-only call runs the product
+        # kernel's stores (no [nImg, nR, nT] write)
+        dvp = torch.empty(nImg, nR, nT, dtype=torch.float32, device=dev) if want_dvp else None
         check(lib().thx_global_scan_dvp(_ptr(rotP), nR, _ptr(traP), nT, _ptr(dat), _ptr(ctf_),
                                         _ptr(sig), nImg, nPxl, _ptr(pR), _ptr(pT), kIdx, nK,
                                         _ptr(wC), _ptr(wR), _ptr(wT), _ptr(baseL), algo,
-                                        4.0 if guard is None else float(guard), _ptr(dvp),
+                                        4.0 if guard is None else float(guard),
+                                        _ptr(dvp) if want_dvp else None,
                                         _ptr(ws), ws.numel(), _stream(dev)), "thx_global_scan_dvp")
         return (wC, wR, wT, baseL, dvp) if want_dvp else (wC, wR, wT, baseL)
     check(lib().thx_global_scan(_ptr(rotP), nR, _ptr(traP), nT, _ptr(dat), _ptr(ctf_), _ptr(sig),
