@@ -555,12 +555,15 @@ def test_acg_degenerate_clouds():
     approach 0 or the normal-range limits (rcp_nr keeps the IEEE quotient
     there): calVari's spreads are finite and in [0, 1] (A(j, j) / A(0, 0) of
     the de-meaned cloud), the perturbation mean is a finite unit axis inside
-    the cloud.  Where the oracle's own value is stable under a permutation of
-    the cloud (one pose stored as q and -q) the spreads match it at 1e-6; on
+    the cloud.  One pose stored as q and -q (the same rotation) has a
+    well-defined answer, and the spreads match the oracle there at 1e-6.  On
     the rank-deficient clouds (two or three ancestors, all-but-one equal) the
-    reference's fixed point runs towards a singular A and the oracle itself
-    moves by up to 10x under a permutation, so there is no parity target
-    (parity unpinned there): both sides must call the cloud collapsed
+    reference's fixed point runs towards a singular A: the oracle moves by up
+    to 10x under a permutation of the cloud, and where the iteration stops
+    depends on when a determinant or a quadratic form leaves the normal range
+    (the all-but-one-equal cloud: 2e-6 in numpy's LU, exactly 0 here once the
+    outlier's 1 / (q^T A^-1 q) is the IEEE 1 / inf), so there is no parity
+    target (parity unpinned there): both sides must call the cloud collapsed
     (spreads <= 1e-2, against ~0.25 for a 30-degree cloud)."""
     from oracle import particle as op
     rng = np.random.default_rng(11)
@@ -574,7 +577,7 @@ def test_acg_degenerate_clouds():
         with np.errstate(all="ignore"):
             r = np.array(op.cal_vari_rot(quat[l]))
             p = np.array(op.cal_vari_rot(quat[l][rng.permutation(m)]))
-        if np.all(np.abs(r - p) <= 1e-6 * np.abs(r)):
+        if l == nImg - 1:     # q / -q
             assert np.allclose(k[l], r, rtol=1e-6, atol=1e-12), (l, k[l], r)
         else:
             assert np.all(k[l] <= 1e-2) and np.all(r <= 1e-2) and np.all(p <= 1e-2), (l, k[l], r, p)

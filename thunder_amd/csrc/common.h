@@ -102,6 +102,18 @@ struct Carver {
 // (include/Image/Volume.h:567-575).
 THX_DEV int wrap_idx(int v, int n) { return v >= 0 ? v : v + n; }
 
+// a * b + c on the full-rate 24-bit multiplier (v_mad_u32_u24) for index
+// arithmetic whose factors are below 2^24 and whose result fits 32 bits.
+// Written out because the compiler folds __umul24 + add into the 64-bit
+// v_mad_u64_u32 (or a v_mul_lo_u32), both quarter rate, and in the local
+// phases VALU issue is what the late phases are bound by.
+THX_DEV unsigned mad24(unsigned a, unsigned b, unsigned c)
+{
+    unsigned r;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 THX_DEV float2 cmul(float2 a, float2 b)
 {
     // operator* of include/Complex.h:195-203

@@ -189,9 +189,11 @@ struct PCell {
 // by element as in the ball: for even z0 a sample's four 16-B elements are
 // one contiguous 64-B piece (full resolution, box 256: 14.0 -> 12.1 ms at 1.5
 // deg, 18.4 -> 16.0 at 2 deg, 27.5 -> 23.0 at 3, profiles/r04_fullres_wzil_ab.jsonl)
+// (24-bit multiplies, mad24: every factor is below 2^24 and every result
+// below 2^32 up to vdim 1024)
 THX_DEV unsigned ypair_elem(unsigned z, unsigned y, unsigned x, unsigned vdim, unsigned nc)
 {
-    return (((z >> 1) * vdim + y) * nc + x) * 2u + (z & 1u);
+    return mad24(mad24(z >> 1, vdim, y), nc, x) * 2u + (z & 1u);
 }
 // In the compact ball slices z and z + 1 (z + R even) are interleaved element
 // by element, so for such z0 a sample's four 16-B elements (x0, x0 + 1 of
@@ -203,7 +205,7 @@ THX_DEV unsigned ypair_ball_elem(int z, int y, int x, int ballR)
 {
     const unsigned Y = 2u * ballR + 2u, X = (unsigned)ballR + 2u;
     const unsigned zc = (unsigned)(z + ballR), yc = (unsigned)(y + ballR);
-    return (((zc >> 1) * Y + yc) * X + (unsigned)x) * 2u + (zc & 1u);
+    return mad24(mad24(zc >> 1, Y, yc), X, (unsigned)x) * 2u + (zc & 1u);
 }
 THX_DEV PCell pcell_of(float x, float y, float z, int vdim, int ballR = 0)
 {
@@ -215,8 +217,11 @@ THX_DEV PCell pcell_of(float x, float y, float z, int vdim, int ballR = 0)
     const unsigned yw = (unsigned)wrap_idx(y0, vdim);
     PCell c;
     if (ballR > 0) {
+        // slice z0 + 1: the other element of the interleaved pair when z0 + R
+        // is even, else the first element of the next pair of slices
         c.e0 = ypair_ball_elem(z0, y0, x0, ballR);
-        c.e1 = ypair_ball_elem(z0 + 1, y0, x0, ballR);
+        const unsigned X2Y = 2u * ((unsigned)ballR + 2u) * (2u * ballR + 2u);   // (uniform)
+        c.e1 = c.e0 + (((unsigned)(z0 + ballR) & 1u) ? X2Y - 1u : 1u);
     } else {
         c.e0 = ypair_elem((unsigned)wrap_idx(z0, vdim), yw, (unsigned)x0, (unsigned)vdim, nc);
         c.e1 = ypair_elem((unsigned)wrap_idx(z0 + 1, vdim), yw, (unsigned)x0, (unsigned)vdim, nc);
@@ -832,7 +837,8 @@ k_local_fused(const float2* __restrict__ vol,
     __shared__ __attribute__((aligned(16))) float sB[PKC * 2 * NC];  // [px][U, V][t]
     // (iCol pf, iRow pf): small integers, exact in FP32 and widened exactly to
     // FP64 by the FP64 rotations
-    __shared__ __attribute__((aligned(8))) float2 sXY[PKC];
+    // (kept in FP64: the rotations read them as doubles, no per-step widening)
+    __shared__ __attribute__((aligned(16))) double2 sXY[PKC];
     __shared__ float sBq[CS ? KC * NC : PKC];                        // b = s c^2 ([px][col] for CS)
     __shared__ int sValid[PKC];                                      // 0: padding entry
     __shared__ float sTr[NC][2];
@@ -959,7 +965,7 @@ k_local_fused(const float2* __restrict__ vol,
                 sValid[q] = ok;
                 // padding entries sample the patch's first pixel (inside the box)
                 const int ic = ok ? x.ic : NOBOX ? 0 : rc.v[17], ir = ok ? x.ir : NOBOX ? 0 : rc.v[18];
-                sXY[q] = make_float2((float)(ic * pf), (float)(ir * pf));
+                sXY[q] = make_double2((double)(ic * pf), (double)(ir * pf));
             }
         }
         __syncthreads();
@@ -1021,7 +1027,7 @@ k_local_fused(const float2* __restrict__ vol,
             // shared across the quad (quad_bcast_cell)
             Cell mine;
             {
-                const double2 xy = make_double2(sXY[4 * s + j].x, sXY[4 * s + j].y);
+                const double2 xy = sXY[4 * s + j];
                 mine = cell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                (float)(m[2] * xy.x + m[5] * xy.y));
             }
@@ -1082,7 +1088,7 @@ k_local_fused(const float2* __restrict__ vol,
             const int j = lane & 1, p = lane >> 4;
             PCell mine;
             {
-                const double2 xy = make_double2(sXY[4 * s + p].x, sXY[4 * s + p].y);
+                const double2 xy = sXY[4 * s + p];
                 mine = pcell_of((float)(m[0] * xy.x + m[3] * xy.y), (float)(m[1] * xy.x + m[4] * xy.y),
                                 (float)(m[2] * xy.x + m[5] * xy.y), vdim, ballR);
             }
@@ -1142,7 +1148,7 @@ k_local_fused(const float2* __restrict__ vol,
 #pragma unroll
             for (int s = 0; s < 4 * PP; s++) {
                 if (pad_step(s)) continue;
-                const double2 xy = make_double2(sXY[4 * s + g].x, sXY[4 * s + g].y);
+                const double2 xy = sXY[4 * s + g];
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
                 const float z = (float)(m[2] * xy.x + m[5] * xy.y);
@@ -1152,7 +1158,7 @@ k_local_fused(const float2* __restrict__ vol,
 #pragma unroll 2
             for (int s = 0; s < 4 * PP; s++) {
                 if (pad_step(s)) continue;
-                const double2 xy = make_double2(sXY[4 * s + g].x, sXY[4 * s + g].y);
+                const double2 xy = sXY[4 * s + g];
                 const float x = (float)(m[0] * xy.x + m[3] * xy.y);
                 const float y = (float)(m[1] * xy.x + m[4] * xy.y);
                 const float z = (float)(m[2] * xy.x + m[5] * xy.y);

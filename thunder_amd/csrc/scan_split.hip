@@ -537,26 +537,52 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
     // Two stages.  Chunk ck+1's T planes and a tile are copied by LDS-DMA into
     // the other stage while chunk ck is multiplied, and its P rows ride in one
     // register; the barrier closing chunk ck retires both.
-    auto issue_chunk = [&](int ck, char* stage) {
-        const char* gTh = reinterpret_cast<const char*>(Thi + (size_t)ck * nTPad * TROW);
-        const char* gTl = reinterpret_cast<const char*>(Tlo + (size_t)ck * nTPad * TROW);
-        const char* gT2 = reinterpret_cast<const char*>(Tl2 + (size_t)ck * nTPad * TROW);
-        const char* gA = reinterpret_cast<const char*>(Ac + ((size_t)ck * nImgPad + l0) * APITCH);
-        const char* gP = reinterpret_cast<const char*>(Pc + ((size_t)ck * nRBk + rb) * ROT_TILE * KC);
+    // A wave's LDS-DMA instructions q = u NWAVE + w are fixed for the whole
+    // launch: their sources (part, first byte, per-chunk stride), LDS slots
+    // and lane counts are worked out once, in scalar registers (w through
+    // readfirstlane), so a chunk's copies cost one scalar multiply-add and no
+    // VALU each.  (Selected per chunk from the wave index they took ~10 VALU
+    // per copy, ~65 per wave and chunk: VALU issue adds to the MFMA time on
+    // gfx950, tools/probes/coexec.hip.)
+    constexpr int QS = (S::NQ + NWAVE - 1) / NWAVE;
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const char* dmaG[QS];
+    size_t dmaStride[QS];
+    int dmaN[QS];               // lanes that copy (0: no instruction)
+    {
+        const size_t tStride = (size_t)nTPad * TROW * 2;
 #pragma unroll
-        for (int u = 0; u < (S::NQ + NWAVE - 1) / NWAVE; u++) {
-            const int q = u * NWAVE + w;                     // wave-uniform instruction
-            if (q < S::NQ) {
-                const char* g;
-                int pc, lim;
-                if (q < S::TQ) { g = gTh; pc = q * 64; lim = S::T_PC; }
-                else if (S::NPLANE >= 2 && q < 2 * S::TQ) { g = gTl; pc = (q - S::TQ) * 64; lim = S::T_PC; }
-                else if (S::NPLANE >= 3 && q < 3 * S::TQ) { g = gT2; pc = (q - 2 * S::TQ) * 64; lim = S::T_PC; }
-                else if (q < S::NQ - S::PQ) { g = gA; pc = (q - S::NPLANE * S::TQ) * 64; lim = S::A_PC; }
-                else { g = gP; pc = (q - (S::NQ - S::PQ)) * 64; lim = S::P_PC; }
-                if (pc + lane < lim) dma16(g + (size_t)(pc + lane) * 16, stage + q * 1024);
+        for (int u = 0; u < QS; u++) {
+            const int q = u * NWAVE + wu;
+            const char* g = nullptr;
+            size_t st = 0;
+            int pc = 0, lim = 0;
+            if (q < S::TQ) {
+                g = reinterpret_cast<const char*>(Thi); st = tStride; pc = q * 64; lim = S::T_PC;
+            } else if (S::NPLANE >= 2 && q < 2 * S::TQ) {
+                g = reinterpret_cast<const char*>(Tlo); st = tStride; pc = (q - S::TQ) * 64; lim = S::T_PC;
+            } else if (S::NPLANE >= 3 && q < 3 * S::TQ) {
+                g = reinterpret_cast<const char*>(Tl2); st = tStride; pc = (q - 2 * S::TQ) * 64; lim = S::T_PC;
+            } else if (q < S::NQ - S::PQ) {
+                g = reinterpret_cast<const char*>(Ac + (size_t)l0 * APITCH);
+                st = (size_t)nImgPad * APITCH * sizeof(float2);
+                pc = (q - S::NPLANE * S::TQ) * 64; lim = S::A_PC;
+            } else if (q < S::NQ) {
+                g = reinterpret_cast<const char*>(Pc + (size_t)rb * ROT_TILE * KC);
+                st = (size_t)nRBk * ROT_TILE * KC * sizeof(float2);
+                pc = (q - (S::NQ - S::PQ)) * 64; lim = S::P_PC;
             }
+            dmaG[u] = g + (size_t)pc * 16;
+            dmaStride[u] = st;
+            dmaN[u] = q < S::NQ ? min(64, lim - pc) : 0;
         }
+    }
+    const unsigned laneB = (unsigned)lane * 16u;
+    auto issue_chunk = [&](int ck, char* stage) {
+#pragma unroll
+        for (int u = 0; u < QS; u++)
+            if (lane < dmaN[u])
+                dma16(dmaG[u] + (size_t)ck * dmaStride[u] + laneB, stage + (u * NWAVE + wu) * 1024);
     };
     auto stage_at = [&](int ck) { return lds + (ck % SCAN_STAGES) * S::STAGE_B; };
     const int nCk = nPxlPad / KC;
