@@ -229,10 +229,13 @@ THX_DEV double group_sum(double v)
 // repeated additions, block for strided order).
 constexpr int QREG = 128 / GROUP;
 
+// idx (optional): particle i is Q[idx[i]] -- a resampled cloud read through
+// its ancestors, in the gathered order, without the gather
 template <bool REG>
 THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, double* A,
-                           int maxIt)
+                           int maxIt, const int* idx = nullptr)
 {
+    auto at = [&](int i) { return Q + 4 * (idx ? idx[i] : i); };
     double qr[REG ? QREG : 1][4];
     int nd = 0, nIn = 0;                          // runs, particles this lane holds
     unsigned runs = 0;                            // bit p: block particle p starts a run
@@ -244,7 +247,7 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
 #pragma unroll
         for (int p = 0; p < QREG; p++) {
             if (p < nIn) {
-                const double* c = Q + 4 * (i0 + p);
+                const double* c = at(i0 + p);
                 const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
                 if (p == 0 || c0 != prev[0] || c1 != prev[1] || c2 != prev[2] || c3 != prev[3])
                     starts |= 1u << p;
@@ -256,7 +259,7 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
 #pragma unroll
         for (int p = 0; p < QREG; p++) {
             if (starts) {
-                const double* c = Q + 4 * (i0 + __builtin_ctz(starts));
+                const double* c = at(i0 + __builtin_ctz(starts));
                 starts &= starts - 1;
                 if (pre) qmul(pre, c, qr[p]);
                 else for (int k = 0; k < 4; k++) qr[p][k] = c[k];
@@ -293,8 +296,9 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
         } else {
             for (int i = lane; i < m; i += GROUP) {
                 double q[4];
-                if (pre) qmul(pre, Q + 4 * i, q);
-                else for (int k = 0; k < 4; k++) q[k] = Q[4 * i + k];
+                const double* c = at(i);
+                if (pre) qmul(pre, c, q);
+                else for (int k = 0; k < 4; k++) q[k] = c[k];
                 term(q, 1.0);
             }
         }
@@ -311,10 +315,10 @@ THX_DEV int infer_acg_impl(const double* Q, int m, const double* pre, int lane, 
 }
 
 THX_DEV int infer_acg(const double* Q, int m, const double* pre, int lane, double* A,
-                      int maxIt = 256)
+                      int maxIt = 256, const int* idx = nullptr)
 {
-    return m <= GROUP * QREG ? infer_acg_impl<true>(Q, m, pre, lane, A, maxIt)
-                             : infer_acg_impl<false>(Q, m, pre, lane, A, maxIt);
+    return m <= GROUP * QREG ? infer_acg_impl<true>(Q, m, pre, lane, A, maxIt, idx)
+                             : infer_acg_impl<false>(Q, m, pre, lane, A, maxIt, idx);
 }
 
 // Unit eigenvector of the largest eigenvalue of a symmetric 4x4 (cyclic
@@ -705,17 +709,22 @@ __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
 // (DirectionalStat.cpp:93-145), capped at acgIters iterations -- then its
 // principal axis (:224-251).  Its own launch so the fixed point can keep the
 // cloud in registers (in k_pf_perturb they would push past 256 VGPRs).
-// itOut (optional): fixed-point iterations per image.
+// itOut (optional): fixed-point iterations per image.  anc (optional): the
+// cloud is quat[l][anc[l][j]] -- the pre-resample cloud read through the
+// resampling's ancestors, so the mean need not wait for the gather (the same
+// particles in the same order as the gathered cloud: the same result).
 __global__ void __launch_bounds__(256) k_pf_mean(int nImg, int mR, const double* __restrict__ quat,
                                                  int acgIters, const int* __restrict__ done,
                                                  double* __restrict__ meanQ,
-                                                 int* __restrict__ itOut)
+                                                 int* __restrict__ itOut,
+                                                 const int* __restrict__ anc = nullptr)
 {
     const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
     const int lane = threadIdx.x % GROUP;
     if (l >= nImg || (done && done[l])) return;
     double A[16], mean[4];
-    const int it = infer_acg(quat + (size_t)l * mR * 4, mR, nullptr, lane, A, acgIters);
+    const int it = infer_acg(quat + (size_t)l * mR * 4, mR, nullptr, lane, A, acgIters,
+                             anc ? anc + (size_t)l * mR : nullptr);
     principal_axis(A, mean);
     if (lane == 0) {
         for (int k = 0; k < 4; k++) meanQ[4 * l + k] = mean[k];
@@ -1291,6 +1300,7 @@ struct Plan {
     float* gWC; float* gWR; float* gWT; float* gBase;
     void* scanWs; size_t scanWsBytes;
     int* anc; double* cdf; int* perm; int* topR; int* topT;
+    int* ancR;                           // the phases' rotation ancestors (read by the side-stream mean)
     double* tmpQ; double* tmpT;
     double* kv; double* sv; double* peakR;   // calVari k1..k3, s0 s1; setPeakFactor(R)
     double* topQ;                            // calRank1st _topR
@@ -1335,6 +1345,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.scanWs = k.take<char>(p.scanWsBytes);
     p.anc = k.take<int>((size_t)nImg * (c.mLR > c.mLT ? (c.mLR > mLD ? c.mLR : mLD)
                                                       : (c.mLT > mLD ? c.mLT : mLD)));
+    p.ancR = k.take<int>((size_t)nImg * c.mLR);
     p.cdf = k.take<double>((size_t)nImg * nMax);
     p.perm = k.take<int>((size_t)nImg * nMax);
     p.topR = k.take<int>(nImg);
@@ -1387,6 +1398,20 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     // the y-pair copy of every class's projectee for the device route's
     // pair-form kernel (phases whose LDS boxes do not pay)
     const bool yp = !c.volCells && !twoD && mLD == 0 && thx::phase_routed(0, c.pf, nPxl, 0);
+    // A/B control of the compact ball's placement (THX_YPAIR_OFFSET = B: the
+    // copy starts B bytes past a 2 MiB boundary of the address space; unset:
+    // right after the buffers before it).  The local phases' speed depends
+    // on it by a few per cent (profiles/r06_ball_placement_ab.jsonl).
+    if (yp) {
+        const char* e = std::getenv("THX_YPAIR_OFFSET");
+        const size_t A2 = size_t(2) << 20;
+        if (!k.base) {
+            k.off += 2 * A2;      // the size query: room for any placement
+        } else if (e) {
+            const uintptr_t a = (uintptr_t)k.base + k.off;
+            k.off += (A2 - a % A2) % A2 + ((size_t)std::strtoull(e, nullptr, 10) % A2 & ~size_t(255));
+        }
+    }
     p.ypair = yp ? k.take<float>((size_t)4 * (c.vdim / 2 + 1) * c.vdim * c.vdim * nK) : nullptr;
     p.bytes = k.off + 256;
     return p;
@@ -2002,15 +2027,13 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         // resample R and T by the phase marginals; ancestors gathered in place
         hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.mLR, c.shuffle), s,
                            nImg, c.mLR, c.mLR, pR,
-                           c.mLR, p.wR, c.mLR, c.seed, (uint32_t)(3000 + phase), p.anc, pR,
+                           c.mLR, p.wR, c.mLR, c.seed, (uint32_t)(3000 + phase), p.ancR, pR,
                            p.topR, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
                            0, done);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, p.tmpQ,
-                           (long)c.mLR * 4, c.mLR, p.anc, quat, done);
-        THX_LAUNCH_CHECK();
         // the next phase's perturbation mean needs only the resampled
-        // rotations: it runs on s2 beside the translations' resampling (an
+        // rotations: it runs on s2 beside the gathers and the translations'
+        // resampling, reading the pre-resample cloud through the ancestors (an
         // image the stopping rule retires below gets a mean nothing reads).
         // It reads the done mask as of the fork (a snapshot), never the
         // buffer k_pf_converge / k_compact write on s after it.
@@ -2021,11 +2044,14 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             THX_HIP(hipEventRecord(side->fork2, s));
             THX_HIP(hipStreamWaitEvent(side->s2, side->fork2, 0));
             sideGuard.open2 = true;
-            hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, side->s2, nImg, c.mLR, quat,
-                               c.acgIters, done ? p.doneSnap : nullptr, p.meanQ, nullptr);
+            hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, side->s2, nImg, c.mLR, p.tmpQ,
+                               c.acgIters, done ? p.doneSnap : nullptr, p.meanQ, nullptr, p.ancR);
             THX_LAUNCH_CHECK();
             meanAhead = true;
         }
+        hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, p.tmpQ,
+                           (long)c.mLR * 4, c.mLR, p.ancR, quat, done);
+        THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg,
                            p.tmpQ, (long)c.mLR * 4, p.topR, p.topQ, done);
         THX_LAUNCH_CHECK();

@@ -139,13 +139,20 @@ THX_DEV void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo)
 // split3 of a (re, im) pair, each level one packed round (v_cvt_pk_bf16_f32),
 // two unpacking bit operations and one packed subtraction: the same three
 // planes as split3 on each component, (re, im) interleaved per plane
-THX_DEV void split3x2(float x, float y, uint32_t& hi, uint32_t& mid, uint32_t& lo)
+typedef float f2v __attribute__((ext_vector_type(2)));
+THX_DEV void split3x2(f2v x, uint32_t& hi, uint32_t& mid, uint32_t& lo)
 {
     auto pk = [](float a, float b) { return __builtin_bit_cast(uint32_t, bf16x2{(__bf16)a, (__bf16)b}); };
-    hi = pk(x, y);
-    const float rx = x - __uint_as_float(hi << 16), ry = y - __uint_as_float(hi & 0xffff0000u);
-    mid = pk(rx, ry);
-    lo = pk(rx - __uint_as_float(mid << 16), ry - __uint_as_float(mid & 0xffff0000u));
+    auto unpk = [](uint32_t v) { return f2v{__uint_as_float(v << 16), __uint_as_float(v & 0xffff0000u)}; };
+    // (the empty asm keeps each packed level opaque: left visible, the
+    // compiler re-derives its low half by a second v_cvt_pk_bf16_f32)
+    hi = pk(x.x, x.y);
+    asm volatile("" : "+v"(hi));
+    const f2v r = x - unpk(hi);
+    mid = pk(r.x, r.y);
+    asm volatile("" : "+v"(mid));
+    const f2v r2 = r - unpk(mid);
+    lo = pk(r2.x, r2.y);
 }
 
 // Per image: A_l = sum s|d|^2
@@ -644,15 +651,21 @@ __global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2)
                     const float2* rowA = sA + (a * 32 + n) * APITCH + px0;
                     const f32x4v a01 = *reinterpret_cast<const f32x4v*>(rowA);
                     const f32x4v a23 = *reinterpret_cast<const f32x4v*>(rowA + 2);
-                    const float ar[4] = {a01.x, a01.z, a23.x, a23.z};
-                    const float ai[4] = {a01.y, a01.w, a23.y, a23.w};
+                    const f2v av[4] = {f2v{a01.x, a01.y}, f2v{a01.z, a01.w}, f2v{a23.x, a23.y},
+                                       f2v{a23.z, a23.w}};   // (re, im) of a, one pixel each
                     u32x4 hq, mq, lq;
 #pragma unroll
                     for (int qd = 0; qd < 4; qd++) {
-                        const float wr = ar[qd] * pr[qd] + ai[qd] * pi[qd];
-                        const float wi = ai[qd] * pr[qd] - ar[qd] * pi[qd];
+                        // w = a conj(P) in two packed operations: (ar pr, ai pr), then
+                        // (ai pi + ar pr, -ar pi + ai pr) -- the swap, the broadcast
+                        // and the sign are operand modifiers of v_pk_fma_f32 (the
+                        // component-wise form compiled to three, half their
+                        // products unused)
+                        const f2v t = av[qd] * (f2v)pr[qd];
+                        const f2v w = __builtin_elementwise_fma(f2v{av[qd].y, av[qd].x},
+                                                                f2v{pi[qd], -pi[qd]}, t);
                         uint32_t x0, x1, x2;
-                        split3x2(wr, wi, x0, x1, x2);
+                        split3x2(w, x0, x1, x2);
                         hq[qd] = x0; mq[qd] = x1; lq[qd] = x2;
                     }
                     wq[0] = __builtin_bit_cast(HV, hq);
