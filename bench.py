@@ -360,7 +360,11 @@ def cpu_baseline(vol_np, N, pf, gset, dat, ctf, sig, px, phases, n_img=4096, run
             "spread": (dts[-1] - dts[0]) / dt,
             "sample": f"{n} images x (global scan nR={len(q)} nT={len(t)} nPxl={px.n} + "
                       f"{phases} local phases {mR}x{mT}), oracle/cpu_fast.c, OpenMP {threads} "
-                      f"threads, median of {runs} runs ({dt:.1f} s)"}
+                      f"threads, median of {runs} runs ({dt:.1f} s)",
+            "note": "the builder's CPU port of the reference's loop structure (FP32, OpenMP, "
+                    "vectorised over images / pixels); its speed relative to the reference's "
+                    "own logDataVSPrior_m_n_huabin_SIMD256 loop (src/Optimiser.cpp:9931-9973) "
+                    "is not calibrated: the reference's CPU path cannot be built here (Boost)"}
 
 
 PEAK_FP32_TFLOPS = PEAK_FP32_MFMA_TFLOPS

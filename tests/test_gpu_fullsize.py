@@ -94,14 +94,17 @@ def test_full_resolution_phase_matches_oracle(orc, c3, layout, spread):
         assert np.max(np.abs(d[l] - rd) / np.abs(rd)) < 1e-5
 
 
-@pytest.mark.parametrize("algo", [2, 4])
-def test_split_scan_every_tile_row_matches_direct(c3, algo):
+@pytest.mark.parametrize("algo,nT", [(2, 151), (4, 151), (4, 120), (4, 90), (4, 50), (4, 20)])
+def test_split_scan_every_tile_row_matches_direct(c3, algo, nT):
     """A whole 64-image tile (both 32-row halves of every MFMA operand, all 16
     accumulator rows per lane) of the split scans' dumped dvp against the
     direct formulation (thx_dvp) at 1e-5, and a repeated call bit-identical.
     A schedule of the bf16x6 main loop once corrupted rows 16-31 of each half
-    nondeterministically ("bf16x6 scan"): this is the guard."""
+    nondeterministically ("bf16x6 scan"): this is the guard, for
+    every instantiation of the kernel's translation fragments (nT 20 / 50 /
+    90 / 120 / 151: NF 1-5, padded to 32 .. 160 columns)."""
     q, t, pR, pT = synth.global_sample_set(2000, seed=2)
+    t, pT = t[:nT], pT[:nT] / pT[:nT].sum()
     px = c3["px"]
     assert c3["dat"].shape[0] == 64
     rotP = ops.project3d(c3["vol"], ops.rotmat(torch.as_tensor(q, device=DEV)), px)
