@@ -44,4 +44,9 @@ for k in range(1, 11):
                       "p90": float(np.percentile(h, 90)), "p99": float(np.percentile(h, 99)),
                       "max": int(h.max()), "capped": int((h >= 100).sum()), "n": n,
                       "runs_p50": float(np.median(runs)),
-                      "runs_capped_p50": float(np.median(runs[h >= 100])) if (h >= 100).any() else None}), flush=True)
+                      "runs_capped_p50": float(np.median(runs[h >= 100])) if (h >= 100).any() else None,
+                      "runs_capped_p90": float(np.percentile(runs[h >= 100], 90)) if (h >= 100).any() else None,
+                      "capped_runs_ge_64": int(((h >= 100) & (runs >= 64)).sum()),
+                      # a wave's pass costs its heaviest lane: runs per lane of 8 lanes
+                      "waves_cost_model": float(np.sum(np.max((h * np.ceil(runs / 8.0))[:n // 8 * 8]
+                                                               .reshape(-1, 8), axis=1)))}), flush=True)
