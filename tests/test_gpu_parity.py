@@ -444,6 +444,26 @@ def test_particle_statistics_match_oracle(spread):
         assert np.allclose(ud[l], op.keep_half_height(u[l], rp), rtol=1e-6, atol=1e-6 * u[l].max())
 
 
+@pytest.mark.parametrize("n", [9, 125, 2000, 2048, 2049, 5000])
+def test_peak_factor_register_and_reread_paths(n):
+    """k_pf_peak keeps rows of up to 2048 marginals in registers for its
+    bisection and re-reads longer ones from memory: both paths, at and across
+    the threshold, against oracle/particle.py -- random rows, rows of few
+    distinct values (ties at the rank), constant rows and rows with zeros."""
+    from oracle import particle as op
+    rng = np.random.default_rng(n + 11)
+    u = (rng.exponential(1.0, (4, n)) ** 4).astype(np.float32)
+    u[1] = np.round(u[1] * 4) / 4 + 0.25            # ties
+    u[2] = 0.75                                     # constant
+    u[3, ::3] = 0.0                                 # zeros among the values
+    ud, peak = ops.pf_peak(T(u).clone())
+    ud, peak = ud.cpu().numpy(), peak.cpu().numpy()
+    for l in range(4):
+        rp = op.peak_factor_rot(u[l])
+        assert peak[l] == pytest.approx(rp, rel=1e-7), (l, peak[l], rp)
+        assert np.allclose(ud[l], op.keep_half_height(u[l], rp), rtol=1e-6, atol=1e-6 * u[l].max())
+
+
 def _runs_cloud(rng, nAnc, m, spread):
     """A resampled cloud: nAnc ancestors drawn around one pose, their copies
     stored next to each other (as k_gather leaves them)."""
