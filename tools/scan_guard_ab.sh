@@ -5,8 +5,9 @@ set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/ab; mkdir -p $O
 for k in $(seq $2); do
-  for g in 1 0; do
-    run=$(timeout -k 10 120 python -u $R/tools/microbench.py scan --guard $g | tail -1)
-    echo "{\"guard\": $g, \"round\": $k, \"run\": $run}" >> $O/$1_guard.jsonl
+  for g in default 0; do
+    arg=""; [ $g = 0 ] && arg="--guard 0"
+    run=$(timeout -k 10 120 python -u $R/tools/microbench.py scan $arg | tail -1)
+    echo "{\"guard\": \"$g\", \"round\": $k, \"run\": $run}" >> $O/$1_guard.jsonl
   done
 done
