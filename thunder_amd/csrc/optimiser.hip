@@ -510,6 +510,122 @@ size_t resample_lds(int nIn, bool shuffle)
     return (size_t)4 * n * sizeof(uint64_t);
 }
 
+
+// Bitonic sort of one wave's 64 KPL distinct 64-bit keys held in registers:
+// position p = KPL lane + r is kv[r] of lane `lane`.  Pairs (p, p ^ j) with
+// j < KPL sit in one lane (BitonicIn); the others are lanes lane ^ (j / KPL)
+// at the same r, exchanged by ds_bpermute (__shfl_xor).  The keys are
+// distinct, so the sorted sequence -- the only thing the caller reads -- is
+// that of any other correct sort (the LDS network it replaces).
+template <int J, int KPL>
+THX_DEV void bitonic_in(uint64_t (&kv)[KPL], int lane, int k)
+{
+#pragma unroll
+    for (int r = 0; r < KPL; r++) {
+        if (r & J) continue;
+        const bool asc = ((KPL * lane + r) & k) == 0;
+        const uint64_t a = kv[r], b = kv[r | J];
+        // ascending pairs put the minimum first, descending ones the maximum
+        const bool sw = (a > b) == asc;
+        kv[r] = sw ? b : a;
+        kv[r | J] = sw ? a : b;
+    }
+}
+
+template <int KPL>
+THX_DEV void wave_bitonic(uint64_t (&kv)[KPL], int lane)
+{
+    constexpr int N = 64 * KPL;
+    for (int k = 2; k <= N; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= KPL) {
+                const int lm = j / KPL;
+                const bool upper = (lane & lm) != 0;
+                // every partner first (the exchanges in flight together), then
+                // the compare-exchanges
+                uint64_t o[KPL];
+#pragma unroll
+                for (int r = 0; r < KPL; r++) {
+                    const uint32_t lo = __shfl_xor((uint32_t)kv[r], lm, 64);
+                    const uint32_t hi = __shfl_xor((uint32_t)(kv[r] >> 32), lm, 64);
+                    o[r] = ((uint64_t)hi << 32) | lo;
+                }
+#pragma unroll
+                for (int r = 0; r < KPL; r++) {
+                    const bool asc = ((KPL * lane + r) & k) == 0;
+                    // the lower position of an ascending pair keeps the minimum
+                    const bool keepMin = upper != asc;
+                    kv[r] = (o[r] < kv[r]) == keepMin ? o[r] : kv[r];
+                }
+            } else if (KPL >= 2 && j == 1) {
+                bitonic_in<1, KPL>(kv, lane, k);
+            } else if (KPL >= 4 && j == 2) {
+                bitonic_in<2, KPL>(kv, lane, k);
+            } else if (KPL >= 8 && j == 4) {
+                bitonic_in<4, KPL>(kv, lane, k);
+            } else if (KPL >= 16 && j == 8) {
+                bitonic_in<8, KPL>(kv, lane, k);
+            } else if (KPL >= 32 && j == 16) {
+                bitonic_in<16, KPL>(kv, lane, k);
+            }
+        }
+}
+
+// The shuffle's keys of one image, sorted in registers: lane `lane` draws the
+// keys of entries i = lane + 64 m (the LDS network's draws, same Philox
+// stream and order), the wave sorts them, and position p's index half goes
+// to k32[p] for p < nIn.
+template <int KPL>
+THX_DEV void shuffle_keys_reg(Philox& sh, int nIn, int lane, uint32_t* k32)
+{
+    uint64_t kv[KPL];
+    uint4 v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < KPL; m++) {
+        if ((m & 3) == 0) v = sh.next();
+        const uint32_t x = (m & 3) == 0 ? v.x : (m & 3) == 1 ? v.y : (m & 3) == 2 ? v.z : v.w;
+        const int i = lane + 64 * m;
+        kv[m] = i < nIn ? ((uint64_t)x << 32) | (uint64_t)i : ~0ull;
+    }
+    wave_bitonic<KPL>(kv, lane);
+#pragma unroll
+    for (int r = 0; r < KPL; r++) {
+        const int p = KPL * lane + r;
+        if (p < nIn) k32[p] = (uint32_t)kv[r];
+    }
+}
+
+// The reseed's shuffle on its own (one wave per image): the permutation of a
+// support of 64 KPL / 2 < nIn <= 64 KPL entries, sorted in registers, into
+// perm[l][.] -- k_pf_resample<.., true> then reads it, so the resampling
+// proper keeps its low register count and occupancy
+template <int KPL>
+__global__ void __launch_bounds__(256) k_pf_shuffle_perm(int nImg, int nIn, uint64_t seed,
+                                                         uint32_t stream, int* __restrict__ perm,
+                                                         const int* __restrict__ done)
+{
+    const int l = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (l >= nImg || (done && done[l])) return;
+    Philox sh(seed, (uint32_t)l, stream, 0x5f1e0000u | (uint32_t)lane);
+    uint64_t kv[KPL];
+    uint4 v = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < KPL; m++) {
+        if ((m & 3) == 0) v = sh.next();
+        const uint32_t x = (m & 3) == 0 ? v.x : (m & 3) == 1 ? v.y : (m & 3) == 2 ? v.z : v.w;
+        const int i = lane + 64 * m;
+        kv[m] = i < nIn ? ((uint64_t)x << 32) | (uint64_t)i : ~0ull;
+    }
+    wave_bitonic<KPL>(kv, lane);
+    int* pl = perm + (size_t)l * nIn;
+#pragma unroll
+    for (int r = 0; r < KPL; r++) {
+        const int p = KPL * lane + r;
+        if (p < nIn) pl[p] = (int)(uint32_t)kv[r];
+    }
+}
+
 // One wave per image: systematic resampling (src/Particle.cpp:1343-1383) of
 // (w, u) -> ancestors and 1/u priors; w may be shared by all images (ldw = 0).
 // u0 ~ U(0, 1/nOut) is drawn from the counter RNG.  w and wOut may alias (the
@@ -517,6 +633,11 @@ size_t resample_lds(int nIn, bool shuffle)
 // before the barrier that precedes the first store to wOut), so neither is
 // __restrict__.  permOut / u0Out (optional) expose the support permutation
 // and the draw for thx_pf_resample's parity tests.
+// REGKPL: supports of 64 .. 64 REGKPL entries (next power of two) sort in
+// registers (wave_bitonic), the rest in LDS; the reseed's 2000-entry support
+// uses 32 keys per lane (the LDS network took ~1.0 ms of its 1.26 ms per
+// 12 500-image call), the phases' supports 4 (fewer VGPRs, more waves)
+template <int REGKPL, bool PRE = false>
 __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut,
                                                      const double* w, int ldw,
                                                      const float* __restrict__ u, int ldu,
@@ -556,7 +677,34 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
     constexpr int KMAX = RESAMPLE_KMAX;
     extern __shared__ __attribute__((aligned(16))) uint64_t sKeyDyn[];
     int* pm = permWs ? permWs + (size_t)l * nIn : nullptr;
-    if (pm && nIn <= KMAX) {
+    int regN = 1;
+    while (regN < nIn) regN <<= 1;
+    const bool regSort = !PRE && pm && regN >= 64 && regN <= 64 * REGKPL;
+    if (PRE && pm && nIn <= KMAX) {
+        // k_pf_shuffle_perm left the permutation in pm: into this wave's LDS row
+        int* k32 = reinterpret_cast<int*>(sKeyDyn + (size_t)(threadIdx.x >> 6) * regN);
+        for (int i = lane; i < nIn; i += 64) k32[i] = pm[i];
+        pm = k32;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else if (PRE && pm) {
+        // (larger supports read the permutation where it lies)
+    } else if (regSort) {
+        uint32_t* k32 = reinterpret_cast<uint32_t*>(sKeyDyn + (size_t)(threadIdx.x >> 6) * regN);
+        Philox sh(seed, (uint32_t)l, stream, 0x5f1e0000u | (uint32_t)lane);
+        const int kpl = regN / 64;
+        if (REGKPL >= 32 && kpl == 32) shuffle_keys_reg<(REGKPL >= 32 ? 32 : 1)>(sh, nIn, lane, k32);
+        else if (REGKPL >= 16 && kpl == 16) shuffle_keys_reg<(REGKPL >= 16 ? 16 : 1)>(sh, nIn, lane, k32);
+        else if (REGKPL >= 8 && kpl == 8) shuffle_keys_reg<(REGKPL >= 8 ? 8 : 1)>(sh, nIn, lane, k32);
+        else if (REGKPL >= 4 && kpl == 4) shuffle_keys_reg<(REGKPL >= 4 ? 4 : 1)>(sh, nIn, lane, k32);
+        else if (REGKPL >= 2 && kpl == 2) shuffle_keys_reg<(REGKPL >= 2 ? 2 : 1)>(sh, nIn, lane, k32);
+        else shuffle_keys_reg<1>(sh, nIn, lane, k32);
+        pm = reinterpret_cast<int*>(k32);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else if (pm && nIn <= KMAX) {
         int ib = 0;
         while ((1 << ib) < nIn) ib++;
         const int N = 1 << ib;
@@ -701,6 +849,25 @@ __global__ void __launch_bounds__(256) k_pf_resample(int nImg, int nIn, int nOut
     s = wave_sum(s);
     for (int j = lane; j < nOut; j += 64)
         wOut[(size_t)l * nOut + j] = s > 0.0 ? wOut[(size_t)l * nOut + j] / s : 1.0 / nOut;
+}
+
+using ResampleKernel = decltype(&k_pf_resample<4>);
+// supports up to 256 entries sort in the resampling kernel's registers; the
+// reseed's 2000 go through k_pf_shuffle_perm first (resample_launch)
+ResampleKernel resample_kernel(int nIn, bool shuffle)
+{
+    return shuffle && nIn > 256 && nIn <= RESAMPLE_KMAX ? &k_pf_resample<4, true> : &k_pf_resample<4>;
+}
+
+// The shuffle's permutation ahead of k_pf_resample<4, true> for supports of
+// 257 .. 2048 entries (nothing for smaller ones or without a shuffle)
+void shuffle_perm_launch(int nImg, int nIn, bool shuffle, uint64_t seed, uint32_t stream, int* perm,
+                         const int* done, hipStream_t s)
+{
+    if (!shuffle || nIn <= 256 || nIn > RESAMPLE_KMAX) return;
+    auto k = nIn <= 512 ? &k_pf_shuffle_perm<8> : nIn <= 1024 ? &k_pf_shuffle_perm<16>
+                                                               : &k_pf_shuffle_perm<32>;
+    hipLaunchKernelGGL(k, dim3(thx::cdiv(nImg, 4)), dim3(256), 0, s, nImg, nIn, seed, stream, perm, done);
 }
 
 // gather ancestors: dst[l][j][:] = src[l (or shared)][anc[l][j]][:]
@@ -1636,10 +1803,13 @@ extern "C" int thx_pf_resample(int nImg, int nIn, int nOut, const double* w, int
     thx::Carver k(workspace, wsBytes);
     double* cdf = k.take<double>((size_t)nImg * nIn);
     int* pw = k.take<int>((size_t)nImg * nIn);
-    hipLaunchKernelGGL(k_pf_resample, dim3(thx::cdiv(nImg, 4)), dim3(256), resample_lds(nIn, shuffle),
+    shuffle_perm_launch(nImg, nIn, shuffle, (uint64_t)seed, (uint32_t)stream_id, pw, nullptr,
+                        thx::as_stream(stream));
+    THX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(resample_kernel(nIn, shuffle), dim3(thx::cdiv(nImg, 4)), dim3(256), resample_lds(nIn, shuffle),
                        thx::as_stream(stream),
                        nImg, nIn, nOut, w, ldw, u, ldu, (uint64_t)seed, (uint32_t)stream_id, anc,
-                       wOut, iMax, cdf, shuffle ? pw : nullptr, perm, u0);
+                       wOut, iMax, cdf, shuffle ? pw : nullptr, perm, u0, nullptr, 0, nullptr);
     THX_LAUNCH_CHECK();
     return THX_OK;
 }
@@ -1868,7 +2038,9 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipLaunchKernelGGL(k_pf_peak, dim3(gImg), dim3(256), 0, s, nImg, c.nR, p.gWR, nK * c.nR,
                            p.peakR, 1, clsSel, c.nR, nullptr, rankDiv);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.nR, c.shuffle), s,
+        shuffle_perm_launch(nImg, c.nR, c.shuffle, c.seed, 1000u, p.perm, nullptr, s);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(resample_kernel(c.nR, c.shuffle), dim3(gImg), dim3(256), resample_lds(c.nR, c.shuffle), s,
                            nImg, c.nR, c.mLR, gPR, 0,
                            p.gWR, nK * c.nR, c.seed, 1000u, p.anc, pR, p.topR, p.cdf,
                            c.shuffle ? p.perm : nullptr, nullptr, nullptr, clsSel, c.nR, nullptr);
@@ -1879,7 +2051,9 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg, gQuat,
                            0L, p.topR, p.topQ, nullptr);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.nT, c.shuffle), s,
+        shuffle_perm_launch(nImg, c.nT, c.shuffle, c.seed, 1001u, p.perm, nullptr, s);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(resample_kernel(c.nT, c.shuffle), dim3(gImg), dim3(256), resample_lds(c.nT, c.shuffle), s,
                            nImg, c.nT, c.mLT, gPT, 0,
                            p.gWT, nK * c.nT, c.seed, 1001u, p.anc, pT, p.topT, p.cdf,
                            c.shuffle ? p.perm : nullptr, nullptr, nullptr, clsSel, c.nT, nullptr);
@@ -2045,7 +2219,9 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         THX_LAUNCH_CHECK();
         THX_RET(join_rec());
         // resample R and T by the phase marginals; ancestors gathered in place
-        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.mLR, c.shuffle), s,
+        shuffle_perm_launch(nImg, c.mLR, c.shuffle, c.seed, (uint32_t)(3000 + phase), p.perm, done, s);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(resample_kernel(c.mLR, c.shuffle), dim3(gImg), dim3(256), resample_lds(c.mLR, c.shuffle), s,
                            nImg, c.mLR, c.mLR, pR,
                            c.mLR, p.wR, c.mLR, c.seed, (uint32_t)(3000 + phase), p.ancR, pR,
                            p.topR, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
@@ -2075,7 +2251,9 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg,
                            p.tmpQ, (long)c.mLR * 4, p.topR, p.topQ, done);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(c.mLT, c.shuffle), s,
+        shuffle_perm_launch(nImg, c.mLT, c.shuffle, c.seed, (uint32_t)(4000 + phase), p.perm, done, s);
+        THX_LAUNCH_CHECK();
+        hipLaunchKernelGGL(resample_kernel(c.mLT, c.shuffle), dim3(gImg), dim3(256), resample_lds(c.mLT, c.shuffle), s,
                            nImg, c.mLT, c.mLT, pT,
                            c.mLT, p.wT, c.mLT, c.seed, (uint32_t)(4000 + phase), p.anc, pT,
                            p.topT, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
@@ -2090,7 +2268,9 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             hipLaunchKernelGGL(k_pf_defocus, dim3(gPf), dim3(256), 0, s, nImg, mLD, 2, 0.0, c.seed,
                                0u, cs->d, cs->pD, p.sdD, done);
             THX_LAUNCH_CHECK();
-            hipLaunchKernelGGL(k_pf_resample, dim3(gImg), dim3(256), resample_lds(mLD, c.shuffle),
+            shuffle_perm_launch(nImg, mLD, c.shuffle, c.seed, (uint32_t)(5000 + phase), p.perm, done, s);
+            THX_LAUNCH_CHECK();
+            hipLaunchKernelGGL(resample_kernel(mLD, c.shuffle), dim3(gImg), dim3(256), resample_lds(mLD, c.shuffle),
                                s, nImg, mLD, mLD, cs->pD, mLD, p.wD, mLD, c.seed,
                                (uint32_t)(5000 + phase), p.anc, cs->pD, p.topD, p.cdf,
                                c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr, 0, done);
