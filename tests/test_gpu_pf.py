@@ -77,6 +77,43 @@ def test_shuffle_is_uniform():
     assert chi2 < dof + 5 * np.sqrt(2 * dof), chi2
 
 
+def _philox_4x32_10(seed, a, b, c, d):
+    """Philox-4x32-10 as thunder_amd/csrc/common.h's Philox::next() draws it:
+    counter (a, b, c, d), key = the 64-bit seed's halves; numpy uint64
+    arithmetic on arrays of counters."""
+    M0, M1, W0, W1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57), 0x9E3779B9, 0xBB67AE85
+    m32 = np.uint64(0xFFFFFFFF)
+    x = [np.asarray(v, np.uint64) & m32 for v in (a, b, c, d)]
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for _ in range(10):
+        p0, p1 = M0 * x[0], M1 * x[2]
+        x = [((p1 >> np.uint64(32)) ^ x[1] ^ np.uint64(k0)) & m32, p1 & m32,
+             ((p0 >> np.uint64(32)) ^ x[3] ^ np.uint64(k1)) & m32, p0 & m32]
+        k0, k1 = (k0 + W0) & 0xFFFFFFFF, (k1 + W1) & 0xFFFFFFFF
+    return x
+
+
+@pytest.mark.parametrize("nIn", [8, 100, 256, 300, 2000])
+def test_shuffle_is_the_sort_of_its_philox_keys(nIn):
+    """The support permutation is the ascending order of the 64-bit keys
+    (32 random bits << 32 | entry): entry i's bits are component i / 64 % 4
+    of draw i / 256 of the Philox stream (image, stream id, 0x5f1e0000 | i %
+    64) -- whichever sort the kernel runs for this size (the LDS network below
+    64 entries, the wave's registers up to 256, k_pf_shuffle_perm above)."""
+    nImg, seed, sid = 3, 1234567, 77
+    rng = np.random.default_rng(nIn)
+    w = rng.uniform(0.5, 1.0, nIn)
+    u = rng.uniform(0.1, 1.0, (nImg, nIn)).astype(np.float32)
+    *_, perm, _ = ops.pf_resample(T(w), T(u), 4, seed=seed, stream_id=sid)
+    perm = perm.cpu().numpy()
+    i = np.arange(nIn)
+    for l in range(nImg):
+        x = _philox_4x32_10(seed, np.full(nIn, l), np.full(nIn, sid), 0x5F1E0000 | (i % 64), i // 256)
+        bits = np.choose((i // 64) % 4, x)
+        keys = (bits.astype(np.uint64) << np.uint64(32)) | i.astype(np.uint64)
+        assert np.array_equal(perm[l], np.argsort(keys, kind="stable")), (nIn, l)
+
+
 def test_seed_and_stream_determine_the_draw():
     rng = np.random.default_rng(1)
     w, u = _inputs(rng, 4, 300)
