@@ -444,6 +444,61 @@ def test_particle_statistics_match_oracle(spread):
         assert np.allclose(ud[l], op.keep_half_height(u[l], rp), rtol=1e-6, atol=1e-6 * u[l].max())
 
 
+def _acg_iters(Q):
+    """Iterations oracle/particle.py's infer_acg takes on cloud Q (the same loop, counted)."""
+    B, it = np.eye(4), 0
+    while True:
+        it += 1
+        A = B
+        with np.errstate(all="ignore"):
+            Ai = np.linalg.inv(A)
+            u = np.einsum("ij,jk,ik->i", Q, Ai, Q)
+            B = np.einsum("ij,ik->jk", Q / u[:, None], Q) * (4.0 / np.sum(1.0 / u))
+        if not np.abs(A - B).sum() > 1e-3:
+            return it
+
+
+def test_calvari_replayed_second_fixed_point():
+    """k_pf_calvari takes the de-meaned cloud's fixed point as the first
+    one's iterates replayed through the de-meaning rotation
+    (calvari_acg_impl), with the second pass's own stopping rule.  Against
+    the oracle's two passes at 1e-6, on clouds where the oracle's second
+    pass stops before, at and after its first (asserted: all three occur),
+    resampled clouds of few ancestors and 200-particle clouds (the strided
+    path)."""
+    from oracle import particle as op
+    rng = np.random.default_rng(29)
+    clouds = []
+    for m in (125, 200):
+        for spread in (1.0, 3.0, 10.0, 30.0, 60.0):
+            clouds.append(synth.clustered_quaternions(6, m, spread, rng))
+        clouds.append(np.stack([_runs_cloud(rng, 12, m, 3.0) for _ in range(6)]))
+    # clouds whose de-meaned fixed point runs past the first (found by a
+    # search over seeds): uniform clouds and a 40-degree cloud squeezed in x
+    special = [synth.uniform_quaternions(125, np.random.default_rng(s)) for s in (1173, 1189)]
+    for s in (1034, 1114):
+        g = np.random.default_rng(s)
+        q = synth.clustered_quaternions(1, 125, 40.0, g)[0]
+        q[:, 1] *= 0.2
+        special.append(q / np.linalg.norm(q, axis=1, keepdims=True))
+    clouds.append(np.stack(special))
+    before = after = same = 0
+    for quat in clouds:
+        nImg, m = quat.shape[:2]
+        trans = rng.standard_normal((nImg, 9, 2))
+        k, _ = ops.pf_calvari(T(quat), T(trans), 0.0, 0.0)
+        k = k.cpu().numpy()
+        for l in range(nImg):
+            mean = op.principal_axis(op.infer_acg(quat[l]))
+            it1 = _acg_iters(quat[l])
+            it2 = _acg_iters(op.qmul(op.conj(mean)[None, :], quat[l]))
+            before += it2 < it1
+            after += it2 > it1
+            same += it2 == it1
+            assert np.allclose(k[l], op.cal_vari_rot(quat[l]), rtol=1e-6, atol=1e-12), (m, l, it1, it2)
+    assert before and after and same, (before, after, same)
+
+
 @pytest.mark.parametrize("n", [9, 125, 2000, 2048, 2049, 5000])
 def test_peak_factor_register_and_reread_paths(n):
     """k_pf_peak keeps rows of up to 2048 marginals in registers for its

@@ -157,6 +157,44 @@ THX_DEV double inv4(const double* m, double* o)
     return det;
 }
 
+// inv4 with every 2x2 minor compensated (Kahan's a d - b c: the product b c
+// and its FMA residual): the minors of a near-rank-1 A cancel by about the
+// ratio of its eigenvalues, and the plain products leave the small
+// eigen-directions of A^-1 -- the ones a de-meaning rotation exposes --
+// with ~1e-6 relative error on a cloud of 1e-4 spread, the compensated ones
+// with ~1e-8.  Used by calvari_acg_impl, whose second fixed point reads them.
+THX_DEV double dop2(double a, double d, double b, double c)
+{
+    const double w = b * c;
+    const double e = fma(-b, c, w);
+    return fma(a, d, -w) + e;
+}
+
+THX_DEV double inv4_acc(const double* m, double* o)
+{
+    const double s0 = dop2(m[0], m[5], m[4], m[1]), s1 = dop2(m[0], m[6], m[4], m[2]);
+    const double s2 = dop2(m[0], m[7], m[4], m[3]), s3 = dop2(m[1], m[6], m[5], m[2]);
+    const double s4 = dop2(m[1], m[7], m[5], m[3]), s5 = dop2(m[2], m[7], m[6], m[3]);
+    const double c5 = dop2(m[10], m[15], m[14], m[11]), c4 = dop2(m[9], m[15], m[13], m[11]);
+    const double c3 = dop2(m[9], m[14], m[13], m[10]), c2 = dop2(m[8], m[15], m[12], m[11]);
+    const double c1 = dop2(m[8], m[14], m[12], m[10]), c0 = dop2(m[8], m[13], m[12], m[9]);
+    const double det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
+    const double r = det != 0.0 ? rcp_nr(det) : __builtin_nan("");
+    o[0] = (m[5] * c5 - m[6] * c4 + m[7] * c3) * r;
+    o[1] = (-m[1] * c5 + m[2] * c4 - m[3] * c3) * r;
+    o[2] = (m[13] * s5 - m[14] * s4 + m[15] * s3) * r;
+    o[3] = (-m[9] * s5 + m[10] * s4 - m[11] * s3) * r;
+    o[5] = (m[0] * c5 - m[2] * c2 + m[3] * c1) * r;
+    o[6] = (-m[12] * s5 + m[14] * s2 - m[15] * s1) * r;
+    o[7] = (m[8] * s5 - m[10] * s2 + m[11] * s1) * r;
+    o[10] = (m[12] * s4 - m[13] * s2 + m[15] * s0) * r;
+    o[11] = (-m[8] * s4 + m[9] * s2 - m[11] * s0) * r;
+    o[15] = (m[8] * s3 - m[9] * s1 + m[10] * s0) * r;
+    o[4] = o[1]; o[8] = o[2]; o[12] = o[3];
+    o[9] = o[6]; o[13] = o[7]; o[14] = o[11];
+    return det;
+}
+
 // A symmetric matrix packed as its upper triangle with the off-diagonal
 // entries doubled, so q^T M q = sum_j q_j sum_{k >= j} Mp_jk q_k (14 FMAs).
 THX_DEV void pack10(const double* M, double* Mp)
@@ -365,6 +403,202 @@ THX_DEV void principal_axis(const double* A0, double* v)
     for (int k = 0; k < 4; k++) v[k] = V[4 * k + best] / n;
 }
 
+// calVari's two fixed points from one (k_pf_calvari with a history buffer).
+// The de-meaned cloud q' = c q (c = conj(mean), a unit quaternion) is the
+// cloud under the orthogonal map M: q -> c q, and Tyler's map commutes with
+// it (q'^T (M A M^T)^-1 q' = q^T A^-1 q, so F(M A M^T) = M F(A) M^T): from
+// B'_0 = I = M I M^T the second fixed point's iterates are B'_k = M B_k M^T,
+// B_k the first's.  The first pass keeps its iterates in hist (10 doubles
+// each, lane 0 of the group); the second pass's stopping rule (sum |A' - B'|,
+// not invariant under M, so it may stop before or after the first) is then
+// evaluated on the replayed iterates, GROUP iterations at a time, one per
+// lane, and the first recurrence is continued when the second needs more
+// iterates than the first pass made.  Equal to the two passes in exact
+// arithmetic; the rounding differs from iterating on c q, as any summation
+// order does.  Returns the second fixed point's A in A2 (every lane).
+constexpr int ACG_HIST_MAX = 256;      // infer_acg's cap, the history's length per image
+constexpr int ACG_HIST = 10 * ACG_HIST_MAX;
+
+// B' = M B M^T of a symmetric B given as its upper triangle u (row-major j <= k)
+THX_DEV void acg_conj(const double* M, const double* u, double* P)
+{
+    double B[16];
+    int t = 0;
+    for (int j = 0; j < 4; j++)
+        for (int k = j; k < 4; k++, t++) B[4 * j + k] = B[4 * k + j] = u[t];
+    double T[16];
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++)
+            T[4 * i + j] = M[4 * i] * B[j] + M[4 * i + 1] * B[4 + j] + M[4 * i + 2] * B[8 + j] +
+                           M[4 * i + 3] * B[12 + j];
+    for (int i = 0; i < 4; i++)
+        for (int j = i; j < 4; j++)
+            P[4 * i + j] = P[4 * j + i] = T[4 * i] * M[4 * j] + T[4 * i + 1] * M[4 * j + 1] +
+                                          T[4 * i + 2] * M[4 * j + 2] + T[4 * i + 3] * M[4 * j + 3];
+}
+
+THX_DEV void acg_conj_hist(const double* M, const double* h, double* P)
+{
+    const double2* h2 = reinterpret_cast<const double2*>(h);
+    double u[10];
+    for (int t = 0; t < 5; t++) {
+        const double2 v = h2[t];
+        u[2 * t] = v.x; u[2 * t + 1] = v.y;
+    }
+    acg_conj(M, u, P);
+}
+
+template <bool REG>
+THX_DEV void calvari_acg_impl(const double* Q, int m, int lane, double* __restrict__ hist,
+                              double* A2)
+{
+    constexpr int maxIt = ACG_HIST_MAX;
+    double qr[REG ? QREG : 1][4];
+    int nd = 0, nIn = 0;
+    unsigned runs = 0;
+    if (REG) {                                     // as infer_acg_impl
+        const int i0 = lane * QREG;
+        nIn = max(0, min(QREG, m - i0));
+        unsigned starts = 0;
+        double prev[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int p = 0; p < QREG; p++) {
+            if (p < nIn) {
+                const double* c = Q + 4 * (i0 + p);
+                const double c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+                if (p == 0 || c0 != prev[0] || c1 != prev[1] || c2 != prev[2] || c3 != prev[3])
+                    starts |= 1u << p;
+                prev[0] = c0; prev[1] = c1; prev[2] = c2; prev[3] = c3;
+            }
+        }
+        runs = starts;
+        nd = __builtin_popcount(starts);
+#pragma unroll
+        for (int p = 0; p < QREG; p++) {
+            if (starts) {
+                const double* c = Q + 4 * (i0 + __builtin_ctz(starts));
+                starts &= starts - 1;
+                for (int k = 0; k < 4; k++) qr[p][k] = c[k];
+            }
+        }
+    }
+    double A[16], B[16];
+    for (int k = 0; k < 16; k++) B[k] = (k % 5 == 0) ? 1.0 : 0.0;
+    // one pass of the fixed point (infer_acg_impl's): A <- B, B <- F(A); sum
+    // |A - B|.  fromMem: the particles re-read from Q (the continuation past
+    // the history, so that the register cloud is dead during the replay)
+    auto step = [&](bool fromMem) -> double {
+        for (int k = 0; k < 16; k++) A[k] = B[k];
+        double Ai[16], Mp[10];
+        inv4_acc(A, Ai);
+        pack10(Ai, Mp);
+        double b[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, nf = 0.0;
+        auto term = [&](const double* q, double w) {
+            const double r = w * rcp_nr(quad10(Mp, q));
+            int t = 0;
+            for (int j = 0; j < 4; j++) {
+                const double qj = q[j] * r;
+                for (int k = j; k < 4; k++) b[t++] += qj * q[k];
+            }
+            nf += r;
+        };
+        if (REG && !fromMem) {
+            unsigned rs = runs;
+#pragma unroll
+            for (int p = 0; p < QREG; p++) {
+                if (p < nd) {
+                    const int s0 = __builtin_ctz(rs);
+                    rs &= rs - 1;
+                    term(qr[p], (double)((rs ? __builtin_ctz(rs) : nIn) - s0));
+                }
+            }
+        } else {
+            for (int i = lane; i < m; i += GROUP) term(Q + 4 * i, 1.0);
+        }
+        for (int t = 0; t < 10; t++) b[t] = group_sum(b[t]);
+        nf = group_sum(nf);
+        int t = 0;
+        for (int j = 0; j < 4; j++)
+            for (int k = j; k < 4; k++, t++) B[4 * j + k] = B[4 * k + j] = b[t] * (4.0 * rcp_nr(nf));
+        double crit = 0.0;
+        for (int k = 0; k < 16; k++) crit += fabs(A[k] - B[k]);
+        return crit;
+    };
+    // first fixed point, its iterates B_1 .. B_it1 kept
+    int it1 = maxIt;
+    for (int it = 0; it < maxIt; it++) {
+        const double crit = step(false);
+        if (lane == 0) {
+            double2* h2 = reinterpret_cast<double2*>(hist + 10 * it);
+            h2[0] = make_double2(B[0], B[1]);
+            h2[1] = make_double2(B[2], B[3]);
+            h2[2] = make_double2(B[5], B[6]);
+            h2[3] = make_double2(B[7], B[10]);
+            h2[4] = make_double2(B[11], B[15]);
+        }
+        if (!(crit > 1e-3)) { it1 = it + 1; break; }
+    }
+    double mean[4];
+    principal_axis(A, mean);
+    // M: q -> qmul(c, q), c = conj(mean)
+    const double ca = mean[0], cb = -mean[1], cc = -mean[2], cd = -mean[3];
+    const double M[16] = {ca, -cb, -cc, -cd, cb, ca, -cd, cc, cc, cd, ca, -cb, cd, -cc, cb, ca};
+    // the group's lane 0 wrote the history: make it visible to the group's lanes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // replay: iteration k of the second pass compares B'_k with B'_{k+1}
+    // (B'_k = M hist[k - 1] M^T, B'_0 = I) and stops at the first k where
+    // !(sum |B'_k - B'_{k+1}| > 1e-3), returning B'_k
+    const int gBase = (int)(threadIdx.x & 63) & ~(GROUP - 1);
+    int kStop = -1;
+    for (int k0 = 0; k0 < it1 && kStop < 0; k0 += GROUP) {
+        const int k = k0 + lane;
+        bool stop = false;
+        if (k < it1) {
+            double Pk[16], Pn[16];
+            if (k == 0) for (int t = 0; t < 16; t++) Pk[t] = (t % 5 == 0) ? 1.0 : 0.0;
+            else acg_conj_hist(M, hist + 10 * (k - 1), Pk);
+            acg_conj_hist(M, hist + 10 * k, Pn);
+            double crit = 0.0;
+            for (int t = 0; t < 16; t++) crit += fabs(Pk[t] - Pn[t]);
+            stop = !(crit > 1e-3);
+        }
+        const unsigned bits = (unsigned)(__ballot(stop) >> gBase) & ((1u << GROUP) - 1);
+        if (bits) kStop = k0 + __builtin_ctz(bits);
+    }
+    if (kStop == 0) {
+        for (int t = 0; t < 16; t++) A2[t] = (t % 5 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    if (kStop > 0 || it1 == maxIt) {               // stopped in the history, or ran to the cap
+        acg_conj_hist(M, hist + 10 * ((kStop > 0 ? kStop : maxIt) - 1), A2);
+        return;
+    }
+    // the second pass needs iterates past the first's: continue the first
+    // recurrence from (B_{it1 - 1}, B_it1)
+    double P[16];
+    {
+        double u[10];
+        int t = 0;
+        for (int j = 0; j < 4; j++)
+            for (int k = j; k < 4; k++, t++) u[t] = B[4 * j + k];
+        acg_conj(M, u, P);                         // B'_it1
+    }
+    for (int k = it1; k < maxIt; k++) {
+        for (int t = 0; t < 16; t++) A2[t] = P[t];
+        step(true);
+        double u[10], Pn[16];
+        int t = 0;
+        for (int j = 0; j < 4; j++)
+            for (int i = j; i < 4; i++, t++) u[t] = B[4 * j + i];
+        acg_conj(M, u, Pn);
+        double crit = 0.0;
+        for (int q = 0; q < 16; q++) crit += fabs(A2[q] - Pn[q]);
+        if (!(crit > 1e-3)) return;
+        for (int q = 0; q < 16; q++) P[q] = Pn[q];
+    }
+}
+
 // Particle::calVari (src/Particle.cpp:1004-1121), 3D: R -- de-mean by the
 // ACG principal axis (PARTICLE_ROT_MEAN_USING_STAT_CAL_VARI), k_j =
 // A(j, j) / A(0, 0) of inferACG on the de-meaned cloud (:184-222), floored at
@@ -375,17 +609,26 @@ __global__ void __launch_bounds__(256) k_pf_calvari(int nImg, int mR, const doub
                                                     double kFloor, double sFloor,
                                                     double* __restrict__ kOut,
                                                     double* __restrict__ sOut,
-                                                    const int* __restrict__ done = nullptr)
+                                                    const int* __restrict__ done = nullptr,
+                                                    double* __restrict__ hist = nullptr)
 {
     const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
     const int lane = threadIdx.x % GROUP;
     if (l >= nImg || (done && done[l])) return;
     const double* Q = quat + (size_t)l * mR * 4;
-    double A[16], mean[4], cm[4];
-    infer_acg(Q, mR, nullptr, lane, A);
-    principal_axis(A, mean);
-    cm[0] = mean[0]; cm[1] = -mean[1]; cm[2] = -mean[2]; cm[3] = -mean[3];
-    infer_acg(Q, mR, cm, lane, A);
+    double A[16];
+    if (hist) {
+        // both fixed points from one (calvari_acg_impl)
+        double* h = hist + (size_t)l * ACG_HIST;
+        if (mR <= GROUP * QREG) calvari_acg_impl<true>(Q, mR, lane, h, A);
+        else calvari_acg_impl<false>(Q, mR, lane, h, A);
+    } else {
+        double mean[4], cm[4];
+        infer_acg(Q, mR, nullptr, lane, A);
+        principal_axis(A, mean);
+        cm[0] = mean[0]; cm[1] = -mean[1]; cm[2] = -mean[2]; cm[3] = -mean[3];
+        infer_acg(Q, mR, cm, lane, A);
+    }
     const double* Tr = trans + (size_t)l * mT * 2;
     double sx = 0, sy = 0;
     for (int i = lane; i < mT; i += GROUP) { sx += Tr[2 * i]; sy += Tr[2 * i + 1]; }
@@ -1141,7 +1384,8 @@ __global__ void __launch_bounds__(256) k_pf_calvari2d(int nImg, int mR, const do
                                                       double kFloor, double sFloor,
                                                       double* __restrict__ kOut,
                                                       double* __restrict__ sOut,
-                                                      const int* __restrict__ done = nullptr)
+                                                      const int* __restrict__ done = nullptr,
+                                                      double* __restrict__ = nullptr)   // k_pf_calvari's hist
 {
     const int l = (blockIdx.x * 256 + threadIdx.x) / GROUP;
     const int lane = threadIdx.x % GROUP;
@@ -1492,6 +1736,7 @@ struct Plan {
     double* kv; double* sv; double* peakR;   // calVari k1..k3, s0 s1; setPeakFactor(R)
     double* topQ;                            // calRank1st _topR
     double* meanQ;                           // k_pf_mean's perturbation mean
+    double* acgHist;                         // calVari's fixed-point iterates (calvari_acg_impl)
     float* wC; float* wR; float* wT; float* base; double* pC;
     int* cls; int* nP; int* done; int* act; int* nAct;   // classes, phases run, active list
     int* doneSnap;                       // done as of a side-stream fork (k_pf_mean on s2)
@@ -1544,6 +1789,7 @@ Plan plan(void* base, const thx_expect_cfg& c, int nImg, int nPxl, int nVisit, i
     p.peakR = k.take<double>(nImg);
     p.topQ = k.take<double>((size_t)nImg * 4);
     p.meanQ = k.take<double>((size_t)nImg * 4);
+    p.acgHist = k.take<double>(!twoD ? (size_t)nImg * ACG_HIST : 0);
     p.wC = k.take<float>(nImg);
     p.wR = k.take<float>((size_t)nImg * c.mLR);
     p.wT = k.take<float>((size_t)nImg * c.mLT);
@@ -1637,9 +1883,15 @@ extern "C" int thx_pf_calvari(int nImg, int mR, const double* quat, int mT, cons
     THX_CHECK_ARG(nImg >= 0 && mR > 0 && mT > 0, "thx_pf_calvari: bad sizes");
     THX_CHECK_ARG(nImg == 0 || (quat && trans && k && sd), "thx_pf_calvari: null argument");
     if (nImg == 0) return THX_OK;
-    hipLaunchKernelGGL(k_pf_calvari, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0,
-                       thx::as_stream(stream), nImg, mR, quat, mT, trans, kFloor, sFloor, k, sd);
-    THX_LAUNCH_CHECK();
+    // the fixed points' history (calvari_acg_impl), stream-ordered scratch
+    hipStream_t s = thx::as_stream(stream);
+    double* hist = nullptr;
+    THX_HIP(hipMallocAsync(reinterpret_cast<void**>(&hist), sizeof(double) * nImg * ACG_HIST, s));
+    hipLaunchKernelGGL(k_pf_calvari, dim3(thx::cdiv(nImg * GROUP, 256)), dim3(256), 0, s, nImg, mR,
+                       quat, mT, trans, kFloor, sFloor, k, sd, nullptr, hist);
+    const hipError_t e = hipGetLastError();
+    THX_HIP(hipFreeAsync(hist, s));
+    THX_HIP(e);
     return THX_OK;
 }
 
@@ -2069,7 +2321,8 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                                               1002u, nullptr, s));
         THX_RET(fork());
         hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, side->s,
-                           nImg, c.mLR, quat, c.mLT, trans, c.kMin, c.sMin, p.kv, p.sv, nullptr);
+                           nImg, c.mLR, quat, c.mLT, trans, c.kMin, c.sMin, p.kv, p.sv, nullptr,
+                           p.acgHist);
         THX_LAUNCH_CHECK();
         THX_RET(join_rec());
     } else {
@@ -2080,7 +2333,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             THX_RET(thx::pf_symmetrise_launch(nImg, c.mLR, quat, 2, nullptr, c.symQuat, nSym, c.seed,
                                               1002u, nullptr, s));
         hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, s, nImg,
-                           c.mLR, quat, c.mLT, trans, 0.0, 0.0, p.kv, p.sv, nullptr);
+                           c.mLR, quat, c.mLT, trans, 0.0, 0.0, p.kv, p.sv, nullptr, p.acgHist);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_top_by_weight, dim3(gOne), dim3(256), 0, s, nImg, c.mLR, quat, pR, p.topQ);
         THX_LAUNCH_CHECK();
@@ -2215,7 +2468,8 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         // perturbation and the stopping rule only)
         THX_RET(fork());
         hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, side->s,
-                           nImg, c.mLR, p.tmpQ, c.mLT, p.tmpT, 0.0, 0.0, p.kv, p.sv, done);
+                           nImg, c.mLR, p.tmpQ, c.mLT, p.tmpT, 0.0, 0.0, p.kv, p.sv, done,
+                           p.acgHist);
         THX_LAUNCH_CHECK();
         THX_RET(join_rec());
         // resample R and T by the phase marginals; ancestors gathered in place
