@@ -371,7 +371,10 @@ int thx_pf_resample(int nImg, int nIn, int nOut, const double* w, int ldw,
  *   k[3 l + j-1] = max(kFloor, A(j,j)/A(0,0)) of inferACG
  *   (src/Geometry/DirectionalStat.cpp:93-222) on the cloud de-meaned by its
  *   ACG principal axis; sd[2 l + c] = max(sFloor, gsl_stats_sd(t_c)).
- *   quat: nImg x mR x 4, trans: nImg x mT x 2.
+ *   quat: nImg x mR x 4, trans: nImg x mT x 2.  The de-meaned fixed point is
+ *   the first one's iterates replayed through the de-meaning rotation (equal
+ *   in exact arithmetic); their history takes 20 KB per image of
+ *   stream-ordered scratch (hipMallocAsync on `stream`) for the call.
  * thx_pf_balance_rot -- Particle::balanceWeight(PAR_R), 3D
  *   (src/Particle.cpp:2330-2340): pR = 1/pdfACG(q, inferACG(Q)), normalised.
  * thx_pf_peak -- Particle::setPeakFactor(PAR_R) (src/Particle.cpp:1920-1925,
