@@ -1114,11 +1114,14 @@ void shuffle_perm_launch(int nImg, int nIn, bool shuffle, uint64_t seed, uint32_
 }
 
 // gather ancestors: dst[l][j][:] = src[l (or shared)][anc[l][j]][:]
+// keepDone: a done image's particles are copied unchanged (src and dst are
+// the two buffers of the phases' ping-pong, lds = nOut * width)
 __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
                                                 const double* __restrict__ src, long lds,
                                                 int nIn, const int* __restrict__ anc,
                                                 double* __restrict__ dst,
-                                                const int* __restrict__ done = nullptr)
+                                                const int* __restrict__ done = nullptr,
+                                                int keepDone = 0)
 {
     const long n = (long)nImg * nOut * width;
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n;
@@ -1126,7 +1129,10 @@ __global__ void __launch_bounds__(256) k_gather(int nImg, int nOut, int width,
         const int c = (int)(q % width);
         const long lj = q / width;
         const int l = (int)(lj / nOut);
-        if (done && done[l]) continue;
+        if (done && done[l]) {
+            if (keepDone) dst[q] = src[q];
+            continue;
+        }
         const int a = anc[lj];
         dst[q] = src[(size_t)l * lds + (size_t)a * width + c];
         (void)nIn;
@@ -2389,13 +2395,21 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         sel.active = p.act;
         sel.nActive = p.nAct;
     }
+    // the particle clouds ping-pong between the caller's buffers and
+    // tmpQ / tmpT: a phase reads the current pair and the resampling gathers
+    // into the other (the pre-resample cloud stays readable for calVari and
+    // the mean without a copy); the caller's buffers get the last one
+    double* cq = quat;
+    double* ct = trans;
+    double* nq = p.tmpQ;
+    double* nt = p.tmpT;
     for (int phase = phase0; phase < phase0 + nPh; phase++) {
         const bool large = phase == phase0 && (!global || c.largeFirst);
         if (twoD) {
             // MODE_2D perturb (von Mises, no mean) + balanceWeight (R, T)
             THX_RET(join());
-            hipLaunchKernelGGL(k_pf_perturb2d, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
-                               trans, pR, pT, p.kv, p.sv,
+            hipLaunchKernelGGL(k_pf_perturb2d, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, cq,
+                               ct, pR, pT, p.kv, p.sv,
                                large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
                                c.seed, (uint32_t)(2000 + phase), done);
             THX_LAUNCH_CHECK();
@@ -2404,15 +2418,15 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                 THX_RET(join2());      // forked after the last phase's rotation resampling
                 meanAhead = false;
             } else {
-                hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, quat,
+                hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, cq,
                                    c.acgIters, done, p.meanQ, nullptr);
                 THX_LAUNCH_CHECK();
             }
         }
         if (!twoD) {
             THX_RET(join());     // the spreads of the previous calVari
-            hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, quat,
-                               trans, pR, pT, p.topQ, p.kv, p.sv,
+            hipLaunchKernelGGL(k_pf_perturb, dim3(gPf), dim3(256), 0, s, nImg, c.mLR, c.mLT, cq,
+                               ct, pR, pT, p.topQ, p.kv, p.sv,
                                large ? c.perturbFactorL : c.perturbFactor, c.transS, c.transM,
                                c.seed, (uint32_t)(2000 + phase), c.perturbMean, p.meanQ, done,
                                c.symQuat, nSym);
@@ -2435,7 +2449,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         hipEvent_t* ev = pi < c.nPhaseEvents ? static_cast<hipEvent_t*>(c.phaseEvents) : nullptr;
         if (twoD) {
             if (ev) THX_HIP(hipEventRecord(ev[2 * pi], s));
-            THX_RET(thx::local_phase2d_launch(vol, c.vdim, c.pf, clsSel, quat, 4, c.mLR, trans,
+            THX_RET(thx::local_phase2d_launch(vol, c.vdim, c.pf, clsSel, cq, 4, c.mLR, ct,
                                               c.mLT, p.pC, pR, pT, dat, cs ? p.ctfD : ctf, sigRcp,
                                               iCol, iRow, nPxl, c.idim, nImg, p.wC, p.wR, p.wT,
                                               p.base, static_cast<float*>(p.localWs), done, s,
@@ -2445,7 +2459,7 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         } else
         THX_RET(thx::local_phase_timed(&sel, ev ? ev[2 * pi] : nullptr, ev ? ev[2 * pi + 1] : nullptr,
                                        phaseVol, phaseLayout, c.vdim,
-                                       c.pf, quat, c.mLR, trans, c.mLT, p.pC, pR, pT,
+                                       c.pf, cq, c.mLR, ct, c.mLT, p.pC, pR, pT,
                                        dat, cs ? p.ctfD : ctf, sigRcp, iCol, iRow, pxOrder, nOrd,
                                        nPxl, c.idim, nImg, p.wC, p.wR, p.wT, p.base, p.localWs,
                                        p.localWsBytes, stream, mLD, cs ? cs->pD : nullptr, p.wD,
@@ -2458,17 +2472,13 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
         // resampling gathers from, then the pre-resample cloud, kept for calVari
         // and the gathers
         if (!twoD)
-            THX_RET(thx::pf_symmetrise_launch(nImg, c.mLR, quat, 2, nullptr, c.symQuat, nSym, c.seed,
+            THX_RET(thx::pf_symmetrise_launch(nImg, c.mLR, cq, 2, nullptr, c.symQuat, nSym, c.seed,
                                               (uint32_t)(5000 + phase), done, s));
-        THX_HIP(hipMemcpyAsync(p.tmpQ, quat, sizeof(double) * nImg * c.mLR * 4,
-                               hipMemcpyDeviceToDevice, s));
-        THX_HIP(hipMemcpyAsync(p.tmpT, trans, sizeof(double) * nImg * c.mLT * 2,
-                               hipMemcpyDeviceToDevice, s));
         // calVari of the pre-resample cloud on the side stream (needed by the next
         // perturbation and the stopping rule only)
         THX_RET(fork());
         hipLaunchKernelGGL(twoD ? k_pf_calvari2d : k_pf_calvari, dim3(gPf), dim3(256), 0, side->s,
-                           nImg, c.mLR, p.tmpQ, c.mLT, p.tmpT, 0.0, 0.0, p.kv, p.sv, done,
+                           nImg, c.mLR, cq, c.mLT, ct, 0.0, 0.0, p.kv, p.sv, done,
                            p.acgHist);
         THX_LAUNCH_CHECK();
         THX_RET(join_rec());
@@ -2494,16 +2504,16 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
             THX_HIP(hipEventRecord(side->fork2, s));
             THX_HIP(hipStreamWaitEvent(side->s2, side->fork2, 0));
             sideGuard.open2 = true;
-            hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, side->s2, nImg, c.mLR, p.tmpQ,
+            hipLaunchKernelGGL(k_pf_mean, dim3(gPf), dim3(256), 0, side->s2, nImg, c.mLR, cq,
                                c.acgIters, done ? p.doneSnap : nullptr, p.meanQ, nullptr, p.ancR);
             THX_LAUNCH_CHECK();
             meanAhead = true;
         }
-        hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, p.tmpQ,
-                           (long)c.mLR * 4, c.mLR, p.ancR, quat, done);
+        hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLR, 4, (const double*)cq,
+                           (long)c.mLR * 4, c.mLR, p.ancR, nq, done, 1);
         THX_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_top_copy, dim3(thx::cdiv(4 * nImg, 256)), dim3(256), 0, s, nImg,
-                           p.tmpQ, (long)c.mLR * 4, p.topR, p.topQ, done);
+                           cq, (long)c.mLR * 4, p.topR, p.topQ, done);
         THX_LAUNCH_CHECK();
         shuffle_perm_launch(nImg, c.mLT, c.shuffle, c.seed, (uint32_t)(4000 + phase), p.perm, done, s);
         THX_LAUNCH_CHECK();
@@ -2513,9 +2523,12 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
                            p.topT, p.cdf, c.shuffle ? p.perm : nullptr, nullptr, nullptr, nullptr,
                            0, done);
         THX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, p.tmpT,
-                           (long)c.mLT * 2, c.mLT, p.anc, trans, done);
+        hipLaunchKernelGGL(k_gather, dim3(1024), dim3(256), 0, s, nImg, c.mLT, 2, (const double*)ct,
+                           (long)c.mLT * 2, c.mLT, p.anc, nt, done, 1);
         THX_LAUNCH_CHECK();
+        // the resampled clouds are current from here
+        std::swap(cq, nq);
+        std::swap(ct, nt);
         if (cs) {
             // calRank1st, calVari, resample (mLD, PAR_D) (src/Optimiser.cpp:1483-1488);
             // no peak factor (OPTIMISER_PEAK_FACTOR_D is off, include/Config.h:220)
@@ -2558,6 +2571,10 @@ static int expectation_impl(const thx_expect_cfg* cfg, const thx_ctf_search_cfg*
     }
     THX_RET(join());     // nothing of this call stays on the side streams
     THX_RET(join2());
+    if (cq != quat) {
+        THX_HIP(hipMemcpyAsync(quat, cq, sizeof(double) * nImg * c.mLR * 4, hipMemcpyDeviceToDevice, s));
+        THX_HIP(hipMemcpyAsync(trans, ct, sizeof(double) * nImg * c.mLT * 2, hipMemcpyDeviceToDevice, s));
+    }
     if (!c.converge) {
         hipLaunchKernelGGL(k_fill_int, dim3(64), dim3(256), 0, s, nPD, (long)nImg,
                            phase0 + c.nPhase - 1);
